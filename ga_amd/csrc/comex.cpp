@@ -1,0 +1,785 @@
+// comex.cpp -- the ComEx C API (include/comex.h) on MI355X.
+//
+// Reference: comex/src-mpi-pr/comex.c (MPI progress-rank transport).  The map:
+//
+//   comex_accs/nbaccs  (985-1007, 1998-2027) -> xfer(X_ACC)
+//     nb_accs (6890-6962): L = 0 -> one _acc; self/SMP -> per-row _acc;
+//     else pack -> progress rank -> unpack-acc.
+//     Here: target = self -> ONE fused strided-acc kernel on this GPU's stream
+//           (no pack, 24 B/element); target = other rank -> pack kernel into
+//           this rank's exported staging HBM, request into the owner's inbox,
+//           the owner's progress thread runs the unpack-acc kernel (reading the
+//           packed bytes over xGMI) on the owner's stream, so accumulates into
+//           one target are serialised by that target's stream as the
+//           reference serialises them with sem_wait(semaphores[target]).
+//   comex_puts/gets (6342-6427, 6617-6696)   -> xfer(X_PUT/X_GET): one strided
+//           copy kernel; a remote side is addressed through its IPC mapping.
+//   comex_malloc (2359-2605)                 -> hipMalloc in HBM + IPC handle
+//           allgather (the reg_entry_t MPI_Allgather at 2461) + IPC open.
+//   comex_fence_* (1074-1191), comex_barrier (1217-1234), comex_wait* (1776-1802).
+//
+// Host (non-HBM) buffers are accepted everywhere: pinned memory is used in
+// place (device-mapped), pageable memory is registered for the call.  All
+// arithmetic runs on the GPU; there is no CPU compute path.
+#include "runtime.hpp"
+#include "gaamd_kernels.h"
+#include "../../include/comex.h"
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+#include <sched.h>
+#include <deque>
+#include <algorithm>
+
+namespace gaamd {
+
+static const long kPage = 4096;
+
+static void ensure_init() {
+    if (!rt().initialized) fatal("comex used before comex_init");
+}
+
+// ---- groups ---------------------------------------------------------------
+static std::vector<std::vector<int>> g_groups;   // group id - 1 -> world ranks
+
+int translate_world(int group, int proc) {
+    Runtime &r = rt();
+    if (group == COMEX_GROUP_WORLD) {
+        if (proc < 0 || proc >= r.size) fatal("proc %d out of range [0,%d)", proc, r.size);
+        return proc;
+    }
+    if (group < 1 || group > (int)g_groups.size() || g_groups[group - 1].empty())
+        fatal("invalid comex group %d", group);
+    const std::vector<int> &g = g_groups[group - 1];
+    if (proc < 0 || proc >= (int)g.size()) fatal("proc %d out of range of group %d", proc, group);
+    return g[proc];
+}
+
+// ---- pointer resolution ---------------------------------------------------
+struct View {
+    char *dev = nullptr;       // device-accessible address of the user pointer
+    void *registered = nullptr;   // page base we registered for this call
+};
+
+static bool find_segment_local(const void *p, int64_t lo, int64_t hi) {
+    Runtime &r = rt();
+    const uintptr_t a = (uintptr_t)p;
+    for (const Segment &s : r.segs) {
+        if (!s.live || s.peer.empty()) continue;
+        const PeerMap &m = s.peer[r.rank];
+        if (m.bytes && a + lo >= m.base && a + hi <= m.base + m.bytes) return true;
+    }
+    return false;
+}
+
+// address of rank `owner`'s byte `p` (owner's address space) in this process
+static char *remote_view(int owner, const void *p, int64_t lo, int64_t hi) {
+    Runtime &r = rt();
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> g(r.seg_mu);
+    for (const Segment &s : r.segs) {
+        if (!s.live) continue;
+        const PeerMap &m = s.peer[owner];
+        if (m.bytes && a + lo >= m.base && a + hi <= m.base + m.bytes) return m.mapped + (a - m.base);
+    }
+    fatal("address %p [%ld,%ld) of rank %d is not inside a comex_malloc segment", p, (long)lo, (long)hi, owner);
+}
+
+static View local_view(void *p, int64_t lo, int64_t hi) {
+    View v;
+    if (find_segment_local(p, lo, hi)) {
+        v.dev = (char *)p;
+        return v;
+    }
+    hipPointerAttribute_t at;
+    memset(&at, 0, sizeof(at));
+    hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e == hipSuccess && (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged)) {
+        v.dev = (char *)p;
+        return v;
+    }
+    if (e == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer) {
+        v.dev = (char *)at.devicePointer;   // pinned / already registered host memory
+        return v;
+    }
+    (void)hipGetLastError();
+    // pageable host memory: pin + map the span for this call
+    const uintptr_t a0 = ((uintptr_t)p + lo) & ~(uintptr_t)(kPage - 1);
+    const uintptr_t a1 = (((uintptr_t)p + hi) + kPage - 1) & ~(uintptr_t)(kPage - 1);
+    GA_HIP(hipHostRegister((void *)a0, a1 - a0, hipHostRegisterMapped));
+    void *dbase = nullptr;
+    GA_HIP(hipHostGetDevicePointer(&dbase, (void *)a0, 0));
+    v.registered = (void *)a0;
+    v.dev = (char *)dbase + ((uintptr_t)p - a0);
+    return v;
+}
+
+static void release_view(View &v) {
+    if (v.registered) GA_HIP(hipHostUnregister(v.registered));
+    v.registered = nullptr;
+}
+
+// ---- non-blocking handles ------------------------------------------------
+static int nb_alloc() {
+    Runtime &r = rt();
+    for (int k = 0; k < kMaxNb; ++k) {
+        const int i = (r.nb_next + k) % kMaxNb;
+        if (!r.nb_used[i]) {
+            r.nb_used[i] = true;
+            r.nb_next = (i + 1) % kMaxNb;
+            return i;
+        }
+    }
+    // table full: complete the oldest like nb_wait_for_handle (comex.c:5653)
+    const int i = r.nb_next;
+    GA_HIP(hipEventSynchronize(r.nb_ev[i]));
+    r.nb_next = (i + 1) % kMaxNb;
+    return i;
+}
+
+static void nb_complete_now(comex_request_t *h) {
+    Runtime &r = rt();
+    const int i = nb_alloc();
+    GA_HIP(hipEventRecord(r.nb_ev[i], r.stream));
+    *h = i;
+}
+
+// ---- remote accumulate: staging ring + owner inbox ------------------------
+struct Pending { uint64_t seq, off, len; };
+static std::vector<std::deque<Pending>> g_pend;   // per target
+
+static size_t sub_ring_bytes() {
+    Runtime &r = rt();
+    return (r.staging_bytes / (size_t)r.size) & ~(size_t)255;
+}
+
+static void reap(int t) {
+    Runtime &r = rt();
+    const uint64_t done = r.shm->done[r.rank][t].load(std::memory_order_acquire);
+    while (!g_pend[t].empty() && g_pend[t].front().seq <= done) g_pend[t].pop_front();
+}
+
+static void wait_done(int t, uint64_t seq) {
+    Runtime &r = rt();
+    for (unsigned spins = 0; r.shm->done[r.rank][t].load(std::memory_order_acquire) < seq; ++spins)
+        if (spins > 256) sched_yield();
+    reap(t);
+}
+
+// reserve `len` bytes in the staging sub-ring for target t (FIFO release)
+static uint64_t stage_alloc(int t, uint64_t len) {
+    Runtime &r = rt();
+    const uint64_t sub = sub_ring_bytes();
+    if (len > sub) fatal("staging request %lu exceeds ring %lu", (unsigned long)len, (unsigned long)sub);
+    for (;;) {
+        reap(t);
+        std::deque<Pending> &q = g_pend[t];
+        uint64_t &head = r.stage_head[t];
+        if (q.empty()) {
+            head = 0;
+            return 0;
+        }
+        const uint64_t tail = q.front().off;   // oldest bytes still being read by the owner
+        if (head > tail) {
+            if (head + len <= sub) return head;
+            if (len <= tail) return 0;             // wrap to the start of the ring
+        } else if (head < tail) {
+            if (head + len <= tail) return head;
+        }                                          // head == tail with pending data: ring full
+        wait_done(t, q.front().seq);
+    }
+}
+
+static void post_request(int t, int op, const void *scale, uint64_t dst_addr, const int *dst_stride,
+                         const int *count, int levels, uint64_t off, uint64_t len, uint64_t rb, uint64_t re) {
+    Runtime &r = rt();
+    Inbox *ib = inbox_of(r.shm, t);
+    const uint64_t ticket = ib->tail.fetch_add(1, std::memory_order_acq_rel);
+    Request &q = ib->slot[ticket % kInboxSlots];
+    // the slot belongs to our lap once the previous lap's ticket is consumed
+    for (unsigned spins = 0; ib->head.load(std::memory_order_acquire) + kInboxSlots <= ticket; ++spins)
+        if (spins > 256) sched_yield();
+    for (unsigned spins = 0;; ++spins) {
+        uint32_t expect = 0;
+        if (q.state.compare_exchange_weak(expect, 1, std::memory_order_acq_rel)) break;
+        if (spins > 256) sched_yield();
+    }
+    q.src_rank = r.rank;
+    q.op = op;
+    q.levels = levels;
+    memset(q.count, 0, sizeof(q.count));
+    memset(q.dst_stride, 0, sizeof(q.dst_stride));
+    for (int j = 0; j <= levels; ++j) q.count[j] = count[j];
+    for (int j = 0; j < levels; ++j) q.dst_stride[j] = dst_stride[j];
+    q.dst_addr = dst_addr;
+    q.staging_off = off;
+    q.bytes = len;
+    q.seq = (rb << 32) | (re & 0xffffffffull);   // row range travels in seq
+    memset(q.scale, 0, sizeof(q.scale));
+    if (scale) memcpy(q.scale, scale, (size_t)elem_size(op));
+    q.state.store(2, std::memory_order_release);
+}
+
+// owner side: drain the inbox in ticket order
+static void progress_loop() {
+    Runtime &r = rt();
+    GA_HIP(hipSetDevice(r.device));
+    Inbox *ib = inbox_of(r.shm, r.rank);
+    struct Inflight { hipEvent_t ev; int src; };
+    std::deque<Inflight> inflight;
+    std::vector<hipEvent_t> pool;
+    unsigned idle = 0;
+    for (;;) {
+        bool worked = false;
+        const uint64_t h = ib->head.load(std::memory_order_relaxed);
+        Request &q = ib->slot[h % kInboxSlots];
+        if (q.state.load(std::memory_order_acquire) == 2) {
+            const int src = q.src_rank;
+            const char *packed = r.peer_staging[src] + q.staging_off;
+            const uint64_t rb = q.seq >> 32, re = q.seq & 0xffffffffull;
+            int pstride[8];
+            {
+                int64_t acc = q.count[0];
+                for (int j = 0; j < q.levels; ++j) { pstride[j] = (int)acc; acc *= q.count[j + 1]; }
+            }
+            // packed rows rb..re start at staging_off; rebase the packed side
+            const char *packed0 = packed - (int64_t)rb * q.count[0];
+            hipEvent_t ev;
+            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            else { ev = pool.back(); pool.pop_back(); }
+            {
+                std::lock_guard<std::mutex> g(r.launch_mu);
+                const int rc = launch_strided(q.op, q.scale, packed0, pstride, (void *)q.dst_addr, q.dst_stride,
+                                              q.count, q.levels, r.stream, nullptr, rb, re);
+                if (rc) fatal("unpack-acc launch failed (%d)", rc);
+                GA_HIP(hipEventRecord(ev, r.stream));
+            }
+            inflight.push_back({ev, src});
+            q.state.store(0, std::memory_order_release);
+            ib->head.store(h + 1, std::memory_order_release);
+            worked = true;
+        }
+        while (!inflight.empty()) {
+            hipError_t e = hipEventQuery(inflight.front().ev);
+            if (e == hipErrorNotReady) break;
+            if (e != hipSuccess) fatal("unpack-acc failed: %s", hipGetErrorString(e));
+            r.shm->done[inflight.front().src][r.rank].fetch_add(1, std::memory_order_release);
+            pool.push_back(inflight.front().ev);
+            inflight.pop_front();
+            worked = true;
+        }
+        if (worked) { idle = 0; continue; }
+        if (r.stop.load(std::memory_order_acquire) && inflight.empty() &&
+            ib->head.load() == ib->tail.load())
+            break;
+        if (++idle > 64) usleep(idle > 4096 ? 200 : 20);
+        else sched_yield();
+    }
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+}
+
+static void remote_acc(int t, int op, const void *scale, void *src, const int *ss, void *dst, const int *ds,
+                       const int *count, int levels) {
+    Runtime &r = rt();
+    const int esz = elem_size(op);
+    const int64_t row_bytes = (int64_t)(count[0] / esz) * esz;
+    uint64_t rows = 1;
+    for (int j = 1; j <= levels; ++j) rows *= (uint64_t)count[j];
+    if (rows == 0 || row_bytes == 0) return;
+    int64_t slo = 0, shi = 0;
+    side_span_host(ss, count, levels, count[0], &slo, &shi);
+    View sv = local_view(src, slo, shi);
+    // destination must be a registered segment of the owner (reg_cache_find)
+    int64_t dlo = 0, dhi = 0;
+    side_span_host(ds, count, levels, count[0], &dlo, &dhi);
+    (void)remote_view(t, dst, dlo, dhi);
+
+    const uint64_t sub = sub_ring_bytes();
+    uint64_t rows_per_req = std::max<uint64_t>(1, sub / (uint64_t)count[0]);
+    if ((uint64_t)count[0] > sub) fatal("row of %d bytes exceeds staging ring", count[0]);
+    int pstride[8];
+    {
+        int64_t acc = count[0];
+        for (int j = 0; j < levels; ++j) { pstride[j] = (int)acc; acc *= count[j + 1]; }
+    }
+    for (uint64_t rb = 0; rb < rows; rb += rows_per_req) {
+        const uint64_t re = std::min(rows, rb + rows_per_req);
+        const uint64_t len = (re - rb) * (uint64_t)count[0];
+        const uint64_t off = stage_alloc(t, len);
+        char *stage = r.staging + (size_t)t * sub + off;
+        {
+            std::lock_guard<std::mutex> g(r.launch_mu);
+            // pack rows [rb, re) of src into the staging slice (rebased so row rb lands at `stage`)
+            const int rc = launch_strided(kOpCopy, nullptr, sv.dev, ss, stage - (int64_t)rb * count[0], pstride,
+                                          count, levels, r.stream, nullptr, rb, re);
+            if (rc) fatal("pack launch failed (%d)", rc);
+        }
+        GA_HIP(hipStreamSynchronize(r.stream));   // packed bytes complete before the owner reads them
+        const uint64_t seq = ++r.posted[t];
+        g_pend[t].push_back({seq, off, len});
+        r.stage_head[t] = off + len;
+        post_request(t, op, scale, (uint64_t)(uintptr_t)dst, ds, count, levels, (uint64_t)t * sub + off, len, rb, re);
+    }
+    release_view(sv);
+}
+
+static void fence_target(int t) {
+    Runtime &r = rt();
+    if (r.size == 1 || t == r.rank || r.posted.empty()) return;
+    wait_done(t, r.posted[t]);
+}
+
+// ---- the one transfer routine ---------------------------------------------
+enum Xfer { X_ACC, X_PUT, X_GET };
+
+static int64_t row_bytes_of(int op, int count0) {
+    const int esz = elem_size(op);
+    return (op == kOpCopy) ? count0 : (int64_t)(count0 / esz) * esz;
+}
+
+static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, int *ds, int *count,
+                int levels, int proc, int group, comex_request_t *hdl) {
+    ensure_init();
+    Runtime &r = rt();
+    if (levels < 0 || levels >= COMEX_MAX_STRIDE_LEVEL) fatal("stride_levels %d out of range", levels);
+    if (!count) fatal("count is NULL");
+    uint64_t rows = 1;
+    for (int j = 1; j <= levels; ++j) {
+        if (count[j] < 0) fatal("count[%d] = %d < 0", j, count[j]);
+        rows *= (uint64_t)count[j];
+    }
+    if (rows > 0 && count[0] <= 0) fatal("count[0] = %d bytes must be > 0", count[0]);   // nb_acc COMEX_ASSERT(bytes > 0)
+    if (!src || !dst) fatal("NULL src or dst");
+    if (kind == X_ACC) {
+        if (!elem_size(op) || op == kOpCopy) fatal("unknown accumulate op %d", op);
+        if (!scale) fatal("NULL scale");
+    }
+    const int world = translate_world(group, proc);
+    const int cop = (kind == X_ACC) ? op : kOpCopy;
+    if (hdl) *hdl = -1;
+    if (rows == 0) {
+        if (hdl) nb_complete_now(hdl);
+        return COMEX_SUCCESS;
+    }
+
+    if (world != r.rank && kind == X_ACC) {
+        remote_acc(world, op, scale, src, ss, dst, ds, count, levels);
+        if (hdl) nb_complete_now(hdl);
+        return COMEX_SUCCESS;
+    }
+
+    const int64_t rb = row_bytes_of(cop, count[0]);
+    int64_t slo = 0, shi = 0, dlo = 0, dhi = 0;
+    side_span_host(ss, count, levels, rb, &slo, &shi);
+    side_span_host(ds, count, levels, rb, &dlo, &dhi);
+    View sv, dv;
+    if (world != r.rank) {
+        // put: remote dst / get: remote src, through the owner's IPC mapping
+        fence_target(world);   // order after our own pending accumulates to it
+        if (kind == X_PUT) {
+            sv = local_view(src, slo, shi);
+            dv.dev = remote_view(world, dst, dlo, dhi);
+        } else {
+            sv.dev = remote_view(world, src, slo, shi);
+            dv = local_view(dst, dlo, dhi);
+        }
+    } else {
+        sv = local_view(src, slo, shi);
+        dv = local_view(dst, dlo, dhi);
+    }
+    {
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        const int rc = launch_strided(cop, scale, sv.dev, ss, dv.dev, ds, count, levels, r.stream, nullptr);
+        if (rc) fatal("strided %s launch failed (code %d): misaligned elements or bad descriptor",
+                      kind == X_ACC ? "acc" : (kind == X_PUT ? "put" : "get"), rc);
+    }
+    const bool host_side = sv.registered || dv.registered;
+    if (host_side || r.blocking_sync) {
+        GA_HIP(hipStreamSynchronize(r.stream));
+        release_view(sv);
+        release_view(dv);
+        if (hdl) nb_complete_now(hdl);
+        return COMEX_SUCCESS;
+    }
+    if (hdl) nb_complete_now(hdl);
+    return COMEX_SUCCESS;
+}
+
+static int xfer_contig(Xfer kind, int op, void *scale, void *src, void *dst, int bytes, int proc, int group,
+                       comex_request_t *hdl) {
+    int count[1] = {bytes};
+    if (bytes <= 0) fatal("contiguous transfer of %d bytes", bytes);   // nb_acc/nb_put assert bytes > 0
+    return xfer(kind, op, scale, src, nullptr, dst, nullptr, count, 0, proc, group, hdl);
+}
+
+static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int proc, int group,
+                    comex_request_t *hdl) {
+    // comex.c:7327-7400 (accv) / putv / getv: every (src[i], dst[i]) pair is one
+    // contiguous transfer of darr[k].bytes
+    for (int k = 0; k < len; ++k)
+        for (int i = 0; i < darr[k].count; ++i)
+            xfer_contig(kind, op, scale, darr[k].src[i], darr[k].dst[i], darr[k].bytes, proc, group, nullptr);
+    if (hdl) nb_complete_now(hdl);
+    return COMEX_SUCCESS;
+}
+
+}  // namespace gaamd
+
+using namespace gaamd;
+
+// ============================================================================
+// C ABI
+extern "C" {
+
+int comex_init() {
+    Runtime &r = rt();
+    if (r.initialized) return COMEX_SUCCESS;
+    boot_init();
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0)
+        fatal("no HIP device visible (%s): libga_amd runs its kernels on an MI355X and has no CPU path",
+              hipGetErrorString(e));
+    const char *dv = getenv("COMEX_AMD_DEVICE");
+    r.device = dv ? atoi(dv) : r.local_rank % ndev;
+    GA_HIP(hipSetDevice(r.device));
+    GA_HIP(hipStreamCreateWithFlags(&r.stream, hipStreamDefault));
+    for (int i = 0; i < kMaxNb; ++i) GA_HIP(hipEventCreateWithFlags(&r.nb_ev[i], hipEventDisableTiming));
+    const char *bs = getenv("COMEX_AMD_BLOCKING_SYNC");
+    r.blocking_sync = bs && atoi(bs) != 0;
+    if (r.size > 1) {
+        // staging HBM for remote accumulates, exported to every local rank
+        const char *mb = getenv("COMEX_AMD_STAGING_MB");
+        r.staging_bytes = (size_t)(mb ? atol(mb) : 256) << 20;
+        GA_HIP(hipMalloc((void **)&r.staging, r.staging_bytes));
+        struct { hipIpcMemHandle_t h; uint64_t bytes; } mine, *all;
+        memset(&mine, 0, sizeof(mine));
+        GA_HIP(hipIpcGetMemHandle(&mine.h, r.staging));
+        mine.bytes = r.staging_bytes;
+        std::vector<char> buf(sizeof(mine) * (size_t)r.size);
+        boot_allgather(&mine, buf.data(), sizeof(mine));
+        all = reinterpret_cast<decltype(all)>(buf.data());
+        r.peer_staging.assign(r.size, nullptr);
+        for (int q = 0; q < r.size; ++q) {
+            if (q == r.rank) { r.peer_staging[q] = r.staging; continue; }
+            void *p = nullptr;
+            GA_HIP(hipIpcOpenMemHandle(&p, all[q].h, hipIpcMemLazyEnablePeerAccess));
+            r.peer_staging[q] = (char *)p;
+        }
+        r.posted.assign(r.size, 0);
+        r.stage_head.assign(r.size, 0);
+        g_pend.assign(r.size, {});
+        r.stop.store(false);
+        r.progress = std::thread(progress_loop);
+    }
+    r.initialized = true;
+    boot_barrier();
+    return COMEX_SUCCESS;
+}
+
+int comex_init_args(int *argc, char ***argv) {
+    (void)argc;
+    (void)argv;
+    return comex_init();
+}
+
+int comex_initialized() { return rt().initialized ? 1 : 0; }
+
+int comex_finalize() {
+    Runtime &r = rt();
+    if (!r.initialized) return COMEX_SUCCESS;
+    comex_barrier(COMEX_GROUP_WORLD);
+    if (r.progress.joinable()) {
+        r.stop.store(true, std::memory_order_release);
+        r.progress.join();
+    }
+    boot_barrier();
+    for (Segment &s : r.segs) {
+        if (!s.live) continue;
+        for (int q = 0; q < (int)s.peer.size(); ++q)
+            if (q != r.rank && s.peer[q].mapped) (void)hipIpcCloseMemHandle(s.peer[q].mapped);
+        if (s.local) (void)(s.device ? hipFree(s.local) : hipHostFree(s.local));
+        s.live = false;
+    }
+    r.segs.clear();
+    for (int q = 0; q < (int)r.peer_staging.size(); ++q)
+        if (q != r.rank && r.peer_staging[q]) (void)hipIpcCloseMemHandle(r.peer_staging[q]);
+    r.peer_staging.clear();
+    boot_barrier();
+    if (r.staging) (void)hipFree(r.staging);
+    r.staging = nullptr;
+    for (int i = 0; i < kMaxNb; ++i) (void)hipEventDestroy(r.nb_ev[i]);
+    (void)hipStreamDestroy(r.stream);
+    r.stream = nullptr;
+    r.initialized = false;
+    boot_finalize();
+    return COMEX_SUCCESS;
+}
+
+void comex_error(const char *msg, int code) { fatal("comex_error: %s (code %d)", msg, code); }
+
+int comex_group_create(int n, int *pid_list, comex_group_t group, comex_group_t *new_group) {
+    ensure_init();
+    std::vector<int> g;
+    for (int i = 0; i < n; ++i) g.push_back(translate_world(group, pid_list[i]));
+    g_groups.push_back(g);
+    *new_group = (comex_group_t)g_groups.size();
+    return COMEX_SUCCESS;
+}
+
+int comex_group_free(comex_group_t group) {
+    if (group >= 1 && group <= (int)g_groups.size()) g_groups[group - 1].clear();
+    return COMEX_SUCCESS;
+}
+
+int comex_group_rank(comex_group_t group, int *rank) {
+    Runtime &r = rt();
+    if (group == COMEX_GROUP_WORLD) { *rank = r.rank; return COMEX_SUCCESS; }
+    const std::vector<int> &g = g_groups.at(group - 1);
+    *rank = -1;
+    for (int i = 0; i < (int)g.size(); ++i) if (g[i] == r.rank) *rank = i;
+    return COMEX_SUCCESS;
+}
+
+int comex_group_size(comex_group_t group, int *size) {
+    *size = (group == COMEX_GROUP_WORLD) ? rt().size : (int)g_groups.at(group - 1).size();
+    return COMEX_SUCCESS;
+}
+
+int comex_group_translate_world(comex_group_t group, int group_rank, int *world_rank) {
+    *world_rank = translate_world(group, group_rank);
+    return COMEX_SUCCESS;
+}
+
+int comex_fence_proc(int proc, comex_group_t group) {
+    ensure_init();
+    fence_target(translate_world(group, proc));
+    GA_HIP(hipStreamSynchronize(rt().stream));
+    return COMEX_SUCCESS;
+}
+
+int comex_fence_all(comex_group_t group) {
+    ensure_init();
+    (void)group;
+    Runtime &r = rt();
+    for (int t = 0; t < r.size; ++t) fence_target(t);
+    GA_HIP(hipStreamSynchronize(r.stream));
+    return COMEX_SUCCESS;
+}
+
+int comex_barrier(comex_group_t group) {
+    ensure_init();
+    if (group != COMEX_GROUP_WORLD) fatal("comex_barrier on a sub-group is not supported");
+    comex_fence_all(group);
+    boot_barrier();
+    return COMEX_SUCCESS;
+}
+
+// ---- put ----
+int comex_put(void *src, void *dst, int bytes, int proc, comex_group_t group) {
+    return xfer_contig(X_PUT, 0, nullptr, src, dst, bytes, proc, group, nullptr);
+}
+int comex_puts(void *src, int *src_stride, void *dst, int *dst_stride, int *count, int stride_levels, int proc,
+               comex_group_t group) {
+    return xfer(X_PUT, 0, nullptr, src, src_stride, dst, dst_stride, count, stride_levels, proc, group, nullptr);
+}
+int comex_putv(comex_giov_t *darr, int len, int proc, comex_group_t group) {
+    return xfer_vec(X_PUT, 0, nullptr, darr, len, proc, group, nullptr);
+}
+int comex_nbput(void *src, void *dst, int bytes, int proc, comex_group_t group, comex_request_t *h) {
+    return xfer_contig(X_PUT, 0, nullptr, src, dst, bytes, proc, group, h);
+}
+int comex_nbputs(void *src, int *src_stride, void *dst, int *dst_stride, int *count, int stride_levels, int proc,
+                 comex_group_t group, comex_request_t *h) {
+    return xfer(X_PUT, 0, nullptr, src, src_stride, dst, dst_stride, count, stride_levels, proc, group, h);
+}
+int comex_nbputv(comex_giov_t *darr, int len, int proc, comex_group_t group, comex_request_t *h) {
+    return xfer_vec(X_PUT, 0, nullptr, darr, len, proc, group, h);
+}
+
+// ---- accumulate ----
+int comex_acc(int op, void *scale, void *src, void *dst, int bytes, int proc, comex_group_t group) {
+    return xfer_contig(X_ACC, op, scale, src, dst, bytes, proc, group, nullptr);
+}
+int comex_accs(int op, void *scale, void *src, int *src_stride, void *dst, int *dst_stride, int *count,
+               int stride_levels, int proc, comex_group_t group) {
+    return xfer(X_ACC, op, scale, src, src_stride, dst, dst_stride, count, stride_levels, proc, group, nullptr);
+}
+int comex_accv(int op, void *scale, comex_giov_t *darr, int len, int proc, comex_group_t group) {
+    return xfer_vec(X_ACC, op, scale, darr, len, proc, group, nullptr);
+}
+int comex_nbacc(int op, void *scale, void *src, void *dst, int bytes, int proc, comex_group_t group,
+                comex_request_t *h) {
+    return xfer_contig(X_ACC, op, scale, src, dst, bytes, proc, group, h);
+}
+int comex_nbaccs(int op, void *scale, void *src, int *src_stride, void *dst, int *dst_stride, int *count,
+                 int stride_levels, int proc, comex_group_t group, comex_request_t *h) {
+    return xfer(X_ACC, op, scale, src, src_stride, dst, dst_stride, count, stride_levels, proc, group, h);
+}
+int comex_nbaccv(int op, void *scale, comex_giov_t *darr, int len, int proc, comex_group_t group,
+                 comex_request_t *h) {
+    return xfer_vec(X_ACC, op, scale, darr, len, proc, group, h);
+}
+
+// ---- get ----
+int comex_get(void *src, void *dst, int bytes, int proc, comex_group_t group) {
+    return xfer_contig(X_GET, 0, nullptr, src, dst, bytes, proc, group, nullptr);
+}
+int comex_gets(void *src, int *src_stride, void *dst, int *dst_stride, int *count, int stride_levels, int proc,
+               comex_group_t group) {
+    return xfer(X_GET, 0, nullptr, src, src_stride, dst, dst_stride, count, stride_levels, proc, group, nullptr);
+}
+int comex_getv(comex_giov_t *darr, int len, int proc, comex_group_t group) {
+    return xfer_vec(X_GET, 0, nullptr, darr, len, proc, group, nullptr);
+}
+int comex_nbget(void *src, void *dst, int bytes, int proc, comex_group_t group, comex_request_t *h) {
+    return xfer_contig(X_GET, 0, nullptr, src, dst, bytes, proc, group, h);
+}
+int comex_nbgets(void *src, int *src_stride, void *dst, int *dst_stride, int *count, int stride_levels, int proc,
+                 comex_group_t group, comex_request_t *h) {
+    return xfer(X_GET, 0, nullptr, src, src_stride, dst, dst_stride, count, stride_levels, proc, group, h);
+}
+int comex_nbgetv(comex_giov_t *darr, int len, int proc, comex_group_t group, comex_request_t *h) {
+    return xfer_vec(X_GET, 0, nullptr, darr, len, proc, group, h);
+}
+
+// ---- completion ----
+int comex_wait(comex_request_t *h) {
+    ensure_init();
+    Runtime &r = rt();
+    if (!h || *h < 0 || *h >= kMaxNb) return COMEX_SUCCESS;
+    if (r.nb_used[*h]) {
+        GA_HIP(hipEventSynchronize(r.nb_ev[*h]));
+        r.nb_used[*h] = false;
+    }
+    *h = -1;
+    return COMEX_SUCCESS;
+}
+
+int comex_test(comex_request_t *h, int *status) {
+    ensure_init();
+    Runtime &r = rt();
+    *status = 0;   // 0 = complete (reference returns status 0 when done)
+    if (!h || *h < 0 || *h >= kMaxNb || !r.nb_used[*h]) return COMEX_SUCCESS;
+    hipError_t e = hipEventQuery(r.nb_ev[*h]);
+    if (e == hipErrorNotReady) { *status = 1; return COMEX_SUCCESS; }
+    if (e != hipSuccess) fatal("request failed: %s", hipGetErrorString(e));
+    r.nb_used[*h] = false;
+    *h = -1;
+    return COMEX_SUCCESS;
+}
+
+int comex_wait_all(comex_group_t group) {
+    ensure_init();
+    (void)group;
+    Runtime &r = rt();
+    GA_HIP(hipStreamSynchronize(r.stream));
+    for (int i = 0; i < kMaxNb; ++i) r.nb_used[i] = false;
+    return COMEX_SUCCESS;
+}
+
+int comex_wait_proc(int proc, comex_group_t group) {
+    (void)proc;
+    return comex_wait_all(group);
+}
+
+// ---- memory ----
+static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool device) {
+    ensure_init();
+    Runtime &r = rt();
+    if (group != COMEX_GROUP_WORLD) fatal("comex_malloc on a sub-group is not supported");
+    struct Info { uint64_t base, bytes; hipIpcMemHandle_t h; int32_t device, pad; } mine;
+    memset(&mine, 0, sizeof(mine));
+    void *p = nullptr;
+    if (bytes) {
+        if (device) {
+            GA_HIP(hipMalloc(&p, bytes));
+            if (r.size > 1) GA_HIP(hipIpcGetMemHandle(&mine.h, p));
+        } else {
+            GA_HIP(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
+        }
+    }
+    mine.base = (uint64_t)(uintptr_t)p;
+    mine.bytes = bytes;
+    mine.device = r.device;
+    std::vector<Info> all(r.size);
+    boot_allgather(&mine, all.data(), sizeof(Info));
+    Segment s;
+    s.live = true;
+    s.device = device;
+    s.local = p;
+    s.peer.resize(r.size);
+    for (int q = 0; q < r.size; ++q) {
+        s.peer[q].base = all[q].base;
+        s.peer[q].bytes = all[q].bytes;
+        ptr_arr[q] = (void *)(uintptr_t)all[q].base;
+        if (q == r.rank) {
+            s.peer[q].mapped = (char *)p;
+        } else if (all[q].bytes) {
+            if (!device) fatal("host-memory segments are rank-private (use device segments for remote access)");
+            void *m = nullptr;
+            GA_HIP(hipIpcOpenMemHandle(&m, all[q].h, hipIpcMemLazyEnablePeerAccess));
+            s.peer[q].mapped = (char *)m;
+        }
+    }
+    {
+        std::lock_guard<std::mutex> g(r.seg_mu);
+        r.segs.push_back(std::move(s));
+    }
+    boot_barrier();
+    return COMEX_SUCCESS;
+}
+
+int comex_malloc(void **ptr_arr, size_t bytes, comex_group_t group) {
+    const char *where = getenv("COMEX_AMD_SEGMENT");
+    const bool host = where && !strcmp(where, "host");
+    return do_malloc(ptr_arr, bytes, group, !host);
+}
+
+int comex_malloc_mem_dev(void **ptr_arr, size_t bytes, comex_group_t group, const char *device) {
+    const bool host = device && (!strcmp(device, "host") || !strcmp(device, "cpu") || !strcmp(device, "dram"));
+    return do_malloc(ptr_arr, bytes, group, !host);
+}
+
+int comex_free(void *ptr, comex_group_t group) {
+    ensure_init();
+    Runtime &r = rt();
+    (void)group;
+    comex_fence_all(COMEX_GROUP_WORLD);
+    std::vector<uint64_t> all(r.size);
+    uint64_t mine = (uint64_t)(uintptr_t)ptr;
+    boot_allgather(&mine, all.data(), sizeof(mine));
+    boot_barrier();   // nobody still reads the segment
+    std::lock_guard<std::mutex> g(r.seg_mu);
+    for (Segment &s : r.segs) {
+        if (!s.live) continue;
+        bool match = true;
+        for (int q = 0; q < r.size; ++q) if (s.peer[q].base != all[q]) { match = false; break; }
+        if (!match) continue;
+        for (int q = 0; q < r.size; ++q)
+            if (q != r.rank && s.peer[q].mapped) GA_HIP(hipIpcCloseMemHandle(s.peer[q].mapped));
+        if (s.local) GA_HIP(s.device ? hipFree(s.local) : hipHostFree(s.local));
+        s.live = false;
+        s.local = nullptr;
+        return COMEX_SUCCESS;
+    }
+    fatal("comex_free(%p): not a comex_malloc segment", ptr);
+}
+
+int comex_free_dev(void *ptr, comex_group_t group) { return comex_free(ptr, group); }
+
+void *comex_malloc_local(size_t bytes) {
+    ensure_init();
+    void *p = nullptr;
+    if (bytes == 0) return nullptr;
+    GA_HIP(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
+    return p;
+}
+
+int comex_free_local(void *ptr) {
+    if (ptr) GA_HIP(hipHostFree(ptr));
+    return COMEX_SUCCESS;
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// gaamd_kernels.h -- internal interface between the host runtime and the
+// gfx950 strided pack/unpack/accumulate kernels (gaamd_kernels.hip).
+//
+// One descriptor covers every operation on the hot path:
+//   * fused strided accumulate   dst[row_d(r)] += scale * src[row_s(r)]
+//       (comex_accs self/SMP path, comex.c:6890-6962 -> _acc acc.h:106-154)
+//   * pack / unpack / put / get  strided byte copy with either side possibly
+//       packed-contiguous (comex.c:1267-1384, 6342-6427, 6617-6696)
+//   * unpack-accumulate          packed src -> strided dst with _acc
+//       (_acc_packed_handler comex.c:4238-4268)
+// A packed buffer is just a strided side whose strides are the running
+// products count[0]*count[1]*...; see gaamd_packed_strides().
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+namespace gaamd {
+
+constexpr int kMaxLevels = 7;       // odometer arrays are int[7] in comex.c:1273
+constexpr int kOpCopy = 0;          // byte copy (put/get/pack/unpack)
+
+// q = n / d for 0 <= n < 2^31 with one mul-hi, an add and a shift
+// (round-up magic number, Granlund & Montgomery).  Shared host/device.
+struct FastDiv {
+    uint32_t d, m, s;
+    __host__ __device__ inline uint32_t div(uint32_t n) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        uint32_t hi = __umulhi(n, m);
+#else
+        uint32_t hi = (uint32_t)(((uint64_t)n * m) >> 32);
+#endif
+        return (uint32_t)(((uint64_t)hi + n) >> s);
+    }
+};
+FastDiv make_fastdiv(uint32_t d);
+
+struct alignas(16) Scale16 { uint64_t w[2]; };
+
+struct Desc {
+    const char *src;
+    char *dst;
+    int64_t s_str[kMaxLevels];   // byte stride of level j+1 (stride[j])
+    int64_t d_str[kMaxLevels];
+    FastDiv cnt[kMaxLevels];     // count[j+1]
+    int32_t levels;              // stride_levels in this launch
+    uint32_t rows;               // rows covered by this launch
+    uint32_t row0;               // global index of the first row
+    uint32_t nvec;               // W-byte vectors per row
+    FastDiv nvec_div;
+    uint32_t chunks;             // row chunks per row (row kernel)
+    FastDiv chunk_div;
+    uint64_t items;              // work items in this launch
+    Scale16 scale;
+};
+
+enum KernelKind { KK_AUTO = 0, KK_ROWS = 1, KK_FLAT = 2, KK_SERIAL = 3 };
+
+struct Tuning {
+    int kind = KK_AUTO;     // force a kernel family
+    int unroll16 = 4;       // vectors per thread for W=16 rows kernel {2,4,8}
+    int nontemporal = 0;    // nt loads/stores on the streaming path
+    int block = 256;        // threads per block {256, 512}
+    int flat_max_nvec = 127;// rows with at most this many vectors use the flat kernel
+    int max_grid = 0;       // cap on blocks (0 = one block per work item)
+};
+Tuning &tuning();
+
+struct LaunchInfo {
+    int kind;      // KernelKind actually used
+    int width;     // vector width in bytes
+    int unroll;
+    int launches;
+    uint64_t blocks;
+};
+
+// Enqueue `op` (kOpCopy or COMEX_ACC_*) over the strided patch.  src/dst
+// must be device-accessible.  Returns 0 or a negative error code; never
+// touches the host copy of the data.  `info` may be null.
+int launch_strided(int op, const void *scale, const void *src, const int *src_stride,
+                   void *dst, const int *dst_stride, const int *count, int stride_levels,
+                   hipStream_t stream, LaunchInfo *info,
+                   uint64_t row_begin = 0, uint64_t row_end = ~0ull);
+
+// byte span [lo, hi) of one side relative to its base pointer
+void side_span_host(const int *stride, const int *count, int stride_levels, int64_t row_bytes,
+                    int64_t *lo, int64_t *hi);
+
+int elem_size(int op);   // bytes per element for op; 1 for copy; 0 if unknown
+
+}  // namespace gaamd

@@ -1,0 +1,193 @@
+// plumbing.hip -- kernel-level C ABI (ga_amd.h section 2) and the device
+// plumbing used by tests and bench.py (section 3).
+#include "gaamd_kernels.h"
+#include "runtime.hpp"
+#include <string.h>
+#include <stdlib.h>
+
+namespace gaamd {
+
+static LaunchInfo g_last;
+
+static hipStream_t stream_of(void *s) {
+    if (s) return (hipStream_t)s;
+    Runtime &r = rt();
+    if (r.stream) return r.stream;
+    return nullptr;   // legacy default stream before comex_init
+}
+
+// splitmix64 element i (state after i+1 increments); must match
+// oracle/comex_oracle.c splitmix64_at bit for bit.
+__device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_fill(void *dst, long n, int type, uint64_t seed) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const uint64_t x = splitmix64_at(seed, (uint64_t)i);
+        switch (type) {
+        case 0: ((double *)dst)[i] = ((double)(x >> 11) * 0x1.0p-53) * 2.0 - 1.0; break;
+        case 1: ((float *)dst)[i] = ((float)(x >> 40) * 0x1.0p-24f) * 2.0f - 1.0f; break;
+        case 2: ((int32_t *)dst)[i] = (int32_t)(x >> 43) - (1 << 20); break;
+        default: ((int64_t *)dst)[i] = (int64_t)(x >> 43) - (1 << 20); break;
+        }
+    }
+}
+
+}  // namespace gaamd
+
+using namespace gaamd;
+
+extern "C" {
+
+int gaamd_strided(int op, const void *scale, const void *src, const int *src_stride, void *dst,
+                  const int *dst_stride, const int *count, int stride_levels, void *stream) {
+    return launch_strided(op, scale, src, src_stride, dst, dst_stride, count, stride_levels, stream_of(stream),
+                          &g_last);
+}
+
+long gaamd_packed_size(const int *count, int stride_levels) {
+    long n = count[0];
+    for (int j = 1; j <= stride_levels; ++j) n *= count[j];
+    return n;
+}
+
+static void packed_strides(const int *count, int levels, int *ps) {
+    long acc = count[0];
+    for (int j = 0; j < levels; ++j) {
+        ps[j] = (int)acc;
+        acc *= count[j + 1];
+    }
+}
+
+int gaamd_pack(const void *src, const int *src_stride, const int *count, int stride_levels, void *packed,
+               void *stream) {
+    int ps[kMaxLevels + 1];
+    if (stride_levels < 0 || stride_levels > kMaxLevels) return -2;
+    packed_strides(count, stride_levels, ps);
+    return launch_strided(kOpCopy, nullptr, src, src_stride, packed, ps, count, stride_levels, stream_of(stream),
+                          &g_last);
+}
+
+int gaamd_unpack(const void *packed, void *dst, const int *dst_stride, const int *count, int stride_levels,
+                 void *stream) {
+    int ps[kMaxLevels + 1];
+    if (stride_levels < 0 || stride_levels > kMaxLevels) return -2;
+    packed_strides(count, stride_levels, ps);
+    return launch_strided(kOpCopy, nullptr, packed, ps, dst, dst_stride, count, stride_levels, stream_of(stream),
+                          &g_last);
+}
+
+int gaamd_unpack_acc(int op, const void *scale, const void *packed, void *dst, const int *dst_stride,
+                     const int *count, int stride_levels, void *stream) {
+    int ps[kMaxLevels + 1];
+    if (stride_levels < 0 || stride_levels > kMaxLevels) return -2;
+    if (op == kOpCopy) return -4;
+    packed_strides(count, stride_levels, ps);
+    return launch_strided(op, scale, packed, ps, dst, dst_stride, count, stride_levels, stream_of(stream),
+                          &g_last);
+}
+
+int gaamd_last_launch(int *kind, int *width, int *unroll, int *launches, unsigned long long *blocks) {
+    if (kind) *kind = g_last.kind;
+    if (width) *width = g_last.width;
+    if (unroll) *unroll = g_last.unroll;
+    if (launches) *launches = g_last.launches;
+    if (blocks) *blocks = g_last.blocks;
+    return 0;
+}
+
+static int *tuning_field(const char *key) {
+    Tuning &t = tuning();
+    if (!strcmp(key, "kind")) return &t.kind;
+    if (!strcmp(key, "unroll16")) return &t.unroll16;
+    if (!strcmp(key, "nontemporal")) return &t.nontemporal;
+    if (!strcmp(key, "flat_max_nvec")) return &t.flat_max_nvec;
+    if (!strcmp(key, "max_grid")) return &t.max_grid;
+    return nullptr;
+}
+
+int gaamd_set_tuning(const char *key, int value) {
+    int *f = tuning_field(key);
+    if (!f) return -1;
+    if (!strcmp(key, "unroll16") && value != 2 && value != 4 && value != 8) return -1;
+    const int old = *f;
+    *f = value;
+    return old;
+}
+
+int gaamd_get_tuning(const char *key) {
+    int *f = tuning_field(key);
+    return f ? *f : -1;
+}
+
+int gaamd_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+int gaamd_set_device(int dev) { return hipSetDevice(dev) == hipSuccess ? 0 : -1; }
+void *gaamd_stream(void) { return rt().stream; }
+
+void *gaamd_dev_malloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    return p;
+}
+int gaamd_dev_free(void *p) { return hipFree(p) == hipSuccess ? 0 : -1; }
+
+void *gaamd_host_malloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) return nullptr;
+    return p;
+}
+int gaamd_host_free(void *p) { return hipHostFree(p) == hipSuccess ? 0 : -1; }
+
+int gaamd_memcpy(void *dst, const void *src, size_t bytes) {
+    return hipMemcpy(dst, src, bytes, hipMemcpyDefault) == hipSuccess ? 0 : -1;
+}
+int gaamd_memset(void *dst, int value, size_t bytes) {
+    return hipMemset(dst, value, bytes) == hipSuccess ? 0 : -1;
+}
+int gaamd_sync(void *stream) {
+    hipStream_t s = stream_of(stream);
+    hipError_t e = s ? hipStreamSynchronize(s) : hipDeviceSynchronize();
+    return e == hipSuccess ? 0 : -(int)e;
+}
+
+int gaamd_fill(void *dst, long n, int type, unsigned long long seed, void *stream) {
+    if (n <= 0) return 0;
+    if (type < 0 || type > 3) return -2;
+    long blocks = (n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(256), 0, stream_of(stream), dst, n, type,
+                       (uint64_t)seed);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+void *gaamd_event_create(void) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return (void *)e;
+}
+int gaamd_event_destroy(void *ev) { return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? 0 : -1; }
+int gaamd_event_record(void *ev, void *stream) {
+    return hipEventRecord((hipEvent_t)ev, stream_of(stream)) == hipSuccess ? 0 : -1;
+}
+int gaamd_event_sync(void *ev) { return hipEventSynchronize((hipEvent_t)ev) == hipSuccess ? 0 : -1; }
+float gaamd_event_elapsed_ms(void *start, void *stop) {
+    float ms = -1.f;
+    if (hipEventElapsedTime(&ms, (hipEvent_t)start, (hipEvent_t)stop) != hipSuccess) return -1.f;
+    return ms;
+}
+
+const char *gaamd_version(void) { return "ga_amd 0.1 (gfx950)"; }
+
+}  // extern "C"

@@ -1,0 +1,138 @@
+// runtime.hpp -- process-wide state of the ComEx/ARMCI runtime on MI355X.
+//
+// Reference counterparts (comex/src-mpi-pr/comex.c):
+//   g_state (rank/size/host table)        -> Runtime::{rank,size,local_rank}
+//   reg_cache (reg_cache.c:380-409)       -> Runtime::segs (owner base -> mapped ptr)
+//   nb_state[COMEX_MAX_NB_OUTSTANDING]    -> Runtime::nb (HIP events)
+//   per-rank POSIX semaphores (2812-2908) -> none: every write into rank t's
+//       HBM is issued on rank t's stream (its own ops, or requests its progress
+//       thread drains), so stream order serialises accumulates per target.
+//   progress rank (_progress_server 3379-3565, _acc_packed_handler 4133-4281)
+//       -> a progress thread per process draining a node-shared inbox.
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+#include <atomic>
+#include <vector>
+#include <mutex>
+#include <thread>
+#include <hip/hip_runtime_api.h>
+#include "../../include/ga_amd.h"
+
+namespace gaamd {
+
+[[noreturn]] void fatal(const char *fmt, ...);
+
+#define GA_HIP(call)                                                                  \
+    do {                                                                              \
+        hipError_t e_ = (call);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            ::gaamd::fatal("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_),     \
+                           __FILE__, __LINE__);                                       \
+    } while (0)
+
+#define GA_ASSERT(cond, msg)                                                          \
+    do {                                                                              \
+        if (!(cond)) ::gaamd::fatal("assertion `%s` failed: %s (%s:%d)", #cond, msg,  \
+                                    __FILE__, __LINE__);                              \
+    } while (0)
+
+constexpr int kMaxNb = 256;          // COMEX_MAX_NB_OUTSTANDING default
+constexpr int kMaxRanks = 64;        // ranks per node
+constexpr int kInboxSlots = 256;     // requests in flight per target
+constexpr size_t kBootSlot = 64 * 1024;
+
+// ---- node-shared memory (one mapping per node, created at init) ----------
+struct alignas(64) Request {
+    std::atomic<uint32_t> state;     // 0 free, 1 writing, 2 ready
+    int32_t src_rank;
+    int32_t op;                      // COMEX_ACC_* (or 0 = copy)
+    int32_t levels;
+    int32_t count[8];
+    int32_t dst_stride[8];
+    uint64_t dst_addr;               // owner's address space
+    uint64_t staging_off;            // offset into src_rank's staging buffer
+    uint64_t bytes;                  // packed bytes
+    uint64_t seq;                    // per (src, dst) sequence number
+    uint8_t scale[16];
+};
+
+struct alignas(64) Inbox {
+    std::atomic<uint64_t> tail;      // producers reserve slots
+    char pad0[56];
+    std::atomic<uint64_t> head;      // consumer position
+    char pad1[56];
+    Request slot[kInboxSlots];
+};
+
+struct alignas(64) NodeShm {
+    std::atomic<uint32_t> magic;
+    int32_t size;
+    std::atomic<uint64_t> bar_count;
+    std::atomic<uint64_t> bar_gen;
+    char pad[40];
+    // done[s][t]: requests from s applied by t (monotonic)
+    std::atomic<uint64_t> done[kMaxRanks][kMaxRanks];
+    Inbox inbox[1];                  // [size] follows; then boot data area
+};
+
+size_t node_shm_bytes(int size);
+Inbox *inbox_of(NodeShm *s, int rank);
+char *boot_area(NodeShm *s, int size);
+
+struct PeerMap {
+    uintptr_t base = 0;   // segment address in the owner's address space
+    size_t bytes = 0;
+    char *mapped = nullptr;   // same bytes as seen from this process
+};
+
+struct Segment {
+    bool live = false;
+    bool device = true;
+    void *local = nullptr;
+    std::vector<PeerMap> peer;   // indexed by world rank
+};
+
+struct Runtime {
+    bool initialized = false;
+    bool boot_ready = false;
+    int rank = 0, size = 1, local_rank = 0, device = 0;
+    hipStream_t stream = nullptr;
+    bool blocking_sync = false;     // COMEX_AMD_BLOCKING_SYNC
+    // bootstrap
+    gaamd_allgather_fn ag = nullptr;
+    gaamd_barrier_fn bar = nullptr;
+    void *ctx = nullptr;
+    bool hooks = false;
+    NodeShm *shm = nullptr;
+    size_t shm_bytes = 0;
+    // memory
+    std::vector<Segment> segs;
+    std::mutex seg_mu;
+    // non-blocking handles
+    hipEvent_t nb_ev[kMaxNb] = {};
+    bool nb_used[kMaxNb] = {};
+    int nb_next = 0;
+    // remote (multi-rank) state
+    char *staging = nullptr;            // this rank's exported staging buffer
+    size_t staging_bytes = 0;
+    std::vector<char *> peer_staging;   // mapped staging of every rank
+    std::vector<uint64_t> posted;       // requests posted to each target
+    std::vector<uint64_t> stage_head;   // per-target staging ring write cursor
+    std::thread progress;
+    std::atomic<bool> stop{false};
+    std::mutex launch_mu;
+};
+
+Runtime &rt();
+
+// bootstrap.cpp
+void boot_init();                                  // rank/size + node shm
+void boot_allgather(const void *send, void *recv, size_t bytes);
+void boot_barrier();
+void boot_finalize();
+
+// comex.cpp helpers shared with armci.cpp
+int translate_world(int group, int proc);
+
+}  // namespace gaamd

@@ -1,0 +1,92 @@
+/*
+ * ga_amd.h -- framework-level C ABI of libga_amd.so beyond comex.h/armci.h.
+ *
+ *  1. Bootstrap hooks.  The reference exchanges segment registrations and
+ *     semaphore names with MPI_Allgather (comex/src-mpi-pr/comex.c:2461, 2874)
+ *     and synchronises with MPI_Barrier (comex.c:1231).  Here the host program
+ *     may hand in its own allgather/barrier (torch.distributed, MPI, ...);
+ *     without hooks comex_init() uses RANK/WORLD_SIZE/LOCAL_RANK (or the
+ *     OMPI_/PMI_ equivalents) and a node-local shared-memory rendezvous.
+ *  2. Kernel-level entry points: the gfx950 kernels that comex_accs/puts/gets
+ *     enqueue, callable directly on device pointers with an explicit stream.
+ *     They replace, element for element:
+ *       gaamd_strided(op=COMEX_ACC_*) : nb_accs per-row _acc  comex.c:6890-6962,
+ *                                       acc.h:106-154
+ *       gaamd_strided(op=GAAMD_OP_COPY): nb_puts/nb_gets       comex.c:6342-6427, 6617-6696
+ *       gaamd_pack                     : pack                   comex.c:1267-1328
+ *       gaamd_unpack                   : unpack                 comex.c:1331-1384
+ *       gaamd_unpack_acc               : _acc_packed_handler    comex.c:4238-4268
+ *  3. Device plumbing used by tests and bench.py (allocation, copies,
+ *     synthetic inputs, HIP-event timing, tuning knobs).
+ *
+ * All functions return 0 on success and a negative code on failure unless
+ * stated otherwise; `stream` arguments are hipStream_t passed as void*
+ * (NULL = the library's own stream).
+ */
+#ifndef GA_AMD_H
+#define GA_AMD_H
+
+#include <stddef.h>
+
+#if defined(__cplusplus)
+extern "C" {
+#endif
+
+#define GAAMD_OP_COPY 0
+
+/* ---- 1. bootstrap ------------------------------------------------------ */
+typedef int (*gaamd_allgather_fn)(const void *send, void *recv, size_t bytes, void *ctx);
+typedef int (*gaamd_barrier_fn)(void *ctx);
+int gaamd_set_bootstrap(int rank, int size, int local_rank,
+                        gaamd_allgather_fn allgather, gaamd_barrier_fn barrier, void *ctx);
+/* exercise the bootstrap alone (no GPU): allgather of ranks + barriers */
+int gaamd_bootstrap_selftest(int rounds);
+int gaamd_rank(void);
+int gaamd_size(void);
+
+/* ---- 2. kernels -------------------------------------------------------- */
+int gaamd_strided(int op, const void *scale, const void *src, const int *src_stride,
+                  void *dst, const int *dst_stride, const int *count, int stride_levels,
+                  void *stream);
+long gaamd_packed_size(const int *count, int stride_levels);
+int gaamd_pack(const void *src, const int *src_stride, const int *count, int stride_levels,
+               void *packed, void *stream);
+int gaamd_unpack(const void *packed, void *dst, const int *dst_stride, const int *count,
+                 int stride_levels, void *stream);
+int gaamd_unpack_acc(int op, const void *scale, const void *packed, void *dst,
+                     const int *dst_stride, const int *count, int stride_levels, void *stream);
+/* kind / vector width / unroll / launches / blocks of the last kernel-level call */
+int gaamd_last_launch(int *kind, int *width, int *unroll, int *launches,
+                      unsigned long long *blocks);
+/* keys: "kind" (0 auto,1 rows,2 flat,3 serial), "unroll16", "nontemporal",
+ * "flat_max_nvec", "max_grid"; returns the previous value or -1 */
+int gaamd_set_tuning(const char *key, int value);
+int gaamd_get_tuning(const char *key);
+
+/* ---- 3. device plumbing ------------------------------------------------ */
+int gaamd_device_count(void);
+int gaamd_set_device(int dev);
+void *gaamd_stream(void);
+void *gaamd_dev_malloc(size_t bytes);
+int gaamd_dev_free(void *p);
+void *gaamd_host_malloc(size_t bytes);   /* pinned, device-mapped */
+int gaamd_host_free(void *p);
+int gaamd_memcpy(void *dst, const void *src, size_t bytes);   /* any direction, synchronous */
+int gaamd_memset(void *dst, int value, size_t bytes);
+int gaamd_sync(void *stream);
+/* synthetic inputs of SURVEY.md 8(d) generated on the device; type:
+ * 0 f64, 1 f32, 2 i32, 3 i64 ; n elements from splitmix64(seed) */
+int gaamd_fill(void *dst, long n, int type, unsigned long long seed, void *stream);
+/* HIP events on the library stream (or `stream`) */
+void *gaamd_event_create(void);
+int gaamd_event_destroy(void *ev);
+int gaamd_event_record(void *ev, void *stream);
+int gaamd_event_sync(void *ev);
+float gaamd_event_elapsed_ms(void *start, void *stop);
+const char *gaamd_version(void);
+
+#if defined(__cplusplus)
+}
+#endif
+
+#endif /* GA_AMD_H */

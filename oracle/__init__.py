@@ -1,0 +1,133 @@
+"""oracle -- CPU parity checker for the ga_amd HIP path.  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this
+package; the product library (ga_amd/libga_amd.so) never links or calls it.
+
+* ``Oracle``: ctypes wrapper of liboracle.so, the C restatement of the reference
+  path (comex_oracle.c: _acc acc.h:106-154, pack/unpack comex.c:1267-1384,
+  nb_accs comex.c:6890-6962, unpack-acc comex.c:4238-4268,
+  armci_check_contiguous armci.c:114-170).
+* ``Ref``: ctypes wrapper of _ref/libref_acc.so, the REFERENCE's own _acc
+  compiled from /root/reference/comex/src-common/acc.h (built only where the
+  reference tree exists; the .so travels to the GPU box).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libref_acc.so")
+
+_ip = ctypes.POINTER(ctypes.c_int)
+_vp = ctypes.c_void_p
+
+
+def _ints(vals):
+    vals = list(vals) if vals is not None else []
+    return (ctypes.c_int * max(1, len(vals)))(*vals)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_vp)
+
+
+class Oracle:
+    def __init__(self, path=ORACLE_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
+        L = ctypes.CDLL(path)
+        sig = {
+            "ora_acc": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
+            "ora_elem_size": (ctypes.c_int, [ctypes.c_int]),
+            "ora_packed_size": (ctypes.c_long, [_ip, ctypes.c_int]),
+            "ora_pack": (ctypes.c_long, [_vp, _ip, _ip, ctypes.c_int, _vp]),
+            "ora_unpack": (ctypes.c_long, [_vp, _vp, _ip, _ip, ctypes.c_int]),
+            "ora_unpack_acc": (ctypes.c_long, [ctypes.c_int, _vp, _vp, _vp, _ip, _ip, ctypes.c_int]),
+            "ora_accs": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
+            "ora_accs_packed": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
+            "ora_puts": (ctypes.c_int, [_vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
+            "ora_gets": (ctypes.c_int, [_vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
+            "ora_check_contiguous": (ctypes.c_int, [_ip, _ip, _ip, ctypes.c_int]),
+            "ora_fill_f64": (None, [_vp, ctypes.c_long, ctypes.c_uint64]),
+            "ora_fill_f32": (None, [_vp, ctypes.c_long, ctypes.c_uint64]),
+            "ora_fill_i32": (None, [_vp, ctypes.c_long, ctypes.c_uint64]),
+            "ora_fill_i64": (None, [_vp, ctypes.c_long, ctypes.c_uint64]),
+            "ora_splitmix64": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
+        }
+        for n, (r, a) in sig.items():
+            f = getattr(L, n)
+            f.restype = r
+            f.argtypes = a
+        self.L = L
+
+    # all byte buffers are numpy arrays; offsets in bytes
+    def accs(self, op, scale, src, src_off, src_stride, dst, dst_off, dst_stride, count, levels):
+        s = np.array([scale], dtype=_scale_dtype(op))
+        rc = self.L.ora_accs(op, _ptr(s), _vp(src.ctypes.data + src_off), _ints(src_stride),
+                             _vp(dst.ctypes.data + dst_off), _ints(dst_stride), _ints(count), levels)
+        assert rc == 0
+
+    def accs_packed(self, op, scale, src, src_off, src_stride, dst, dst_off, dst_stride, count, levels):
+        s = np.array([scale], dtype=_scale_dtype(op))
+        rc = self.L.ora_accs_packed(op, _ptr(s), _vp(src.ctypes.data + src_off), _ints(src_stride),
+                                    _vp(dst.ctypes.data + dst_off), _ints(dst_stride), _ints(count), levels)
+        assert rc == 0
+
+    def puts(self, src, src_off, src_stride, dst, dst_off, dst_stride, count, levels):
+        self.L.ora_puts(_vp(src.ctypes.data + src_off), _ints(src_stride), _vp(dst.ctypes.data + dst_off),
+                        _ints(dst_stride), _ints(count), levels)
+
+    def packed_size(self, count, levels):
+        return self.L.ora_packed_size(_ints(count), levels)
+
+    def pack(self, src, src_off, src_stride, count, levels):
+        out = np.zeros(max(1, self.packed_size(count, levels)), dtype=np.uint8)
+        self.L.ora_pack(_vp(src.ctypes.data + src_off), _ints(src_stride), _ints(count), levels, _ptr(out))
+        return out[: self.packed_size(count, levels)]
+
+    def unpack(self, packed, dst, dst_off, dst_stride, count, levels):
+        self.L.ora_unpack(_ptr(packed), _vp(dst.ctypes.data + dst_off), _ints(dst_stride), _ints(count), levels)
+
+    def unpack_acc(self, op, scale, packed, dst, dst_off, dst_stride, count, levels):
+        s = np.array([scale], dtype=_scale_dtype(op))
+        self.L.ora_unpack_acc(op, _ptr(s), _ptr(packed), _vp(dst.ctypes.data + dst_off), _ints(dst_stride),
+                              _ints(count), levels)
+
+    def check_contiguous(self, src_stride, dst_stride, count, n_stride):
+        return self.L.ora_check_contiguous(_ints(src_stride), _ints(dst_stride), _ints(count), n_stride)
+
+    def fill(self, arr, seed):
+        n = arr.size
+        fn = {np.dtype(np.float64): self.L.ora_fill_f64, np.dtype(np.float32): self.L.ora_fill_f32,
+              np.dtype(np.int32): self.L.ora_fill_i32, np.dtype(np.int64): self.L.ora_fill_i64}[arr.dtype]
+        fn(_ptr(arr), n, seed)
+        return arr
+
+
+class Ref:
+    """The reference's own _acc (acc.h) driven per row; None-able if not built."""
+
+    def __init__(self, path=REF_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        L = ctypes.CDLL(path)
+        L.ref_acc.restype = ctypes.c_int
+        L.ref_acc.argtypes = [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]
+        L.ref_accs.restype = ctypes.c_int
+        L.ref_accs.argtypes = [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int]
+        self.L = L
+
+    def accs(self, op, scale, src, src_off, src_stride, dst, dst_off, dst_stride, count, levels):
+        s = np.array([scale], dtype=_scale_dtype(op))
+        self.L.ref_accs(op, _ptr(s), _vp(src.ctypes.data + src_off), _ints(src_stride),
+                        _vp(dst.ctypes.data + dst_off), _ints(dst_stride), _ints(count), levels)
+
+
+def ref_available():
+    return os.path.exists(REF_SO)
+
+
+def _scale_dtype(op):
+    return {37: np.int32, 38: np.float64, 39: np.float32, 40: np.complex64, 41: np.complex128, 42: np.int64}[op]

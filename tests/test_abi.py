@@ -1,0 +1,118 @@
+"""CPU: the C-ABI library loads, exports every symbol include/*.h declares, keeps
+the reference's constants, and its host-only logic is right.  No GPU calls."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import ga_amd
+from ga_amd._lib import LIB_PATH, SIGNATURES
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("comex.h", "armci.h", "ga_amd.h")]
+
+
+def declared_functions(path):
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"#ifdef MPI_VERSION.*?#endif", "", text, flags=re.S)   # needs <mpi.h>
+    text = re.sub(r"^\s*typedef[^;]*;", "", text, flags=re.M | re.S)
+    names = set()
+    for m in re.finditer(r"^\s*(?:extern\s+)?[A-Za-z_][\w\s\*]*?[\s\*](\w+)\s*\(", text, flags=re.M):
+        name = m.group(1)
+        if name in ("if", "while", "for", "return", "sizeof") or name.startswith("_"):
+            continue
+        names.add(name)
+    typedef_fns = set(re.findall(r"typedef\s+\w+\s*\(\*(\w+)\)", text))
+    return names - typedef_fns
+
+
+def exported_symbols():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True, check=True)
+    syms = {}
+    for line in out.stdout.splitlines():
+        parts = line.split()
+        if len(parts) == 3:
+            syms[parts[2]] = parts[1]
+    return syms
+
+
+def test_library_loads():
+    L = ga_amd.lib()
+    assert L.gaamd_version().startswith(b"ga_amd")
+
+
+@pytest.mark.parametrize("header", HEADERS, ids=os.path.basename)
+def test_every_declared_symbol_is_exported(header):
+    syms = exported_symbols()
+    decl = declared_functions(header)
+    assert decl, header
+    missing = sorted(n for n in decl if n not in syms)
+    assert not missing, f"{os.path.basename(header)} declares but the library lacks: {missing}"
+
+
+def test_python_binding_covers_headers():
+    decl = set()
+    for h in HEADERS:
+        decl |= declared_functions(h)
+    decl -= {n for n in decl if n.startswith("PARMCI_")}
+    assert not sorted(decl - set(SIGNATURES)), sorted(decl - set(SIGNATURES))
+
+
+def test_armci_names_are_weak_aliases():
+    """capi.c:14-27: ARMCI_X is a weak symbol so profilers can interpose."""
+    syms = exported_symbols()
+    for name in ("ARMCI_AccS", "ARMCI_PutS", "ARMCI_GetS", "ARMCI_NbAccS", "ARMCI_Malloc"):
+        assert syms[name] in ("W", "V"), (name, syms[name])
+        assert syms["P" + name] == "T"
+
+
+def test_constants_match_reference():
+    text = open(os.path.join(ROOT, "include", "comex.h")).read()
+    want = {"COMEX_ACC_OFF": "36", "COMEX_MAX_STRIDE_LEVEL": "8", "COMEX_SUCCESS": "0",
+            "COMEX_GROUP_WORLD": "0", "COMEX_SWAP": "10", "COMEX_FETCH_AND_ADD_LONG": "13"}
+    for k, v in want.items():
+        assert re.search(rf"#define {k} {v}\b", text), k
+    assert (ga_amd.COMEX_ACC_INT, ga_amd.COMEX_ACC_DBL, ga_amd.COMEX_ACC_FLT, ga_amd.COMEX_ACC_CPL,
+            ga_amd.COMEX_ACC_DCP, ga_amd.COMEX_ACC_LNG) == (37, 38, 39, 40, 41, 42)
+
+
+def test_library_check_contiguous_matches_oracle(oracle):
+    """armci_check_contiguous in the library (host code) == restated armci.c:114-170."""
+    L = ga_amd.lib()
+    rng = np.random.default_rng(3)
+    for _ in range(400):
+        n = int(rng.integers(1, 5))
+        count = [int(rng.choice([8, 16, 24, 40]))] + [int(rng.integers(1, 4)) for _ in range(n)]
+        ss, ds, a, b = [], [], count[0], count[0]
+        for j in range(n):
+            a += 8 * int(rng.integers(0, 2))
+            b += 8 * int(rng.integers(0, 2))
+            ss.append(a)
+            ds.append(b)
+            a *= count[j + 1] + int(rng.integers(0, 2))
+            b *= count[j + 1] + int(rng.integers(0, 2))
+        got = L.armci_check_contiguous(ga_amd.int_array(ss), ga_amd.int_array(ds), ga_amd.int_array(count), n)
+        assert got == oracle.check_contiguous(ss, ds, count, n), (ss, ds, count)
+
+
+def test_no_oracle_in_product_library():
+    """The product .so must not link or embed the CPU checker."""
+    out = subprocess.run(["nm", "-D", LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "ora_" not in out and "ref_acc" not in out
+    ldd = subprocess.run(["ldd", LIB_PATH], capture_output=True, text=True).stdout
+    assert "liboracle" not in ldd and "libref_acc" not in ldd
+
+
+def test_comex_without_gpu_fails_loudly():
+    """On a host with no GPU, comex_init must abort, not fall back to the CPU."""
+    code = ("import ga_amd,sys; L=ga_amd.lib(); "
+            "sys.exit(0 if L.gaamd_device_count()>0 else (L.comex_init() or 3))")
+    r = subprocess.run(["python", "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=120)
+    if r.returncode == 0:
+        pytest.skip("a GPU is visible here")
+    assert r.returncode != 3 and r.returncode != 0
+    assert "no HIP device" in r.stderr

@@ -1,0 +1,253 @@
+"""GPU parity: the HIP path through the C ABI against the reference's golden
+vectors (bit-exact; NaN payloads excepted) and the oracle.  Runs on the MI355X."""
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import cases as C
+import ga_amd
+from helpers import same_bits_nan_aware, first_mismatch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_case_device(L, case, src, dst_in, api="comex", kind=None):
+    sbuf = ga_amd.DeviceBuffer(max(16, src.size))
+    dbuf = ga_amd.DeviceBuffer(max(16, dst_in.size))
+    sbuf.upload(src)
+    dbuf.upload(dst_in)
+    op = case["op"]
+    keep, sp = ga_amd.scale_buffer(op, C.SCALE[op])
+    ss, ds, cnt = ga_amd.int_array(case["src_stride"]), ga_amd.int_array(case["dst_stride"]), ga_amd.int_array(case["count"])
+    sptr = ctypes.c_void_p(sbuf.ptr + case["src_off"])
+    dptr = ctypes.c_void_p(dbuf.ptr + case["dst_off"])
+    if api == "comex":
+        rc = L.comex_accs(op, sp, sptr, ss, dptr, ds, cnt, case["levels"], 0, 0)
+    elif api == "armci":
+        rc = L.ARMCI_AccS(op, sp, sptr, ss, dptr, ds, cnt, case["levels"], 0)
+    elif api == "nb":
+        h = ctypes.c_int(-1)
+        rc = L.comex_nbaccs(op, sp, sptr, ss, dptr, ds, cnt, case["levels"], 0, 0, ctypes.byref(h))
+        assert rc == 0
+        rc = L.comex_wait(ctypes.byref(h))
+    elif api == "kernel":
+        rc = L.gaamd_strided(op, sp, sptr, ss, dptr, ds, cnt, case["levels"], None)
+    assert rc == 0
+    assert L.comex_fence_all(0) == 0
+    out = dbuf.download(np.uint8, dst_in.size)
+    sbuf.free()
+    dbuf.free()
+    return out
+
+
+def test_golden_cases_comex_accs(gpu_lib, manifest, golden):
+    bad = []
+    for case in manifest["cases"]:
+        n = case["name"]
+        out = run_case_device(gpu_lib, case, golden[f"{n}/src"], golden[f"{n}/dst_in"])
+        if not same_bits_nan_aware(out, golden[f"{n}/dst_out"], case["op"]):
+            bad.append(f"{n}: {first_mismatch(out, golden[f'{n}/dst_out'], case['op'])}")
+    assert not bad, "\n".join(bad)
+
+
+def test_golden_cases_armci_and_nb(gpu_lib, manifest, golden):
+    bad = []
+    for case in manifest["cases"][::3]:
+        n = case["name"]
+        for api in ("armci", "nb"):
+            out = run_case_device(gpu_lib, case, golden[f"{n}/src"], golden[f"{n}/dst_in"], api=api)
+            if not same_bits_nan_aware(out, golden[f"{n}/dst_out"], case["op"]):
+                bad.append(f"{api} {n}")
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("knob", [("kind", 1), ("kind", 2), ("kind", 3), ("unroll16", 2), ("unroll16", 8),
+                                  ("nontemporal", 1), ("max_grid", 7)])
+def test_kernel_variants_identical(gpu_lib, manifest, golden, knob):
+    """Every kernel family / tuning gives the same bits as the reference."""
+    key, val = knob
+    old = ga_amd.set_tuning(key, val)
+    try:
+        bad = []
+        for case in manifest["cases"]:
+            n = case["name"]
+            if key == "kind" and val == 3 and case["count"][0] * np.prod(case["count"][1:]) > 200000:
+                continue
+            out = run_case_device(gpu_lib, case, golden[f"{n}/src"], golden[f"{n}/dst_in"], api="kernel")
+            if not same_bits_nan_aware(out, golden[f"{n}/dst_out"], case["op"]):
+                bad.append(n)
+        assert not bad, bad
+    finally:
+        ga_amd.set_tuning(key, old)
+
+
+def _random_patch(rng, levels, esz):
+    count = [int(rng.integers(1, 40)) * esz] + [int(rng.integers(1, 6)) for _ in range(levels)]
+    ss, ds, a, b = [], [], count[0] + esz * int(rng.integers(0, 3)), count[0] + esz * int(rng.integers(0, 3))
+    for j in range(levels):
+        ss.append(a)
+        ds.append(b)
+        a = a * count[j + 1] + esz * int(rng.integers(0, 2))
+        b = b * count[j + 1] + esz * int(rng.integers(0, 2))
+    return count, ss, ds
+
+
+@pytest.mark.parametrize("levels", [0, 1, 2, 3, 5, 7])
+def test_pack_unpack_unpack_acc(gpu_lib, oracle, levels):
+    rng = np.random.default_rng(100 + levels)
+    for op in (C.DBL, C.DCP, C.INT):
+        esz = C.ESZ[op]
+        count, ss, ds = _random_patch(rng, levels, esz)
+        src = C.fill_bytes(op, C.span(ss, count, levels)[1], 5)
+        dst = C.fill_bytes(op, C.span(ds, count, levels)[1], 6)
+        P = oracle.packed_size(count, levels)
+        sb, db, pb = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size), ga_amd.DeviceBuffer(P)
+        sb.upload(src)
+        db.upload(dst)
+        ga_amd.pack(sb.ptr, ss, count, levels, pb.ptr)
+        ga_amd.sync()
+        packed = pb.download(np.uint8, P)
+        assert np.array_equal(packed, oracle.pack(src, 0, ss, count, levels))
+        ga_amd.unpack_acc(op, C.SCALE[op], pb.ptr, db.ptr, ds, count, levels)
+        ga_amd.sync()
+        want = dst.copy()
+        oracle.unpack_acc(op, C.SCALE[op], packed, want, 0, ds, count, levels)
+        assert np.array_equal(db.download(np.uint8, dst.size), want)
+        ga_amd.unpack(pb.ptr, db.ptr, ds, count, levels)
+        ga_amd.sync()
+        oracle.unpack(packed, want, 0, ds, count, levels)
+        assert np.array_equal(db.download(np.uint8, dst.size), want)
+
+
+@pytest.mark.parametrize("levels", [0, 1, 2, 4, 6])
+def test_puts_gets_local(gpu_lib, oracle, levels):
+    rng = np.random.default_rng(200 + levels)
+    count, ss, ds = _random_patch(rng, levels, 1)
+    count[0] += 3   # odd byte rows exercise the byte-wide copy
+    src = rng.integers(0, 256, C.span(ss, count, levels)[1] + 8, dtype=np.uint8)
+    dst = rng.integers(0, 256, C.span(ds, count, levels)[1] + 8, dtype=np.uint8)
+    sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+    sb.upload(src)
+    db.upload(dst)
+    assert ga_amd.comex_puts(sb.ptr + 1, ss, db.ptr + 2, ds, count, levels, 0) == 0
+    ga_amd.comex_fence_all()
+    want = dst.copy()
+    oracle.puts(src, 1, ss, want, 2, ds, count, levels)
+    assert np.array_equal(db.download(np.uint8, dst.size), want)
+    back = np.zeros_like(src)
+    bb = ga_amd.DeviceBuffer(back.size)
+    bb.upload(back)
+    assert ga_amd.comex_gets(db.ptr + 2, ds, bb.ptr + 1, ss, count, levels, 0) == 0
+    ga_amd.comex_fence_all()
+    want_back = back.copy()
+    oracle.puts(want, 2, ds, want_back, 1, ss, count, levels)
+    assert np.array_equal(bb.download(np.uint8, back.size), want_back)
+
+
+def test_host_memory_operands(gpu_lib, manifest, golden):
+    """MA-style host buffers: pageable src + device dst, device src + pinned dst,
+    pageable both (test.c:1028-1128 accumulates from a malloc'd local buffer)."""
+    L = gpu_lib
+    for case in manifest["cases"][::5]:
+        n, op = case["name"], case["op"]
+        src, dst_in, want = golden[f"{n}/src"], golden[f"{n}/dst_in"], golden[f"{n}/dst_out"]
+        keep, sp = ga_amd.scale_buffer(op, C.SCALE[op])
+        ss, ds, cnt = (ga_amd.int_array(case["src_stride"]), ga_amd.int_array(case["dst_stride"]),
+                       ga_amd.int_array(case["count"]))
+        # pageable host src, device dst
+        hsrc = src.copy()
+        dbuf = ga_amd.DeviceBuffer(max(16, dst_in.size))
+        dbuf.upload(dst_in)
+        rc = L.comex_accs(op, sp, ctypes.c_void_p(hsrc.ctypes.data + case["src_off"]), ss,
+                          ctypes.c_void_p(dbuf.ptr + case["dst_off"]), ds, cnt, case["levels"], 0, 0)
+        assert rc == 0
+        L.comex_fence_all(0)
+        assert same_bits_nan_aware(dbuf.download(np.uint8, dst_in.size), want, op), ("host src", n)
+        # pageable host src and pageable host dst
+        hdst = dst_in.copy()
+        rc = L.comex_accs(op, sp, ctypes.c_void_p(hsrc.ctypes.data + case["src_off"]), ss,
+                          ctypes.c_void_p(hdst.ctypes.data + case["dst_off"]), ds, cnt, case["levels"], 0, 0)
+        assert rc == 0
+        L.comex_fence_all(0)
+        assert same_bits_nan_aware(hdst, want, op), ("host both", n)
+        # pinned (comex_malloc_local) dst, device src
+        pin = L.comex_malloc_local(max(16, dst_in.size))
+        ctypes.memmove(pin, dst_in.ctypes.data, dst_in.size)
+        sbuf = ga_amd.DeviceBuffer(max(16, src.size))
+        sbuf.upload(src)
+        rc = L.comex_accs(op, sp, ctypes.c_void_p(sbuf.ptr + case["src_off"]), ss,
+                          ctypes.c_void_p(pin + case["dst_off"]), ds, cnt, case["levels"], 0, 0)
+        assert rc == 0
+        L.comex_fence_all(0)
+        got = np.ctypeslib.as_array((ctypes.c_uint8 * dst_in.size).from_address(pin)).copy()
+        L.comex_free_local(ctypes.c_void_p(pin))
+        assert same_bits_nan_aware(got, want, op), ("pinned dst", n)
+
+
+@pytest.mark.parametrize("type_code,dtype", [(0, np.float64), (1, np.float32), (2, np.int32), (3, np.int64)])
+def test_device_generator_matches_host(gpu_lib, type_code, dtype):
+    n = 100003
+    b = ga_amd.DeviceBuffer(n * np.dtype(dtype).itemsize)
+    ga_amd.fill(b.ptr, n, type_code, C.SEED + 7)
+    ga_amd.sync()
+    assert np.array_equal(b.download(dtype, n), C.fill_real(dtype, n, C.SEED + 7))
+
+
+def _fill_device(buf, op, nbytes, seed):
+    rt = np.dtype(C.REAL[op])
+    code = {np.dtype(np.float64): 0, np.dtype(np.float32): 1, np.dtype(np.int32): 2, np.dtype(np.int64): 3}[rt]
+    ga_amd.fill(buf.ptr, nbytes // rt.itemsize, code, seed)
+    tail = nbytes % rt.itemsize
+    if tail:
+        ga_amd.lib().gaamd_memset(ctypes.c_void_p(buf.ptr + nbytes - tail), 0, tail)
+
+
+@pytest.mark.parametrize("idx", range(5))
+def test_full_size_digest(gpu_lib, manifest, idx):
+    """Full BASELINE sizes (C2, H ld 8192/8200, C3, C4): sha256 of the whole dst
+    after one comex_accs equals the reference _acc's (oracle/_ref, manifest)."""
+    cfg = manifest["full_size"][idx]
+    op = cfg["op"]
+    sb, db = ga_amd.DeviceBuffer(cfg["src_bytes"]), ga_amd.DeviceBuffer(cfg["dst_bytes"])
+    _fill_device(sb, op, cfg["src_bytes"], C.SEED)
+    _fill_device(db, op, cfg["dst_bytes"], C.SEED + 1)
+    ga_amd.sync()
+    assert hashlib.sha256(sb.download(np.uint8, cfg["src_bytes"]).tobytes()).hexdigest() == cfg["src_sha256"]
+    rc = ga_amd.comex_accs(op, C.SCALE[op], sb.ptr, cfg["src_stride"], db.ptr, cfg["dst_stride"], cfg["count"],
+                           cfg["levels"], 0)
+    assert rc == 0
+    ga_amd.comex_fence_all()
+    got = hashlib.sha256(db.download(np.uint8, cfg["dst_bytes"]).tobytes()).hexdigest()
+    assert got == cfg["dst_sha256"], cfg["name"]
+
+
+def test_full_size_integer_roundtrip(gpu_lib):
+    """Linearity at the headline shape in int64: acc(+a) then acc(-a) restores dst
+    exactly (size-independent property; bit-exact integer path)."""
+    count, stride = [2048 * 8, 4096], [8192 * 8]
+    nbytes = stride[0] * 4095 + count[0]
+    sb, db = ga_amd.DeviceBuffer(nbytes), ga_amd.DeviceBuffer(nbytes)
+    _fill_device(sb, C.LNG, nbytes, 1)
+    _fill_device(db, C.LNG, nbytes, 2)
+    ga_amd.sync()
+    before = hashlib.sha256(db.download(np.uint8, nbytes).tobytes()).hexdigest()
+    assert ga_amd.comex_accs(C.LNG, 12345, sb.ptr, stride, db.ptr, stride, count, 1, 0) == 0
+    mid = hashlib.sha256(db.download(np.uint8, nbytes).tobytes()).hexdigest()
+    assert ga_amd.comex_accs(C.LNG, -12345, sb.ptr, stride, db.ptr, stride, count, 1, 0) == 0
+    ga_amd.comex_fence_all()
+    after = hashlib.sha256(db.download(np.uint8, nbytes).tobytes()).hexdigest()
+    assert mid != before and after == before
+
+
+def test_empty_patches_are_noops(gpu_lib):
+    """count[j]=0 (j>=1) -> n1dim = 0 -> the reference loop runs zero times."""
+    b = ga_amd.DeviceBuffer(64)
+    b.upload(np.arange(8, dtype=np.float64))
+    assert ga_amd.comex_accs(C.DBL, 2.0, b.ptr, [16], b.ptr + 32, [16], [16, 0], 1, 0) == 0
+    ga_amd.comex_fence_all()
+    assert np.array_equal(b.download(np.float64, 8), np.arange(8, dtype=np.float64))
