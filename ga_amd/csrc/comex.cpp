@@ -58,8 +58,12 @@ int translate_world(int group, int proc) {
 
 // ---- pointer resolution ---------------------------------------------------
 struct View {
-    char *dev = nullptr;       // device-accessible address of the user pointer
+    char *dev = nullptr;          // device-accessible address of the user pointer
     void *registered = nullptr;   // page base we registered for this call
+    char *staged = nullptr;       // fallback: device copy of [host+lo, host+hi)
+    char *host = nullptr;
+    int64_t lo = 0, hi = 0;
+    bool copy_back = false;
 };
 
 static bool find_segment_local(const void *p, int64_t lo, int64_t hi) {
@@ -86,36 +90,114 @@ static char *remote_view(int owner, const void *p, int64_t lo, int64_t hi) {
     fatal("address %p [%ld,%ld) of rank %d is not inside a comex_malloc segment", p, (long)lo, (long)hi, owner);
 }
 
-static View local_view(void *p, int64_t lo, int64_t hi) {
-    View v;
-    if (find_segment_local(p, lo, hi)) {
-        v.dev = (char *)p;
-        return v;
-    }
+// device-visible without help: our segments, HBM, managed, pinned/registered host
+static bool direct_view(void *p, char **dev) {
+    if (find_segment_local(p, 0, 1)) { *dev = (char *)p; return true; }
     hipPointerAttribute_t at;
     memset(&at, 0, sizeof(at));
     hipError_t e = hipPointerGetAttributes(&at, p);
     if (e == hipSuccess && (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged)) {
-        v.dev = (char *)p;
-        return v;
+        *dev = (char *)p;
+        return true;
     }
     if (e == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer) {
-        v.dev = (char *)at.devicePointer;   // pinned / already registered host memory
-        return v;
+        *dev = (char *)at.devicePointer;
+        return true;
     }
     (void)hipGetLastError();
-    // pageable host memory: pin + map the span for this call
-    const uintptr_t a0 = ((uintptr_t)p + lo) & ~(uintptr_t)(kPage - 1);
-    const uintptr_t a1 = (((uintptr_t)p + hi) + kPage - 1) & ~(uintptr_t)(kPage - 1);
-    GA_HIP(hipHostRegister((void *)a0, a1 - a0, hipHostRegisterMapped));
-    void *dbase = nullptr;
-    GA_HIP(hipHostGetDevicePointer(&dbase, (void *)a0, 0));
-    v.registered = (void *)a0;
-    v.dev = (char *)dbase + ((uintptr_t)p - a0);
+    return false;
+}
+
+static void page_range(const void *p, int64_t lo, int64_t hi, uintptr_t &a0, uintptr_t &a1) {
+    a0 = ((uintptr_t)p + lo) & ~(uintptr_t)(kPage - 1);
+    a1 = (((uintptr_t)p + hi) + kPage - 1) & ~(uintptr_t)(kPage - 1);
+}
+
+// pin + map pageable host pages for this call; on failure (pages already
+// registered by someone else) stage the span through a device copy instead
+static bool register_range(uintptr_t a0, uintptr_t a1, char **dbase) {
+    hipError_t e = hipHostRegister((void *)a0, a1 - a0, hipHostRegisterMapped);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    void *d = nullptr;
+    GA_HIP(hipHostGetDevicePointer(&d, (void *)a0, 0));
+    *dbase = (char *)d;
+    return true;
+}
+
+static void stage_view(View &v, void *p, int64_t lo, int64_t hi, bool is_dst) {
+    Runtime &r = rt();
+    v.host = (char *)p;
+    v.lo = lo;
+    v.hi = hi;
+    GA_HIP(hipMalloc((void **)&v.staged, (size_t)(hi - lo)));
+    GA_HIP(hipMemcpyAsync(v.staged, (char *)p + lo, (size_t)(hi - lo), hipMemcpyHostToDevice, r.stream));
+    v.dev = v.staged - lo;
+    v.copy_back = is_dst;
+}
+
+// resolve src and dst of one local transfer; a pageable pair whose page
+// ranges overlap is registered once as a union
+static void local_views(void *src, int64_t slo, int64_t shi, void *dst, int64_t dlo, int64_t dhi,
+                        View &sv, View &dv) {
+    char *d = nullptr;
+    const bool sd = direct_view(src, &d);
+    if (sd) sv.dev = d;
+    const bool dd = direct_view(dst, &d);
+    if (dd) dv.dev = d;
+    uintptr_t s0 = 0, s1 = 0, d0 = 0, d1 = 0;
+    if (!sd) page_range(src, slo, shi, s0, s1);
+    if (!dd) page_range(dst, dlo, dhi, d0, d1);
+    if (!sd && !dd && s0 < d1 && d0 < s1) {
+        const uintptr_t u0 = std::min(s0, d0), u1 = std::max(s1, d1);
+        char *base = nullptr;
+        if (register_range(u0, u1, &base)) {
+            sv.registered = (void *)u0;
+            sv.dev = base + ((uintptr_t)src - u0);
+            dv.dev = base + ((uintptr_t)dst - u0);
+            return;
+        }
+        stage_view(sv, src, slo, shi, false);
+        stage_view(dv, dst, dlo, dhi, true);
+        return;
+    }
+    char *base = nullptr;
+    if (!sd) {
+        if (register_range(s0, s1, &base)) { sv.registered = (void *)s0; sv.dev = base + ((uintptr_t)src - s0); }
+        else stage_view(sv, src, slo, shi, false);
+    }
+    if (!dd) {
+        if (register_range(d0, d1, &base)) { dv.registered = (void *)d0; dv.dev = base + ((uintptr_t)dst - d0); }
+        else stage_view(dv, dst, dlo, dhi, true);
+    }
+}
+
+static View local_view(void *p, int64_t lo, int64_t hi) {
+    View v, unused;
+    char *d = nullptr;
+    if (direct_view(p, &d)) { v.dev = d; return v; }
+    uintptr_t a0, a1;
+    page_range(p, lo, hi, a0, a1);
+    char *base = nullptr;
+    if (register_range(a0, a1, &base)) { v.registered = (void *)a0; v.dev = base + ((uintptr_t)p - a0); }
+    else stage_view(v, p, lo, hi, false);
     return v;
 }
 
+static bool needs_sync(const View &v) { return v.registered || v.staged; }
+
+// after the kernel: copy a staged dst back, then unpin / free (stream synced by caller)
 static void release_view(View &v) {
+    Runtime &r = rt();
+    if (v.staged) {
+        if (v.copy_back)
+            GA_HIP(hipMemcpy(v.host + v.lo, v.staged, (size_t)(v.hi - v.lo), hipMemcpyDeviceToHost));
+        GA_HIP(hipStreamSynchronize(r.stream));
+        GA_HIP(hipFree(v.staged));
+        v.staged = nullptr;
+    }
     if (v.registered) GA_HIP(hipHostUnregister(v.registered));
     v.registered = nullptr;
 }
@@ -385,8 +467,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
             dv = local_view(dst, dlo, dhi);
         }
     } else {
-        sv = local_view(src, slo, shi);
-        dv = local_view(dst, dlo, dhi);
+        local_views(src, slo, shi, dst, dlo, dhi, sv, dv);
     }
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
@@ -394,7 +475,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         if (rc) fatal("strided %s launch failed (code %d): misaligned elements or bad descriptor",
                       kind == X_ACC ? "acc" : (kind == X_PUT ? "put" : "get"), rc);
     }
-    const bool host_side = sv.registered || dv.registered;
+    const bool host_side = needs_sync(sv) || needs_sync(dv);
     if (host_side || r.blocking_sync) {
         GA_HIP(hipStreamSynchronize(r.stream));
         release_view(sv);
