@@ -1,0 +1,342 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident strided f64 accumulate through the ComEx C ABI.
+
+Metric (BASELINE.json): GiB/s device-resident 2-D strided f64 accumulate,
+64 MiB patch; % HBM peak.
+
+A "step" is one comex_accs call (include/comex.h; reference comex_accs,
+comex/src-mpi-pr/comex.c:985) applying dst += alpha*src over the workload's
+patch, both sides resident in HBM.  Default workload "H": count = {2048*8 B,
+4096 rows}, src & dst leading dimension 8192 doubles (65 536 B) -- 64 MiB of
+payload, 192 MiB of algorithmic HBM traffic (src read + dst read + dst write,
+24 B per element).  Steps rotate over --sets independent buffer sets (default
+8 x 512 MiB) so the 256 MiB Infinity Cache cannot serve the working set.
+
+value = whole-job algorithmic traffic GiB/s = ranks * steps * bytes / max-over-
+ranks wall time.  roofline.achieved = the same algorithmic bytes / the average
+kernel duration from HIP events recorded on the library's stream around every
+timed launch.  cpu_baseline = the reference's own _acc (oracle/_ref, compiled
+from comex/src-common/acc.h) driven per row on one host core over a bounded
+sample of the same workload.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank accumulates
+into its own partition (GA owner-aligned patches) with no
+data-path collective -> "scaling": "weak".  torch.distributed (gloo, CPU) only
+carries the bootstrap allgather/barrier and the max-over-ranks reduction.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident 2-D strided f64 accumulate, 64 MiB patch; % HBM peak"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md chip table (8.0 TB/s)
+DBL, DCP = 38, 41
+
+WORKLOADS = {
+    # name: (op, count, src_stride, dst_stride, description)
+    "H": (DBL, [2048 * 8, 4096], [8192 * 8], [8192 * 8],
+          "2-D f64 2048x4096 patch, ld 8192 (64 MiB payload)"),
+    "H8200": (DBL, [2048 * 8, 4096], [8200 * 8], [8200 * 8],
+              "2-D f64 2048x4096 patch, ld 8200 (64 MiB payload)"),
+    "C2": (DBL, [64 << 20], [], [], "1-D contiguous f64, 64 MiB"),
+    "C3": (DBL, [4096 * 8, 4096], [8192 * 8], [8192 * 8], "2-D f64 4096x4096 patch, ld 8192 (128 MiB)"),
+    "C4": (DCP, [4096, 256, 256], [4096, 1048576], [4224, 1115136],
+           "3-D double-complex 256^3 patch, dst in 264x264x256 (256 MiB)"),
+}
+ESZ = {DBL: 8, DCP: 16}
+SCALE = {DBL: 0.7071067811865476, DCP: 0.6 - 0.8j}
+
+
+def span_bytes(count, strides):
+    hi = count[0]
+    for j, s in enumerate(strides):
+        hi += s * (count[j + 1] - 1)
+    return hi
+
+
+def patch_bytes(count):
+    n = 1
+    for c in count:
+        n *= c
+    return n
+
+
+# ---------------------------------------------------------------- distributed
+class Dist:
+    def __init__(self, n_gpus):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.size = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        self.pg = None
+        if self.size > 1:
+            import torch
+            import torch.distributed as td
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            td.init_process_group("gloo", rank=self.rank, world_size=self.size)
+            self.torch, self.td = torch, td
+        if n_gpus != self.size and self.rank == 0:
+            print(f"warning: --gpus {n_gpus} but WORLD_SIZE {self.size}", file=sys.stderr)
+
+    def hooks(self):
+        """bootstrap allgather/barrier for gaamd_set_bootstrap (replaces MPI_Allgather)."""
+        import ga_amd
+        torch, td = self.torch, self.td
+
+        def allgather(send, recv, nbytes, ctx):
+            buf = torch.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=torch.uint8)
+            out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.size)]
+            td.all_gather(out, buf)
+            ctypes.memmove(recv, torch.cat(out).numpy().ctypes.data, nbytes * self.size)
+            return 0
+
+        def barrier(ctx):
+            td.barrier()
+            return 0
+
+        self._ag = ga_amd.ALLGATHER_FN(allgather)
+        self._bar = ga_amd.BARRIER_FN(barrier)
+        return self._ag, self._bar
+
+    def max(self, x):
+        if self.size == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64)
+        self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
+        return float(t.item())
+
+    def barrier(self):
+        if self.size > 1:
+            self.td.barrier()
+
+
+# ---------------------------------------------------------------- GPU leg
+def run_gpu(args, dist):
+    import ga_amd
+    L = ga_amd.lib()
+    if dist.size > 1:
+        ag, bar = dist.hooks()
+        rc = L.gaamd_set_bootstrap(dist.rank, dist.size, dist.local_rank, ctypes.cast(ag, ctypes.c_void_p),
+                                   ctypes.cast(bar, ctypes.c_void_p), None)
+        assert rc == 0, rc
+    assert ga_amd.comex_init() == 0
+    for kv in args.tune or []:
+        k, v = kv.split("=")
+        ga_amd.set_tuning(k, int(v))
+
+    op, count, sstr, dstr, desc = WORKLOADS[args.workload]
+    esz = ESZ[op]
+    levels = len(count) - 1
+    sbytes, dbytes = span_bytes(count, sstr), span_bytes(count, dstr)
+    payload = patch_bytes(count)
+    elems = payload // esz
+    alg_bytes = 3 * payload            # src read + dst read + dst write
+    type_code = 0                      # f64 reals (dcpl = 2 f64 each)
+
+    # --sets independent (src, dst) pairs; rotate so the MALL cannot hold them
+    sets = []
+    for i in range(args.sets):
+        s = ga_amd.DeviceBuffer(sbytes)
+        d = ga_amd.DeviceBuffer(dbytes)
+        ga_amd.fill(s.ptr, sbytes // 8, type_code, 0x5EED0000 + dist.rank)
+        ga_amd.fill(d.ptr, dbytes // 8, type_code, 0x5EED0001 + dist.rank + 977 * i)
+        sets.append((s, d))
+    ga_amd.sync()
+
+    keep, sp = ga_amd.scale_buffer(op, SCALE[op])
+    ss, ds, cnt = ga_amd.int_array(sstr), ga_amd.int_array(dstr), ga_amd.int_array(count)
+    ptrs = [(ctypes.c_void_p(s.ptr), ctypes.c_void_p(d.ptr)) for s, d in sets]
+    stream = L.gaamd_stream()
+
+    def step(i):
+        sp_, dp_ = ptrs[i % len(ptrs)]
+        rc = L.comex_accs(op, sp, sp_, ss, dp_, ds, cnt, levels, dist.rank, 0)
+        if rc:
+            raise RuntimeError(f"comex_accs returned {rc}")
+
+    for i in range(args.warmup):
+        step(i)
+    ga_amd.sync()
+    launch = ga_amd.last_launch()
+
+    # one HIP event pair on the library stream brackets the K launches of the
+    # timed region: average launch duration = region / K.  (An event pair around
+    # every launch would put a release between kernels and slow them down.)
+    ev0, ev1 = L.gaamd_event_create(), L.gaamd_event_create()
+    L.comex_barrier(0)
+    dist.barrier()
+    ga_amd.sync()
+    t0 = time.perf_counter()
+    L.gaamd_event_record(ev0, stream)
+    for i in range(args.steps):
+        step(args.warmup + i)
+    L.gaamd_event_record(ev1, stream)
+    ga_amd.sync()
+    t1 = time.perf_counter()
+    dist.barrier()
+    elapsed = dist.max(t1 - t0)
+    region_ms = L.gaamd_event_elapsed_ms(ev0, ev1)
+    L.gaamd_event_destroy(ev0)
+    L.gaamd_event_destroy(ev1)
+    avg_kernel_s = dist.max(region_ms / 1e3 / args.steps)
+
+    res = dict(op=op, desc=desc, payload=payload, alg_bytes=alg_bytes, elems=elems, elapsed=elapsed,
+               avg_kernel_s=avg_kernel_s, launch=launch)
+    if args.host_rates and dist.rank == 0:
+        res["host"] = host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_bytes)
+    for s, d in sets:
+        s.free()
+        d.free()
+    ga_amd.comex_finalize()
+    return res
+
+
+def host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_bytes, iters=5):
+    """Host-inclusive rates (recorded in DESIGN.md, never `value`): the patch starts
+    and ends in host memory (MA segments).  (a) explicit hipMemcpy H2D of the src and
+    dst spans + device kernel + D2H of the dst span, pinned and pageable; (b)
+    comex_accs directly on host pointers (per-call pinning, zero-copy kernel)."""
+    out = {}
+    keep, sp = ga_amd.scale_buffer(op, SCALE[op])
+    ss, ds, cnt = ga_amd.int_array(sstr), ga_amd.int_array(dstr), ga_amd.int_array(count)
+    dsrc, ddst = ga_amd.DeviceBuffer(sbytes), ga_amd.DeviceBuffer(dbytes)
+    for kind in ("pinned", "pageable"):
+        if kind == "pinned":
+            hs, hd = ga_amd.DeviceBuffer(sbytes, host=True), ga_amd.DeviceBuffer(dbytes, host=True)
+            hsp, hdp = hs.ptr, hd.ptr
+        else:
+            hs_a, hd_a = np.ones(sbytes, np.uint8), np.zeros(dbytes, np.uint8)
+            hsp, hdp = hs_a.ctypes.data, hd_a.ctypes.data
+        ts = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            L.gaamd_memcpy(ctypes.c_void_p(dsrc.ptr), ctypes.c_void_p(hsp), sbytes)
+            L.gaamd_memcpy(ctypes.c_void_p(ddst.ptr), ctypes.c_void_p(hdp), dbytes)
+            L.comex_accs(op, sp, ctypes.c_void_p(dsrc.ptr), ss, ctypes.c_void_p(ddst.ptr), ds, cnt, levels, 0, 0)
+            L.gaamd_memcpy(ctypes.c_void_p(hdp), ctypes.c_void_p(ddst.ptr), dbytes)
+            ts.append(time.perf_counter() - t0)
+        out[f"staged_{kind}_GiBps"] = alg_bytes / min(ts) / 2 ** 30
+        ts = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            L.comex_accs(op, sp, ctypes.c_void_p(hsp), ss, ctypes.c_void_p(hdp), ds, cnt, levels, 0, 0)
+            L.comex_fence_all(0)
+            ts.append(time.perf_counter() - t0)
+        out[f"zerocopy_{kind}_GiBps"] = alg_bytes / min(ts) / 2 ** 30
+        if kind == "pinned":
+            hs.free()
+            hd.free()
+    dsrc.free()
+    ddst.free()
+    return out
+
+
+# ---------------------------------------------------------------- CPU leg
+def run_cpu_baseline(workload, seconds):
+    """The reference's _acc per row (oracle/_ref), or the restatement if _ref is absent,
+    on one core; as many full steps as fit in ~`seconds` (at least 2)."""
+    from oracle import Oracle, Ref, ref_available
+    op, count, sstr, dstr, _ = WORKLOADS[workload]
+    sbytes, dbytes = span_bytes(count, sstr), span_bytes(count, dstr)
+    src = np.empty(sbytes, np.uint8)
+    dst = np.empty(dbytes, np.uint8)
+    o = Oracle()
+    o.fill(src[: sbytes // 8 * 8].view(np.float64), 0x5EED0000)
+    o.fill(dst[: dbytes // 8 * 8].view(np.float64), 0x5EED0001)
+    if ref_available():
+        impl, kind = Ref(), "reference"
+    else:
+        impl, kind = o, "port"
+    levels = len(count) - 1
+    impl.accs(op, SCALE[op], src, 0, sstr, dst, 0, dstr, count, levels)   # warm-up (page-in)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        impl.accs(op, SCALE[op], src, 0, sstr, dst, 0, dstr, count, levels)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds and n >= 2) or n >= 10000:
+            break
+    alg = 3 * patch_bytes(count) * n
+    return {"value": round(alg / el / 2 ** 30, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": f"{n} full {workload} steps ({el:.1f} s) on 1 host core; "
+                      + ("reference comex/src-common/acc.h _acc (HAVE_BLAS=0, gcc -O2) per row, "
+                         "odometer of comex.c:6936-6961" if kind == "reference" else "oracle restatement")}
+
+
+def load_traffic(workload, launch_bytes):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if it is for
+    this workload (profiles/pmc_latest.json, written by tools/pmc_traffic.py)."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="H", choices=sorted(WORKLOADS))
+    ap.add_argument("--sets", type=int, default=8, help="rotating buffer sets (MALL defeat)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--host-rates", action="store_true", help="also measure host-inclusive rates")
+    ap.add_argument("--tune", action="append", help="key=value tuning knob (gaamd_set_tuning)")
+    args = ap.parse_args()
+
+    dist = Dist(args.gpus)
+    r = run_gpu(args, dist)
+    if dist.rank != 0:
+        return
+    n = dist.size
+    alg = r["alg_bytes"]
+    value = n * args.steps * alg / r["elapsed"] / 2 ** 30
+    achieved = alg / r["avg_kernel_s"] / 1e9
+    traffic = load_traffic(args.workload, alg)
+    cpu = None
+    if not args.no_cpu and n == 1:
+        cpu = run_cpu_baseline(args.workload, args.cpu_seconds)
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64" if r["op"] == DBL else "c128",
+        "data": "synthetic (splitmix64, SURVEY.md 8(d)); device-resident src+dst, %d rotating buffer sets" % args.sets,
+        "config": {"workload": args.workload, "patch": r["desc"], "payload_bytes": r["payload"],
+                   "algorithmic_bytes_per_step": alg, "parallelism": f"owner-aligned x{n} (no collective)",
+                   "kernel": r["launch"]},
+        "payload_GiB_per_s": round(value / 3, 2),
+        "hbm_peak_frac": round(value * 2 ** 30 / (HBM_PEAK_GBS * 1e9), 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_ms_avg": round(r["avg_kernel_s"] * 1e3, 4),
+                     "timing": "HIP event pair on the library stream around the timed launches / steps"},
+        "cpu_baseline": cpu,
+    }
+    if "host" in r:
+        line["host_inclusive_GiB_per_s"] = {k: round(v, 2) for k, v in r["host"].items()}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -471,7 +471,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     }
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
-        const int rc = launch_strided(cop, scale, sv.dev, ss, dv.dev, ds, count, levels, r.stream, nullptr);
+        const int rc = launch_strided(cop, scale, sv.dev, ss, dv.dev, ds, count, levels, r.stream, last_launch_info());
         if (rc) fatal("strided %s launch failed (code %d): misaligned elements or bad descriptor",
                       kind == X_ACC ? "acc" : (kind == X_PUT ? "put" : "get"), rc);
     }

@@ -57,8 +57,8 @@ enum KernelKind { KK_AUTO = 0, KK_ROWS = 1, KK_FLAT = 2, KK_SERIAL = 3 };
 
 struct Tuning {
     int kind = KK_AUTO;     // force a kernel family
-    int unroll16 = 4;       // vectors per thread for W=16 rows kernel {2,4,8}
-    int nontemporal = 0;    // nt loads/stores on the streaming path
+    int unroll16 = 1;       // vectors per thread for the W=16 rows kernels {1,2,4,8}
+    int nontemporal = 1;    // nt loads/stores on the rows kernels (streamed once)
     int block = 256;        // threads per block {256, 512}
     int flat_max_nvec = 127;// rows with at most this many vectors use the flat kernel
     int max_grid = 0;       // cap on blocks (0 = one block per work item)
@@ -85,6 +85,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
 void side_span_host(const int *stride, const int *count, int stride_levels, int64_t row_bytes,
                     int64_t *lo, int64_t *hi);
 
-int elem_size(int op);   // bytes per element for op; 1 for copy; 0 if unknown
+int elem_size(int op);
+LaunchInfo *last_launch_info();   // most recent launch_strided (any caller)   // bytes per element for op; 1 for copy; 0 if unknown
 
 }  // namespace gaamd

@@ -149,13 +149,17 @@ typedef AccCplx<float> AccCpl;
 typedef AccCplx<double> AccDcp;
 
 // ---------------------------------------------------------------------------
-// row decode: byte offsets of row r on both sides (mixed radix over count[1..L])
+// row decode: byte offsets of row r on both sides (mixed radix over count[1..L]).
+// LV > 0: exactly LV levels known at compile time (only those fields are read,
+// which keeps the kernel's SGPR footprint small); LV == 0: runtime d.levels.
+template <int LV>
 __device__ __forceinline__ void row_offsets(const Desc &d, uint32_t r, int64_t &so, int64_t &dof) {
     so = 0;
     dof = 0;
+    constexpr int N = LV > 0 ? LV : kMaxLevels;
 #pragma unroll
-    for (int j = 0; j < kMaxLevels; ++j) {
-        if (j >= d.levels) break;
+    for (int j = 0; j < N; ++j) {
+        if (LV == 0 && j >= d.levels) break;
         const uint32_t q = d.cnt[j].div(r);
         const uint32_t dig = r - q * d.cnt[j].d;
         so += (int64_t)dig * d.s_str[j];
@@ -164,53 +168,89 @@ __device__ __forceinline__ void row_offsets(const Desc &d, uint32_t r, int64_t &
     }
 }
 
-// ---------------------------------------------------------------------------
-// ROWS kernel: work item w = (row, chunk); chunk = BS*U vectors of that row.
+// the U vectors of one thread: all loads first, then the ops and the stores.
+// `full` (wave-uniform) says the whole chunk lies inside the row, so the
+// vectors need no predicate and their addresses fold into immediate offsets.
 template <class OP, int W, int U, int BS, bool NT>
-__global__ __launch_bounds__(BS) void k_rows(const Desc d, const OP op) {
+__device__ __forceinline__ void chunk_op(const char *sp, char *dp, uint32_t v0, uint32_t nvec, bool full,
+                                         const OP &op) {
     typedef typename Vec<W>::T V;
-    for (uint64_t w = blockIdx.x; w < d.items; w += gridDim.x) {
-        const uint32_t rl = d.chunk_div.div((uint32_t)w);
-        const uint32_t chunk = (uint32_t)w - rl * d.chunks;
+    V a[U], b[U];
+    const char *s0 = sp + (size_t)v0 * W;
+    char *d0 = dp + (size_t)v0 * W;
+    if (full) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            a[k] = vload<W, NT>(s0 + k * BS * W);
+            if constexpr (OP::kReadsDst) b[k] = vload<W, NT>(d0 + k * BS * W);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) vstore<W, NT>(d0 + k * BS * W, op.template apply<W>(b[k], a[k]));
+        return;
+    }
+    // row tail: one vector at a time (keeps the register budget of the full path)
+    for (int k = 0; k < U; ++k) {
+        if (v0 + (uint32_t)(k * BS) >= nvec) break;
+        V x = vload<W, NT>(s0 + k * BS * W), y = x;
+        if constexpr (OP::kReadsDst) y = vload<W, NT>(d0 + k * BS * W);
+        vstore<W, NT>(d0 + k * BS * W, op.template apply<W>(y, x));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// ROWS kernel (N-D): work item w = (row, chunk); chunk = BS*U vectors of a row.
+template <class OP, int W, int U, int BS, bool NT, int LV>
+__global__ __launch_bounds__(BS) void k_rows(const Desc d, const OP op) {
+    for (uint32_t w = blockIdx.x; w < (uint32_t)d.items; w += gridDim.x) {
+        const uint32_t rl = d.chunk_div.div(w);
+        const uint32_t chunk = w - rl * d.chunks;
         int64_t so, dof;
-        row_offsets(d, d.row0 + rl, so, dof);
-        const char *sp = d.src + so;
-        char *dp = d.dst + dof;
-        const uint32_t v0 = chunk * (uint32_t)(BS * U) + threadIdx.x;
-        V a[U], b[U];
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            const uint32_t v = v0 + (uint32_t)(k * BS);
-            if (v < d.nvec) {
-                a[k] = vload<W, NT>(sp + (size_t)v * W);
-                if constexpr (OP::kReadsDst) b[k] = vload<W, NT>(dp + (size_t)v * W);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            const uint32_t v = v0 + (uint32_t)(k * BS);
-            if (v < d.nvec) vstore<W, NT>(dp + (size_t)v * W, op.template apply<W>(b[k], a[k]));
-        }
+        row_offsets<LV>(d, d.row0 + rl, so, dof);
+        const uint32_t c0 = chunk * (uint32_t)(BS * U);
+        chunk_op<OP, W, U, BS, NT>(d.src + so, d.dst + dof, c0 + threadIdx.x, d.nvec, c0 + BS * U <= d.nvec, op);
+    }
+}
+
+// ROWS2 kernel: the common <= 1 stride-level case (2-D patches, contiguous
+// runs).  Row r sits at r*stride on each side -- no digit division -- and the
+// small argument block keeps the kernel at ~32 SGPRs (full occupancy).
+struct Desc2 {
+    const char *src;
+    char *dst;
+    int64_t s_str, d_str;
+    uint32_t row0, nvec, chunks, items;
+    FastDiv chunk_div;
+};
+
+template <class OP, int W, int U, int BS, bool NT>
+__global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
+    for (uint32_t w = blockIdx.x; w < d.items; w += gridDim.x) {
+        const uint32_t rl = d.chunk_div.div(w);
+        const uint32_t chunk = w - rl * d.chunks;
+        const int64_t r = (int64_t)(d.row0 + rl);
+        const uint32_t c0 = chunk * (uint32_t)(BS * U);
+        chunk_op<OP, W, U, BS, NT>(d.src + r * d.s_str, d.dst + r * d.d_str, c0 + threadIdx.x, d.nvec,
+                                   c0 + BS * U <= d.nvec, op);
     }
 }
 
 // FLAT kernel: vectors of all rows flattened, each lane decodes its own row.
-template <class OP, int W, int U, int BS>
+template <class OP, int W, int U, int BS, int LV>
 __global__ __launch_bounds__(BS) void k_flat(const Desc d, const OP op) {
     typedef typename Vec<W>::T V;
-    const uint64_t span = (uint64_t)BS * U;
-    for (uint64_t base = (uint64_t)blockIdx.x * span; base < d.items; base += (uint64_t)gridDim.x * span) {
+    const uint32_t span = (uint32_t)BS * U;
+    for (uint32_t base = blockIdx.x * span; base < (uint32_t)d.items; base += gridDim.x * span) {
         V a[U], b[U];
         char *dps[U];
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            const uint64_t g = base + threadIdx.x + (uint64_t)k * BS;
+            const uint32_t g = base + threadIdx.x + (uint32_t)(k * BS);
             dps[k] = nullptr;
-            if (g < d.items) {
-                const uint32_t rl = d.nvec_div.div((uint32_t)g);
-                const uint32_t v = (uint32_t)g - rl * d.nvec;
+            if (g < (uint32_t)d.items) {
+                const uint32_t rl = d.nvec_div.div(g);
+                const uint32_t v = g - rl * d.nvec;
                 int64_t so, dof;
-                row_offsets(d, d.row0 + rl, so, dof);
+                row_offsets<LV>(d, d.row0 + rl, so, dof);
                 dps[k] = d.dst + dof + (size_t)v * W;
                 a[k] = vload<W, false>(d.src + so + (size_t)v * W);
                 if constexpr (OP::kReadsDst) b[k] = vload<W, false>(dps[k]);
@@ -228,7 +268,7 @@ __global__ __launch_bounds__(64) void k_serial(const Desc d, const OP op) {
     if (threadIdx.x != 0) return;
     for (uint32_t r = 0; r < d.rows; ++r) {
         int64_t so, dof;
-        row_offsets(d, d.row0 + r, so, dof);
+        row_offsets<0>(d, d.row0 + r, so, dof);
         for (uint32_t v = 0; v < d.nvec; ++v) {
             char *dp = d.dst + dof + (size_t)v * W;
             typename Vec<W>::T a = vload<W, false>(d.src + so + (size_t)v * W);
@@ -241,23 +281,55 @@ __global__ __launch_bounds__(64) void k_serial(const Desc d, const OP op) {
 
 // ---------------------------------------------------------------------------
 // host launch plumbing
+//
+// Instantiation policy: the 2-D kernel of the ops on the headline paths
+// (f64, double complex, byte copy) carries every tuning variant (U 1/2/4/8,
+// 512-thread blocks, nt on/off); every other (op, kernel) pair is built once
+// with the default shape (16 B per thread per stream) and nt on/off.
+template <class OP> struct Tunable { static constexpr bool value = false; };
+template <> struct Tunable<AccDbl> { static constexpr bool value = true; };
+template <> struct Tunable<AccDcp> { static constexpr bool value = true; };
+template <> struct Tunable<CopyOp> { static constexpr bool value = true; };
+
+// vectors per thread for the default shape: 16 B per thread per stream
 static int unroll_for(int W, int u16) {
     switch (W) {
     case 16: return u16;
-    case 8: return 8;
-    default: return 16;
+    case 8: return 2;
+    case 4: return 4;
+    default: return 8;
     }
 }
+template <int W> struct DefaultU { static constexpr int value = W == 16 ? 1 : (W == 8 ? 2 : (W == 4 ? 4 : 8)); };
 
-template <class OP, int W, int U>
-static hipError_t go_rows(const Desc &d, const OP &op, uint64_t blocks, int nt, hipStream_t st) {
-    if (nt) hipLaunchKernelGGL((k_rows<OP, W, U, 256, true>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
-    else hipLaunchKernelGGL((k_rows<OP, W, U, 256, false>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+template <class OP, int W, int U, int BS>
+static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt, hipStream_t st) {
+    Desc2 e;
+    e.src = d.src;
+    e.dst = d.dst;
+    e.s_str = d.levels ? d.s_str[0] : 0;
+    e.d_str = d.levels ? d.d_str[0] : 0;
+    e.row0 = d.row0;
+    e.nvec = d.nvec;
+    e.chunks = d.chunks;
+    e.items = (uint32_t)d.items;
+    e.chunk_div = d.chunk_div;
+    if (nt) hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
+    else hipLaunchKernelGGL((k_rows2<OP, W, U, BS, false>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
+    return hipGetLastError();
+}
+
+template <class OP, int W, int LV>
+static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, int nt, hipStream_t st) {
+    constexpr int U = DefaultU<W>::value;
+    if (nt) hipLaunchKernelGGL((k_rows<OP, W, U, 256, true, LV>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+    else hipLaunchKernelGGL((k_rows<OP, W, U, 256, false, LV>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
     return hipGetLastError();
 }
 
 template <class OP, int W>
-static hipError_t dispatch_w(int kind, int U, int nt, const Desc &d, const OP &op, uint64_t blocks, hipStream_t st) {
+static hipError_t dispatch_w(int kind, int U, int BS, int nt, const Desc &d, const OP &op, uint64_t blocks,
+                             hipStream_t st) {
     if constexpr (W < OP::kElem) {
         return hipErrorInvalidValue;
     } else {
@@ -267,43 +339,53 @@ static hipError_t dispatch_w(int kind, int U, int nt, const Desc &d, const OP &o
         }
         if (kind == KK_FLAT) {
             constexpr int UF = (W == 16) ? 2 : 4;
-            hipLaunchKernelGGL((k_flat<OP, W, UF, 256>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+            if (d.levels == 1)
+                hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 1>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+            else if (d.levels == 2)
+                hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 2>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+            else
+                hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 0>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
             return hipGetLastError();
         }
-        if constexpr (W == 16) {
-            if (U == 2) return go_rows<OP, W, 2>(d, op, blocks, nt, st);
-            if (U == 8) return go_rows<OP, W, 8>(d, op, blocks, nt, st);
-            return go_rows<OP, W, 4>(d, op, blocks, nt, st);
-        } else if constexpr (W == 8) {
-            return go_rows<OP, W, 8>(d, op, blocks, 0, st);
-        } else {
-            return go_rows<OP, W, 16>(d, op, blocks, 0, st);
+        if (d.levels == 2) return go_rows_nd<OP, W, 2>(d, op, blocks, nt, st);
+        if (d.levels == 3) return go_rows_nd<OP, W, 3>(d, op, blocks, nt, st);
+        if (d.levels > 3) return go_rows_nd<OP, W, 0>(d, op, blocks, nt, st);
+        if constexpr (W == 16 && Tunable<OP>::value) {
+            if (BS == 512) {
+                if (U == 2) return go_rows2<OP, W, 2, 512>(d, op, blocks, nt, st);
+                return go_rows2<OP, W, 1, 512>(d, op, blocks, nt, st);
+            }
+            if (U == 2) return go_rows2<OP, W, 2, 256>(d, op, blocks, nt, st);
+            if (U == 4) return go_rows2<OP, W, 4, 256>(d, op, blocks, nt, st);
+            if (U == 8) return go_rows2<OP, W, 8, 256>(d, op, blocks, nt, st);
         }
+        return go_rows2<OP, W, DefaultU<W>::value, 256>(d, op, blocks, nt, st);
     }
 }
 
 template <class OP>
-static hipError_t dispatch_op(int W, int kind, int U, int nt, const Desc &d, const OP &op, uint64_t blocks, hipStream_t st) {
+static hipError_t dispatch_op(int W, int kind, int U, int BS, int nt, const Desc &d, const OP &op, uint64_t blocks,
+                              hipStream_t st) {
     switch (W) {
-    case 16: return dispatch_w<OP, 16>(kind, U, nt, d, op, blocks, st);
-    case 8: return dispatch_w<OP, 8>(kind, U, nt, d, op, blocks, st);
-    case 4: return dispatch_w<OP, 4>(kind, U, nt, d, op, blocks, st);
-    case 2: return dispatch_w<OP, 2>(kind, U, nt, d, op, blocks, st);
-    case 1: return dispatch_w<OP, 1>(kind, U, nt, d, op, blocks, st);
+    case 16: return dispatch_w<OP, 16>(kind, U, BS, nt, d, op, blocks, st);
+    case 8: return dispatch_w<OP, 8>(kind, U, BS, nt, d, op, blocks, st);
+    case 4: return dispatch_w<OP, 4>(kind, U, BS, nt, d, op, blocks, st);
+    case 2: return dispatch_w<OP, 2>(kind, U, BS, nt, d, op, blocks, st);
+    case 1: return dispatch_w<OP, 1>(kind, U, BS, nt, d, op, blocks, st);
     }
     return hipErrorInvalidValue;
 }
 
-static hipError_t dispatch(int op, const void *scale, int W, int kind, int U, int nt,
+static hipError_t dispatch(int op, const void *scale, int W, int kind, int U, int BS, int nt,
                            const Desc &d, uint64_t blocks, hipStream_t st) {
     switch (op) {
-    case kOpCopy: return dispatch_op(W, kind, U, nt, d, CopyOp{}, blocks, st);
-    case 37: { AccInt o; int32_t s; memcpy(&s, scale, 4); o.s = (uint32_t)s; return dispatch_op(W, kind, U, nt, d, o, blocks, st); }
-    case 42: { AccLng o; int64_t s; memcpy(&s, scale, 8); o.s = (uint64_t)s; return dispatch_op(W, kind, U, nt, d, o, blocks, st); }
-    case 39: { AccFlt o; memcpy(&o.s, scale, 4); return dispatch_op(W, kind, U, nt, d, o, blocks, st); }
-    case 38: { AccDbl o; memcpy(&o.s, scale, 8); return dispatch_op(W, kind, U, nt, d, o, blocks, st); }
-    case 40: { AccCpl o; float s[2]; memcpy(s, scale, 8); o.sr = s[0]; o.si = s[1]; return dispatch_op(W, kind, U, nt, d, o, blocks, st); }
-    case 41: { AccDcp o; double s[2]; memcpy(s, scale, 16); o.sr = s[0]; o.si = s[1]; return dispatch_op(W, kind, U, nt, d, o, blocks, st); }
+    case kOpCopy: return dispatch_op(W, kind, U, BS, nt, d, CopyOp{}, blocks, st);
+    case 37: { AccInt o; int32_t s; memcpy(&s, scale, 4); o.s = (uint32_t)s; return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
+    case 42: { AccLng o; int64_t s; memcpy(&s, scale, 8); o.s = (uint64_t)s; return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
+    case 39: { AccFlt o; memcpy(&o.s, scale, 4); return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
+    case 38: { AccDbl o; memcpy(&o.s, scale, 8); return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
+    case 40: { AccCpl o; float s[2]; memcpy(s, scale, 8); o.sr = s[0]; o.si = s[1]; return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
+    case 41: { AccDcp o; double s[2]; memcpy(s, scale, 16); o.sr = s[0]; o.si = s[1]; return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
     }
     return hipErrorInvalidValue;
 }
@@ -446,8 +528,14 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
 
     int kind = serial ? KK_SERIAL : tn.kind;
     if (kind == KK_AUTO) kind = ((int64_t)d.nvec <= tn.flat_max_nvec) ? KK_FLAT : KK_ROWS;
-    const int U = unroll_for(W, tn.unroll16);
-    const uint32_t per_chunk = 256u * (uint32_t)U;
+    // the (U, BS) the dispatcher will pick -- chunking must agree with it
+    const bool tunable = (op == kOpCopy || op == 38 || op == 41);
+    int U = unroll_for(W, 1), BS = 256;
+    if (kind == KK_ROWS && L <= 1 && W == 16 && tunable) {
+        U = tn.unroll16;
+        if (tn.block == 512 && U <= 2) BS = 512;
+    }
+    const uint32_t per_chunk = (uint32_t)BS * (uint32_t)U;
     d.chunks = (d.nvec + per_chunk - 1) / per_chunk;
     d.chunk_div = make_fastdiv(d.chunks);
 
@@ -477,7 +565,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         }
         if (tn.max_grid > 0 && blocks > (uint64_t)tn.max_grid) blocks = (uint64_t)tn.max_grid;
         if (blocks > lim) blocks = lim;
-        hipError_t e = dispatch(op, scale, W, kind, U, tn.nontemporal, d, blocks, stream);
+        hipError_t e = dispatch(op, scale, W, kind, U, BS, tn.nontemporal, d, blocks, stream);
         if (e != hipSuccess) return -100 - (int)e;
         ++launches;
         total_blocks += blocks;

@@ -7,7 +7,8 @@
 
 namespace gaamd {
 
-static LaunchInfo g_last;
+LaunchInfo g_last;
+LaunchInfo *last_launch_info() { return &g_last; }
 
 static hipStream_t stream_of(void *s) {
     if (s) return (hipStream_t)s;
@@ -107,13 +108,15 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "nontemporal")) return &t.nontemporal;
     if (!strcmp(key, "flat_max_nvec")) return &t.flat_max_nvec;
     if (!strcmp(key, "max_grid")) return &t.max_grid;
+    if (!strcmp(key, "block")) return &t.block;
     return nullptr;
 }
 
 int gaamd_set_tuning(const char *key, int value) {
     int *f = tuning_field(key);
     if (!f) return -1;
-    if (!strcmp(key, "unroll16") && value != 2 && value != 4 && value != 8) return -1;
+    if (!strcmp(key, "unroll16") && value != 1 && value != 2 && value != 4 && value != 8) return -1;
+    if (!strcmp(key, "block") && value != 256 && value != 512) return -1;
     const int old = *f;
     *f = value;
     return old;

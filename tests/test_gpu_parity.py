@@ -66,8 +66,8 @@ def test_golden_cases_armci_and_nb(gpu_lib, manifest, golden):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("knob", [("kind", 1), ("kind", 2), ("kind", 3), ("unroll16", 2), ("unroll16", 8),
-                                  ("nontemporal", 1), ("max_grid", 7)])
+@pytest.mark.parametrize("knob", [("kind", 1), ("kind", 2), ("kind", 3), ("unroll16", 2), ("unroll16", 4),
+                                  ("unroll16", 8), ("nontemporal", 0), ("max_grid", 7), ("block", 512)])
 def test_kernel_variants_identical(gpu_lib, manifest, golden, knob):
     """Every kernel family / tuning gives the same bits as the reference."""
     key, val = knob
