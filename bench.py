@@ -94,7 +94,8 @@ class Dist:
             buf = torch.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=torch.uint8)
             out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.size)]
             td.all_gather(out, buf)
-            ctypes.memmove(recv, torch.cat(out).numpy().ctypes.data, nbytes * self.size)
+            cat = torch.cat(out).numpy()   # keep alive across the memmove
+            ctypes.memmove(recv, cat.ctypes.data, nbytes * self.size)
             return 0
 
         def barrier(ctx):

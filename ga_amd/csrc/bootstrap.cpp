@@ -145,6 +145,7 @@ void boot_init() {
         if (r.ag(mine, all.data(), sizeof(mine), r.ctx) != 0) fatal("bootstrap allgather hook failed");
         memcpy(name, all.data(), sizeof(mine));
         name[63] = 0;
+        if (strncmp(name, "/gaamd_", 7) != 0) fatal("bootstrap allgather hook returned a corrupt segment name");
         r.shm = open_shm(name, bytes, r.rank == 0);
         if (r.bar(r.ctx) != 0) fatal("bootstrap barrier hook failed");
     } else {

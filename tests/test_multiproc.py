@@ -1,0 +1,68 @@
+"""world_size-2 multi-process coverage.
+
+CPU (no GPU): the rank bootstrap both ways the runtime supports -- the built-in
+node shared-memory rendezvous (RANK/WORLD_SIZE from the environment) and
+torch.distributed gloo as the allgather/barrier hooks.
+GPU: two ranks on one MI355X exercise comex_malloc + IPC mapping, the remote
+accumulate through the owner's progress thread, and remote put/get.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(mode, n=2, timeout=240):
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port, COMEX_AMD_JOBID=f"t{port}", COMEX_AMD_STAGING_MB="16")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "mp_worker.py"), mode], cwd=ROOT, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append((p.returncode, out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, (rc, out) in enumerate(outs):
+        assert rc == 0 and f"RANK {r} OK" in out, f"rank {r} rc={rc}\n{out[-3000:]}"
+
+
+def test_bootstrap_env_shm_two_ranks():
+    launch("boot-env")
+
+
+def test_bootstrap_torch_gloo_two_ranks():
+    launch("boot-gloo")
+
+
+def test_bootstrap_env_shm_four_ranks():
+    launch("boot-env", n=4)
+
+
+@pytest.mark.gpu
+def test_remote_acc_put_get_two_ranks_one_gpu():
+    launch("remote", n=2, timeout=300)
+
+
+@pytest.mark.gpu
+def test_remote_three_ranks_gloo_hooks():
+    launch("remote-gloo", n=3, timeout=300)
