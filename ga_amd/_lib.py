@@ -147,6 +147,28 @@ SIGNATURES = {
     "gaamd_event_sync": (ctypes.c_int, [ctypes.c_void_p]),
     "gaamd_event_elapsed_ms": (ctypes.c_float, [ctypes.c_void_p, ctypes.c_void_p]),
     "gaamd_version": (ctypes.c_char_p, []),
+    "gaamd_ga_proc_grid": (ctypes.c_int, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_int, c_int_p]),
+    # ga.h
+    "GA_Initialize": (ctypes.c_int, []),
+    "GA_Terminate": (None, []),
+    "GA_Nodeid": (ctypes.c_int, []),
+    "GA_Nnodes": (ctypes.c_int, []),
+    "GA_Sync": (None, []),
+    "GA_Error": (None, [ctypes.c_char_p, ctypes.c_int]),
+    "NGA_Create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_int_p, ctypes.c_char_p, c_int_p]),
+    "NGA_Create_irreg": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_int_p, ctypes.c_char_p, c_int_p, c_int_p]),
+    "GA_Destroy": (None, [ctypes.c_int]),
+    "GA_Zero": (None, [ctypes.c_int]),
+    "NGA_Distribution": (None, [ctypes.c_int, ctypes.c_int, c_int_p, c_int_p]),
+    "NGA_Locate_num_blocks": (ctypes.c_int, [ctypes.c_int, c_int_p, c_int_p]),
+    "NGA_Acc": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p, ctypes.c_void_p]),
+    "NGA_Put": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p]),
+    "NGA_Get": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p]),
+    "NGA_Access": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p]),
+    "NGA_Release": (None, [ctypes.c_int, c_int_p, c_int_p]),
+    "NGA_Release_update": (None, [ctypes.c_int, c_int_p, c_int_p]),
+    "GA_Get_proc_grid": (None, [ctypes.c_int, c_int_p]),
+    "GA_Print_stats": (None, []),
 }
 
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)

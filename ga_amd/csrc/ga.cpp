@@ -1,0 +1,529 @@
+// ga.cpp -- the Global Arrays caller of the accumulate path (SURVEY.md §8(a)
+// row a15) over the MI355X ARMCI/ComEx runtime.
+//
+// Reference (paths in the GA tree):
+//   NGA_Create / NGA_Create_irreg / NGA_Acc ...  global/src/capi.c:164-265, 2079-2089
+//     (C order, 0-based  ->  Fortran order, 1-based: COPYC2F/COPYINDEX_C2F capi.c:54-61)
+//   process grid            ddb, ddb_h2, ddb_ex, dd_ev, dd_su  global/src/decomp.c:125-758
+//   block map               pnga_allocate  global/src/base.c:2550-2630
+//   owner iteration         gai_iterator_*  global/src/iterator.c:188-771 (REGULAR)
+//   ngai_acc_common         global/src/onesided.c:1334-1453: per owner
+//       pbuf = buf + size*gam_ComputePatchIndex (onesided.c:330-337)
+//       count = gam_ComputeCount, count[0] *= size (base.h:341-344)
+//       stride_loc/stride_rem = gam_setstride (base.h:322-331)
+//       remote owners first, then SMP-local; ARMCI_NbAccS for all but the last
+//   statistics              GAstat.numacc, GAbytes.acctot/accloc (onesided.c:1372-1419)
+// Each rank's block is column-major with the block's extents as leading
+// dimensions (no ghosts), in one comex_malloc segment per array (HBM).
+#include "../../include/ga.h"
+#include "../../include/armci.h"
+#include "../../include/comex.h"
+#include "runtime.hpp"
+#include <stdio.h>
+#include <string.h>
+#include <algorithm>
+#include <string>
+#include <vector>
+
+namespace gaamd {
+
+struct GArray {
+    bool live = false;
+    int type = 0, ndim = 0, elemsize = 0, optype = 0;
+    std::string name;
+    long dims[GA_MAX_DIM] = {0};        // Fortran order
+    int nblock[GA_MAX_DIM] = {0};       // blocks (processes) per dimension
+    std::vector<long> map[GA_MAX_DIM];  // 1-based first index of every block
+    std::vector<void *> ptr;            // each rank's block (owner's address space)
+    int nproc_grid = 0;
+};
+
+static std::vector<GArray> g_arrays;
+static struct { long numacc = 0, numput = 0, numget = 0; double acctot = 0, accloc = 0; } g_stat;
+
+static GArray &arr(int g_a) {
+    if (g_a < 1 || g_a > (int)g_arrays.size() || !g_arrays[g_a - 1].live) fatal("invalid global array handle %d", g_a);
+    return g_arrays[g_a - 1];
+}
+
+static int type_size(int type, int *optype) {
+    switch (type) {   // onesided.c:1362-1368
+    case C_DBL: *optype = COMEX_ACC_DBL; return 8;
+    case C_FLOAT: *optype = COMEX_ACC_FLT; return 4;
+    case C_DCPL: *optype = COMEX_ACC_DCP; return 16;
+    case C_SCPL: *optype = COMEX_ACC_CPL; return 8;
+    case C_INT: *optype = COMEX_ACC_INT; return 4;
+    case C_LONG: *optype = COMEX_ACC_LNG; return 8;
+    }
+    fatal("type %d not supported", type);
+}
+
+// ---- process grid: decomp.c restated ---------------------------------------
+// dd_ev (decomp.c:711-722): load-balance ratio of a grid
+static double dd_ev(int ndims, const long *ardims, const long *pedims) {
+    double t = 1.0;
+    for (int k = 0; k < ndims; k++) {
+        const double q = (double)((ardims[k] / pedims[k]) * pedims[k]);
+        t = t * (q / (double)ardims[k]);
+    }
+    return t;
+}
+
+// dd_su (decomp.c:730-738)
+static void dd_su(int ndims, const long *ardims, const long *pedims, long *blk) {
+    for (int i = 0; i < ndims; i++) {
+        blk[i] = ardims[i] / pedims[i];
+        if (blk[i] < 1) blk[i] = 1;
+    }
+}
+
+// ddb_ex (decomp.c:213-333): exhaustive search over factorisations of npes,
+// best load balance first, then least communication volume
+static void ddb_ex(int ndims, const long *ardims, long npes, double threshold, long *blk, long *pedims) {
+    if (ndims == 1) {
+        pedims[0] = npes;
+        dd_su(1, ardims, pedims, blk);
+        return;
+    }
+    std::vector<long> tard(ndims), tdims(ndims, 0), stack(ndims, 0);
+    for (int i = 0; i < ndims; i++) if (blk[i] < 1) blk[i] = 1;
+    for (int i = 0; i < ndims; i++) tard[i] = ardims[i] / blk[i];
+    for (int i = 0; i < ndims; i++) if (tard[i] < 1) { tard[i] = 1; blk[i] = ardims[i]; }
+    double blb = -1.0;
+    long bev = 1;
+    for (int i = 0; i < ndims; i++) bev *= tard[i];
+    pedims[0] = npes;
+    for (int i = 1; i < ndims; i++) pedims[i] = 1;
+    tdims[0] = 0;
+    stack[0] = npes;
+    int pc = 0;
+    bool done = false;
+    do {
+        if (pc == ndims - 1) {
+            tdims[pc] = stack[pc];
+            const double clb = dd_ev(ndims, tard.data(), tdims.data());
+            long cev = 0;
+            for (int k = 0; k < ndims; k++) {
+                long r = 1;
+                for (int j = 0; j < ndims; j++) if (j != k) r = r * (tard[j] / tdims[j]);
+                cev = cev + r;
+            }
+            if (clb > blb || (clb == blb && cev < bev)) {
+                for (int j = 0; j < ndims; j++) pedims[j] = tdims[j];
+                blb = clb;
+                bev = cev;
+            }
+            if (blb > threshold) break;
+            tdims[pc] = 0;
+            pc -= 1;
+        } else {
+            if (tdims[pc] == stack[pc]) {
+                done = (pc == 0);
+                tdims[pc] = 0;
+                pc -= 1;
+            } else {
+                for (tdims[pc] += 1; stack[pc] % tdims[pc] != 0; tdims[pc] += 1) {}
+                pc += 1;
+                stack[pc] = npes;
+                for (int i = 0; i < pc; i++) stack[pc] /= tdims[i];
+                tdims[pc] = 0;
+            }
+        }
+    } while (!done);
+    dd_su(ndims, ardims, pedims, blk);
+}
+
+// ddb_h2 (decomp.c:611-703): deal the prime factors of npes to the axes
+static void ddb_h2(int ndims, const long *ardims, long npes, double threshold, long bias, long *blk, long *pedims) {
+    std::vector<long> tard(ndims);
+    for (int i = 0; i < ndims; i++) if (blk[i] < 1) blk[i] = 1;
+    for (int i = 0; i < ndims; i++) tard[i] = (ardims[i] + blk[i] - 1) / blk[i];
+    for (int i = 0; i < ndims; i++) if (tard[i] < 1) { tard[i] = 1; blk[i] = ardims[i]; }
+    std::vector<long> pdivs;
+    for (long i = 1; i <= npes; i++) if (npes % i == 0) pdivs.push_back(i);
+    long npdivs = (long)pdivs.size();
+    if (npdivs > 1) {   // prime divisors with repetition
+        long k = 1;
+        do {
+            long h = k + 1;
+            for (long j = h; j < npdivs; j++)
+                if (pdivs[j] % pdivs[k] == 0) pdivs[h++] = pdivs[j] / pdivs[k];
+            npdivs = h;
+            k = k + 1;
+        } while (k < npdivs);
+    }
+    long istep = 1, istart = 0;
+    if (bias > 0) { istep = -1; istart = ndims - 1; }
+    for (int j = 0; j < ndims; j++) pedims[j] = 1;
+    for (long k = npdivs - 1; k >= 1; k--) {
+        const long p0 = pdivs[k];
+        long h = istart;
+        double q = (tard[istart] < p0 * pedims[istart]) ? 1.1
+                   : (double)(tard[istart] % (p0 * pedims[istart])) / (double)tard[istart];
+        for (int j = 1; j < ndims; j++) {
+            const long ilook = (istart + istep * j) % ndims;
+            const double w = (tard[ilook] < p0 * pedims[ilook]) ? 1.1
+                             : (double)(tard[ilook] % (p0 * pedims[ilook])) / (double)tard[ilook];
+            if (w < q) { q = w; h = ilook; }
+        }
+        pedims[h] *= p0;
+        if (bias == 0) istart = (istart + 1) % ndims;
+    }
+    const double ub = dd_ev(ndims, tard.data(), pedims);
+    if (ub < threshold) ddb_ex(ndims, tard.data(), npes, threshold, blk, pedims);
+    dd_su(ndims, ardims, pedims, blk);
+    for (int i = 0; i < ndims; i++) {
+        if (pedims[i] <= 0) fatal("process dimension is zero: ddb_h2");
+        blk[i] = (tard[i] + pedims[i] - 1) / pedims[i];
+    }
+}
+
+// ddb (decomp.c:125-199): user-chunked axes first, ddb_h2 on the rest
+static void ddb(int ndims, const long *ardims, long npes, long *blk, long *pedims) {
+    const double threshold = 0.1;
+    long tp = npes, count = 0;
+    for (int i = ndims - 1; i >= 0; i--) {
+        if (blk[i] <= 0) {
+            pedims[i] = -1;
+            count += 1;
+        } else {
+            long sp = (ardims[i] + blk[i] - 1) / blk[i];
+            if (sp > tp) {
+                sp = tp;
+                tp = 1;
+                pedims[i] = sp;
+            } else {
+                long j;
+                for (j = sp; j < tp && (tp % j != 0); j++) {}
+                pedims[i] = j;
+                tp = tp / j;
+            }
+        }
+    }
+    if (count > 0) {
+        std::vector<long> tardim, tblk(count, 1), tpedim(count, 0);
+        for (int j = 0; j < ndims; j++) if (pedims[j] < 0) tardim.push_back(ardims[j]);
+        ddb_h2((int)count, tardim.data(), tp, threshold, 0, tblk.data(), tpedim.data());
+        for (int i = 0, j = 0; j < ndims; j++)
+            if (pedims[j] < 0) { blk[j] = (tardim[i] + tpedim[i] - 1) / tpedim[i]; i++; }
+        for (int i = 0, j = 0; j < ndims; j++) if (pedims[j] < 0) pedims[j] = tpedim[i++];
+    }
+}
+
+// ---- allocation --------------------------------------------------------------
+static long block_elems(const GArray &a, int proc, long *lo, long *hi) {
+    // ga_ownsM_no_handle (base.h:153-180): proc -> block coordinates, dim 0 fastest
+    long n = 1;
+    int idx = proc;
+    for (int d = 0; d < a.ndim; d++) {
+        const int loc = idx % a.nblock[d];
+        idx /= a.nblock[d];
+        lo[d] = a.map[d][loc];
+        hi[d] = (loc + 1 < a.nblock[d]) ? a.map[d][loc + 1] - 1 : a.dims[d];
+        n *= std::max(0L, hi[d] - lo[d] + 1);
+    }
+    if (proc >= a.nproc_grid) {
+        for (int d = 0; d < a.ndim; d++) { lo[d] = 0; hi[d] = -1; }
+        return 0;
+    }
+    return n;
+}
+
+static int allocate(GArray &a) {
+    Runtime &r = rt();
+    long lo[GA_MAX_DIM], hi[GA_MAX_DIM];
+    a.nproc_grid = 1;
+    for (int d = 0; d < a.ndim; d++) a.nproc_grid *= a.nblock[d];
+    if (a.nproc_grid > r.size) fatal("distribution needs %d processes, have %d", a.nproc_grid, r.size);
+    const long n = block_elems(a, r.rank, lo, hi);
+    a.ptr.assign(r.size, nullptr);
+    if (comex_malloc(a.ptr.data(), (size_t)n * a.elemsize, COMEX_GROUP_WORLD) != COMEX_SUCCESS) return 0;
+    if (n) GA_HIP(hipMemsetAsync(a.ptr[r.rank], 0, (size_t)n * a.elemsize, r.stream));
+    comex_barrier(COMEX_GROUP_WORLD);
+    a.live = true;
+    g_arrays.push_back(a);
+    return (int)g_arrays.size();
+}
+
+// ---- owner iteration + the per-owner ARMCI call (ngai_*_common) ---------------
+enum GaOp { GA_ACC, GA_PUT, GA_GET };
+
+static void patch_op(GaOp kind, int g_a, const long *lo, const long *hi, void *buf, const long *ld, void *alpha) {
+    GArray &a = arr(g_a);
+    Runtime &r = rt();
+    const int nd = a.ndim, size = a.elemsize;
+    for (int d = 0; d < nd; d++)
+        if (lo[d] < 1 || hi[d] > a.dims[d] || lo[d] > hi[d]) fatal("patch out of range in dim %d", d);
+    // blocks of every dimension that intersect [lo, hi] (pnga_locate_region)
+    int b0[GA_MAX_DIM], b1[GA_MAX_DIM];
+    for (int d = 0; d < nd; d++) {
+        const std::vector<long> &m = a.map[d];
+        b0[d] = (int)(std::upper_bound(m.begin(), m.end(), lo[d]) - m.begin()) - 1;
+        b1[d] = (int)(std::upper_bound(m.begin(), m.end(), hi[d]) - m.begin()) - 1;
+    }
+    long elems = 1;
+    for (int d = 0; d < nd; d++) elems *= hi[d] - lo[d] + 1;
+    if (kind == GA_ACC) { g_stat.numacc++; g_stat.acctot += (double)size * elems; }
+    else if (kind == GA_PUT) g_stat.numput++;
+    else g_stat.numget++;
+
+    struct Owner { int proc; long plo[GA_MAX_DIM], phi[GA_MAX_DIM], ldrem[GA_MAX_DIM], blo[GA_MAX_DIM]; };
+    std::vector<Owner> owners;
+    int bi[GA_MAX_DIM];
+    for (int d = 0; d < nd; d++) bi[d] = b0[d];
+    for (;;) {
+        Owner o;
+        int proc = 0, mul = 1;
+        for (int d = 0; d < nd; d++) { proc += bi[d] * mul; mul *= a.nblock[d]; }
+        long blo[GA_MAX_DIM], bhi[GA_MAX_DIM];
+        block_elems(a, proc, blo, bhi);
+        o.proc = proc;
+        for (int d = 0; d < nd; d++) {
+            o.plo[d] = std::max(lo[d], blo[d]);
+            o.phi[d] = std::min(hi[d], bhi[d]);
+            o.ldrem[d] = bhi[d] - blo[d] + 1;
+            o.blo[d] = blo[d];
+        }
+        owners.push_back(o);
+        int d = 0;
+        while (d < nd && ++bi[d] > b1[d]) { bi[d] = b0[d]; ++d; }
+        if (d == nd) break;
+    }
+    // remote owners first, then the local one (onesided.c:1387-1400)
+    std::stable_partition(owners.begin(), owners.end(), [&](const Owner &o) { return o.proc != r.rank; });
+    std::vector<armci_hdl_t> hdl;
+    for (size_t k = 0; k < owners.size(); ++k) {
+        Owner &o = owners[k];
+        // gam_ComputePatchIndex (onesided.c:330-337)
+        long idx = o.plo[0] - lo[0], factor = 1;
+        for (int d = 0; d < nd - 1; d++) { factor *= ld[d]; idx += factor * (o.plo[d + 1] - lo[d + 1]); }
+        char *pbuf = (char *)buf + (long)size * idx;
+        // remote address: owner's block base + offset of plo in its column-major block
+        long roff = 0, rf = 1;
+        for (int d = 0; d < nd; d++) { roff += (o.plo[d] - o.blo[d]) * rf; rf *= o.ldrem[d]; }
+        char *prem = (char *)a.ptr[o.proc] + (long)size * roff;
+        int count[GA_MAX_DIM], stride_rem[GA_MAX_DIM], stride_loc[GA_MAX_DIM];
+        for (int d = 0; d < nd; d++) count[d] = (int)(o.phi[d] - o.plo[d] + 1);   // gam_ComputeCount
+        count[0] *= size;
+        stride_rem[0] = stride_loc[0] = size;                                       // gam_setstride
+        for (int d = 0; d < nd - 1; d++) {
+            stride_rem[d] *= (int)o.ldrem[d];
+            stride_loc[d] *= (int)ld[d];
+            stride_rem[d + 1] = stride_rem[d];
+            stride_loc[d + 1] = stride_loc[d];
+        }
+        if (kind == GA_ACC && o.proc == r.rank) {
+            long e = 1;
+            for (int d = 0; d < nd; d++) e *= o.phi[d] - o.plo[d] + 1;
+            g_stat.accloc += (double)size * e;
+        }
+        const bool last = (k + 1 == owners.size());
+        armci_hdl_t h = -1;
+        if (kind == GA_ACC) {
+            if (last) ARMCI_AccS(a.optype, alpha, pbuf, stride_loc, prem, stride_rem, count, nd - 1, o.proc);
+            else ARMCI_NbAccS(a.optype, alpha, pbuf, stride_loc, prem, stride_rem, count, nd - 1, o.proc, &h);
+        } else if (kind == GA_PUT) {
+            if (last) ARMCI_PutS(pbuf, stride_loc, prem, stride_rem, count, nd - 1, o.proc);
+            else ARMCI_NbPutS(pbuf, stride_loc, prem, stride_rem, count, nd - 1, o.proc, &h);
+        } else {
+            if (last) ARMCI_GetS(prem, stride_rem, pbuf, stride_loc, count, nd - 1, o.proc);
+            else ARMCI_NbGetS(prem, stride_rem, pbuf, stride_loc, count, nd - 1, o.proc, &h);
+        }
+        if (h >= 0) hdl.push_back(h);
+    }
+    for (armci_hdl_t &h : hdl) ARMCI_Wait(&h);   // nga_wait_internal
+    if (kind == GA_GET) comex_fence_all(COMEX_GROUP_WORLD);   // data is in `buf` on return
+}
+
+// C (row-major, 0-based) -> Fortran (column-major, 1-based): capi.c:54-61
+static void c2f_index(int nd, const int *c, long *f) { for (int i = 0; i < nd; i++) f[nd - i - 1] = (long)c[i] + 1; }
+static void c2f(int nd, const int *c, long *f) { for (int i = 0; i < nd; i++) f[nd - i - 1] = c[i]; }
+
+}  // namespace gaamd
+
+using namespace gaamd;
+
+extern "C" {
+
+int GA_Initialize(void) { return ARMCI_Init(); }
+void GA_Terminate(void) {
+    for (size_t i = 0; i < g_arrays.size(); ++i)
+        if (g_arrays[i].live) GA_Destroy((int)i + 1);
+    ARMCI_Finalize();
+}
+int GA_Nodeid(void) { return rt().rank; }
+int GA_Nnodes(void) { return rt().size; }
+void GA_Sync(void) { comex_barrier(COMEX_GROUP_WORLD); }
+void GA_Error(char *msg, int code) { comex_error(msg, code); }
+
+int NGA_Create(int type, int ndim, int dims[], char *name, int chunk[]) {
+    if (ndim < 1 || ndim > GA_MAX_DIM) return 0;
+    GArray a;
+    a.type = type;
+    a.ndim = ndim;
+    a.name = name ? name : "";
+    a.elemsize = type_size(type, &a.optype);
+    long fdims[GA_MAX_DIM], fchunk[GA_MAX_DIM] = {0};
+    c2f(ndim, dims, fdims);
+    if (chunk) c2f(ndim, chunk, fchunk);
+    for (int d = 0; d < ndim; d++) {
+        if (fdims[d] < 1) fatal("NGA_Create: dimension %d is %ld", d, fdims[d]);
+        a.dims[d] = fdims[d];
+    }
+    // pnga_allocate (base.c:2550-2630)
+    long blk[GA_MAX_DIM], pe[GA_MAX_DIM];
+    if (fchunk[0] != 0)
+        for (int d = 0; d < ndim; d++) blk[d] = std::min(fchunk[d], fdims[d]);
+    else
+        for (int d = 0; d < ndim; d++) blk[d] = -1;
+    for (int d = 0; d < ndim; d++) if (fdims[d] == 1) blk[d] = 1;
+    ddb(ndim, fdims, rt().size, blk, pe);
+    for (int d = 0; d < ndim; d++) {
+        long pcut;
+        if (fchunk[d] > 1) {
+            const long ddim = (fdims[d] - 1) / std::min(fchunk[d], fdims[d]) + 1;
+            pcut = ddim - (blk[d] - 1) * pe[d];
+        } else {
+            pcut = fdims[d] - (blk[d] - 1) * pe[d];
+        }
+        long i = 0, nblock = 0;
+        for (long p = 0; p < pe[d] && i < fdims[d]; p++, nblock++) {
+            long b = blk[d];
+            if (p >= pcut) b = b - 1;
+            a.map[d].push_back(i + 1);
+            if (fchunk[d] > 1) b *= std::min(fchunk[d], fdims[d]);
+            i += b;
+        }
+        a.nblock[d] = (int)std::min(pe[d], nblock);
+        a.map[d].resize(a.nblock[d]);
+    }
+    return allocate(a);
+}
+
+int NGA_Create_irreg(int type, int ndim, int dims[], char *name, int block[], int map[]) {
+    if (ndim < 1 || ndim > GA_MAX_DIM) return 0;
+    GArray a;
+    a.type = type;
+    a.ndim = ndim;
+    a.name = name ? name : "";
+    a.elemsize = type_size(type, &a.optype);
+    long fdims[GA_MAX_DIM];
+    c2f(ndim, dims, fdims);
+    for (int d = 0; d < ndim; d++) a.dims[d] = fdims[d];
+    // copy_map (capi.c): C dimension i's block starts follow those of i-1 in `map`
+    int off[GA_MAX_DIM];
+    for (int i = 0, o = 0; i < ndim; i++) { off[i] = o; o += block[i]; }
+    for (int i = 0; i < ndim; i++) {
+        const int fd = ndim - 1 - i;
+        a.nblock[fd] = block[i];
+        for (int k = 0; k < block[i]; k++) a.map[fd].push_back((long)map[off[i] + k] + 1);
+    }
+    return allocate(a);
+}
+
+void GA_Destroy(int g_a) {
+    GArray &a = arr(g_a);
+    comex_free(a.ptr[rt().rank], COMEX_GROUP_WORLD);
+    a.live = false;
+    a.ptr.clear();
+}
+
+void GA_Zero(int g_a) {
+    GArray &a = arr(g_a);
+    Runtime &r = rt();
+    long lo[GA_MAX_DIM], hi[GA_MAX_DIM];
+    const long n = block_elems(a, r.rank, lo, hi);
+    comex_fence_all(COMEX_GROUP_WORLD);
+    if (n) GA_HIP(hipMemsetAsync(a.ptr[r.rank], 0, (size_t)n * a.elemsize, r.stream));
+    comex_barrier(COMEX_GROUP_WORLD);
+}
+
+void NGA_Distribution(int g_a, int iproc, int lo[], int hi[]) {
+    GArray &a = arr(g_a);
+    long flo[GA_MAX_DIM], fhi[GA_MAX_DIM];
+    block_elems(a, iproc, flo, fhi);
+    for (int i = 0; i < a.ndim; i++) {   // COPYINDEX_F2C
+        lo[a.ndim - i - 1] = (int)flo[i] - 1;
+        hi[a.ndim - i - 1] = (int)fhi[i] - 1;
+    }
+}
+
+int NGA_Locate_num_blocks(int g_a, int lo[], int hi[]) {
+    GArray &a = arr(g_a);
+    long flo[GA_MAX_DIM], fhi[GA_MAX_DIM];
+    c2f_index(a.ndim, lo, flo);
+    c2f_index(a.ndim, hi, fhi);
+    int n = 1;
+    for (int d = 0; d < a.ndim; d++) {
+        const std::vector<long> &m = a.map[d];
+        const int b0 = (int)(std::upper_bound(m.begin(), m.end(), flo[d]) - m.begin()) - 1;
+        const int b1 = (int)(std::upper_bound(m.begin(), m.end(), fhi[d]) - m.begin()) - 1;
+        n *= b1 - b0 + 1;
+    }
+    return n;
+}
+
+static void c_patch(GaOp kind, int g_a, int lo[], int hi[], void *buf, int ld[], void *alpha) {
+    GArray &a = arr(g_a);
+    long flo[GA_MAX_DIM], fhi[GA_MAX_DIM], fld[GA_MAX_DIM] = {0};
+    c2f_index(a.ndim, lo, flo);
+    c2f_index(a.ndim, hi, fhi);
+    if (a.ndim > 1) c2f(a.ndim - 1, ld, fld);
+    patch_op(kind, g_a, flo, fhi, buf, fld, alpha);
+}
+
+void NGA_Acc(int g_a, int lo[], int hi[], void *buf, int ld[], void *alpha) { c_patch(GA_ACC, g_a, lo, hi, buf, ld, alpha); }
+void NGA_Put(int g_a, int lo[], int hi[], void *buf, int ld[]) { c_patch(GA_PUT, g_a, lo, hi, buf, ld, nullptr); }
+void NGA_Get(int g_a, int lo[], int hi[], void *buf, int ld[]) { c_patch(GA_GET, g_a, lo, hi, buf, ld, nullptr); }
+
+void NGA_Access(int g_a, int lo[], int hi[], void *ptr, int ld[]) {
+    GArray &a = arr(g_a);
+    Runtime &r = rt();
+    long blo[GA_MAX_DIM], bhi[GA_MAX_DIM], flo[GA_MAX_DIM], fhi[GA_MAX_DIM];
+    block_elems(a, r.rank, blo, bhi);
+    c2f_index(a.ndim, lo, flo);
+    c2f_index(a.ndim, hi, fhi);
+    long off = 0, f = 1;
+    for (int d = 0; d < a.ndim; d++) {
+        if (flo[d] < blo[d] || fhi[d] > bhi[d]) fatal("NGA_Access: patch not local");
+        off += (flo[d] - blo[d]) * f;
+        f *= bhi[d] - blo[d] + 1;
+    }
+    comex_fence_all(COMEX_GROUP_WORLD);   // pending writes land before the caller reads
+    *(char **)ptr = (char *)a.ptr[r.rank] + off * a.elemsize;
+    for (int i = 0; i < a.ndim - 1; i++) ld[a.ndim - 2 - i] = (int)(bhi[i] - blo[i] + 1);
+}
+
+void NGA_Release(int g_a, int lo[], int hi[]) { (void)arr(g_a); (void)lo; (void)hi; }
+void NGA_Release_update(int g_a, int lo[], int hi[]) { (void)arr(g_a); (void)lo; (void)hi; }
+
+void GA_Get_proc_grid(int g_a, int dims[]) {
+    GArray &a = arr(g_a);
+    for (int i = 0; i < a.ndim; i++) dims[a.ndim - 1 - i] = a.nblock[i];
+}
+
+// The process grid NGA_Create picks for `npes` processes (C order), without
+// allocating anything: host-only, used by the CPU tests of the restated ddb.
+int gaamd_ga_proc_grid(int ndim, const int *dims, const int *chunk, int npes, int *grid) {
+    if (ndim < 1 || ndim > GA_MAX_DIM || npes < 1) return -1;
+    long fdims[GA_MAX_DIM], fchunk[GA_MAX_DIM] = {0}, blk[GA_MAX_DIM], pe[GA_MAX_DIM];
+    c2f(ndim, dims, fdims);
+    if (chunk) c2f(ndim, chunk, fchunk);
+    if (fchunk[0] != 0)
+        for (int d = 0; d < ndim; d++) blk[d] = std::min(fchunk[d], fdims[d]);
+    else
+        for (int d = 0; d < ndim; d++) blk[d] = -1;
+    for (int d = 0; d < ndim; d++) if (fdims[d] == 1) blk[d] = 1;
+    ddb(ndim, fdims, npes, blk, pe);
+    for (int i = 0; i < ndim; i++) grid[ndim - 1 - i] = (int)pe[i];
+    return 0;
+}
+
+void GA_Print_stats(void) {
+    printf("[%d] GA statistics: acc calls %ld, put calls %ld, get calls %ld\n", rt().rank, g_stat.numacc,
+           g_stat.numput, g_stat.numget);
+    printf("[%d] accumulate bytes total %.0f, local %.0f (%.1f%%)\n", rt().rank, g_stat.acctot, g_stat.accloc,
+           g_stat.acctot > 0 ? 100.0 * g_stat.accloc / g_stat.acctot : 0.0);
+}
+
+}  // extern "C"

@@ -59,7 +59,10 @@ def main():
         assert L.gaamd_rank() == rank and L.gaamd_size() == size
         print(f"RANK {rank} OK", flush=True)
         return
-    remote_test(L, rank, size)
+    if mode == "ga":
+        ga_test(L, rank, size)
+    else:
+        remote_test(L, rank, size)
     print(f"RANK {rank} OK", flush=True)
 
 
@@ -141,6 +144,109 @@ def remote_test(L, rank, size):
     ga_amd.comex_barrier()
     assert ga_amd.comex_free(seg[rank]) == 0
     ga_amd.comex_finalize()
+
+
+def ga_test(L, rank, size):
+    """GA caller layer (onesided.c:1334-1453) on device partitions: NGA_Acc of a
+    host patch spanning several owners, the testc.c:69-89 exact KAT, put/get,
+    a 3-D int array, NGA_Access."""
+    import ga_amd
+    ia = ga_amd.int_array
+    C_DBL, C_INT = 1004, 1001
+    assert L.GA_Initialize() == 0
+    assert L.GA_Nnodes() == size and L.GA_Nodeid() == rank
+    dims = [300, 200]                          # C order: 300 rows x 200 columns
+    g = L.NGA_Create(C_DBL, 2, ia(dims), b"a", None)
+    assert g > 0
+    # the blocks tile the array exactly
+    cover = np.zeros(dims, dtype=np.int32)
+    for p in range(size):
+        lo, hi = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
+        L.NGA_Distribution(g, p, lo, hi)
+        if hi[0] >= lo[0]:
+            cover[lo[0]:hi[0] + 1, lo[1]:hi[1] + 1] += 1
+    assert (cover == 1).all(), "distribution does not tile the array"
+
+    # every rank accumulates an integer-valued patch spanning several owners
+    lo, hi = [10 + rank, 5], [250, 190]
+    rows, cols = hi[0] - lo[0] + 1, hi[1] - lo[1] + 1
+    ldc = cols + 3
+    buf = (np.arange(rows * ldc, dtype=np.float64) % 37 - 18).reshape(rows, ldc)
+    alpha = ctypes.c_double(rank + 1)
+    L.NGA_Acc(g, ia(lo), ia(hi), buf.ctypes.data_as(ctypes.c_void_p), ia([ldc]), ctypes.byref(alpha))
+    L.GA_Sync()
+    if rank == 0:
+        got = np.zeros(dims, dtype=np.float64)
+        L.NGA_Get(g, ia([0, 0]), ia([dims[0] - 1, dims[1] - 1]), got.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]))
+        want = np.zeros(dims)
+        for r in range(size):
+            lo_r = [10 + r, 5]
+            rr = hi[0] - lo_r[0] + 1
+            b = (np.arange(rr * (cols + 3), dtype=np.float64) % 37 - 18).reshape(rr, cols + 3)
+            want[lo_r[0]:hi[0] + 1, lo_r[1]:hi[1] + 1] += (r + 1) * b[:, :cols]
+        assert np.array_equal(got, want), "NGA_Acc result differs"
+    L.GA_Sync()
+
+    # testc.c:69-89: everybody accumulates buf[i] = i into the same row, alpha 1
+    L.GA_Zero(g)
+    row = dims[0] // 2
+    b = np.arange(dims[1], dtype=np.float64)
+    one = ctypes.c_double(1.0)
+    L.NGA_Acc(g, ia([row, 0]), ia([row, dims[1] - 1]), b.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]),
+              ctypes.byref(one))
+    L.GA_Sync()
+    if rank == 0:
+        out = np.zeros(dims[1])
+        L.NGA_Get(g, ia([row, 0]), ia([row, dims[1] - 1]), out.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]))
+        assert np.array_equal(out, size * np.arange(dims[1], dtype=np.float64)), "testc.c KAT failed"
+    L.GA_Sync()
+
+    # put / get round trip of a patch owned by several ranks
+    p = (np.arange(40 * 50, dtype=np.float64) + 1e5 * (rank + 1)).reshape(40, 50)
+    plo, phi = [100 + 45 * rank, 60], [139 + 45 * rank, 109]
+    if phi[0] < dims[0]:
+        L.NGA_Put(g, ia(plo), ia(phi), p.ctypes.data_as(ctypes.c_void_p), ia([50]))
+    L.GA_Sync()
+    q = np.zeros((40, 50))
+    if phi[0] < dims[0]:
+        L.NGA_Get(g, ia(plo), ia(phi), q.ctypes.data_as(ctypes.c_void_p), ia([50]))
+        assert np.array_equal(p, q), "put/get round trip"
+
+    # local block through NGA_Access is an HBM address
+    lo_m, hi_m = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
+    L.NGA_Distribution(g, rank, lo_m, hi_m)
+    if hi_m[0] >= lo_m[0]:
+        ptr, ld = ctypes.c_void_p(), (ctypes.c_int * 1)()
+        L.NGA_Access(g, lo_m, hi_m, ctypes.byref(ptr), ld)
+        nr, nc = hi_m[0] - lo_m[0] + 1, hi_m[1] - lo_m[1] + 1
+        assert ld[0] == nc
+        mine = np.zeros(nr * nc)
+        assert L.gaamd_memcpy(mine.ctypes.data_as(ctypes.c_void_p), ptr, mine.nbytes) == 0
+        ref = np.zeros((nr, nc))
+        L.NGA_Get(g, lo_m, hi_m, ref.ctypes.data_as(ctypes.c_void_p), ia([nc]))
+        assert np.array_equal(mine.reshape(nr, nc), ref)
+        L.NGA_Release(g, lo_m, hi_m)
+    L.GA_Sync()
+    L.GA_Destroy(g)
+
+    # 3-D int array, accumulate with alpha 3 (integer arithmetic, exact)
+    d3 = [17, 23, 29]
+    g3 = L.NGA_Create(C_INT, 3, ia(d3), b"i3", None)
+    v = (np.arange(10 * 12 * 14, dtype=np.int32) % 11 - 5).reshape(10, 12, 14)
+    three = ctypes.c_int(3)
+    L.NGA_Acc(g3, ia([3, 5, 7]), ia([12, 16, 20]), v.ctypes.data_as(ctypes.c_void_p), ia([12, 14]),
+              ctypes.byref(three))
+    L.GA_Sync()
+    out3 = np.zeros(d3, dtype=np.int32)
+    L.NGA_Get(g3, ia([0, 0, 0]), ia([16, 22, 28]), out3.ctypes.data_as(ctypes.c_void_p), ia([23, 29]))
+    w3 = np.zeros(d3, dtype=np.int32)
+    w3[3:13, 5:17, 7:21] = 3 * size * v
+    assert np.array_equal(out3, w3), "3-D int NGA_Acc"
+    L.GA_Sync()
+    L.GA_Destroy(g3)
+    if rank == 0:
+        L.GA_Print_stats()
+    L.GA_Terminate()
 
 
 if __name__ == "__main__":

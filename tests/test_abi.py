@@ -12,7 +12,7 @@ import ga_amd
 from ga_amd._lib import LIB_PATH, SIGNATURES
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("comex.h", "armci.h", "ga_amd.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("comex.h", "armci.h", "ga_amd.h", "ga.h")]
 
 
 def declared_functions(path):
@@ -116,3 +116,28 @@ def test_comex_without_gpu_fails_loudly():
         pytest.skip("a GPU is visible here")
     assert r.returncode != 3 and r.returncode != 0
     assert "no HIP device" in r.stderr
+
+
+@pytest.mark.parametrize("npes,grid", [(1, [1, 1]), (2, [1, 2]), (4, [2, 2]), (8, [2, 4])])
+def test_ga_process_grid_matches_reference_survey(npes, grid):
+    """NGA_Create's REGULAR grid for 32768^2 (C order).  The survey ran the reference
+    decomp.c: Fortran-order pedims 2 -> [2,1], 4 -> [2,2], 8 -> [4,2]."""
+    L = ga_amd.lib()
+    out = (ctypes.c_int * 2)()
+    assert L.gaamd_ga_proc_grid(2, ga_amd.int_array([32768, 32768]), None, npes, out) == 0
+    assert list(out) == grid
+
+
+def test_ga_process_grid_properties():
+    """The grid always multiplies out to at most npes and covers every process
+    when the dimensions allow it (ddb_h2 deals all prime factors)."""
+    L = ga_amd.lib()
+    rng = np.random.default_rng(5)
+    for _ in range(300):
+        nd = int(rng.integers(1, 4))
+        dims = [int(rng.integers(1, 2000)) for _ in range(nd)]
+        npes = int(rng.integers(1, 65))
+        out = (ctypes.c_int * nd)()
+        assert L.gaamd_ga_proc_grid(nd, ga_amd.int_array(dims), None, npes, out) == 0
+        prod = int(np.prod(list(out)))
+        assert prod == npes, (dims, npes, list(out))

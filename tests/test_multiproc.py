@@ -66,3 +66,10 @@ def test_remote_acc_put_get_two_ranks_one_gpu():
 @pytest.mark.gpu
 def test_remote_three_ranks_gloo_hooks():
     launch("remote-gloo", n=3, timeout=300)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_ga_layer_nga_acc(n):
+    """NGA_Create/NGA_Acc/NGA_Put/NGA_Get/NGA_Access over n ranks on one GPU."""
+    launch("ga", n=n, timeout=300)
