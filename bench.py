@@ -178,6 +178,7 @@ def run_gpu(args, dist):
     L.gaamd_event_record(ev0, stream)
     for i in range(args.steps):
         step(args.warmup + i)
+    L.gaamd_join()                      # the primary stream waits for the library's other streams
     L.gaamd_event_record(ev1, stream)
     ga_amd.sync()
     t1 = time.perf_counter()

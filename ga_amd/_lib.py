@@ -139,8 +139,12 @@ SIGNATURES = {
     "gaamd_memcpy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     "gaamd_memset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]),
     "gaamd_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "gaamd_join": (ctypes.c_int, []),
+    "gaamd_num_streams": (ctypes.c_int, []),
     "gaamd_fill": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_ulonglong,
                                   ctypes.c_void_p]),
+    "gaamd_stream_create": (ctypes.c_void_p, []),
+    "gaamd_stream_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "gaamd_event_create": (ctypes.c_void_p, []),
     "gaamd_event_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "gaamd_event_record": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

@@ -220,11 +220,19 @@ static int nb_alloc() {
     return i;
 }
 
-static void nb_complete_now(comex_request_t *h) {
+// handle = an event on the stream the operation went to (0: the primary)
+static void nb_complete_now(comex_request_t *h, int stream_idx = 0) {
     Runtime &r = rt();
     const int i = nb_alloc();
-    GA_HIP(hipEventRecord(r.nb_ev[i], r.stream));
+    GA_HIP(hipEventRecord(r.nb_ev[i], r.streams.empty() ? r.stream : r.streams[stream_idx]));
     *h = i;
+}
+
+static Span span_of(const void *base, int64_t lo, int64_t hi) {
+    Span s;
+    s.lo = (int64_t)(uintptr_t)base + lo;
+    s.hi = (int64_t)(uintptr_t)base + hi;
+    return s;
 }
 
 // ---- remote accumulate: staging ring + owner inbox ------------------------
@@ -332,10 +340,13 @@ static void progress_loop() {
             else { ev = pool.back(); pool.pop_back(); }
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
+                int64_t dlo = 0, dhi = 0;
+                side_span_host(q.dst_stride, q.count, q.levels, q.count[0], &dlo, &dhi);
+                const int si = sched_pick(span_of(packed, 0, (int64_t)q.bytes), span_of((void *)q.dst_addr, dlo, dhi));
                 const int rc = launch_strided(q.op, q.scale, packed0, pstride, (void *)q.dst_addr, q.dst_stride,
-                                              q.count, q.levels, r.stream, nullptr, rb, re);
+                                              q.count, q.levels, r.streams[si], nullptr, rb, re);
                 if (rc) fatal("unpack-acc launch failed (%d)", rc);
-                GA_HIP(hipEventRecord(ev, r.stream));
+                GA_HIP(hipEventRecord(ev, r.streams[si]));
             }
             inflight.push_back({ev, src});
             q.state.store(0, std::memory_order_release);
@@ -390,14 +401,17 @@ static void remote_acc(int t, int op, const void *scale, void *src, const int *s
         const uint64_t len = (re - rb) * (uint64_t)count[0];
         const uint64_t off = stage_alloc(t, len);
         char *stage = r.staging + (size_t)t * sub + off;
+        int si = 0;
         {
             std::lock_guard<std::mutex> g(r.launch_mu);
+            if (needs_sync(sv)) sched_join();   // a staged src copy sits on stream 0
+            si = needs_sync(sv) ? 0 : sched_pick(span_of(sv.dev, slo, shi), span_of(stage, 0, (int64_t)len));
             // pack rows [rb, re) of src into the staging slice (rebased so row rb lands at `stage`)
             const int rc = launch_strided(kOpCopy, nullptr, sv.dev, ss, stage - (int64_t)rb * count[0], pstride,
-                                          count, levels, r.stream, nullptr, rb, re);
+                                          count, levels, r.streams[si], nullptr, rb, re);
             if (rc) fatal("pack launch failed (%d)", rc);
         }
-        GA_HIP(hipStreamSynchronize(r.stream));   // packed bytes complete before the owner reads them
+        GA_HIP(hipStreamSynchronize(r.streams[si]));   // packed bytes complete before the owner reads them
         const uint64_t seq = ++r.posted[t];
         g_pend[t].push_back({seq, off, len});
         r.stage_head[t] = off + len;
@@ -469,21 +483,23 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     } else {
         local_views(src, slo, shi, dst, dlo, dhi, sv, dv);
     }
+    const bool host_side = needs_sync(sv) || needs_sync(dv);
+    int si = 0;
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
-        const int rc = launch_strided(cop, scale, sv.dev, ss, dv.dev, ds, count, levels, r.stream, last_launch_info());
+        if (host_side) sched_join();   // staged copies sit on stream 0: run there, after everything
+        else si = sched_pick(span_of(sv.dev, slo, shi), span_of(dv.dev, dlo, dhi));
+        const int rc = launch_strided(cop, scale, sv.dev, ss, dv.dev, ds, count, levels, r.streams[si],
+                                      last_launch_info());
         if (rc) fatal("strided %s launch failed (code %d): misaligned elements or bad descriptor",
                       kind == X_ACC ? "acc" : (kind == X_PUT ? "put" : "get"), rc);
+        if (host_side || r.blocking_sync) sched_sync_all();
     }
-    const bool host_side = needs_sync(sv) || needs_sync(dv);
-    if (host_side || r.blocking_sync) {
-        GA_HIP(hipStreamSynchronize(r.stream));
+    if (host_side) {
         release_view(sv);
         release_view(dv);
-        if (hdl) nb_complete_now(hdl);
-        return COMEX_SUCCESS;
     }
-    if (hdl) nb_complete_now(hdl);
+    if (hdl) nb_complete_now(hdl, si);
     return COMEX_SUCCESS;
 }
 
@@ -526,6 +542,10 @@ int comex_init() {
     r.device = dv ? atoi(dv) : r.local_rank % ndev;
     GA_HIP(hipSetDevice(r.device));
     GA_HIP(hipStreamCreateWithFlags(&r.stream, hipStreamDefault));
+    {
+        const char *ns = getenv("COMEX_AMD_STREAMS");
+        sched_init(ns ? atoi(ns) : 2);
+    }
     for (int i = 0; i < kMaxNb; ++i) GA_HIP(hipEventCreateWithFlags(&r.nb_ev[i], hipEventDisableTiming));
     const char *bs = getenv("COMEX_AMD_BLOCKING_SYNC");
     r.blocking_sync = bs && atoi(bs) != 0;
@@ -591,6 +611,8 @@ int comex_finalize() {
     if (r.staging) (void)hipFree(r.staging);
     r.staging = nullptr;
     for (int i = 0; i < kMaxNb; ++i) (void)hipEventDestroy(r.nb_ev[i]);
+    sched_sync_all();
+    sched_fini();
     (void)hipStreamDestroy(r.stream);
     r.stream = nullptr;
     r.initialized = false;
@@ -636,7 +658,8 @@ int comex_group_translate_world(comex_group_t group, int group_rank, int *world_
 int comex_fence_proc(int proc, comex_group_t group) {
     ensure_init();
     fence_target(translate_world(group, proc));
-    GA_HIP(hipStreamSynchronize(rt().stream));
+    std::lock_guard<std::mutex> g(rt().launch_mu);
+    sched_sync_all();
     return COMEX_SUCCESS;
 }
 
@@ -645,7 +668,8 @@ int comex_fence_all(comex_group_t group) {
     (void)group;
     Runtime &r = rt();
     for (int t = 0; t < r.size; ++t) fence_target(t);
-    GA_HIP(hipStreamSynchronize(r.stream));
+    std::lock_guard<std::mutex> g(r.launch_mu);
+    sched_sync_all();
     return COMEX_SUCCESS;
 }
 
@@ -755,7 +779,10 @@ int comex_wait_all(comex_group_t group) {
     ensure_init();
     (void)group;
     Runtime &r = rt();
-    GA_HIP(hipStreamSynchronize(r.stream));
+    {
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        sched_sync_all();
+    }
     for (int i = 0; i < kMaxNb; ++i) r.nb_used[i] = false;
     return COMEX_SUCCESS;
 }

@@ -50,6 +50,7 @@ struct Desc {
     uint32_t chunks;             // row chunks per row (row kernel)
     FastDiv chunk_div;
     uint64_t items;              // work items in this launch
+    uint32_t align_mask;         // 2-D rows kernel: chunk alignment of dst (0 = off)
     Scale16 scale;
 };
 
@@ -62,6 +63,7 @@ struct Tuning {
     int block = 256;        // threads per block {256, 512}
     int flat_max_nvec = 127;// rows with at most this many vectors use the flat kernel
     int max_grid = 0;       // cap on blocks (0 = one block per work item)
+    int align = 0;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses
 };
 Tuning &tuning();
 

@@ -172,12 +172,12 @@ __device__ __forceinline__ void row_offsets(const Desc &d, uint32_t r, int64_t &
 // `full` (wave-uniform) says the whole chunk lies inside the row, so the
 // vectors need no predicate and their addresses fold into immediate offsets.
 template <class OP, int W, int U, int BS, bool NT>
-__device__ __forceinline__ void chunk_op(const char *sp, char *dp, uint32_t v0, uint32_t nvec, bool full,
+__device__ __forceinline__ void chunk_op(const char *sp, char *dp, int64_t v0, uint32_t nvec, bool full,
                                          const OP &op) {
     typedef typename Vec<W>::T V;
     V a[U], b[U];
-    const char *s0 = sp + (size_t)v0 * W;
-    char *d0 = dp + (size_t)v0 * W;
+    const char *s0 = sp + v0 * W;
+    char *d0 = dp + v0 * W;
     if (full) {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
@@ -188,9 +188,9 @@ __device__ __forceinline__ void chunk_op(const char *sp, char *dp, uint32_t v0, 
         for (int k = 0; k < U; ++k) vstore<W, NT>(d0 + k * BS * W, op.template apply<W>(b[k], a[k]));
         return;
     }
-    // row tail: one vector at a time (keeps the register budget of the full path)
+    // row head/tail: one vector at a time (keeps the register budget of the full path)
     for (int k = 0; k < U; ++k) {
-        if (v0 + (uint32_t)(k * BS) >= nvec) break;
+        if ((uint64_t)(v0 + k * BS) >= (uint64_t)nvec) continue;   // negative or past the row
         V x = vload<W, NT>(s0 + k * BS * W), y = x;
         if constexpr (OP::kReadsDst) y = vload<W, NT>(d0 + k * BS * W);
         vstore<W, NT>(d0 + k * BS * W, op.template apply<W>(y, x));
@@ -207,7 +207,8 @@ __global__ __launch_bounds__(BS) void k_rows(const Desc d, const OP op) {
         int64_t so, dof;
         row_offsets<LV>(d, d.row0 + rl, so, dof);
         const uint32_t c0 = chunk * (uint32_t)(BS * U);
-        chunk_op<OP, W, U, BS, NT>(d.src + so, d.dst + dof, c0 + threadIdx.x, d.nvec, c0 + BS * U <= d.nvec, op);
+        chunk_op<OP, W, U, BS, NT>(d.src + so, d.dst + dof, (int64_t)c0 + threadIdx.x, d.nvec,
+                                   c0 + BS * U <= d.nvec, op);
     }
 }
 
@@ -220,6 +221,7 @@ struct Desc2 {
     int64_t s_str, d_str;
     uint32_t row0, nvec, chunks, items;
     FastDiv chunk_div;
+    uint32_t align_mask;   // != 0: chunk boundaries at dst addresses = 0 mod (mask+1)
 };
 
 template <class OP, int W, int U, int BS, bool NT>
@@ -228,9 +230,13 @@ __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
         const uint32_t rl = d.chunk_div.div(w);
         const uint32_t chunk = w - rl * d.chunks;
         const int64_t r = (int64_t)(d.row0 + rl);
-        const uint32_t c0 = chunk * (uint32_t)(BS * U);
-        chunk_op<OP, W, U, BS, NT>(d.src + r * d.s_str, d.dst + r * d.d_str, c0 + threadIdx.x, d.nvec,
-                                   c0 + BS * U <= d.nvec, op);
+        const char *sp = d.src + r * d.s_str;
+        char *dp = d.dst + r * d.d_str;
+        // shift the chunk grid so that chunks start on aligned dst addresses
+        const int64_t shift = (int64_t)(((uintptr_t)dp & d.align_mask) / W);
+        const int64_t c0 = (int64_t)chunk * (BS * U) - shift;
+        const bool full = c0 >= 0 && c0 + BS * U <= (int64_t)d.nvec;
+        chunk_op<OP, W, U, BS, NT>(sp, dp, c0 + threadIdx.x, d.nvec, full, op);
     }
 }
 
@@ -314,6 +320,7 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
     e.chunks = d.chunks;
     e.items = (uint32_t)d.items;
     e.chunk_div = d.chunk_div;
+    e.align_mask = d.align_mask;
     if (nt) hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
     else hipLaunchKernelGGL((k_rows2<OP, W, U, BS, false>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
     return hipGetLastError();
@@ -536,7 +543,15 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         if (tn.block == 512 && U <= 2) BS = 512;
     }
     const uint32_t per_chunk = (uint32_t)BS * (uint32_t)U;
-    d.chunks = (d.nvec + per_chunk - 1) / per_chunk;
+    d.align_mask = 0;
+    if (tn.align && kind == KK_ROWS && L <= 1 && d.nvec >= 2 * per_chunk) {
+        d.align_mask = per_chunk * (uint32_t)W - 1;   // a chunk spans per_chunk*W bytes
+        // rows whose start is not chunk-aligned need one more (partial) chunk
+        bool any = ((uintptr_t)dst & d.align_mask) != 0;
+        for (int j = 0; j < L; ++j) any = any || (ds[j] & (int64_t)d.align_mask) != 0;
+        if (!any) d.align_mask = 0;
+    }
+    d.chunks = (d.nvec + per_chunk - 1 + (d.align_mask ? per_chunk - 1 : 0)) / per_chunk;
     d.chunk_div = make_fastdiv(d.chunks);
 
     const uint64_t lim = (1ull << 31) - 1;

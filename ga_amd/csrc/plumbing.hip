@@ -109,6 +109,7 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "flat_max_nvec")) return &t.flat_max_nvec;
     if (!strcmp(key, "max_grid")) return &t.max_grid;
     if (!strcmp(key, "block")) return &t.block;
+    if (!strcmp(key, "align")) return &t.align;
     return nullptr;
 }
 
@@ -160,10 +161,26 @@ int gaamd_memset(void *dst, int value, size_t bytes) {
     return hipMemset(dst, value, bytes) == hipSuccess ? 0 : -1;
 }
 int gaamd_sync(void *stream) {
+    Runtime &r = rt();
+    if (!stream && r.initialized) {   // every library stream
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        sched_sync_all();
+        return 0;
+    }
     hipStream_t s = stream_of(stream);
     hipError_t e = s ? hipStreamSynchronize(s) : hipDeviceSynchronize();
     return e == hipSuccess ? 0 : -(int)e;
 }
+
+int gaamd_join(void) {
+    Runtime &r = rt();
+    if (!r.initialized) return -1;
+    std::lock_guard<std::mutex> g(r.launch_mu);
+    sched_join();
+    return 0;
+}
+
+int gaamd_num_streams(void) { return (int)rt().streams.size(); }
 
 int gaamd_fill(void *dst, long n, int type, unsigned long long seed, void *stream) {
     if (n <= 0) return 0;
@@ -174,6 +191,13 @@ int gaamd_fill(void *dst, long n, int type, unsigned long long seed, void *strea
                        (uint64_t)seed);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+void *gaamd_stream_create(void) {
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamDefault) != hipSuccess) return nullptr;
+    return (void *)s;
+}
+int gaamd_stream_destroy(void *s) { return hipStreamDestroy((hipStream_t)s) == hipSuccess ? 0 : -1; }
 
 void *gaamd_event_create(void) {
     hipEvent_t e = nullptr;

@@ -80,6 +80,11 @@ size_t node_shm_bytes(int size);
 Inbox *inbox_of(NodeShm *s, int rank);
 char *boot_area(NodeShm *s, int size);
 
+// a device-view byte range [lo, hi) touched by one operation (lo == hi: none)
+struct Span {
+    int64_t lo = 0, hi = 0;
+};
+
 struct PeerMap {
     uintptr_t base = 0;   // segment address in the owner's address space
     size_t bytes = 0;
@@ -97,7 +102,8 @@ struct Runtime {
     bool initialized = false;
     bool boot_ready = false;
     int rank = 0, size = 1, local_rank = 0, device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;              // primary stream (= streams[0])
+    std::vector<hipStream_t> streams;          // COMEX_AMD_STREAMS streams (sched.cpp)
     bool blocking_sync = false;     // COMEX_AMD_BLOCKING_SYNC
     // bootstrap
     gaamd_allgather_fn ag = nullptr;
@@ -131,6 +137,13 @@ void boot_init();                                  // rank/size + node shm
 void boot_allgather(const void *send, void *recv, size_t bytes);
 void boot_barrier();
 void boot_finalize();
+
+// sched.cpp (callers hold launch_mu)
+void sched_init(int nstreams);
+void sched_fini();
+int sched_pick(const Span &src, const Span &dst);   // stream index for an op
+void sched_join();
+void sched_sync_all();
 
 // comex.cpp helpers shared with armci.cpp
 int translate_world(int group, int proc);

@@ -1,0 +1,109 @@
+// sched.cpp -- dependency-aware assignment of operations to HIP streams.
+//
+// The reference executes every accumulate synchronously under the target's
+// semaphore (comex/src-mpi-pr/comex.c:6228-6260), so two accumulates never
+// overlap.  On the GPU a single in-order stream gives the same exclusivity but
+// leaves each kernel's ramp-up and tail (≈1.5 µs of a 33 µs launch at the
+// headline size) with idle CUs.  Operations whose byte ranges are independent
+// (no write of one overlaps a read or write of the other) commute, so they may
+// run on different streams and overlap those edges; dependent ones are ordered
+// on one stream, with cross-stream event waits where a dependency spans two.
+//
+//   * history: the ranges (device views) of the ops enqueued since the last
+//     join, with their stream; capped at kHist entries, then a join.
+//   * join: every stream waits for every other's enqueued work (events), so
+//     history can be forgotten.
+//   * sync_all: host waits for all streams (fences, barriers, waits).
+// Callers hold Runtime::launch_mu around pick + launch.
+#include "runtime.hpp"
+#include <string.h>
+
+namespace gaamd {
+
+namespace {
+constexpr int kHist = 64;
+struct Entry {
+    int stream;
+    Span src, dst;
+};
+std::vector<Entry> g_hist;
+std::vector<hipEvent_t> g_ev;   // one reusable event per stream for cross waits
+int g_rr = 0;
+
+inline bool overlap(const Span &a, const Span &b) { return a.lo < b.hi && b.lo < a.hi && a.lo < a.hi && b.lo < b.hi; }
+}  // namespace
+
+void sched_init(int n) {
+    Runtime &r = rt();
+    if (n < 1) n = 1;
+    if (n > 8) n = 8;
+    r.streams.assign(1, r.stream);
+    for (int i = 1; i < n; ++i) {
+        hipStream_t s;
+        GA_HIP(hipStreamCreateWithFlags(&s, hipStreamDefault));
+        r.streams.push_back(s);
+    }
+    g_ev.assign(n, nullptr);
+    for (int i = 0; i < n; ++i) GA_HIP(hipEventCreateWithFlags(&g_ev[i], hipEventDisableTiming));
+    g_hist.clear();
+    g_rr = 0;
+}
+
+void sched_fini() {
+    Runtime &r = rt();
+    for (size_t i = 1; i < r.streams.size(); ++i) (void)hipStreamDestroy(r.streams[i]);
+    for (hipEvent_t e : g_ev) (void)hipEventDestroy(e);
+    g_ev.clear();
+    r.streams.clear();
+    g_hist.clear();
+}
+
+static void wait_on(int waiter, int producer) {
+    Runtime &r = rt();
+    GA_HIP(hipEventRecord(g_ev[producer], r.streams[producer]));
+    GA_HIP(hipStreamWaitEvent(r.streams[waiter], g_ev[producer], 0));
+}
+
+void sched_join() {
+    Runtime &r = rt();
+    const int n = (int)r.streams.size();
+    if (n > 1) {
+        for (int x = 1; x < n; ++x) wait_on(0, x);   // stream 0 after everything
+        for (int x = 1; x < n; ++x) wait_on(x, 0);   // everything after stream 0
+    }
+    g_hist.clear();
+}
+
+void sched_sync_all() {
+    Runtime &r = rt();
+    for (hipStream_t s : r.streams) GA_HIP(hipStreamSynchronize(s));
+    g_hist.clear();
+}
+
+int sched_pick(const Span &src, const Span &dst) {
+    Runtime &r = rt();
+    const int n = (int)r.streams.size();
+    if (n <= 1) return 0;
+    if ((int)g_hist.size() >= kHist) sched_join();
+    unsigned mask = 0;
+    int last = -1;
+    for (const Entry &e : g_hist) {
+        if (overlap(dst, e.dst) || overlap(dst, e.src) || overlap(src, e.dst)) {
+            mask |= 1u << e.stream;
+            last = e.stream;
+        }
+    }
+    int s;
+    if (!mask) {
+        g_rr = (g_rr + 1) % n;
+        s = g_rr;
+    } else {
+        s = last;   // the most recent dependency's stream; wait for the others
+        for (int x = 0; x < n; ++x)
+            if (x != s && (mask & (1u << x))) wait_on(s, x);
+    }
+    g_hist.push_back({s, src, dst});
+    return s;
+}
+
+}  // namespace gaamd

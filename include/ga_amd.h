@@ -73,10 +73,16 @@ void *gaamd_host_malloc(size_t bytes);   /* pinned, device-mapped */
 int gaamd_host_free(void *p);
 int gaamd_memcpy(void *dst, const void *src, size_t bytes);   /* any direction, synchronous */
 int gaamd_memset(void *dst, int value, size_t bytes);
-int gaamd_sync(void *stream);
+int gaamd_sync(void *stream);          /* NULL: all library streams */
+/* order the primary stream (gaamd_stream()) after everything enqueued on the
+ * library's other streams, and them after it (COMEX_AMD_STREAMS > 1) */
+int gaamd_join(void);
+int gaamd_num_streams(void);
 /* synthetic inputs of SURVEY.md 8(d) generated on the device; type:
  * 0 f64, 1 f32, 2 i32, 3 i64 ; n elements from splitmix64(seed) */
 int gaamd_fill(void *dst, long n, int type, unsigned long long seed, void *stream);
+void *gaamd_stream_create(void);       /* an extra blocking HIP stream */
+int gaamd_stream_destroy(void *stream);
 /* HIP events on the library stream (or `stream`) */
 void *gaamd_event_create(void);
 int gaamd_event_destroy(void *ev);

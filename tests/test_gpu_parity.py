@@ -67,7 +67,8 @@ def test_golden_cases_armci_and_nb(gpu_lib, manifest, golden):
 
 
 @pytest.mark.parametrize("knob", [("kind", 1), ("kind", 2), ("kind", 3), ("unroll16", 2), ("unroll16", 4),
-                                  ("unroll16", 8), ("nontemporal", 0), ("max_grid", 7), ("block", 512)])
+                                  ("unroll16", 8), ("nontemporal", 0), ("max_grid", 7), ("block", 512),
+                                  ("align", 1)])
 def test_kernel_variants_identical(gpu_lib, manifest, golden, knob):
     """Every kernel family / tuning gives the same bits as the reference."""
     key, val = knob
@@ -251,3 +252,79 @@ def test_empty_patches_are_noops(gpu_lib):
     assert ga_amd.comex_accs(C.DBL, 2.0, b.ptr, [16], b.ptr + 32, [16], [16, 0], 1, 0) == 0
     ga_amd.comex_fence_all()
     assert np.array_equal(b.download(np.float64, 8), np.arange(8, dtype=np.float64))
+
+
+@pytest.mark.parametrize("knobs", [{}, {"align": 1}, {"align": 1, "unroll16": 2}, {"unroll16": 4},
+                                   {"align": 1, "block": 512}, {"nontemporal": 0}])
+def test_wide_rows_odd_strides_all_knobs(gpu_lib, oracle, knobs):
+    """Rows of 8-40 KiB (several chunks per row) at odd leading dimensions and
+    offsets, so chunk splitting, the aligned-chunk grid and row tails are all
+    exercised on the 2-D kernel; f64 and double complex, bit-exact vs oracle."""
+    old = {k: ga_amd.set_tuning(k, v) for k, v in knobs.items()}
+    try:
+        rng = np.random.default_rng(42)
+        for op in (C.DBL, C.DCP, C.FLT):
+            esz = C.ESZ[op]
+            for _ in range(3):
+                w = int(rng.integers(1024, 5000)) * 8 // esz
+                rows = int(rng.integers(3, 40))
+                lds, ldd = w + int(rng.integers(0, 70)), w + int(rng.integers(0, 70))
+                so, do = esz * int(rng.integers(0, 9)), esz * int(rng.integers(0, 9))
+                count = [w * esz, rows]
+                src = C.fill_bytes(op, so + lds * esz * rows, 11)
+                dst = C.fill_bytes(op, do + ldd * esz * rows, 12)
+                sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+                sb.upload(src)
+                db.upload(dst)
+                assert ga_amd.comex_accs(op, C.SCALE[op], sb.ptr + so, [lds * esz], db.ptr + do, [ldd * esz],
+                                         count, 1, 0) == 0
+                ga_amd.comex_fence_all()
+                want = dst.copy()
+                oracle.accs(op, C.SCALE[op], src, so, [lds * esz], want, do, [ldd * esz], count, 1)
+                got = db.download(np.uint8, dst.size)
+                assert np.array_equal(got, want), (op, w, rows, lds, ldd, so, do, knobs)
+    finally:
+        for k, v in old.items():
+            ga_amd.set_tuning(k, v)
+
+
+def test_stream_scheduler_random_dependencies(gpu_lib, oracle):
+    """Random chains of accumulates and puts over a few buffers, with overlapping
+    and disjoint ranges, issued back to back: independent ops may run on
+    different streams (sched.cpp), dependent ones must keep program order.  The
+    final buffers equal the oracle applying the same ops one by one (int64 data,
+    exact)."""
+    assert gpu_lib.gaamd_num_streams() >= 2
+    rng = np.random.default_rng(2024)
+    nbuf, nbytes = 4, 8 << 20
+    host = [C.fill_bytes(C.LNG, nbytes, 100 + i) for i in range(nbuf)]
+    dev = [ga_amd.DeviceBuffer(nbytes) for _ in range(nbuf)]
+    for h, d in zip(host, dev):
+        d.upload(h)
+    for it in range(160):
+        op = C.LNG if rng.random() < 0.7 else 0
+        w = int(rng.integers(1, 2048)) * 8
+        rows = int(rng.integers(1, 64))
+        ld_s = w + 8 * int(rng.integers(0, 64))
+        ld_d = w + 8 * int(rng.integers(0, 64))
+        bs, bd = int(rng.integers(0, nbuf)), int(rng.integers(0, nbuf))
+        so = 8 * int(rng.integers(0, (nbytes - ld_s * rows) // 8))
+        do = 8 * int(rng.integers(0, (nbytes - ld_d * rows) // 8))
+        if bs == bd and rng.random() < 0.5:
+            do = so   # same patch: in-place self-accumulate / copy
+            ld_d = ld_s
+        count = [w, rows]
+        if op:
+            a = int(rng.integers(-3, 4))
+            assert ga_amd.comex_accs(op, a, dev[bs].ptr + so, [ld_s], dev[bd].ptr + do, [ld_d], count, 1, 0) == 0
+            oracle.accs(op, a, host[bs], so, [ld_s], host[bd], do, [ld_d], count, 1)
+        else:
+            assert ga_amd.comex_puts(dev[bs].ptr + so, [ld_s], dev[bd].ptr + do, [ld_d], count, 1, 0) == 0
+            if bs == bd:
+                tmp = host[bs].copy()
+                oracle.puts(tmp, so, [ld_s], host[bd], do, [ld_d], count, 1)
+            else:
+                oracle.puts(host[bs], so, [ld_s], host[bd], do, [ld_d], count, 1)
+    ga_amd.comex_fence_all()
+    for i in range(nbuf):
+        assert np.array_equal(dev[i].download(np.uint8, nbytes), host[i]), f"buffer {i} diverged"

@@ -50,7 +50,9 @@ def main():
     stream = L.gaamd_stream()
     K = args.steps
     ev = [L.gaamd_event_create() for _ in range(2 * K)]
-    res = {m: [] for m in ("events", "plain", "kernel", "region")}
+    res = {m: [] for m in ("events", "plain", "kernel", "region", "two_streams", "four_streams")}
+    extra = [L.gaamd_stream_create() for _ in range(3)]
+    streams4 = [stream] + extra
     for rnd in range(args.rounds):
         for mode in res:
             for i in range(3):
@@ -66,6 +68,10 @@ def main():
                     L.gaamd_event_record(ev[2 * i], stream)
                 if mode == "kernel":
                     L.gaamd_strided(op, sp, s[0], ss, s[1], ds, cnt, levels, stream)
+                elif mode == "two_streams":
+                    L.gaamd_strided(op, sp, s[0], ss, s[1], ds, cnt, levels, streams4[i % 2])
+                elif mode == "four_streams":
+                    L.gaamd_strided(op, sp, s[0], ss, s[1], ds, cnt, levels, streams4[i % 4])
                 else:
                     L.comex_accs(op, sp, s[0], ss, s[1], ds, cnt, levels, 0, 0)
                 if mode == "events":
@@ -73,6 +79,8 @@ def main():
             if mode == "region":
                 L.gaamd_event_record(ev[1], stream)
             t_enq = time.perf_counter() - t0
+            for x in streams4:
+                ga_amd.sync(x)
             ga_amd.sync()
             t = time.perf_counter() - t0
             r = {"wall_GBps": alg * K / t / 1e9, "enqueue_us": t_enq / K * 1e6}

@@ -24,11 +24,19 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sets", type=int, default=8)
+    ap.add_argument("--ld", type=int, default=0, help="override the leading dimension (elements) of a 2-D workload")
+    ap.add_argument("--rows", type=int, default=0, help="override the row count of a 2-D workload")
     ap.add_argument("--variants", default="default;unroll16=2;unroll16=8;nontemporal=1;unroll16=8,nontemporal=1")
     args = ap.parse_args()
     L = ga_amd.lib()
     assert ga_amd.comex_init() == 0
     op, count, sstr, dstr, desc = bench.WORKLOADS[args.workload]
+    if args.ld:
+        sstr, dstr = [args.ld * 8], [args.ld * 8]
+        desc += f" [ld overridden to {args.ld}]"
+    if args.rows:
+        count = [count[0], args.rows]
+        desc += f" [rows overridden to {args.rows}]"
     levels = len(count) - 1
     sb, db = bench.span_bytes(count, sstr), bench.span_bytes(count, dstr)
     alg = 3 * bench.patch_bytes(count)
@@ -73,7 +81,8 @@ def main():
             res[v].append(alg / (ms / 1e3) / 1e9)
             wall[v].append(alg * args.steps / t_all / 1e9)
             enq[v].append(t_enq / args.steps * 1e6)
-    out = {"workload": args.workload, "desc": desc, "alg_bytes": alg,
+    out = {"workload": args.workload + (f"@ld{args.ld}" if args.ld else "") + (f"@rows{args.rows}" if args.rows else ""),
+           "desc": desc, "alg_bytes": alg,
            "GBps": {v: {"median": round(float(np.median(x)), 1), "min": round(float(np.min(x)), 1),
                         "max": round(float(np.max(x)), 1), "wall_median": round(float(np.median(wall[v])), 1),
                         "enqueue_us": round(float(np.median(enq[v])), 2)} for v, x in res.items()}}
