@@ -64,6 +64,7 @@ struct Tuning {
     int flat_max_nvec = 127;// rows with at most this many vectors use the flat kernel
     int max_grid = 0;       // cap on blocks (0 = one block per work item)
     int align = 0;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses
+    int cpol = 0;           // f64 2-D kernel via buffer ops: load | store<<8 cache bits (0 = off)
 };
 Tuning &tuning();
 

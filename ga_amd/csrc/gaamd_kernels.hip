@@ -30,6 +30,7 @@
 #include "gaamd_kernels.h"
 #include <string.h>
 #include <algorithm>
+#include <type_traits>
 
 namespace gaamd {
 
@@ -240,6 +241,36 @@ __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
     }
 }
 
+// ROWS2 via buffer loads/stores: a per-row SRD whose num_records is the row
+// length, so lanes past the row (or before an aligned chunk start) read zeros
+// and their stores are dropped by the hardware range check -- no predicate.
+// LA/SA are the cache-policy bits of the loads/stores (sc0 = 1, nt = 2,
+// sc1 = 16): a tuning experiment on the headline kernel.
+template <class OP, int U, int BS, int LA, int SA>
+__global__ __launch_bounds__(BS) void k_rows2_buf(const Desc2 d, const OP op) {
+    typedef typename Vec<16>::T V;
+    const uint32_t row_bytes = d.nvec * 16u;
+    for (uint32_t w = blockIdx.x; w < d.items; w += gridDim.x) {
+        const uint32_t rl = d.chunk_div.div(w);
+        const uint32_t chunk = w - rl * d.chunks;
+        const int64_t r = (int64_t)(d.row0 + rl);
+        const char *sp = d.src + r * d.s_str;
+        char *dp = d.dst + r * d.d_str;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)sp, 0, row_bytes, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)dp, 0, row_bytes, 0x00020000);
+        const uint32_t off0 = (chunk * (uint32_t)(BS * U) + threadIdx.x) * 16u;
+        V a[U], b[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            a[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off0 + k * BS * 16, 0, LA);
+            b[k] = __builtin_amdgcn_raw_buffer_load_b128(rd, off0 + k * BS * 16, 0, LA);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(op.template apply<16>(b[k], a[k]), rd, off0 + k * BS * 16, 0, SA);
+    }
+}
+
 // FLAT kernel: vectors of all rows flattened, each lane decodes its own row.
 template <class OP, int W, int U, int BS, int LV>
 __global__ __launch_bounds__(BS) void k_flat(const Desc d, const OP op) {
@@ -321,6 +352,18 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
     e.items = (uint32_t)d.items;
     e.chunk_div = d.chunk_div;
     e.align_mask = d.align_mask;
+    if constexpr (W == 16 && U == 1 && BS == 256 && std::is_same<OP, AccDbl>::value) {
+        const int cp = g_tuning.cpol;
+        if (cp && !d.align_mask) {
+#define GAAMD_CPOL(LA, SA) \
+    if (cp == ((LA) | ((SA) << 8))) { \
+        hipLaunchKernelGGL((k_rows2_buf<OP, U, BS, LA, SA>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op); \
+        return hipGetLastError(); }
+            GAAMD_CPOL(2, 2) GAAMD_CPOL(0, 2) GAAMD_CPOL(2, 0) GAAMD_CPOL(0, 0)
+            GAAMD_CPOL(16, 2) GAAMD_CPOL(2, 16) GAAMD_CPOL(18, 18) GAAMD_CPOL(3, 3) GAAMD_CPOL(1, 2)
+#undef GAAMD_CPOL
+        }
+    }
     if (nt) hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
     else hipLaunchKernelGGL((k_rows2<OP, W, U, BS, false>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
     return hipGetLastError();

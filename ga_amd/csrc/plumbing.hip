@@ -110,10 +110,19 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "max_grid")) return &t.max_grid;
     if (!strcmp(key, "block")) return &t.block;
     if (!strcmp(key, "align")) return &t.align;
+    if (!strcmp(key, "cpol")) return &t.cpol;
     return nullptr;
 }
 
 int gaamd_set_tuning(const char *key, int value) {
+    if (!strcmp(key, "streams")) {   // library streams used by the scheduler (sched.cpp)
+        Runtime &r = rt();
+        if (!r.initialized || value < 1 || value > 8) return -1;
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        const int old = (int)r.streams.size();
+        sched_resize(value);
+        return old;
+    }
     int *f = tuning_field(key);
     if (!f) return -1;
     if (!strcmp(key, "unroll16") && value != 1 && value != 2 && value != 4 && value != 8) return -1;
@@ -124,6 +133,7 @@ int gaamd_set_tuning(const char *key, int value) {
 }
 
 int gaamd_get_tuning(const char *key) {
+    if (!strcmp(key, "streams")) return (int)rt().streams.size();
     int *f = tuning_field(key);
     return f ? *f : -1;
 }

@@ -141,6 +141,7 @@ void boot_finalize();
 // sched.cpp (callers hold launch_mu)
 void sched_init(int nstreams);
 void sched_fini();
+void sched_resize(int nstreams);
 int sched_pick(const Span &src, const Span &dst);   // stream index for an op
 void sched_join();
 void sched_sync_all();

@@ -49,6 +49,15 @@ void sched_init(int n) {
     g_rr = 0;
 }
 
+// change the number of library streams at run time (all work drained first)
+void sched_resize(int n) {
+    sched_sync_all();
+    sched_fini();
+    Runtime &r = rt();
+    r.streams.clear();
+    sched_init(n);
+}
+
 void sched_fini() {
     Runtime &r = rt();
     for (size_t i = 1; i < r.streams.size(); ++i) (void)hipStreamDestroy(r.streams[i]);

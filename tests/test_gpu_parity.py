@@ -68,7 +68,7 @@ def test_golden_cases_armci_and_nb(gpu_lib, manifest, golden):
 
 @pytest.mark.parametrize("knob", [("kind", 1), ("kind", 2), ("kind", 3), ("unroll16", 2), ("unroll16", 4),
                                   ("unroll16", 8), ("nontemporal", 0), ("max_grid", 7), ("block", 512),
-                                  ("align", 1)])
+                                  ("align", 1), ("cpol", 2 | 2 << 8), ("cpol", 16 | 2 << 8)])
 def test_kernel_variants_identical(gpu_lib, manifest, golden, knob):
     """Every kernel family / tuning gives the same bits as the reference."""
     key, val = knob
@@ -255,7 +255,8 @@ def test_empty_patches_are_noops(gpu_lib):
 
 
 @pytest.mark.parametrize("knobs", [{}, {"align": 1}, {"align": 1, "unroll16": 2}, {"unroll16": 4},
-                                   {"align": 1, "block": 512}, {"nontemporal": 0}])
+                                   {"align": 1, "block": 512}, {"nontemporal": 0}, {"cpol": 2 | 2 << 8},
+                                   {"streams": 2}])
 def test_wide_rows_odd_strides_all_knobs(gpu_lib, oracle, knobs):
     """Rows of 8-40 KiB (several chunks per row) at odd leading dimensions and
     offsets, so chunk splitting, the aligned-chunk grid and row tails are all
@@ -294,7 +295,15 @@ def test_stream_scheduler_random_dependencies(gpu_lib, oracle):
     different streams (sched.cpp), dependent ones must keep program order.  The
     final buffers equal the oracle applying the same ops one by one (int64 data,
     exact)."""
-    assert gpu_lib.gaamd_num_streams() >= 2
+    old_streams = ga_amd.set_tuning("streams", 3)
+    assert gpu_lib.gaamd_num_streams() == 3
+    try:
+        _random_dependency_chain(oracle)
+    finally:
+        ga_amd.set_tuning("streams", old_streams)
+
+
+def _random_dependency_chain(oracle):
     rng = np.random.default_rng(2024)
     nbuf, nbytes = 4, 8 << 20
     host = [C.fill_bytes(C.LNG, nbytes, 100 + i) for i in range(nbuf)]

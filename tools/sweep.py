@@ -56,7 +56,9 @@ def main():
     wall = {v: [] for v in variants}
     enq = {v: [] for v in variants}
     ev = [L.gaamd_event_create() for _ in range(2 * args.steps)]
-    for rnd in range(args.rounds):
+    # round 0 is a discarded warm-up of every variant: the first variant of a
+    # cold process otherwise reads 5-10 % low (clock/ramp), biasing the A/B
+    for rnd in range(args.rounds + 1):
         for v in variants:
             for k, val in defaults.items():
                 ga_amd.set_tuning(k, val)
@@ -78,6 +80,8 @@ def main():
             ga_amd.sync()
             t_all = time.perf_counter() - t0
             ms = L.gaamd_event_elapsed_ms(ev[0], ev[1]) / args.steps
+            if rnd == 0:
+                continue
             res[v].append(alg / (ms / 1e3) / 1e9)
             wall[v].append(alg * args.steps / t_all / 1e9)
             enq[v].append(t_enq / args.steps * 1e6)
