@@ -159,6 +159,43 @@ def fill(ptr, n, type_code, seed, stream=None):
         raise RuntimeError("gaamd_fill failed")
 
 
+# ---- io-vector descriptors (comex.h:13-18, armci.h:17-22) ------------------
+class GIOV(ctypes.Structure):
+    _fields_ = [("src", ctypes.POINTER(ctypes.c_void_p)), ("dst", ctypes.POINTER(ctypes.c_void_p)),
+                ("count", ctypes.c_int), ("bytes", ctypes.c_int)]
+
+
+def make_giov(descs):
+    """descs: list of (src_addrs, dst_addrs, bytes) -> (array of GIOV, keep-alive list)."""
+    arr = (GIOV * len(descs))()
+    keep = []
+    for k, (src, dst, nbytes) in enumerate(descs):
+        s = (ctypes.c_void_p * max(1, len(src)))(*src)
+        d = (ctypes.c_void_p * max(1, len(dst)))(*dst)
+        keep += [s, d]
+        arr[k].src = ctypes.cast(s, ctypes.POINTER(ctypes.c_void_p))
+        arr[k].dst = ctypes.cast(d, ctypes.POINTER(ctypes.c_void_p))
+        arr[k].count = len(src)
+        arr[k].bytes = nbytes
+    return arr, keep
+
+
+def comex_accv(op, scale, descs, proc, group=COMEX_GROUP_WORLD):
+    keep_s, sp = scale_buffer(op, scale)
+    arr, keep = make_giov(descs)
+    return lib().comex_accv(op, sp, ctypes.cast(arr, ctypes.c_void_p), len(descs), proc, group)
+
+
+def comex_putv(descs, proc, group=COMEX_GROUP_WORLD):
+    arr, keep = make_giov(descs)
+    return lib().comex_putv(ctypes.cast(arr, ctypes.c_void_p), len(descs), proc, group)
+
+
+def comex_getv(descs, proc, group=COMEX_GROUP_WORLD):
+    arr, keep = make_giov(descs)
+    return lib().comex_getv(ctypes.cast(arr, ctypes.c_void_p), len(descs), proc, group)
+
+
 # ---- ComEx API (comex.h) ----------------------------------------------------
 def comex_init():
     return lib().comex_init()

@@ -308,8 +308,49 @@ static void post_request(int t, int op, const void *scale, uint64_t dst_addr, co
     q.seq = (rb << 32) | (re & 0xffffffffull);   // row range travels in seq
     memset(q.scale, 0, sizeof(q.scale));
     if (scale) memcpy(q.scale, scale, (size_t)elem_size(op));
+    q.kind = 0;
+    q.iov_serial = 0;
+    q.iov_align = 0;
+    q.dst_hi = 0;
     q.state.store(2, std::memory_order_release);
 }
+
+// io-vector request: staging holds n packed source runs, then the n owner
+// addresses (8-byte aligned)
+static void post_request_iov(int t, int op, const void *scale, int bytes, int n, uint64_t off, uint64_t len,
+                             uint64_t dlo, uint64_t dhi, uint64_t align_or, bool serial) {
+    Runtime &r = rt();
+    Inbox *ib = inbox_of(r.shm, t);
+    const uint64_t ticket = ib->tail.fetch_add(1, std::memory_order_acq_rel);
+    Request &q = ib->slot[ticket % kInboxSlots];
+    for (unsigned spins = 0; ib->head.load(std::memory_order_acquire) + kInboxSlots <= ticket; ++spins)
+        if (spins > 256) sched_yield();
+    for (unsigned spins = 0;; ++spins) {
+        uint32_t expect = 0;
+        if (q.state.compare_exchange_weak(expect, 1, std::memory_order_acq_rel)) break;
+        if (spins > 256) sched_yield();
+    }
+    q.src_rank = r.rank;
+    q.op = op;
+    q.levels = 0;
+    memset(q.count, 0, sizeof(q.count));
+    memset(q.dst_stride, 0, sizeof(q.dst_stride));
+    q.count[0] = bytes;
+    q.count[1] = n;
+    q.dst_addr = dlo;
+    q.dst_hi = dhi;
+    q.staging_off = off;
+    q.bytes = len;
+    q.seq = 0;
+    memset(q.scale, 0, sizeof(q.scale));
+    if (scale) memcpy(q.scale, scale, (size_t)elem_size(op));
+    q.kind = 1;
+    q.iov_serial = serial ? 1 : 0;
+    q.iov_align = align_or;
+    q.state.store(2, std::memory_order_release);
+}
+
+static uint64_t iov_list_off(int n, int bytes) { return (((uint64_t)n * (uint64_t)bytes) + 15) & ~15ull; }
 
 // owner side: drain the inbox in ticket order
 static void progress_loop() {
@@ -324,7 +365,34 @@ static void progress_loop() {
         bool worked = false;
         const uint64_t h = ib->head.load(std::memory_order_relaxed);
         Request &q = ib->slot[h % kInboxSlots];
-        if (q.state.load(std::memory_order_acquire) == 2) {
+        if (q.state.load(std::memory_order_acquire) == 2 && q.kind == 1) {
+            // io-vector accumulate (the _acc_iov_handler analogue, comex.c:4284-4397)
+            const int src = q.src_rank;
+            const char *packed = r.peer_staging[src] + q.staging_off;
+            IovDesc d;
+            memset(&d, 0, sizeof(d));
+            d.src_base = packed;
+            d.dst_list = (const uint64_t *)(packed + iov_list_off(q.count[1], q.count[0]));
+            d.bytes = q.count[0];
+            d.n = (uint32_t)q.count[1];
+            hipEvent_t ev;
+            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            else { ev = pool.back(); pool.pop_back(); }
+            {
+                std::lock_guard<std::mutex> g(r.launch_mu);
+                Span dsp;
+                dsp.lo = (int64_t)q.dst_addr;
+                dsp.hi = (int64_t)q.dst_hi;
+                const int si = sched_pick(span_of(packed, 0, (int64_t)q.bytes), dsp);
+                const int rc = launch_iov(q.op, q.scale, d, q.iov_align, q.iov_serial != 0, r.streams[si]);
+                if (rc) fatal("io-vector accumulate launch failed (%d)", rc);
+                GA_HIP(hipEventRecord(ev, r.streams[si]));
+            }
+            inflight.push_back({ev, src});
+            q.state.store(0, std::memory_order_release);
+            ib->head.store(h + 1, std::memory_order_release);
+            worked = true;
+        } else if (q.state.load(std::memory_order_acquire) == 2) {
             const int src = q.src_rank;
             const char *packed = r.peer_staging[src] + q.staging_off;
             const uint64_t rb = q.seq >> 32, re = q.seq & 0xffffffffull;
@@ -510,13 +578,175 @@ static int xfer_contig(Xfer kind, int op, void *scale, void *src, void *dst, int
     return xfer(kind, op, scale, src, nullptr, dst, nullptr, count, 0, proc, group, hdl);
 }
 
+// ---- vector (io-vector) transfers: comex_accv/putv/getv --------------------
+// Reference: comex.c:7327-7400 (nb_accv: per-pair nb_acc, or the iov message to
+// the progress rank), _acc_iov_handler 4284-4397.  Here one kernel applies all
+// n pairs of a descriptor (k_iov); pairs whose destinations overlap (GA
+// scatter-acc duplicates) run one by one in order.
+static char *g_iov_scratch = nullptr;
+static size_t g_iov_scratch_bytes = 0;
+
+static char *iov_scratch(size_t bytes) {   // caller holds launch_mu
+    if (bytes <= g_iov_scratch_bytes) return g_iov_scratch;
+    sched_sync_all();
+    if (g_iov_scratch) GA_HIP(hipFree(g_iov_scratch));
+    g_iov_scratch_bytes = std::max<size_t>(bytes, 1 << 20);
+    GA_HIP(hipMalloc((void **)&g_iov_scratch, g_iov_scratch_bytes));
+    return g_iov_scratch;
+}
+
+static bool ranges_overlap(std::vector<std::pair<uint64_t, uint64_t>> v) {
+    std::sort(v.begin(), v.end());
+    for (size_t i = 1; i < v.size(); ++i)
+        if (v[i].first < v[i - 1].second) return true;
+    return false;
+}
+
+static bool any_cross_overlap(std::vector<std::pair<uint64_t, uint64_t>> a, std::vector<std::pair<uint64_t, uint64_t>> b) {
+    std::sort(a.begin(), a.end());
+    std::sort(b.begin(), b.end());
+    size_t i = 0, j = 0;
+    while (i < a.size() && j < b.size()) {
+        if (a[i].first < b[j].second && b[j].first < a[i].second) return true;
+        if (a[i].second <= b[j].second) ++i; else ++j;
+    }
+    return false;
+}
+
+// one descriptor whose every address is device-accessible in this process
+static void iov_local(int cop, const void *scale, const std::vector<uint64_t> &src, const std::vector<uint64_t> &dst,
+                      int bytes) {
+    Runtime &r = rt();
+    const int n = (int)src.size();
+    std::vector<std::pair<uint64_t, uint64_t>> sr(n), dr(n);
+    uint64_t align_or = 0, slo = ~0ull, shi = 0, dlo = ~0ull, dhi = 0;
+    for (int i = 0; i < n; ++i) {
+        sr[i] = {src[i], src[i] + (uint64_t)bytes};
+        dr[i] = {dst[i], dst[i] + (uint64_t)bytes};
+        align_or |= src[i] | dst[i];
+        slo = std::min(slo, src[i]);
+        shi = std::max(shi, src[i] + (uint64_t)bytes);
+        dlo = std::min(dlo, dst[i]);
+        dhi = std::max(dhi, dst[i] + (uint64_t)bytes);
+    }
+    const bool serial = ranges_overlap(dr) || any_cross_overlap(sr, dr);
+    std::vector<uint64_t> lists(2 * (size_t)n);
+    memcpy(lists.data(), src.data(), (size_t)n * 8);
+    memcpy(lists.data() + n, dst.data(), (size_t)n * 8);
+    std::lock_guard<std::mutex> g(r.launch_mu);
+    char *dev = iov_scratch((size_t)n * 16);
+    sched_sync_all();   // the previous io-vector kernel has finished reading the scratch lists
+    GA_HIP(hipMemcpy(dev, lists.data(), (size_t)n * 16, hipMemcpyHostToDevice));
+    IovDesc d;
+    memset(&d, 0, sizeof(d));
+    d.src_list = (const uint64_t *)dev;
+    d.dst_list = (const uint64_t *)dev + n;
+    d.bytes = bytes;
+    d.n = (uint32_t)n;
+    Span ss, ds;
+    ss.lo = (int64_t)slo; ss.hi = (int64_t)shi;
+    ds.lo = (int64_t)dlo; ds.hi = (int64_t)dhi;
+    const int si = sched_pick(ss, ds);
+    const int rc = launch_iov(cop, scale, d, align_or, serial, r.streams[si]);
+    if (rc) fatal("io-vector launch failed (%d): misaligned elements?", rc);
+    if (r.blocking_sync) sched_sync_all();
+}
+
 static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int proc, int group,
                     comex_request_t *hdl) {
-    // comex.c:7327-7400 (accv) / putv / getv: every (src[i], dst[i]) pair is one
-    // contiguous transfer of darr[k].bytes
-    for (int k = 0; k < len; ++k)
-        for (int i = 0; i < darr[k].count; ++i)
-            xfer_contig(kind, op, scale, darr[k].src[i], darr[k].dst[i], darr[k].bytes, proc, group, nullptr);
+    ensure_init();
+    Runtime &r = rt();
+    const int world = translate_world(group, proc);
+    const int cop = (kind == X_ACC) ? op : kOpCopy;
+    if (kind == X_ACC && (!elem_size(op) || op == kOpCopy || !scale)) fatal("bad accumulate op/scale");
+    for (int k = 0; k < len; ++k) {
+        const int n = darr[k].count, bytes = darr[k].bytes;
+        if (n <= 0) continue;
+        if (bytes <= 0) fatal("io-vector of %d bytes", bytes);
+        const bool remote_side_is_dst = (kind != X_GET);
+        std::vector<uint64_t> sv((size_t)n), dv((size_t)n);
+        bool host_bounce = false;
+        for (int i = 0; i < n; ++i) {
+            void *sp = darr[k].src[i], *dp = darr[k].dst[i];
+            char *d = nullptr;
+            if (world != r.rank && !remote_side_is_dst) {
+                sv[i] = (uint64_t)(uintptr_t)remote_view(world, sp, 0, bytes);
+            } else if (direct_view(sp, &d)) {
+                sv[i] = (uint64_t)(uintptr_t)d;
+            } else {
+                host_bounce = true;
+                break;
+            }
+            if (world != r.rank && remote_side_is_dst) {
+                if (kind == X_ACC) dv[i] = (uint64_t)(uintptr_t)dp;   // owner's address, checked below
+                else dv[i] = (uint64_t)(uintptr_t)remote_view(world, dp, 0, bytes);
+            } else if (direct_view(dp, &d)) {
+                dv[i] = (uint64_t)(uintptr_t)d;
+            } else {
+                host_bounce = true;
+                break;
+            }
+        }
+        if (host_bounce) {
+            // pageable host pairs: per-pair transfers (each maps its pages)
+            for (int i = 0; i < n; ++i)
+                xfer_contig(kind, op, scale, darr[k].src[i], darr[k].dst[i], bytes, proc, group, nullptr);
+            continue;
+        }
+        if (world == r.rank || kind != X_ACC) {
+            if (world != r.rank) fence_target(world);
+            iov_local(cop, scale, sv, dv, bytes);
+            continue;
+        }
+        // remote io-vector accumulate: pack the sources + the owner addresses into
+        // staging, the owner's progress thread applies them (k_iov)
+        const uint64_t sub = sub_ring_bytes();
+        const uint64_t per_pair = (uint64_t)bytes + 8;
+        const int pairs_per_req = (int)std::max<uint64_t>(1, (sub - 32) / per_pair);
+        for (int i0 = 0; i0 < n; i0 += pairs_per_req) {
+            const int m = std::min(pairs_per_req, n - i0);
+            std::vector<std::pair<uint64_t, uint64_t>> dr((size_t)m);
+            uint64_t align_or = 0, dlo = ~0ull, dhi = 0;
+            for (int i = 0; i < m; ++i) {
+                const uint64_t a = dv[(size_t)i0 + i];
+                (void)remote_view(world, (void *)(uintptr_t)a, 0, bytes);   // reg_cache_find
+                dr[i] = {a, a + (uint64_t)bytes};
+                align_or |= a;
+                dlo = std::min(dlo, a);
+                dhi = std::max(dhi, a + (uint64_t)bytes);
+            }
+            const bool serial = ranges_overlap(dr);
+            const uint64_t loff = iov_list_off(m, bytes);
+            const uint64_t len_b = loff + (uint64_t)m * 8;
+            const uint64_t off = stage_alloc(world, len_b);
+            char *stage = r.staging + (size_t)world * sub + off;
+            {
+                std::lock_guard<std::mutex> g(r.launch_mu);
+                char *dev = iov_scratch((size_t)m * 8);
+                sched_sync_all();
+                GA_HIP(hipMemcpy(dev, sv.data() + i0, (size_t)m * 8, hipMemcpyHostToDevice));
+                uint64_t salign = 0;
+                for (int i = 0; i < m; ++i) salign |= sv[(size_t)i0 + i];
+                IovDesc d;
+                memset(&d, 0, sizeof(d));
+                d.src_list = (const uint64_t *)dev;
+                d.dst_base = stage;
+                d.bytes = bytes;
+                d.n = (uint32_t)m;
+                sched_join();
+                const int rc = launch_iov(kOpCopy, nullptr, d, salign, false, r.streams[0]);
+                if (rc) fatal("io-vector pack failed (%d)", rc);
+                GA_HIP(hipMemcpyAsync(stage + loff, dv.data() + i0, (size_t)m * 8, hipMemcpyHostToDevice,
+                                      r.streams[0]));
+                GA_HIP(hipStreamSynchronize(r.streams[0]));
+            }
+            const uint64_t seq = ++r.posted[world];
+            g_pend[world].push_back({seq, off, len_b});
+            r.stage_head[world] = off + len_b;
+            post_request_iov(world, op, scale, bytes, m, (uint64_t)world * sub + off, len_b, dlo, dhi, align_or,
+                             serial);
+        }
+    }
     if (hdl) nb_complete_now(hdl);
     return COMEX_SUCCESS;
 }
@@ -613,6 +843,9 @@ int comex_finalize() {
     for (int i = 0; i < kMaxNb; ++i) (void)hipEventDestroy(r.nb_ev[i]);
     sched_sync_all();
     sched_fini();
+    if (g_iov_scratch) (void)hipFree(g_iov_scratch);
+    g_iov_scratch = nullptr;
+    g_iov_scratch_bytes = 0;
     (void)hipStreamDestroy(r.stream);
     r.stream = nullptr;
     r.initialized = false;

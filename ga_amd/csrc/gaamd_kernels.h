@@ -88,7 +88,23 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
 void side_span_host(const int *stride, const int *count, int stride_levels, int64_t row_bytes,
                     int64_t *lo, int64_t *hi);
 
-int elem_size(int op);
-LaunchInfo *last_launch_info();   // most recent launch_strided (any caller)   // bytes per element for op; 1 for copy; 0 if unknown
+int elem_size(int op);            // bytes per element for op; 1 for copy; 0 if unknown
+LaunchInfo *last_launch_info();   // most recent launch_strided (any caller)
+
+// I/O-vector descriptor: n pairs of `bytes`; a side is a device array of n
+// addresses (list) or, when the list is null, base + i*bytes (packed)
+struct IovDesc {
+    const uint64_t *src_list;
+    const uint64_t *dst_list;
+    const char *src_base;
+    char *dst_base;
+    int32_t bytes;
+    uint32_t n;
+    uint32_t nvec, items;   // filled by launch_iov
+    FastDiv nvec_div;
+};
+// `align_or` = OR of every listed address (the launcher cannot read device lists);
+// `serial` applies the pairs one by one in order (overlapping destinations)
+int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool serial, hipStream_t stream);
 
 }  // namespace gaamd

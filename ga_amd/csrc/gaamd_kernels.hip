@@ -638,4 +638,113 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// I/O-vector kernels: n (src[i], dst[i]) pairs of `bytes` each -- comex_accv /
+// putv / getv (comex/src-mpi-pr/comex.c:7327-7400; the server side
+// _acc_iov_handler 4284-4397).  A side is either a device array of n 64-bit
+// addresses or one packed buffer (address = base + i*bytes).  Vectors of all
+// pairs are flattened so short pairs (GA scatter-acc: one element each) still
+// fill every lane.
+template <class OP, int W, int U>
+__global__ __launch_bounds__(256) void k_iov(const IovDesc d, const OP op) {
+    typedef typename Vec<W>::T V;
+    const uint32_t span = 256u * U;
+    for (uint32_t base = blockIdx.x * span; base < d.items; base += gridDim.x * span) {
+        V a[U], b[U];
+        char *dps[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint32_t g = base + threadIdx.x + (uint32_t)(k * 256);
+            dps[k] = nullptr;
+            if (g < d.items) {
+                const uint32_t i = d.nvec_div.div(g);
+                const uint32_t v = g - i * d.nvec;
+                const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
+                char *dp = d.dst_list ? (char *)d.dst_list[i] : d.dst_base + (size_t)i * d.bytes;
+                dps[k] = dp + (size_t)v * W;
+                a[k] = vload<W, false>(sp + (size_t)v * W);
+                if constexpr (OP::kReadsDst) b[k] = vload<W, false>(dps[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (dps[k]) vstore<W, false>(dps[k], op.template apply<W>(b[k], a[k]));
+    }
+}
+
+// pairs in reference order when destinations overlap (duplicates in a scatter-acc)
+template <class OP, int W>
+__global__ __launch_bounds__(64) void k_iov_serial(const IovDesc d, const OP op) {
+    if (threadIdx.x != 0) return;
+    for (uint32_t i = 0; i < d.n; ++i) {
+        const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
+        char *dp = d.dst_list ? (char *)d.dst_list[i] : d.dst_base + (size_t)i * d.bytes;
+        for (uint32_t v = 0; v < d.nvec; ++v) {
+            typename Vec<W>::T x = vload<W, false>(sp + (size_t)v * W), y = x;
+            if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
+            vstore<W, false>(dp + (size_t)v * W, op.template apply<W>(y, x));
+        }
+    }
+}
+
+template <class OP, int W>
+static hipError_t iov_w(const IovDesc &d, const OP &op, bool serial, hipStream_t st) {
+    if constexpr (W < OP::kElem) {
+        return hipErrorInvalidValue;
+    } else {
+        if (serial) {
+            hipLaunchKernelGGL((k_iov_serial<OP, W>), dim3(1), dim3(64), 0, st, d, op);
+        } else {
+            constexpr int U = 2;
+            uint64_t blocks = ((uint64_t)d.items + 256u * U - 1) / (256u * U);
+            if (blocks > 65536) blocks = 65536;
+            hipLaunchKernelGGL((k_iov<OP, W, U>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+        }
+        return hipGetLastError();
+    }
+}
+
+template <class OP>
+static hipError_t iov_op(int W, const IovDesc &d, const OP &op, bool serial, hipStream_t st) {
+    switch (W) {
+    case 16: return iov_w<OP, 16>(d, op, serial, st);
+    case 8: return iov_w<OP, 8>(d, op, serial, st);
+    case 4: return iov_w<OP, 4>(d, op, serial, st);
+    case 2: return iov_w<OP, 2>(d, op, serial, st);
+    case 1: return iov_w<OP, 1>(d, op, serial, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool serial, hipStream_t stream) {
+    const int esz = elem_size(op);
+    if (!esz || d.bytes <= 0) return -4;
+    if (op != kOpCopy && !scale) return -5;
+    const int64_t row = (op == kOpCopy) ? d.bytes : (int64_t)(d.bytes / esz) * esz;   // acc.h:122
+    if (d.n == 0 || row == 0) return 0;
+    uint64_t a = align_or | (uint64_t)row | 16;
+    if (!d.src_list) a |= (uint64_t)(uintptr_t)d.src_base | (uint64_t)d.bytes;
+    if (!d.dst_list) a |= (uint64_t)(uintptr_t)d.dst_base | (uint64_t)d.bytes;
+    int W = (int)lowbit(a);
+    if (W > 16) W = 16;
+    if (W < esz) return -8;
+    if (serial) W = esz;
+    d.nvec = (uint32_t)(row / W);
+    d.nvec_div = make_fastdiv(d.nvec);
+    if ((uint64_t)d.n * d.nvec >= (1ull << 31)) return -7;
+    d.items = d.n * d.nvec;
+    hipError_t e;
+    switch (op) {
+    case kOpCopy: e = iov_op(W, d, CopyOp{}, serial, stream); break;
+    case 37: { AccInt o; int32_t s; memcpy(&s, scale, 4); o.s = (uint32_t)s; e = iov_op(W, d, o, serial, stream); break; }
+    case 42: { AccLng o; int64_t s; memcpy(&s, scale, 8); o.s = (uint64_t)s; e = iov_op(W, d, o, serial, stream); break; }
+    case 39: { AccFlt o; memcpy(&o.s, scale, 4); e = iov_op(W, d, o, serial, stream); break; }
+    case 38: { AccDbl o; memcpy(&o.s, scale, 8); e = iov_op(W, d, o, serial, stream); break; }
+    case 40: { AccCpl o; float s[2]; memcpy(s, scale, 8); o.sr = s[0]; o.si = s[1]; e = iov_op(W, d, o, serial, stream); break; }
+    case 41: { AccDcp o; double s[2]; memcpy(s, scale, 16); o.sr = s[0]; o.si = s[1]; e = iov_op(W, d, o, serial, stream); break; }
+    default: return -4;
+    }
+    return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
 }  // namespace gaamd

@@ -53,8 +53,12 @@ struct alignas(64) Request {
     uint64_t dst_addr;               // owner's address space
     uint64_t staging_off;            // offset into src_rank's staging buffer
     uint64_t bytes;                  // packed bytes
-    uint64_t seq;                    // per (src, dst) sequence number
+    uint64_t seq;                    // strided: row range (begin << 32 | end)
     uint8_t scale[16];
+    int32_t kind;                    // 0 strided (count/dst_stride), 1 io-vector
+    int32_t iov_serial;              // io-vector: destinations overlap -> in order
+    uint64_t iov_align;              // io-vector: OR of the destination addresses
+    uint64_t dst_hi;                 // io-vector: [dst_addr, dst_hi) covers every pair
 };
 
 struct alignas(64) Inbox {

@@ -141,6 +141,26 @@ def remote_test(L, rank, size):
     exp2[:, 3:7] += cnt_into_me * src[:3, :4]
     assert np.array_equal(got2.reshape(3, ld), exp2), f"rank {rank}: many-small mismatch"
 
+    # remote io-vector accumulate (scatter-acc with duplicates) into the next rank
+    ga_amd.comex_barrier()
+    vsrc = np.arange(64, dtype=np.float64) + 1.0 + rank
+    vb = ga_amd.DeviceBuffer(vsrc.nbytes)
+    vb.upload(vsrc)
+    idx = [(7 * i) % 20 for i in range(64)]        # duplicates: 64 pairs onto 20 slots
+    vbase = (260 * ld - 40) * 8                    # last 40 elements of my block stay free
+    descs = [([vb.ptr + 8 * i for i in range(64)], [seg[nxt] + vbase + 8 * j for j in idx], 8)]
+    assert ga_amd.comex_accv(DBL, 2.0, descs, nxt) == 0
+    ga_amd.comex_barrier()
+    tail = np.zeros(40, dtype=np.float64)
+    assert ga_amd.lib().comex_get(ctypes.c_void_p(seg[rank] + vbase), tail.ctypes.data_as(ctypes.c_void_p), 320,
+                                  rank, 0) == 0
+    ga_amd.comex_fence_all()
+    exp_t = base[-40:].copy()
+    psrc = np.arange(64, dtype=np.float64) + 1.0 + prv
+    for i, j in enumerate(idx):
+        exp_t[j] += 2.0 * psrc[i]
+    assert np.array_equal(tail, exp_t), f"rank {rank}: remote accv mismatch"
+
     ga_amd.comex_barrier()
     assert ga_amd.comex_free(seg[rank]) == 0
     ga_amd.comex_finalize()

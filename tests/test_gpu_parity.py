@@ -337,3 +337,77 @@ def _random_dependency_chain(oracle):
     ga_amd.comex_fence_all()
     for i in range(nbuf):
         assert np.array_equal(dev[i].download(np.uint8, nbytes), host[i]), f"buffer {i} diverged"
+
+
+def _oracle_acc_pairs(oracle, op, scale, host_src, host_dst, pairs, nbytes):
+    s = np.array([scale], dtype=C.REAL[op] if op not in (C.CPL, C.DCP) else
+                 (np.complex64 if op == C.CPL else np.complex128))
+    for so, do in pairs:
+        oracle.L.ora_acc(op, nbytes, ctypes.c_void_p(host_dst.ctypes.data + do),
+                         ctypes.c_void_p(host_src.ctypes.data + so), s.ctypes.data_as(ctypes.c_void_p))
+
+
+@pytest.mark.parametrize("op,nbytes,dups", [(C.DBL, 8, False), (C.DBL, 8, True), (C.DCP, 16 * 5, False),
+                                            (C.INT, 4 * 7, True), (C.FLT, 4 * 33, False), (C.LNG, 8 * 3, True)])
+def test_accv_local(gpu_lib, oracle, op, nbytes, dups):
+    """comex_accv (comex.c:7327-7400): n (src, dst) pairs in one descriptor through one
+    io-vector kernel; duplicate destinations (GA scatter-acc) must apply in order."""
+    rng = np.random.default_rng(nbytes + dups)
+    esz = C.ESZ[op]
+    nslots = 4000
+    src = C.fill_bytes(op, nslots * nbytes, 1)
+    dst = C.fill_bytes(op, nslots * nbytes, 2)
+    sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+    sb.upload(src)
+    db.upload(dst)
+    n = 1500
+    so = [int(x) * nbytes for x in rng.integers(0, nslots, n)]
+    if dups:
+        do = [int(x) * nbytes for x in rng.integers(0, 40, n)]      # many duplicates
+    else:
+        do = [int(x) * nbytes for x in rng.permutation(nslots)[:n]]
+    descs = [([sb.ptr + a for a in so[:700]], [db.ptr + b for b in do[:700]], nbytes),
+             ([sb.ptr + a for a in so[700:]], [db.ptr + b for b in do[700:]], nbytes)]
+    assert ga_amd.comex_accv(op, C.SCALE[op], descs, 0) == 0
+    ga_amd.comex_fence_all()
+    want = dst.copy()
+    _oracle_acc_pairs(oracle, op, C.SCALE[op], src, want, list(zip(so, do)), nbytes)
+    got = db.download(np.uint8, dst.size)
+    assert np.array_equal(got, want)
+
+
+def test_putv_getv_local(gpu_lib):
+    rng = np.random.default_rng(9)
+    nbytes, n = 24, 900
+    src = rng.integers(0, 256, 4000 * nbytes, dtype=np.uint8)
+    sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(src.size)
+    sb.upload(src)
+    db.upload(np.zeros_like(src))
+    perm = rng.permutation(4000)[:n]
+    descs = [([sb.ptr + i * nbytes for i in range(n)], [db.ptr + int(p) * nbytes for p in perm], nbytes)]
+    assert ga_amd.comex_putv(descs, 0) == 0
+    ga_amd.comex_fence_all()
+    got = db.download(np.uint8, src.size).reshape(4000, nbytes)
+    assert np.array_equal(got[perm], src.reshape(4000, nbytes)[:n])
+    back = ga_amd.DeviceBuffer(n * nbytes)
+    descs = [([db.ptr + int(p) * nbytes for p in perm], [back.ptr + i * nbytes for i in range(n)], nbytes)]
+    assert ga_amd.comex_getv(descs, 0) == 0
+    ga_amd.comex_fence_all()
+    assert np.array_equal(back.download(np.uint8, n * nbytes), src[: n * nbytes])
+
+
+def test_accv_host_source_pairs(gpu_lib, oracle):
+    """Pageable host sources (MA buffers) fall back to per-pair transfers; same bits."""
+    op, nbytes, n = C.DBL, 16, 50
+    src = C.fill_bytes(op, n * nbytes, 3)
+    dst = C.fill_bytes(op, n * nbytes, 4)
+    db = ga_amd.DeviceBuffer(dst.size)
+    db.upload(dst)
+    descs = [([src.ctypes.data + i * nbytes for i in range(n)], [db.ptr + (n - 1 - i) * nbytes for i in range(n)],
+              nbytes)]
+    assert ga_amd.comex_accv(op, C.SCALE[op], descs, 0) == 0
+    ga_amd.comex_fence_all()
+    want = dst.copy()
+    _oracle_acc_pairs(oracle, op, C.SCALE[op], src, want, [(i * nbytes, (n - 1 - i) * nbytes) for i in range(n)],
+                      nbytes)
+    assert np.array_equal(db.download(np.uint8, dst.size), want)
