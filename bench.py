@@ -241,9 +241,11 @@ def host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_byt
 
 
 # ---------------------------------------------------------------- CPU leg
-def run_cpu_baseline(workload, seconds):
-    """The reference's _acc per row (oracle/_ref), or the restatement if _ref is absent,
-    on one core; as many full steps as fit in ~`seconds` (at least 2)."""
+def run_cpu_baseline(workload, seconds, threads):
+    """The reference's _acc per row (oracle/_ref), or the restatement if _ref is absent.
+    SURVEY.md 8(d): P host workers, each on its own slab of the patch (oracle/mt_split.h),
+    for P = 1 and P = `threads`; each as many full steps as fit in ~seconds/2 (at least 2).
+    `value` is the P = `threads` rate; the single-core rate is reported beside it."""
     from oracle import Oracle, Ref, ref_available
     op, count, sstr, dstr, _ = WORKLOADS[workload]
     sbytes, dbytes = span_bytes(count, sstr), span_bytes(count, dstr)
@@ -257,17 +259,21 @@ def run_cpu_baseline(workload, seconds):
     else:
         impl, kind = o, "port"
     levels = len(count) - 1
-    impl.accs(op, SCALE[op], src, 0, sstr, dst, 0, dstr, count, levels)   # warm-up (page-in)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        impl.accs(op, SCALE[op], src, 0, sstr, dst, 0, dstr, count, levels)
-        n += 1
-        el = time.perf_counter() - t0
-        if (el >= seconds and n >= 2) or n >= 10000:
-            break
-    alg = 3 * patch_bytes(count) * n
-    return {"value": round(alg / el / 2 ** 30, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
-            "sample": f"{n} full {workload} steps ({el:.1f} s) on 1 host core; "
+    rates, notes = {}, []
+    for p in sorted({1, max(1, threads)}):
+        impl.accs_mt(op, SCALE[op], src, 0, sstr, dst, 0, dstr, count, levels, p)   # warm-up (page-in)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            impl.accs_mt(op, SCALE[op], src, 0, sstr, dst, 0, dstr, count, levels, p)
+            n += 1
+            el = time.perf_counter() - t0
+            if (el >= seconds / 2 and n >= 2) or n >= 10000:
+                break
+        rates[p] = round(3 * patch_bytes(count) * n / el / 2 ** 30, 3)
+        notes.append(f"P={p}: {n} full {workload} steps in {el:.1f} s")
+    P = max(rates)
+    return {"value": rates[P], "unit": "GiB/s", "cores": P, "kind": kind, "single_core_value": rates[1],
+            "sample": "; ".join(notes) + "; P host threads each on its own slab of the patch (outer level); "
                       + ("reference comex/src-common/acc.h _acc (HAVE_BLAS=0, gcc -O2) per row, "
                          "odometer of comex.c:6936-6961" if kind == "reference" else "oracle restatement")}
 
@@ -294,6 +300,7 @@ def main():
     ap.add_argument("--workload", default="H", choices=sorted(WORKLOADS))
     ap.add_argument("--sets", type=int, default=8, help="rotating buffer sets (MALL defeat)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=8, help="host workers of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--host-rates", action="store_true", help="also measure host-inclusive rates")
     ap.add_argument("--tune", action="append", help="key=value tuning knob (gaamd_set_tuning)")
@@ -310,7 +317,7 @@ def main():
     traffic = load_traffic(args.workload, alg)
     cpu = None
     if not args.no_cpu and n == 1:
-        cpu = run_cpu_baseline(args.workload, args.cpu_seconds)
+        cpu = run_cpu_baseline(args.workload, args.cpu_seconds, args.cpu_threads)
     line = {
         "metric": METRIC,
         "value": round(value, 2),

@@ -46,6 +46,7 @@ class Oracle:
             "ora_unpack": (ctypes.c_long, [_vp, _vp, _ip, _ip, ctypes.c_int]),
             "ora_unpack_acc": (ctypes.c_long, [ctypes.c_int, _vp, _vp, _vp, _ip, _ip, ctypes.c_int]),
             "ora_accs": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
+            "ora_accs_mt": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int, ctypes.c_int]),
             "ora_accs_packed": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
             "ora_puts": (ctypes.c_int, [_vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
             "ora_gets": (ctypes.c_int, [_vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
@@ -67,6 +68,12 @@ class Oracle:
         s = np.array([scale], dtype=_scale_dtype(op))
         rc = self.L.ora_accs(op, _ptr(s), _vp(src.ctypes.data + src_off), _ints(src_stride),
                              _vp(dst.ctypes.data + dst_off), _ints(dst_stride), _ints(count), levels)
+        assert rc == 0
+
+    def accs_mt(self, op, scale, src, src_off, src_stride, dst, dst_off, dst_stride, count, levels, nthreads):
+        s = np.array([scale], dtype=_scale_dtype(op))
+        rc = self.L.ora_accs_mt(op, _ptr(s), _vp(src.ctypes.data + src_off), _ints(src_stride),
+                                _vp(dst.ctypes.data + dst_off), _ints(dst_stride), _ints(count), levels, nthreads)
         assert rc == 0
 
     def accs_packed(self, op, scale, src, src_off, src_stride, dst, dst_off, dst_stride, count, levels):
@@ -117,12 +124,20 @@ class Ref:
         L.ref_acc.argtypes = [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]
         L.ref_accs.restype = ctypes.c_int
         L.ref_accs.argtypes = [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int]
+        L.ref_accs_mt.restype = ctypes.c_int
+        L.ref_accs_mt.argtypes = [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int, ctypes.c_int]
         self.L = L
 
     def accs(self, op, scale, src, src_off, src_stride, dst, dst_off, dst_stride, count, levels):
         s = np.array([scale], dtype=_scale_dtype(op))
         self.L.ref_accs(op, _ptr(s), _vp(src.ctypes.data + src_off), _ints(src_stride),
                         _vp(dst.ctypes.data + dst_off), _ints(dst_stride), _ints(count), levels)
+
+    def accs_mt(self, op, scale, src, src_off, src_stride, dst, dst_off, dst_stride, count, levels, nthreads):
+        s = np.array([scale], dtype=_scale_dtype(op))
+        rc = self.L.ref_accs_mt(op, _ptr(s), _vp(src.ctypes.data + src_off), _ints(src_stride),
+                                _vp(dst.ctypes.data + dst_off), _ints(dst_stride), _ints(count), levels, nthreads)
+        assert rc == 0
 
 
 def ref_available():

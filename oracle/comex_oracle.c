@@ -329,3 +329,14 @@ void ora_fill_i64(int64_t *p, long n, uint64_t seed)
 }
 
 uint64_t ora_splitmix64(uint64_t seed, uint64_t i) { return splitmix64_at(seed, i); }
+
+#include "mt_split.h"
+
+/* P workers on P slabs of the patch (bench.py CPU baseline) */
+int ora_accs_mt(int op, const void *scale, const char *src, const int *src_stride,
+                char *dst, const int *dst_stride, const int *count, int stride_levels,
+                int nthreads)
+{
+    return mt_accs(ora_accs, ora_elem_size(op), op, scale, src, src_stride, dst, dst_stride, count,
+                   stride_levels, nthreads);
+}

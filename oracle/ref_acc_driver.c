@@ -68,3 +68,27 @@ int ref_accs(int op, const void *scale, const char *src, const int *src_stride,
     }
     return 0;
 }
+
+#include "mt_split.h"
+
+static int ref_esize(int op)
+{
+    switch (op) {
+    case COMEX_ACC_INT: return sizeof(int);
+    case COMEX_ACC_DBL: return sizeof(double);
+    case COMEX_ACC_FLT: return sizeof(float);
+    case COMEX_ACC_CPL: return sizeof(SingleComplex);
+    case COMEX_ACC_DCP: return sizeof(DoubleComplex);
+    case COMEX_ACC_LNG: return sizeof(long);
+    }
+    return 1;
+}
+
+/* P workers on P slabs of the patch (bench.py CPU baseline) */
+int ref_accs_mt(int op, const void *scale, const char *src, const int *src_stride,
+                char *dst, const int *dst_stride, const int *count, int stride_levels,
+                int nthreads)
+{
+    return mt_accs(ref_accs, ref_esize(op), op, scale, src, src_stride, dst, dst_stride, count,
+                   stride_levels, nthreads);
+}

@@ -135,3 +135,20 @@ def test_restatement_vs_reference_random(oracle):
         oracle.accs(op, C.SCALE[op], src, 0, ss, d1, 0, ds, count, levels)
         ref.accs(op, C.SCALE[op], src, 0, ss, d2, 0, ds, count, levels)
         assert np.array_equal(d1, d2), (op, levels)
+
+
+@pytest.mark.parametrize("nthreads", [1, 3, 8])
+def test_multi_worker_baseline_matches_single(oracle, manifest, golden, nthreads):
+    """The P-worker CPU baseline (mt_split.h) splits a patch into disjoint slabs:
+    same bytes as one worker on every non-overlapping golden case."""
+    impls = [oracle] + ([Ref()] if ref_available() else [])
+    for case in manifest["cases"]:
+        n = case["name"]
+        if "overlap" in n or "zero_dst_stride" in n:   # slabs would race on shared dst bytes
+            continue
+        src = golden[f"{n}/src"]
+        for impl in impls:
+            dst = golden[f"{n}/dst_in"].copy()
+            impl.accs_mt(case["op"], C.SCALE[case["op"]], src, case["src_off"], case["src_stride"], dst,
+                         case["dst_off"], case["dst_stride"], case["count"], case["levels"], nthreads)
+            assert np.array_equal(dst, golden[f"{n}/dst_out"]), (n, type(impl).__name__)
