@@ -65,6 +65,7 @@ struct Tuning {
     int max_grid = 0;       // cap on blocks (0 = one block per work item)
     int align = 0;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses
     int cpol = 0;           // f64 2-D kernel via buffer ops: load | store<<8 cache bits (0 = off)
+    int xcd = 0;            // f64 2-D kernel: XCD-contiguous work ranges (experiment)
 };
 Tuning &tuning();
 

@@ -223,11 +223,17 @@ struct Desc2 {
     uint32_t row0, nvec, chunks, items;
     FastDiv chunk_div;
     uint32_t align_mask;   // != 0: chunk boundaries at dst addresses = 0 mod (mask+1)
+    uint32_t xcd_per;      // XCD-contiguous work (tuning experiment): items / 8, 0 = off
 };
 
-template <class OP, int W, int U, int BS, bool NT>
+// XCD: blocks are dealt round-robin to the 8 XCDs (block b -> XCD b % 8); with
+// XCD set, XCD x takes the contiguous work range [x*items/8, (x+1)*items/8)
+// instead of every 8th chunk (launched with grid == items, items % 8 == 0).
+template <class OP, int W, int U, int BS, bool NT, bool XCD = false>
 __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
-    for (uint32_t w = blockIdx.x; w < d.items; w += gridDim.x) {
+    uint32_t w0 = blockIdx.x;
+    if constexpr (XCD) w0 = (w0 & 7u) * d.xcd_per + (w0 >> 3);
+    for (uint32_t w = w0; w < d.items; w += gridDim.x) {
         const uint32_t rl = d.chunk_div.div(w);
         const uint32_t chunk = w - rl * d.chunks;
         const int64_t r = (int64_t)(d.row0 + rl);
@@ -352,7 +358,13 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
     e.items = (uint32_t)d.items;
     e.chunk_div = d.chunk_div;
     e.align_mask = d.align_mask;
+    e.xcd_per = 0;
     if constexpr (W == 16 && U == 1 && BS == 256 && std::is_same<OP, AccDbl>::value) {
+        if (g_tuning.xcd && nt && blocks == e.items && e.items % 8 == 0) {
+            e.xcd_per = e.items / 8;
+            hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
+            return hipGetLastError();
+        }
         const int cp = g_tuning.cpol;
         if (cp && !d.align_mask) {
 #define GAAMD_CPOL(LA, SA) \

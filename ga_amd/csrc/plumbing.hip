@@ -111,6 +111,7 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "block")) return &t.block;
     if (!strcmp(key, "align")) return &t.align;
     if (!strcmp(key, "cpol")) return &t.cpol;
+    if (!strcmp(key, "xcd")) return &t.xcd;
     return nullptr;
 }
 
