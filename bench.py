@@ -13,11 +13,17 @@ payload, 192 MiB of algorithmic HBM traffic (src read + dst read + dst write,
 8 x 512 MiB) so the 256 MiB Infinity Cache cannot serve the working set.
 
 value = whole-job algorithmic traffic GiB/s = ranks * steps * bytes / max-over-
-ranks wall time.  roofline.achieved = the same algorithmic bytes / the average
-kernel duration from HIP events recorded on the library's stream around every
-timed launch.  cpu_baseline = the reference's own _acc (oracle/_ref, compiled
-from comex/src-common/acc.h) driven per row on one host core over a bounded
-sample of the same workload.
+ranks wall time.  roofline.achieved = the same algorithmic bytes per launch /
+the average launch duration, from ONE HIP event pair recorded on the library's
+stream around the K timed launches (per-launch event pairs slowed the kernels
+by ~8 %; profiles/r01/gapprobe_H.json), so it includes the kernel-boundary gap;
+the rocprofv3 --kernel-trace --stats summary of the same command is committed
+under profiles/ and its average duration agrees.  roofline.traffic = HBM bytes
+per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE (tools/pmc_traffic.py,
+profiles/pmc_latest.json).  cpu_baseline = the reference's own _acc
+(oracle/_ref, compiled from comex/src-common/acc.h) driven per row by P host
+threads, each on its own slab of the same workload, over a bounded sample
+(P = 1 reported beside it).
 
 Multi-GPU: one process per GPU (torch.distributed.run); every rank accumulates
 into its own partition (GA owner-aligned patches) with no
