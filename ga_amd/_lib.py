@@ -169,6 +169,12 @@ SIGNATURES = {
     "NGA_Put": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p]),
     "NGA_Get": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p]),
     "NGA_Access": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p]),
+    "NGA_Scatter": (None, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "NGA_Scatter_flat": (None, [ctypes.c_int, ctypes.c_void_p, c_int_p, ctypes.c_int]),
+    "NGA_Scatter_acc": (None, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "NGA_Scatter_acc_flat": (None, [ctypes.c_int, ctypes.c_void_p, c_int_p, ctypes.c_int, ctypes.c_void_p]),
+    "NGA_Gather": (None, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "NGA_Gather_flat": (None, [ctypes.c_int, ctypes.c_void_p, c_int_p, ctypes.c_int]),
     "NGA_Release": (None, [ctypes.c_int, c_int_p, c_int_p]),
     "NGA_Release_update": (None, [ctypes.c_int, c_int_p, c_int_p]),
     "GA_Get_proc_grid": (None, [ctypes.c_int, c_int_p]),

@@ -39,7 +39,10 @@ struct GArray {
 };
 
 static std::vector<GArray> g_arrays;
-static struct { long numacc = 0, numput = 0, numget = 0; double acctot = 0, accloc = 0; } g_stat;
+static struct {
+    long numacc = 0, numput = 0, numget = 0, numsca = 0, numgat = 0;
+    double acctot = 0, accloc = 0, scatot = 0, scaloc = 0, gattot = 0, gatloc = 0;
+} g_stat;
 
 static GArray &arr(int g_a) {
     if (g_a < 1 || g_a > (int)g_arrays.size() || !g_arrays[g_a - 1].live) fatal("invalid global array handle %d", g_a);
@@ -335,6 +338,80 @@ static void patch_op(GaOp kind, int g_a, const long *lo, const long *hi, void *b
     if (kind == GA_GET) comex_fence_all(COMEX_GROUP_WORLD);   // data is in `buf` on return
 }
 
+// ---- gather / scatter / scatter-accumulate --------------------------------
+// gai_gatscat (onesided.c:2747-3370, the default build: USE_GATSCAT_NEW is not
+// defined): locate the owner of every subscript (pnga_locate), group the
+// elements by owner -- owners in ascending rank order, elements in input order
+// within an owner -- and issue ONE ARMCI_GetV / PutV / AccV per owner with
+// `bytes = elemsize` and the (local, remote) address pairs (gam_Loc_ptr).
+// Repeated subscripts of a scatter-accumulate are applied in that order (the
+// io-vector kernel falls back to its in-order variant when destinations repeat).
+enum GatScat { GS_GATHER, GS_SCATTER, GS_SCATTER_ACC };
+
+static int locate(const GArray &a, const long *sub, long *off) {
+    int proc = 0, mul = 1;
+    long blo[GA_MAX_DIM], bhi[GA_MAX_DIM];
+    int bi[GA_MAX_DIM];
+    for (int d = 0; d < a.ndim; d++) {
+        if (sub[d] < 1 || sub[d] > a.dims[d]) return -1;
+        const std::vector<long> &m = a.map[d];
+        bi[d] = (int)(std::upper_bound(m.begin(), m.end(), sub[d]) - m.begin()) - 1;
+        proc += bi[d] * mul;
+        mul *= a.nblock[d];
+    }
+    block_elems(a, proc, blo, bhi);
+    long o = 0, f = 1;   // gam_Loc_ptr: column-major offset inside the owner's block
+    for (int d = 0; d < a.ndim; d++) { o += (sub[d] - blo[d]) * f; f *= bhi[d] - blo[d] + 1; }
+    *off = o;
+    return proc;
+}
+
+static void gatscat(GatScat op, int g_a, void *v, const long *fsub, long nv, void *alpha) {
+    if (nv < 1) return;   // pnga_gather / pnga_scatter: nv < 1 returns
+    GArray &a = arr(g_a);
+    Runtime &r = rt();
+    const int size = a.elemsize;
+    std::vector<int> proc(nv);
+    std::vector<long> off(nv);
+    std::vector<long> nelem(r.size, 0);
+    for (long k = 0; k < nv; k++) {
+        proc[k] = locate(a, fsub + k * a.ndim, &off[k]);
+        if (proc[k] < 0) fatal("gather/scatter: invalid subscript of element %ld", k);
+        nelem[proc[k]]++;
+    }
+    std::vector<long> first(r.size, 0), fill(r.size, 0);
+    for (int p = 1; p < r.size; p++) first[p] = first[p - 1] + nelem[p - 1];
+    std::vector<void *> loc(nv), rem(nv);
+    for (long k = 0; k < nv; k++) {
+        const long j = first[proc[k]] + fill[proc[k]]++;
+        loc[j] = (char *)v + (long)size * k;
+        rem[j] = (char *)a.ptr[proc[k]] + (long)size * off[k];
+    }
+    double &tot = op == GS_GATHER ? g_stat.gattot : g_stat.scatot;
+    double &lcl = op == GS_GATHER ? g_stat.gatloc : g_stat.scaloc;
+    (op == GS_GATHER ? g_stat.numgat : g_stat.numsca)++;
+    tot += (double)size * nv;
+    lcl += (double)size * nelem[r.rank];
+    for (int p = 0; p < r.size; p++) {
+        if (!nelem[p]) continue;
+        armci_giov_t desc;
+        desc.bytes = size;
+        desc.ptr_array_len = (int)nelem[p];
+        int rc;
+        if (op == GS_GATHER) {
+            desc.src_ptr_array = &rem[first[p]];
+            desc.dst_ptr_array = &loc[first[p]];
+            rc = ARMCI_GetV(&desc, 1, p);
+        } else {
+            desc.src_ptr_array = &loc[first[p]];
+            desc.dst_ptr_array = &rem[first[p]];
+            rc = op == GS_SCATTER ? ARMCI_PutV(&desc, 1, p) : ARMCI_AccV(a.optype, alpha, &desc, 1, p);
+        }
+        if (rc) fatal("gather/scatter failed in armci (%d)", rc);
+    }
+    if (op == GS_GATHER) comex_fence_all(COMEX_GROUP_WORLD);   // data is in `v` on return
+}
+
 // C (row-major, 0-based) -> Fortran (column-major, 1-based): capi.c:54-61
 static void c2f_index(int nd, const int *c, long *f) { for (int i = 0; i < nd; i++) f[nd - i - 1] = (long)c[i] + 1; }
 static void c2f(int nd, const int *c, long *f) { for (int i = 0; i < nd; i++) f[nd - i - 1] = c[i]; }
@@ -497,6 +574,33 @@ void NGA_Access(int g_a, int lo[], int hi[], void *ptr, int ld[]) {
 void NGA_Release(int g_a, int lo[], int hi[]) { (void)arr(g_a); (void)lo; (void)hi; }
 void NGA_Release_update(int g_a, int lo[], int hi[]) { (void)arr(g_a); (void)lo; (void)hi; }
 
+// capi.c:3026-3160 (NGA_Scatter*, NGA_Gather*): C subscripts -> Fortran order, +1
+static std::vector<long> c2f_subs(int g_a, int *const *subs, const int *flat, int n) {
+    const int nd = arr(g_a).ndim;
+    std::vector<long> f((size_t)std::max(n, 0) * nd);
+    for (int k = 0; k < n; k++) c2f_index(nd, subs ? subs[k] : flat + (long)k * nd, &f[(size_t)k * nd]);
+    return f;
+}
+
+void NGA_Scatter(int g_a, void *v, int *subsArray[], int n) {
+    gatscat(GS_SCATTER, g_a, v, c2f_subs(g_a, subsArray, nullptr, n).data(), n, nullptr);
+}
+void NGA_Scatter_flat(int g_a, void *v, int subsArray[], int n) {
+    gatscat(GS_SCATTER, g_a, v, c2f_subs(g_a, nullptr, subsArray, n).data(), n, nullptr);
+}
+void NGA_Scatter_acc(int g_a, void *v, int *subsArray[], int n, void *alpha) {
+    gatscat(GS_SCATTER_ACC, g_a, v, c2f_subs(g_a, subsArray, nullptr, n).data(), n, alpha);
+}
+void NGA_Scatter_acc_flat(int g_a, void *v, int subsArray[], int n, void *alpha) {
+    gatscat(GS_SCATTER_ACC, g_a, v, c2f_subs(g_a, nullptr, subsArray, n).data(), n, alpha);
+}
+void NGA_Gather(int g_a, void *v, int *subsArray[], int n) {
+    gatscat(GS_GATHER, g_a, v, c2f_subs(g_a, subsArray, nullptr, n).data(), n, nullptr);
+}
+void NGA_Gather_flat(int g_a, void *v, int subsArray[], int n) {
+    gatscat(GS_GATHER, g_a, v, c2f_subs(g_a, nullptr, subsArray, n).data(), n, nullptr);
+}
+
 void GA_Get_proc_grid(int g_a, int dims[]) {
     GArray &a = arr(g_a);
     for (int i = 0; i < a.ndim; i++) dims[a.ndim - 1 - i] = a.nblock[i];
@@ -520,8 +624,8 @@ int gaamd_ga_proc_grid(int ndim, const int *dims, const int *chunk, int npes, in
 }
 
 void GA_Print_stats(void) {
-    printf("[%d] GA statistics: acc calls %ld, put calls %ld, get calls %ld\n", rt().rank, g_stat.numacc,
-           g_stat.numput, g_stat.numget);
+    printf("[%d] GA statistics: acc calls %ld, put calls %ld, get calls %ld, scatter calls %ld, gather calls %ld\n",
+           rt().rank, g_stat.numacc, g_stat.numput, g_stat.numget, g_stat.numsca, g_stat.numgat);
     printf("[%d] accumulate bytes total %.0f, local %.0f (%.1f%%)\n", rt().rank, g_stat.acctot, g_stat.accloc,
            g_stat.acctot > 0 ? 100.0 * g_stat.accloc / g_stat.acctot : 0.0);
 }

@@ -46,6 +46,16 @@ void NGA_Put(int g_a, int lo[], int hi[], void *buf, int ld[]);
 void NGA_Get(int g_a, int lo[], int hi[], void *buf, int ld[]);
 
 /* direct access to the local block (an HBM address) */
+/* gather / scatter / scatter-accumulate of single elements: capi.c:3026-3160 ->
+   gai_gatscat onesided.c:2747 (one ARMCI_GetV/PutV/AccV per owner).  subsArray[k]
+   points at the ndim C subscripts of element k; *_flat takes them as one array. */
+void NGA_Scatter(int g_a, void *v, int *subsArray[], int n);
+void NGA_Scatter_flat(int g_a, void *v, int subsArray[], int n);
+void NGA_Scatter_acc(int g_a, void *v, int *subsArray[], int n, void *alpha);
+void NGA_Scatter_acc_flat(int g_a, void *v, int subsArray[], int n, void *alpha);
+void NGA_Gather(int g_a, void *v, int *subsArray[], int n);
+void NGA_Gather_flat(int g_a, void *v, int subsArray[], int n);
+
 void NGA_Access(int g_a, int lo[], int hi[], void *ptr, int ld[]);
 void NGA_Release(int g_a, int lo[], int hi[]);
 void NGA_Release_update(int g_a, int lo[], int hi[]);

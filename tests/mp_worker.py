@@ -232,6 +232,70 @@ def ga_test(L, rank, size):
         L.NGA_Get(g, ia(plo), ia(phi), q.ctypes.data_as(ctypes.c_void_p), ia([50]))
         assert np.array_equal(p, q), "put/get round trip"
 
+    # gather / scatter / scatter-acc (gai_gatscat, onesided.c:2747): random
+    # subscripts over every owner, repeated ones included
+    L.GA_Zero(g)
+    rng = np.random.default_rng(50 + rank)
+    nv = 500
+    subs = np.stack([rng.integers(0, dims[0], nv), rng.integers(0, dims[1], nv)], axis=1).astype(np.int32)
+    subs[nv // 2:nv // 2 + 40] = subs[:40]                     # repeats
+    ptrs = (ctypes.POINTER(ctypes.c_int) * nv)(*[subs[k].ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+                                                  for k in range(nv)])
+    vals = (rng.integers(-50, 50, nv)).astype(np.float64)     # integer-valued: any rank order is exact
+    two = ctypes.c_double(2.0)
+    L.NGA_Scatter_acc(g, vals.ctypes.data_as(ctypes.c_void_p), ptrs, nv, ctypes.byref(two))
+    L.GA_Sync()
+    full = np.zeros(dims)
+    L.NGA_Get(g, ia([0, 0]), ia([dims[0] - 1, dims[1] - 1]), full.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]))
+    want = np.zeros(dims)
+    for r in range(size):
+        rr = np.random.default_rng(50 + r)
+        sb = np.stack([rr.integers(0, dims[0], nv), rr.integers(0, dims[1], nv)], axis=1)
+        sb[nv // 2:nv // 2 + 40] = sb[:40]
+        vv = rr.integers(-50, 50, nv).astype(np.float64)
+        for k in range(nv):
+            want[sb[k, 0], sb[k, 1]] += 2.0 * vv[k]
+    assert np.array_equal(full, want), "NGA_Scatter_acc (integer-valued) differs"
+    # gather the same subscripts (flat form) and compare with the full copy
+    got = np.zeros(nv)
+    L.NGA_Gather_flat(g, got.ctypes.data_as(ctypes.c_void_p), subs.ravel().ctypes.data_as(ctypes.POINTER(ctypes.c_int)), nv)
+    assert np.array_equal(got, full[subs[:, 0], subs[:, 1]]), "NGA_Gather_flat"
+    got2 = np.zeros(nv)
+    L.NGA_Gather(g, got2.ctypes.data_as(ctypes.c_void_p), ptrs, nv)
+    assert np.array_equal(got2, got), "NGA_Gather"
+    L.GA_Sync()
+    # rank 0 alone: non-integer values with repeated subscripts, applied in input
+    # order per owner -> bit-exact against the sequential _acc order
+    L.GA_Zero(g)
+    if rank == 0:
+        fv = rng.standard_normal(nv) * 1e3
+        alpha = 0.7071067811865476
+        a_c = ctypes.c_double(alpha)
+        L.NGA_Scatter_acc_flat(g, fv.ctypes.data_as(ctypes.c_void_p),
+                               subs.ravel().ctypes.data_as(ctypes.POINTER(ctypes.c_int)), nv, ctypes.byref(a_c))
+        exp = {}
+        for k in range(nv):
+            key = (int(subs[k, 0]), int(subs[k, 1]))
+            exp[key] = exp.get(key, 0.0) + float(fv[k]) * alpha
+        got3 = np.zeros(nv)
+        L.NGA_Gather(g, got3.ctypes.data_as(ctypes.c_void_p), ptrs, nv)
+        want3 = np.array([exp[(int(subs[k, 0]), int(subs[k, 1]))] for k in range(nv)])
+        assert np.array_equal(got3.view(np.int64), want3.view(np.int64)), "NGA_Scatter_acc order"
+    L.GA_Sync()
+    # scatter (put) of unique subscripts
+    L.GA_Zero(g)
+    uniq = np.unique(subs, axis=0)
+    if rank == size - 1:
+        uv = np.arange(1, len(uniq) + 1, dtype=np.float64) * 1.5
+        L.NGA_Scatter_flat(g, uv.ctypes.data_as(ctypes.c_void_p),
+                           np.ascontiguousarray(uniq).ravel().ctypes.data_as(ctypes.POINTER(ctypes.c_int)), len(uniq))
+    L.GA_Sync()
+    L.NGA_Get(g, ia([0, 0]), ia([dims[0] - 1, dims[1] - 1]), full.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]))
+    want = np.zeros(dims)
+    want[uniq[:, 0], uniq[:, 1]] = np.arange(1, len(uniq) + 1) * 1.5
+    assert np.array_equal(full, want), "NGA_Scatter"
+    L.GA_Sync()
+
     # local block through NGA_Access is an HBM address
     lo_m, hi_m = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
     L.NGA_Distribution(g, rank, lo_m, hi_m)
