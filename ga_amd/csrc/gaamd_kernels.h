@@ -66,6 +66,7 @@ struct Tuning {
     int align = 0;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses
     int cpol = 0;           // f64 2-D kernel via buffer ops: load | store<<8 cache bits (0 = off)
     int xcd = 0;            // f64 2-D kernel: XCD-contiguous work ranges (experiment)
+    int order = 0;          // f64 2-D kernel: 1 chunk-major, 2 scattered rows (experiment)
 };
 Tuning &tuning();
 

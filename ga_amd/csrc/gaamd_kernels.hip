@@ -247,6 +247,31 @@ __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
     }
 }
 
+// ROWS2 with a different block -> (row, chunk) order (tuning experiment on the
+// f64 2-D kernel; which rows are in flight together decides how the traffic
+// spreads over HBM channels):
+//   ORD 1: chunk-major  -- w = chunk * rows + row
+//   ORD 2: row-scattered -- row = (w_row * mult) mod rows, mult coprime to rows
+template <class OP, int ORD>
+__global__ __launch_bounds__(256) void k_rows2_ord(const Desc2 d, const OP op, uint32_t rows, uint32_t mult) {
+    for (uint32_t w = blockIdx.x; w < d.items; w += gridDim.x) {
+        uint32_t rl, chunk;
+        if constexpr (ORD == 1) {
+            chunk = w / rows;
+            rl = w - chunk * rows;
+        } else {
+            const uint32_t q = d.chunk_div.div(w);
+            chunk = w - q * d.chunks;
+            rl = (uint32_t)(((uint64_t)q * mult) % rows);
+        }
+        const int64_t r = (int64_t)(d.row0 + rl);
+        const char *sp = d.src + r * d.s_str;
+        char *dp = d.dst + r * d.d_str;
+        const int64_t c0 = (int64_t)chunk * 256;
+        chunk_op<OP, 16, 1, 256, true>(sp, dp, c0 + threadIdx.x, d.nvec, c0 + 256 <= (int64_t)d.nvec, op);
+    }
+}
+
 // ROWS2 via buffer loads/stores: a per-row SRD whose num_records is the row
 // length, so lanes past the row (or before an aligned chunk start) read zeros
 // and their stores are dropped by the hardware range check -- no predicate.
@@ -360,6 +385,21 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
     e.align_mask = d.align_mask;
     e.xcd_per = 0;
     if constexpr (W == 16 && U == 1 && BS == 256 && std::is_same<OP, AccDbl>::value) {
+        if ((g_tuning.order == 1 || g_tuning.order == 2) && nt && !d.align_mask && blocks == e.items) {
+            const uint32_t rows = e.items / e.chunks;
+            uint32_t mult = 1;
+            if (g_tuning.order == 2) {   // an odd multiplier near rows * 0.618 that is coprime to rows
+                auto gcd = [](uint64_t a, uint64_t b) { while (b) { uint64_t t = a % b; a = b; b = t; } return a; };
+                mult = (uint32_t)(rows * 0.6180339887) | 1u;
+                while (mult > 1 && gcd(mult, rows) != 1) mult += 2;
+                if (mult >= rows) mult = 1;
+            }
+            if (g_tuning.order == 1)
+                hipLaunchKernelGGL((k_rows2_ord<OP, 1>), dim3((uint32_t)blocks), dim3(256), 0, st, e, op, rows, mult);
+            else
+                hipLaunchKernelGGL((k_rows2_ord<OP, 2>), dim3((uint32_t)blocks), dim3(256), 0, st, e, op, rows, mult);
+            return hipGetLastError();
+        }
         if (g_tuning.xcd && nt && blocks == e.items && e.items % 8 == 0) {
             e.xcd_per = e.items / 8;
             hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);

@@ -112,6 +112,7 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "align")) return &t.align;
     if (!strcmp(key, "cpol")) return &t.cpol;
     if (!strcmp(key, "xcd")) return &t.xcd;
+    if (!strcmp(key, "order")) return &t.order;
     return nullptr;
 }
 

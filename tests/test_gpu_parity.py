@@ -68,7 +68,7 @@ def test_golden_cases_armci_and_nb(gpu_lib, manifest, golden):
 
 @pytest.mark.parametrize("knob", [("kind", 1), ("kind", 2), ("kind", 3), ("unroll16", 2), ("unroll16", 4),
                                   ("unroll16", 8), ("nontemporal", 0), ("max_grid", 7), ("block", 512),
-                                  ("align", 1), ("cpol", 2 | 2 << 8), ("cpol", 16 | 2 << 8), ("xcd", 1)])
+                                  ("align", 1), ("cpol", 2 | 2 << 8), ("cpol", 16 | 2 << 8), ("xcd", 1), ("order", 1), ("order", 2)])
 def test_kernel_variants_identical(gpu_lib, manifest, golden, knob):
     """Every kernel family / tuning gives the same bits as the reference."""
     key, val = knob
@@ -256,7 +256,7 @@ def test_empty_patches_are_noops(gpu_lib):
 
 @pytest.mark.parametrize("knobs", [{}, {"align": 1}, {"align": 1, "unroll16": 2}, {"unroll16": 4},
                                    {"align": 1, "block": 512}, {"nontemporal": 0}, {"cpol": 2 | 2 << 8},
-                                   {"streams": 2}, {"xcd": 1}])
+                                   {"streams": 2}, {"xcd": 1}, {"order": 1}, {"order": 2}])
 def test_wide_rows_odd_strides_all_knobs(gpu_lib, oracle, knobs):
     """Rows of 8-40 KiB (several chunks per row) at odd leading dimensions and
     offsets, so chunk splitting, the aligned-chunk grid and row tails are all
