@@ -26,6 +26,8 @@
 #include <time.h>
 #include <sched.h>
 
+#include <string>
+
 namespace gaamd {
 
 static Runtime g_rt;
@@ -125,6 +127,10 @@ void boot_init() {
 
     const size_t bytes = node_shm_bytes(r.size);
     r.shm_bytes = bytes;
+    r.node_of.assign(r.size, 0);
+    r.nnodes = 1;
+    r.node = 0;
+    r.node_size = r.size;
     if (r.size == 1) {
         void *p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
         if (p == MAP_FAILED) fatal("mmap(anon) failed");
@@ -133,20 +139,51 @@ void boot_init() {
         r.boot_ready = true;
         return;
     }
+    // nodes: ranks that share a host (MPI_Comm_split by hostname, groups.c:408-588).
+    // COMEX_AMD_NODE overrides the host name (several "nodes" on one host: the
+    // cross-node wire path can then be exercised on a single machine).
+    const char *node_env = getenv("COMEX_AMD_NODE");
+    r.node_of.assign(r.size, 0);
+    r.nnodes = 1;
+    if (r.hooks) {
+        char key[64] = {0};
+        if (node_env) snprintf(key, sizeof(key), "env:%s", node_env);
+        else if (gethostname(key, sizeof(key) - 1) != 0) fatal("gethostname failed");
+        std::vector<char> keys((size_t)r.size * sizeof(key));
+        if (r.ag(key, keys.data(), sizeof(key), r.ctx) != 0) fatal("bootstrap allgather hook failed");
+        std::vector<std::string> seen;
+        for (int q = 0; q < r.size; ++q) {
+            std::string k(keys.data() + (size_t)q * sizeof(key), strnlen(keys.data() + (size_t)q * sizeof(key), sizeof(key)));
+            int idx = -1;
+            for (int i = 0; i < (int)seen.size(); ++i) if (seen[i] == k) idx = i;
+            if (idx < 0) { idx = (int)seen.size(); seen.push_back(k); }
+            r.node_of[q] = idx;
+        }
+        r.nnodes = (int)seen.size();
+    } else if (node_env) {
+        fatal("COMEX_AMD_NODE needs bootstrap hooks (gaamd_set_bootstrap): the node-shm rendezvous is per host");
+    }
+    r.node = r.node_of[r.rank];
+    r.node_size = 0;
+    int leader = -1;
+    for (int q = 0; q < r.size; ++q)
+        if (r.node_of[q] == r.node) { if (leader < 0) leader = q; ++r.node_size; }
+
     char name[128];
     if (r.hooks) {
+        // each node's leader names its segment; the names travel by the hook
         char mine[64] = {0};
-        if (r.rank == 0) {
+        if (r.rank == leader) {
             struct timespec ts;
             clock_gettime(CLOCK_REALTIME, &ts);
             snprintf(mine, sizeof(mine), "/gaamd_%d_%d_%ld", (int)getuid(), (int)getpid(), (long)ts.tv_nsec);
         }
         std::vector<char> all((size_t)r.size * sizeof(mine));
         if (r.ag(mine, all.data(), sizeof(mine), r.ctx) != 0) fatal("bootstrap allgather hook failed");
-        memcpy(name, all.data(), sizeof(mine));
+        memcpy(name, all.data() + (size_t)leader * sizeof(mine), sizeof(mine));
         name[63] = 0;
         if (strncmp(name, "/gaamd_", 7) != 0) fatal("bootstrap allgather hook returned a corrupt segment name");
-        r.shm = open_shm(name, bytes, r.rank == 0);
+        r.shm = open_shm(name, bytes, r.rank == leader);
         if (r.bar(r.ctx) != 0) fatal("bootstrap barrier hook failed");
     } else {
         const char *port = getenv("MASTER_PORT");
@@ -156,23 +193,32 @@ void boot_init() {
         r.shm = open_shm(name, bytes, true);
     }
     r.boot_ready = true;
-    shm_barrier(r.shm, r.size);
-    if (r.rank == 0) shm_unlink(name);
+    shm_barrier(r.shm, r.node_size);
+    if (r.rank == leader) shm_unlink(name);
     r.shm->size = r.size;
-    shm_barrier(r.shm, r.size);
+    shm_barrier(r.shm, r.node_size);
 }
 
 void boot_barrier() {
     Runtime &r = g_rt;
     if (r.size == 1) return;
+    if (r.nnodes > 1) {   // across nodes: the launcher's barrier (MPI, torch.distributed)
+        if (r.bar(r.ctx) != 0) fatal("bootstrap barrier hook failed");
+        return;
+    }
     shm_barrier(r.shm, r.size);
 }
 
 // allgather through the shm boot area, kBootSlot bytes per rank per round
+// (several nodes: the launcher's allgather)
 void boot_allgather(const void *send, void *recv, size_t bytes) {
     Runtime &r = g_rt;
     if (r.size == 1) {
         memcpy(recv, send, bytes);
+        return;
+    }
+    if (r.nnodes > 1) {
+        if (r.ag(send, recv, bytes, r.ctx) != 0) fatal("bootstrap allgather hook failed");
         return;
     }
     char *area = boot_area(r.shm, r.size);

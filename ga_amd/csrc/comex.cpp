@@ -77,6 +77,28 @@ static bool find_segment_local(const void *p, int64_t lo, int64_t hi) {
     return false;
 }
 
+bool segment_local(const void *p, int64_t lo, int64_t hi) {
+    std::lock_guard<std::mutex> g(rt().seg_mu);
+    return find_segment_local(p, lo, hi);
+}
+
+// reg_cache_find for a rank on another node: inside one of its segments
+bool segment_of_rank(int owner, uint64_t p, int64_t lo, int64_t hi) {
+    Runtime &r = rt();
+    std::lock_guard<std::mutex> g(r.seg_mu);
+    for (const Segment &s : r.segs) {
+        if (!s.live) continue;
+        const PeerMap &m = s.peer[owner];
+        if (m.bytes && p + lo >= m.base && p + hi <= m.base + m.bytes) return true;
+    }
+    return false;
+}
+
+static void check_remote(int owner, const void *p, int64_t lo, int64_t hi) {
+    if (!segment_of_rank(owner, (uint64_t)(uintptr_t)p, lo, hi))
+        fatal("address %p [%ld,%ld) of rank %d is not inside a comex_malloc segment", p, (long)lo, (long)hi, owner);
+}
+
 // address of rank `owner`'s byte `p` (owner's address space) in this process
 static char *remote_view(int owner, const void *p, int64_t lo, int64_t hi) {
     Runtime &r = rt();
@@ -85,7 +107,10 @@ static char *remote_view(int owner, const void *p, int64_t lo, int64_t hi) {
     for (const Segment &s : r.segs) {
         if (!s.live) continue;
         const PeerMap &m = s.peer[owner];
-        if (m.bytes && a + lo >= m.base && a + hi <= m.base + m.bytes) return m.mapped + (a - m.base);
+        if (m.bytes && a + lo >= m.base && a + hi <= m.base + m.bytes) {
+            if (!m.mapped) fatal("rank %d is on another node: its memory is not mapped here", owner);
+            return m.mapped + (a - m.base);
+        }
     }
     fatal("address %p [%ld,%ld) of rank %d is not inside a comex_malloc segment", p, (long)lo, (long)hi, owner);
 }
@@ -174,15 +199,15 @@ static void local_views(void *src, int64_t slo, int64_t shi, void *dst, int64_t 
     }
 }
 
-static View local_view(void *p, int64_t lo, int64_t hi) {
-    View v, unused;
+static View local_view(void *p, int64_t lo, int64_t hi, bool is_dst = false) {
+    View v;
     char *d = nullptr;
     if (direct_view(p, &d)) { v.dev = d; return v; }
     uintptr_t a0, a1;
     page_range(p, lo, hi, a0, a1);
     char *base = nullptr;
     if (register_range(a0, a1, &base)) { v.registered = (void *)a0; v.dev = base + ((uintptr_t)p - a0); }
-    else stage_view(v, p, lo, hi, false);
+    else stage_view(v, p, lo, hi, is_dst);
     return v;
 }
 
@@ -490,7 +515,9 @@ static void remote_acc(int t, int op, const void *scale, void *src, const int *s
 
 static void fence_target(int t) {
     Runtime &r = rt();
-    if (r.size == 1 || t == r.rank || r.posted.empty()) return;
+    if (r.size == 1 || t == r.rank) return;
+    if (!r.same_node(t)) { wire_fence(t); return; }
+    if (r.posted.empty()) return;
     wait_done(t, r.posted[t]);
 }
 
@@ -527,6 +554,29 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         return COMEX_SUCCESS;
     }
 
+    if (world != r.rank && !r.same_node(world)) {
+        // another node: the message protocol (wire.cpp)
+        const int64_t rb = row_bytes_of(cop, count[0]);
+        int64_t slo = 0, shi = 0, dlo = 0, dhi = 0;
+        if (kind == X_GET) {
+            side_span_host(ss, count, levels, count[0], &slo, &shi);
+            side_span_host(ds, count, levels, count[0], &dlo, &dhi);
+            check_remote(world, src, slo, shi);
+            View dv = local_view(dst, dlo, dhi, true);
+            wire_get_strided((uint64_t)(uintptr_t)src, ss, dv.dev, ds, count, levels, world);
+            release_view(dv);
+        } else {
+            side_span_host(ss, count, levels, count[0], &slo, &shi);
+            side_span_host(ds, count, levels, rb, &dlo, &dhi);
+            check_remote(world, dst, dlo, dhi);
+            View sv = local_view(src, slo, shi);
+            wire_send_strided(cop, scale, sv.dev, ss, (uint64_t)(uintptr_t)dst, ds, count, levels, world);
+            release_view(sv);
+        }
+        if (hdl) nb_complete_now(hdl);
+        return COMEX_SUCCESS;
+    }
+
     if (world != r.rank && kind == X_ACC) {
         remote_acc(world, op, scale, src, ss, dst, ds, count, levels);
         if (hdl) nb_complete_now(hdl);
@@ -546,7 +596,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
             dv.dev = remote_view(world, dst, dlo, dhi);
         } else {
             sv.dev = remote_view(world, src, slo, shi);
-            dv = local_view(dst, dlo, dhi);
+            dv = local_view(dst, dlo, dhi, true);
         }
     } else {
         local_views(src, slo, shi, dst, dlo, dhi, sv, dv);
@@ -666,6 +716,35 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         const bool remote_side_is_dst = (kind != X_GET);
         std::vector<uint64_t> sv((size_t)n), dv((size_t)n);
         bool host_bounce = false;
+        if (world != r.rank && !r.same_node(world)) {
+            // another node: one io-vector message per descriptor chunk (wire.cpp)
+            for (int i = 0; i < n && !host_bounce; ++i) {
+                void *sp = darr[k].src[i], *dp = darr[k].dst[i];
+                char *d = nullptr;
+                if (remote_side_is_dst) {
+                    check_remote(world, dp, 0, bytes);
+                    dv[i] = (uint64_t)(uintptr_t)dp;
+                    if (direct_view(sp, &d)) sv[i] = (uint64_t)(uintptr_t)d;
+                    else host_bounce = true;
+                } else {
+                    check_remote(world, sp, 0, bytes);
+                    sv[i] = (uint64_t)(uintptr_t)sp;
+                    if (direct_view(dp, &d)) dv[i] = (uint64_t)(uintptr_t)d;
+                    else host_bounce = true;
+                }
+            }
+            if (host_bounce) {
+                for (int i = 0; i < n; ++i)
+                    xfer_contig(kind, op, scale, darr[k].src[i], darr[k].dst[i], bytes, proc, group, nullptr);
+            } else if (kind == X_GET) {
+                wire_get_iov(sv.data(), dv.data(), n, bytes, world);
+            } else {
+                std::vector<std::pair<uint64_t, uint64_t>> dr((size_t)n);
+                for (int i = 0; i < n; ++i) dr[i] = {dv[i], dv[i] + (uint64_t)bytes};
+                wire_send_iov(cop, scale, sv.data(), dv.data(), n, bytes, ranges_overlap(dr), world);
+            }
+            continue;
+        }
         for (int i = 0; i < n; ++i) {
             void *sp = darr[k].src[i], *dp = darr[k].dst[i];
             char *d = nullptr;
@@ -794,6 +873,7 @@ int comex_init() {
         r.peer_staging.assign(r.size, nullptr);
         for (int q = 0; q < r.size; ++q) {
             if (q == r.rank) { r.peer_staging[q] = r.staging; continue; }
+            if (!r.same_node(q)) continue;   // another node: reached through wire.cpp
             void *p = nullptr;
             GA_HIP(hipIpcOpenMemHandle(&p, all[q].h, hipIpcMemLazyEnablePeerAccess));
             r.peer_staging[q] = (char *)p;
@@ -803,6 +883,7 @@ int comex_init() {
         g_pend.assign(r.size, {});
         r.stop.store(false);
         r.progress = std::thread(progress_loop);
+        wire_init();
     }
     r.initialized = true;
     boot_barrier();
@@ -821,6 +902,7 @@ int comex_finalize() {
     Runtime &r = rt();
     if (!r.initialized) return COMEX_SUCCESS;
     comex_barrier(COMEX_GROUP_WORLD);
+    wire_finalize();
     if (r.progress.joinable()) {
         r.stop.store(true, std::memory_order_release);
         r.progress.join();
@@ -1057,7 +1139,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         ptr_arr[q] = (void *)(uintptr_t)all[q].base;
         if (q == r.rank) {
             s.peer[q].mapped = (char *)p;
-        } else if (all[q].bytes) {
+        } else if (all[q].bytes && r.same_node(q)) {
             if (!device) fatal("host-memory segments are rank-private (use device segments for remote access)");
             void *m = nullptr;
             GA_HIP(hipIpcOpenMemHandle(&m, all[q].h, hipIpcMemLazyEnablePeerAccess));

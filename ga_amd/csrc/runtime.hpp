@@ -106,6 +106,10 @@ struct Runtime {
     bool initialized = false;
     bool boot_ready = false;
     int rank = 0, size = 1, local_rank = 0, device = 0;
+    // nodes (hosts): ranks of one node share the node shm and map each other's HBM
+    int nnodes = 1, node = 0, node_size = 1;
+    std::vector<int> node_of;                  // node index of every rank
+    bool same_node(int q) const { return node_of.empty() || node_of[q] == node; }
     hipStream_t stream = nullptr;              // primary stream (= streams[0])
     std::vector<hipStream_t> streams;          // COMEX_AMD_STREAMS streams (sched.cpp)
     bool blocking_sync = false;     // COMEX_AMD_BLOCKING_SYNC
@@ -149,6 +153,25 @@ void sched_resize(int nstreams);
 int sched_pick(const Span &src, const Span &dst);   // stream index for an op
 void sched_join();
 void sched_sync_all();
+
+// wire.cpp: the host fallback between nodes (MPI-PR message protocol over TCP)
+void wire_init();                                   // collective; no-op on one node
+void wire_finalize();                               // collective
+bool wire_active();
+// put (op == 0) / accumulate of a local strided patch into rank t's `dst`
+void wire_send_strided(int op, const void *scale, const char *src_dev, const int *ss, uint64_t dst,
+                       const int *ds, const int *count, int levels, int t);
+// get of rank t's strided patch at `src` into a local patch
+void wire_get_strided(uint64_t src, const int *ss, char *dst_dev, const int *ds, const int *count, int levels,
+                      int t);
+// io-vector put (op == 0) / accumulate: n local device sources -> n addresses of rank t
+void wire_send_iov(int op, const void *scale, const uint64_t *src_dev, const uint64_t *dst, int n, int bytes,
+                   bool serial, int t);
+// io-vector get: n addresses of rank t -> n local device destinations
+void wire_get_iov(const uint64_t *src, const uint64_t *dst_dev, int n, int bytes, int t);
+void wire_fence(int t);                             // remote completion of everything sent to t
+bool segment_of_rank(int owner, uint64_t p, int64_t lo, int64_t hi);   // comex.cpp (reg_cache_find)
+bool segment_local(const void *p, int64_t lo, int64_t hi);              // comex.cpp
 
 // comex.cpp helpers shared with armci.cpp
 int translate_world(int group, int proc);

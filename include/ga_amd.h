@@ -43,6 +43,12 @@ int gaamd_set_bootstrap(int rank, int size, int local_rank,
 int gaamd_bootstrap_selftest(int rounds);
 int gaamd_rank(void);
 int gaamd_size(void);
+/* nodes: ranks sharing a host (or the same COMEX_AMD_NODE value) map each other's
+   HBM; ranks on different nodes exchange the MPI-PR messages over TCP (wire.cpp).
+   After bootstrap: this rank's node index, the node count, ranks on this node. */
+int gaamd_node_info(int *node, int *nnodes, int *node_size);
+/* exercise the cross-node transport alone (no GPU): PING frames between all ranks */
+int gaamd_wire_selftest(int rounds);
 
 /* ---- 2. kernels -------------------------------------------------------- */
 int gaamd_strided(int op, const void *scale, const void *src, const int *src_stride,

@@ -4,6 +4,11 @@ Modes:
   boot-env   : built-in node-shm bootstrap from RANK/WORLD_SIZE; bootstrap
                self-test only (no GPU).
   boot-gloo  : torch.distributed gloo as the bootstrap hooks; self-test only.
+  boot-nodes : gloo hooks + COMEX_AMD_NODE (several "nodes" on one host): per-node
+               shm, cross-node collectives through the hooks, and the cross-node
+               TCP transport (PING frames between all ranks).  No GPU.
+  remote-gloo / ga-gloo: as remote / ga with gloo hooks; with COMEX_AMD_NODE set
+               the ranks of different nodes talk through the wire protocol.
   remote     : comex on the GPU (every rank may share one device): segments by
                comex_malloc, remote accumulate through the owner's progress
                thread, remote put/get through IPC mappings, checked against the
@@ -49,7 +54,7 @@ def main():
     rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import ga_amd
     L = ga_amd.lib()
-    if mode in ("boot-gloo", "remote-gloo"):
+    if mode in ("boot-gloo", "remote-gloo", "boot-nodes", "ga-gloo"):
         ag, bar = torch_hooks(rank, size)
         keep = (ag, bar)  # noqa: F841
         assert L.gaamd_set_bootstrap(rank, size, rank, ctypes.cast(ag, ctypes.c_void_p),
@@ -57,9 +62,17 @@ def main():
     if mode.startswith("boot"):
         assert L.gaamd_bootstrap_selftest(5) == 0
         assert L.gaamd_rank() == rank and L.gaamd_size() == size
+        if mode == "boot-nodes":
+            nodes = [int(x) for x in os.environ["TEST_NODES"].split(",")]
+            nd, nn, ns = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+            assert L.gaamd_node_info(ctypes.byref(nd), ctypes.byref(nn), ctypes.byref(ns)) == 0
+            order = list(dict.fromkeys(nodes))
+            assert nd.value == order.index(nodes[rank]), (nd.value, nodes)
+            assert nn.value == len(order) and ns.value == nodes.count(nodes[rank])
+            assert L.gaamd_wire_selftest(3) == 0
         print(f"RANK {rank} OK", flush=True)
         return
-    if mode == "ga":
+    if mode in ("ga", "ga-gloo"):
         ga_test(L, rank, size)
     else:
         remote_test(L, rank, size)
@@ -160,6 +173,27 @@ def remote_test(L, rank, size):
     for i, j in enumerate(idx):
         exp_t[j] += 2.0 * psrc[i]
     assert np.array_equal(tail, exp_t), f"rank {rank}: remote accv mismatch"
+
+    # remote io-vector get of the next rank's tail (what I accumulated there)
+    gb = ga_amd.DeviceBuffer(40 * 8)
+    gdesc = [([seg[nxt] + vbase + 8 * j for j in range(40)], [gb.ptr + 8 * (39 - j) for j in range(40)], 8)]
+    assert ga_amd.comex_getv(gdesc, nxt) == 0
+    ga_amd.comex_fence_all()
+    exp_n = (np.arange(ld * ncol, dtype=np.float64) % 1000 + 1000 * nxt)[-40:].copy()
+    for i, j in enumerate(idx):
+        exp_n[j] += 2.0 * vsrc[i]
+    assert np.array_equal(gb.download(np.float64, 40)[::-1], exp_n), f"rank {rank}: remote getv mismatch"
+    # remote io-vector put of 8 singles into the next rank's tail slots 32..39
+    ga_amd.comex_barrier()
+    pv = ga_amd.DeviceBuffer(64)
+    pv.upload(np.arange(8, dtype=np.float64) - 100.0 * rank)
+    pdesc = [([pv.ptr + 8 * i for i in range(8)], [seg[nxt] + vbase + 8 * (32 + i) for i in range(8)], 8)]
+    assert ga_amd.comex_putv(pdesc, nxt) == 0
+    ga_amd.comex_barrier()
+    assert ga_amd.lib().comex_get(ctypes.c_void_p(seg[rank] + vbase), tail.ctypes.data_as(ctypes.c_void_p), 320,
+                                  rank, 0) == 0
+    ga_amd.comex_fence_all()
+    assert np.array_equal(tail[32:], np.arange(8, dtype=np.float64) - 100.0 * prv), f"rank {rank}: putv"
 
     ga_amd.comex_barrier()
     assert ga_amd.comex_free(seg[rank]) == 0

@@ -25,12 +25,18 @@ def free_port():
     return p
 
 
-def launch(mode, n=2, timeout=240):
+def launch(mode, n=2, timeout=240, nodes=None, extra_env=None):
+    """nodes: node id of every rank (COMEX_AMD_NODE), None = all on this host."""
     port = str(free_port())
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=port, COMEX_AMD_JOBID=f"t{port}", COMEX_AMD_STAGING_MB="16")
+        if nodes is not None:
+            env["COMEX_AMD_NODE"] = str(nodes[r])
+            env["TEST_NODES"] = ",".join(str(x) for x in nodes)
+            env["COMEX_AMD_WIRE_ADDR"] = "127.0.0.1"
+        env.update(extra_env or {})
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "mp_worker.py"), mode], cwd=ROOT, env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
@@ -58,6 +64,12 @@ def test_bootstrap_env_shm_four_ranks():
     launch("boot-env", n=4)
 
 
+@pytest.mark.parametrize("nodes", [[0, 1], [0, 0, 1, 1], [1, 0, 1, 2]])
+def test_bootstrap_several_nodes_and_wire(nodes):
+    """Per-node shm + cross-node collectives through the hooks + TCP PING frames."""
+    launch("boot-nodes", n=len(nodes), nodes=nodes)
+
+
 @pytest.mark.gpu
 def test_remote_acc_put_get_two_ranks_one_gpu():
     launch("remote", n=2, timeout=300)
@@ -66,6 +78,25 @@ def test_remote_acc_put_get_two_ranks_one_gpu():
 @pytest.mark.gpu
 def test_remote_three_ranks_gloo_hooks():
     launch("remote-gloo", n=3, timeout=300)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nodes", [[0, 1], [0, 0, 1, 1]])
+def test_remote_across_nodes_wire(nodes):
+    """Ranks on different (simulated) nodes: acc/put/get/accv/getv/putv through the
+    MPI-PR message protocol over TCP (wire.cpp); [0,0,1,1] mixes IPC and wire."""
+    launch("remote-gloo", n=len(nodes), timeout=300, nodes=nodes)
+
+
+@pytest.mark.gpu
+def test_remote_across_nodes_wire_small_chunks():
+    """Payloads cut into many row-range frames (1 MiB pinned chunks)."""
+    launch("remote-gloo", n=2, timeout=300, nodes=[0, 1], extra_env={"COMEX_AMD_WIRE_MB": "1"})
+
+
+@pytest.mark.gpu
+def test_ga_layer_across_nodes():
+    launch("ga-gloo", n=3, timeout=300, nodes=[0, 0, 1])
 
 
 @pytest.mark.gpu
