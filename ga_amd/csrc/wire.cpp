@@ -31,12 +31,19 @@
 // message ordering.  The target applies a frame's kernel on its library
 // streams through the dependency scheduler, so accumulates into one target
 // stay mutually exclusive (the reference's per-target semaphores).
+//
+// Exposure: the listener binds ONE interface -- COMEX_AMD_WIRE_ADDR, default
+// 127.0.0.1 (a job spanning hosts must name the interface explicitly) -- and a
+// connection is served only after it presents the job's 32-byte secret, drawn
+// from /dev/urandom by rank 0 and handed to every rank through the bootstrap
+// allgather (the launcher's channel).  Every address a frame names must lie
+// inside one of the target's comex_malloc segments (reg_cache_find) or the
+// target aborts.
 #include "runtime.hpp"
 #include "gaamd_kernels.h"
 #include "../../include/comex.h"
 #include <arpa/inet.h>
 #include <errno.h>
-#include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <poll.h>
@@ -110,6 +117,8 @@ Pinned g_cli[2];
 Pinned g_srv[2];
 int g_srv_next = 0;
 size_t g_chunk = 64u << 20;
+constexpr size_t kSecret = 32;
+unsigned char g_secret[kSecret];
 
 void wait_pinned(Pinned &b) {
     if (b.pending) GA_HIP(hipEventSynchronize(b.ev));
@@ -183,8 +192,30 @@ Peer &connect_to(int t) {
         fatal("wire: connect to rank %d (%s:%d) failed (%s)", t, inet_ntoa(a.sin_addr), ntohs(a.sin_port),
               strerror(errno));
     tune_socket(fd);
+    send_all(fd, g_secret, kSecret);   // the job secret opens the connection
     p.fd = fd;
     return p;
+}
+
+// a new connection must present the job secret within a few seconds
+bool admit(int c) {
+    timeval tv;
+    tv.tv_sec = 5;
+    tv.tv_usec = 0;
+    (void)setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    unsigned char got[kSecret];
+    size_t n = 0;
+    while (n < kSecret) {
+        const ssize_t k = ::recv(c, got + n, kSecret - n, 0);
+        if (k < 0 && errno == EINTR) continue;
+        if (k <= 0) return false;
+        n += (size_t)k;
+    }
+    unsigned char diff = 0;
+    for (size_t i = 0; i < kSecret; ++i) diff |= (unsigned char)(got[i] ^ g_secret[i]);
+    tv.tv_sec = 0;
+    (void)setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    return diff == 0;
 }
 
 uint64_t fnv1a(const char *p, size_t n) {
@@ -437,37 +468,30 @@ void server_loop() {
         if (pf[0].revents & POLLIN) {
             const int c = ::accept(g_listen, nullptr, nullptr);
             if (c >= 0) {
-                tune_socket(c);
-                keep.push_back(c);
+                if (admit(c)) {
+                    tune_socket(c);
+                    keep.push_back(c);
+                } else {
+                    fprintf(stderr, "[%d] wire: refused a connection without the job secret\n", r.rank);
+                    ::close(c);
+                }
             }
         }
         conns.swap(keep);
         if (stopping && conns.empty() && !(pf[0].revents & POLLIN) && k == 0) break;
     }
-    (void)r;
     wait_pinned(g_srv[0]);
     wait_pinned(g_srv[1]);
 }
 
-uint32_t advertised_addr() {
-    if (const char *a = getenv("COMEX_AMD_WIRE_ADDR")) {
-        in_addr x;
-        if (inet_aton(a, &x)) return x.s_addr;
-        fatal("COMEX_AMD_WIRE_ADDR=%s is not an IPv4 address", a);
-    }
-    char host[256] = {0};
-    if (gethostname(host, sizeof(host) - 1) == 0) {
-        addrinfo hints, *res = nullptr;
-        memset(&hints, 0, sizeof(hints));
-        hints.ai_family = AF_INET;
-        hints.ai_socktype = SOCK_STREAM;
-        if (getaddrinfo(host, nullptr, &hints, &res) == 0 && res) {
-            const uint32_t a = ((sockaddr_in *)res->ai_addr)->sin_addr.s_addr;
-            freeaddrinfo(res);
-            return a;
-        }
-    }
-    return htonl(INADDR_LOOPBACK);
+// the one interface the listener binds and advertises
+uint32_t wire_addr() {
+    const char *a = getenv("COMEX_AMD_WIRE_ADDR");
+    if (!a) return htonl(INADDR_LOOPBACK);
+    in_addr x;
+    if (!inet_aton(a, &x)) fatal("COMEX_AMD_WIRE_ADDR=%s is not an IPv4 address", a);
+    if (x.s_addr == htonl(INADDR_ANY)) fatal("COMEX_AMD_WIRE_ADDR must name one interface, not 0.0.0.0");
+    return x.s_addr;
 }
 
 void start_sockets() {
@@ -479,7 +503,7 @@ void start_sockets() {
     sockaddr_in a;
     memset(&a, 0, sizeof(a));
     a.sin_family = AF_INET;
-    a.sin_addr.s_addr = htonl(INADDR_ANY);
+    a.sin_addr.s_addr = wire_addr();
     a.sin_port = 0;
     if (::bind(g_listen, (sockaddr *)&a, sizeof(a)) != 0) fatal("wire: bind failed (%s)", strerror(errno));
     if (::listen(g_listen, 256) != 0) fatal("wire: listen failed (%s)", strerror(errno));
@@ -487,10 +511,20 @@ void start_sockets() {
     if (::getsockname(g_listen, (sockaddr *)&a, &len) != 0) fatal("wire: getsockname failed");
     Endpoint mine;
     memset(&mine, 0, sizeof(mine));
-    mine.addr = advertised_addr();
+    mine.addr = a.sin_addr.s_addr;
     mine.port = a.sin_port;
     g_ep.assign(r.size, Endpoint());
     boot_allgather(&mine, g_ep.data(), sizeof(Endpoint));
+    // the job secret: rank 0's random bytes, through the launcher's allgather
+    unsigned char rnd[kSecret] = {0};
+    if (r.rank == 0) {
+        FILE *f = fopen("/dev/urandom", "rb");
+        if (!f || fread(rnd, 1, kSecret, f) != kSecret) fatal("wire: cannot read /dev/urandom");
+        fclose(f);
+    }
+    std::vector<unsigned char> all((size_t)r.size * kSecret);
+    boot_allgather(rnd, all.data(), kSecret);
+    memcpy(g_secret, all.data(), kSecret);
     g_peer.clear();
     for (int q = 0; q < r.size; ++q) g_peer.emplace_back(new Peer());
     if (::pipe(g_wake) != 0) fatal("wire: pipe failed");
@@ -540,6 +574,7 @@ void wire_finalize() {
     for (Pinned &b : g_srv) free_pinned(b);
     g_peer.clear();
     g_ep.clear();
+    memset(g_secret, 0, kSecret);
     g_active = false;
 }
 
@@ -738,6 +773,36 @@ extern "C" int gaamd_wire_selftest(int rounds) {
                 if (h != (fnv1a(buf.data(), n) ^ (uint64_t)t)) ++bad;
             }
         }
+        boot_barrier();
+    }
+    // a connection without the job secret is closed unanswered
+    if (r.size > 1) {
+        const int t = (r.rank + 1) % r.size;
+        const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+        sockaddr_in a;
+        memset(&a, 0, sizeof(a));
+        a.sin_family = AF_INET;
+        a.sin_addr.s_addr = g_ep[t].addr;
+        a.sin_port = g_ep[t].port;
+        timeval tv;
+        tv.tv_sec = 20;
+        tv.tv_usec = 0;
+        (void)setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+        if (fd < 0 || ::connect(fd, (sockaddr *)&a, sizeof(a)) != 0) {
+            ++bad;
+        } else {
+            unsigned char wrong[kSecret];
+            for (size_t i = 0; i < kSecret; ++i) wrong[i] = (unsigned char)(g_secret[i] ^ 0x5a);
+            Frame f = make_frame(W_PING, t, 0, nullptr, nullptr, 0);
+            (void)::send(fd, wrong, kSecret, MSG_NOSIGNAL);
+            (void)::send(fd, &f, sizeof(f), MSG_NOSIGNAL);
+            uint64_t h = 0;
+            const ssize_t k = ::recv(fd, &h, sizeof(h), 0);
+            // closed (EOF, or a reset because the refused frame was never read) -- not
+            // answered, not left hanging until the timeout
+            if (k > 0 || (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK))) ++bad;
+        }
+        if (fd >= 0) ::close(fd);
         boot_barrier();
     }
     if (own) wire_finalize();
