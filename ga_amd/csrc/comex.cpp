@@ -838,9 +838,23 @@ using namespace gaamd;
 // C ABI
 extern "C" {
 
+// a process that exits without comex_finalize (an error path) must not die in
+// std::thread's destructor: let the helper threads go with the process
+static void exit_without_finalize() {
+    Runtime &r = rt();
+    if (!r.initialized) return;
+    if (r.progress.joinable()) r.progress.detach();
+    wire_detach();
+}
+
 int comex_init() {
     Runtime &r = rt();
     if (r.initialized) return COMEX_SUCCESS;
+    static bool hook = false;
+    if (!hook) {
+        atexit(exit_without_finalize);
+        hook = true;
+    }
     boot_init();
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);

@@ -157,6 +157,7 @@ void sched_sync_all();
 // wire.cpp: the host fallback between nodes (MPI-PR message protocol over TCP)
 void wire_init();                                   // collective; no-op on one node
 void wire_finalize();                               // collective
+void wire_detach();                                 // process exit without finalize
 bool wire_active();
 // put (op == 0) / accumulate of a local strided patch into rank t's `dst`
 void wire_send_strided(int op, const void *scale, const char *src_dev, const int *ss, uint64_t dst,

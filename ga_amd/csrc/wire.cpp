@@ -578,6 +578,10 @@ void wire_finalize() {
     g_active = false;
 }
 
+void wire_detach() {
+    if (g_server.joinable()) g_server.detach();
+}
+
 void wire_fence(int t) {
     if (!g_active) return;
     Peer &p = *g_peer[t];

@@ -318,7 +318,9 @@ def ga_test(L, rank, size):
     L.GA_Sync()
     # scatter (put) of unique subscripts
     L.GA_Zero(g)
-    uniq = np.unique(subs, axis=0)
+    rs = np.random.default_rng(77)                              # same subscripts on every rank
+    uniq = np.unique(np.stack([rs.integers(0, dims[0], 300), rs.integers(0, dims[1], 300)], axis=1).astype(np.int32),
+                     axis=0)
     if rank == size - 1:
         uv = np.arange(1, len(uniq) + 1, dtype=np.float64) * 1.5
         L.NGA_Scatter_flat(g, uv.ctypes.data_as(ctypes.c_void_p),
