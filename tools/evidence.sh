@@ -2,8 +2,8 @@
 # tools/evidence.sh TAG -- the measurement evidence of one round, on a GPU box:
 #   1. PMC HBM traffic of the H kernel (two separate rocprofv3 --pmc passes)
 #   2. bench.py default line (N=1, workload H, CPU baseline included)
-#   3. rocprofv3 --kernel-trace --stats of the same bench command (no CPU leg)
-#   4. bench lines for the other single-GPU configs (C2, C3, C4, H8200)
+#   3. bench lines for the other single-GPU configs (C2, C3, C4, H8200)
+#   4. rocprofv3 --kernel-trace --stats of the same bench command (no CPU leg)
 # Each GPU step has its own time limit; the first failure ends the script.
 # Summaries land in gpurun_out/evidence/ (copy into profiles/<TAG>/ afterwards).
 set -euo pipefail
@@ -15,10 +15,11 @@ timeout -k 10 300 python3 tools/pmc_traffic.py --workload H --tag "$TAG" > "$OUT
 cp profiles/pmc_latest.json "$OUT/pmc_latest.json"
 cp profiles/pmc_"$TAG"*.json "$OUT/" 2>/dev/null || true
 timeout -k 10 300 python3 bench.py > "$OUT/bench_H.json" 2> "$OUT/bench_H.err"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
-    python3 bench.py --no-cpu > "$OUT/bench_H_prof.json" 2> "$OUT/bench_H_prof.err"
 for w in C2 C3 C4 H8200; do
     timeout -k 10 300 python3 bench.py --workload "$w" --no-cpu > "$OUT/bench_$w.json" 2> "$OUT/bench_$w.err"
 done
+# the profiled run last: a bench started right after rocprofv3 once read half speed
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
+    python3 bench.py --no-cpu > "$OUT/bench_H_prof.json" 2> "$OUT/bench_H_prof.err"
 find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/rocprofv3_kernel_stats_H.csv" \;
 echo done
