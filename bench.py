@@ -341,7 +341,7 @@ def main():
                    "algorithmic_bytes_per_step": alg, "parallelism": f"owner-aligned x{n} (no collective)",
                    "kernel": r["launch"]},
         "payload_GiB_per_s": round(value / 3, 2),
-        "hbm_peak_frac": round(value * 2 ** 30 / (HBM_PEAK_GBS * 1e9), 4),
+        "hbm_peak_frac": round(value * 2 ** 30 / (dist.size * HBM_PEAK_GBS * 1e9), 4),   # per GPU
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel_ms_avg": round(r["avg_kernel_s"] * 1e3, 4),
