@@ -147,24 +147,39 @@ def run_gpu(args, dist):
     alg_bytes = 3 * payload            # src read + dst read + dst write
     type_code = 0                      # f64 reals (dcpl = 2 f64 each)
 
-    # --sets independent (src, dst) pairs; rotate so the MALL cannot hold them
-    sets = []
+    # --sets independent (src, dst) pairs; rotate so the MALL cannot hold them.
+    # --exchange: dst are comex_malloc segments and rank r accumulates into rank
+    # r+1's (the remote path, pack -> owner's unpack-acc).
+    exchange = args.exchange and dist.size > 1
+    target = (dist.rank + 1) % dist.size if exchange else dist.rank
+    sets, segs = [], []
     for i in range(args.sets):
         s = ga_amd.DeviceBuffer(sbytes)
-        d = ga_amd.DeviceBuffer(dbytes)
         ga_amd.fill(s.ptr, sbytes // 8, type_code, 0x5EED0000 + dist.rank)
-        ga_amd.fill(d.ptr, dbytes // 8, type_code, 0x5EED0001 + dist.rank + 977 * i)
-        sets.append((s, d))
+        if exchange:
+            seg = ga_amd.comex_malloc(dbytes, dist.size)
+            ga_amd.fill(seg[dist.rank], dbytes // 8, type_code, 0x5EED0001 + dist.rank + 977 * i)
+            segs.append(seg)
+            sets.append((s, None))
+        else:
+            d = ga_amd.DeviceBuffer(dbytes)
+            ga_amd.fill(d.ptr, dbytes // 8, type_code, 0x5EED0001 + dist.rank + 977 * i)
+            sets.append((s, d))
     ga_amd.sync()
+    if exchange:
+        L.comex_barrier(0)
 
     keep, sp = ga_amd.scale_buffer(op, SCALE[op])
     ss, ds, cnt = ga_amd.int_array(sstr), ga_amd.int_array(dstr), ga_amd.int_array(count)
-    ptrs = [(ctypes.c_void_p(s.ptr), ctypes.c_void_p(d.ptr)) for s, d in sets]
+    if exchange:
+        ptrs = [(ctypes.c_void_p(s.ptr), ctypes.c_void_p(seg[target])) for (s, _), seg in zip(sets, segs)]
+    else:
+        ptrs = [(ctypes.c_void_p(s.ptr), ctypes.c_void_p(d.ptr)) for s, d in sets]
     stream = L.gaamd_stream()
 
     def step(i):
         sp_, dp_ = ptrs[i % len(ptrs)]
-        rc = L.comex_accs(op, sp, sp_, ss, dp_, ds, cnt, levels, dist.rank, 0)
+        rc = L.comex_accs(op, sp, sp_, ss, dp_, ds, cnt, levels, target, 0)
         if rc:
             raise RuntimeError(f"comex_accs returned {rc}")
 
@@ -187,6 +202,8 @@ def run_gpu(args, dist):
     L.gaamd_join()                      # the primary stream waits for the library's other streams
     L.gaamd_event_record(ev1, stream)
     ga_amd.sync()
+    if exchange:
+        L.comex_fence_all(0)            # remote completion: the owner has applied every request
     t1 = time.perf_counter()
     dist.barrier()
     elapsed = dist.max(t1 - t0)
@@ -194,6 +211,8 @@ def run_gpu(args, dist):
     L.gaamd_event_destroy(ev0)
     L.gaamd_event_destroy(ev1)
     avg_kernel_s = dist.max(region_ms / 1e3 / args.steps)
+    if exchange:
+        avg_kernel_s = elapsed / args.steps   # the work runs on the owners' streams
 
     res = dict(op=op, desc=desc, payload=payload, alg_bytes=alg_bytes, elems=elems, elapsed=elapsed,
                avg_kernel_s=avg_kernel_s, launch=launch)
@@ -201,7 +220,13 @@ def run_gpu(args, dist):
         res["host"] = host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_bytes)
     for s, d in sets:
         s.free()
-        d.free()
+        if d is not None:
+            d.free()
+    if exchange:
+        L.comex_barrier(0)
+        for seg in segs:
+            ga_amd.comex_free(seg[dist.rank])
+    res["exchange"] = exchange
     ga_amd.comex_finalize()
     return res
 
@@ -309,6 +334,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=8, help="host workers of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--host-rates", action="store_true", help="also measure host-inclusive rates")
+    ap.add_argument("--exchange", action="store_true",
+                    help="N>1: rank r accumulates into rank r+1's partition (remote path, SURVEY 8(d) M2)")
     ap.add_argument("--tune", action="append", help="key=value tuning knob (gaamd_set_tuning)")
     args = ap.parse_args()
 
@@ -338,7 +365,9 @@ def main():
         "dtype": "f64" if r["op"] == DBL else "c128",
         "data": "synthetic (splitmix64, SURVEY.md 8(d)); device-resident src+dst, %d rotating buffer sets" % args.sets,
         "config": {"workload": args.workload, "patch": r["desc"], "payload_bytes": r["payload"],
-                   "algorithmic_bytes_per_step": alg, "parallelism": f"owner-aligned x{n} (no collective)",
+                   "algorithmic_bytes_per_step": alg,
+                   "parallelism": (f"exchange x{n}: rank r -> rank r+1, pack + owner unpack-acc over xGMI"
+                                   if r["exchange"] else f"owner-aligned x{n} (no collective)"),
                    "kernel": r["launch"]},
         "payload_GiB_per_s": round(value / 3, 2),
         "hbm_peak_frac": round(value * 2 ** 30 / (dist.size * HBM_PEAK_GBS * 1e9), 4),   # per GPU
@@ -348,6 +377,11 @@ def main():
                      "timing": "HIP event pair on the library stream around the timed launches / steps"},
         "cpu_baseline": cpu,
     }
+    if r["exchange"]:
+        # the kernels run on the owners' streams: no single-kernel roofline; the
+        # per-step time is the whole exchange (pack, hand-off, unpack-acc)
+        line["roofline"] = None
+        line["exchange_achieved_GBps_per_rank"] = round(achieved, 1)
     if "host" in r:
         line["host_inclusive_GiB_per_s"] = {k: round(v, 2) for k, v in r["host"].items()}
     print(json.dumps(line), flush=True)
