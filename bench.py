@@ -14,11 +14,15 @@ payload, 192 MiB of algorithmic HBM traffic (src read + dst read + dst write,
 
 value = whole-job algorithmic traffic GiB/s = ranks * steps * bytes / max-over-
 ranks wall time.  roofline.achieved = the same algorithmic bytes per launch /
-the average launch duration, from ONE HIP event pair recorded on the library's
-stream around the K timed launches (per-launch event pairs slowed the kernels
-by ~8 %; profiles/r01/gapprobe_H.json), so it includes the kernel-boundary gap;
-the rocprofv3 --kernel-trace --stats summary of the same command is committed
-under profiles/ and its average duration agrees.  roofline.traffic = HBM bytes
+the average launch duration, from ONE HIP event pair around the K timed
+launches (all library streams joined to it; per-launch event pairs slowed the
+kernels by ~8 %; profiles/r01/gapprobe_H.json), so it includes the
+kernel-boundary gap.  The library runs independent accumulates on two HIP
+streams (ga_amd/csrc/sched.cpp), so consecutive launches overlap at their
+edges: the rocprofv3 --kernel-trace summary of the same command is committed
+under profiles/, and the per-launch time it agrees with is the merged busy time
+of the dispatches / dispatches (tools/kernel_union.py), not AverageNs, which
+counts shared time twice.  roofline.traffic = HBM bytes
 per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE (tools/pmc_traffic.py,
 profiles/pmc_latest.json).  cpu_baseline = the reference's own _acc
 (oracle/_ref, compiled from comex/src-common/acc.h) driven per row by P host
@@ -197,6 +201,7 @@ def run_gpu(args, dist):
     ga_amd.sync()
     t0 = time.perf_counter()
     L.gaamd_event_record(ev0, stream)
+    L.gaamd_join()                      # every library stream starts after ev0
     for i in range(args.steps):
         step(args.warmup + i)
     L.gaamd_join()                      # the primary stream waits for the library's other streams
@@ -215,7 +220,7 @@ def run_gpu(args, dist):
         avg_kernel_s = elapsed / args.steps   # the work runs on the owners' streams
 
     res = dict(op=op, desc=desc, payload=payload, alg_bytes=alg_bytes, elems=elems, elapsed=elapsed,
-               avg_kernel_s=avg_kernel_s, launch=launch)
+               avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams())
     if args.host_rates and dist.rank == 0:
         res["host"] = host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_bytes)
     for s, d in sets:
@@ -374,7 +379,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel_ms_avg": round(r["avg_kernel_s"] * 1e3, 4),
-                     "timing": "HIP event pair on the library stream around the timed launches / steps"},
+                     "timing": "HIP event pair around the timed launches (all library streams joined) / steps",
+                     "streams": r["streams"]},
         "cpu_baseline": cpu,
     }
     if r["exchange"]:

@@ -867,7 +867,7 @@ int comex_init() {
     GA_HIP(hipStreamCreateWithFlags(&r.stream, hipStreamDefault));
     {
         const char *ns = getenv("COMEX_AMD_STREAMS");
-        sched_init(ns ? atoi(ns) : 1);
+        sched_init(ns ? atoi(ns) : 2);   // 2: independent ops overlap kernel edges
     }
     for (int i = 0; i < kMaxNb; ++i) GA_HIP(hipEventCreateWithFlags(&r.nb_ev[i], hipEventDisableTiming));
     const char *bs = getenv("COMEX_AMD_BLOCKING_SYNC");

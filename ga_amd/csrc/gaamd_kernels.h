@@ -60,13 +60,14 @@ struct Tuning {
     int kind = KK_AUTO;     // force a kernel family
     int unroll16 = 1;       // vectors per thread for the W=16 rows kernels {1,2,4,8}
     int nontemporal = 1;    // nt loads/stores on the rows kernels (streamed once)
-    int block = 256;        // threads per block {256, 512}
+    int block = 128;        // threads per block of the rows kernels {64, 128, 256, 512}
     int flat_max_nvec = 127;// rows with at most this many vectors use the flat kernel
     int max_grid = 0;       // cap on blocks (0 = one block per work item)
     int align = 0;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses
     int cpol = 0;           // f64 2-D kernel via buffer ops: load | store<<8 cache bits (0 = off)
     int xcd = 0;            // f64 2-D kernel: XCD-contiguous work ranges (experiment)
     int order = 0;          // f64 2-D kernel: 1 chunk-major, 2 scattered rows (experiment)
+    int direct = 1;         // 2-D rows of whole chunks: loop-free one-block-per-chunk kernel
 };
 Tuning &tuning();
 

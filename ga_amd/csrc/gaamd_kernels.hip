@@ -247,6 +247,35 @@ __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
     }
 }
 
+// DIRECT 2-D kernel: the common case of ROWS2 where every row is a whole number
+// of chunks and the grid has one block per chunk -- no loop, no bounds test, and
+// one kernel-argument fetch (s_load_dwordx8 + x4 issued together before the
+// first wait).  ROWS2 fetches its loop bound first and the rest after a wait:
+// one more scalar-cache round trip at the head of each of the 64 Ki waves of a
+// headline launch, which measured 2-3 % of the launch (tools/hbm_ceiling.hip
+// vs k_rows2).
+struct Desc2D {
+    const char *src;
+    char *dst;
+    int64_t s_str, d_str;
+    FastDiv chunk_div;   // chunks per row
+    uint32_t row0;
+};
+
+template <class OP, int W, int BS>
+__global__ __launch_bounds__(BS) void k_rows2d(const Desc2D d, const OP op) {
+    const uint32_t w = blockIdx.x;
+    const uint32_t rl = d.chunk_div.div(w);
+    const uint32_t chunk = w - rl * d.chunk_div.d;
+    const int64_t r = (int64_t)(d.row0 + rl);
+    const int64_t v = (int64_t)chunk * BS + threadIdx.x;
+    const char *sp = d.src + r * d.s_str + v * W;
+    char *dp = d.dst + r * d.d_str + v * W;
+    typename Vec<W>::T a = vload<W, true>(sp), b = a;
+    if constexpr (OP::kReadsDst) b = vload<W, true>(dp);
+    vstore<W, true>(dp, op.template apply<W>(b, a));
+}
+
 // ROWS2 with a different block -> (row, chunk) order (tuning experiment on the
 // f64 2-D kernel; which rows are in flight together decides how the traffic
 // spreads over HBM channels):
@@ -384,6 +413,21 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
     e.chunk_div = d.chunk_div;
     e.align_mask = d.align_mask;
     e.xcd_per = 0;
+    if constexpr (U == 1) {
+        // whole chunks, one block each, nt on, no experiment knob active
+        if (g_tuning.direct && nt && !d.align_mask && blocks == e.items && d.nvec % (uint32_t)BS == 0 &&
+            !g_tuning.cpol && !g_tuning.xcd && !g_tuning.order) {
+            Desc2D f;
+            f.src = d.src;
+            f.dst = d.dst;
+            f.s_str = e.s_str;
+            f.d_str = e.d_str;
+            f.chunk_div = d.chunk_div;
+            f.row0 = d.row0;
+            hipLaunchKernelGGL((k_rows2d<OP, W, BS>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
+            return hipGetLastError();
+        }
+    }
     if constexpr (W == 16 && U == 1 && BS == 256 && std::is_same<OP, AccDbl>::value) {
         if ((g_tuning.order == 1 || g_tuning.order == 2) && nt && !d.align_mask && blocks == e.items) {
             const uint32_t rows = e.items / e.chunks;
@@ -421,12 +465,18 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
     return hipGetLastError();
 }
 
-template <class OP, int W, int LV>
+template <class OP, int W, int LV, int BS>
 static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, int nt, hipStream_t st) {
     constexpr int U = DefaultU<W>::value;
-    if (nt) hipLaunchKernelGGL((k_rows<OP, W, U, 256, true, LV>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
-    else hipLaunchKernelGGL((k_rows<OP, W, U, 256, false, LV>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+    if (nt) hipLaunchKernelGGL((k_rows<OP, W, U, BS, true, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, d, op);
+    else hipLaunchKernelGGL((k_rows<OP, W, U, BS, false, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, d, op);
     return hipGetLastError();
+}
+template <class OP, int W, int LV>
+static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, int BS, int nt, hipStream_t st) {
+    if (BS == 64) return go_rows_nd<OP, W, LV, 64>(d, op, blocks, nt, st);
+    if (BS == 128) return go_rows_nd<OP, W, LV, 128>(d, op, blocks, nt, st);
+    return go_rows_nd<OP, W, LV, 256>(d, op, blocks, nt, st);
 }
 
 template <class OP, int W>
@@ -449,18 +499,27 @@ static hipError_t dispatch_w(int kind, int U, int BS, int nt, const Desc &d, con
                 hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 0>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
             return hipGetLastError();
         }
-        if (d.levels == 2) return go_rows_nd<OP, W, 2>(d, op, blocks, nt, st);
-        if (d.levels == 3) return go_rows_nd<OP, W, 3>(d, op, blocks, nt, st);
-        if (d.levels > 3) return go_rows_nd<OP, W, 0>(d, op, blocks, nt, st);
+        if (d.levels == 2) return go_rows_nd<OP, W, 2>(d, op, blocks, BS, nt, st);
+        if (d.levels == 3) return go_rows_nd<OP, W, 3>(d, op, blocks, BS, nt, st);
+        if (d.levels > 3) return go_rows_nd<OP, W, 0>(d, op, blocks, BS, nt, st);
         if constexpr (W == 16 && Tunable<OP>::value) {
-            if (BS == 512) {
-                if (U == 2) return go_rows2<OP, W, 2, 512>(d, op, blocks, nt, st);
-                return go_rows2<OP, W, 1, 512>(d, op, blocks, nt, st);
+#define GAAMD_U(B) \
+    switch (U) { \
+    case 1: return go_rows2<OP, W, 1, B>(d, op, blocks, nt, st); \
+    case 2: return go_rows2<OP, W, 2, B>(d, op, blocks, nt, st); \
+    case 4: return go_rows2<OP, W, 4, B>(d, op, blocks, nt, st); \
+    case 8: return go_rows2<OP, W, 8, B>(d, op, blocks, nt, st); \
+    }
+            switch (BS) {
+            case 64: GAAMD_U(64) break;
+            case 128: GAAMD_U(128) break;
+            case 256: GAAMD_U(256) break;
+            case 512: GAAMD_U(512) break;
             }
-            if (U == 2) return go_rows2<OP, W, 2, 256>(d, op, blocks, nt, st);
-            if (U == 4) return go_rows2<OP, W, 4, 256>(d, op, blocks, nt, st);
-            if (U == 8) return go_rows2<OP, W, 8, 256>(d, op, blocks, nt, st);
+#undef GAAMD_U
         }
+        if (BS == 64) return go_rows2<OP, W, DefaultU<W>::value, 64>(d, op, blocks, nt, st);
+        if (BS == 128) return go_rows2<OP, W, DefaultU<W>::value, 128>(d, op, blocks, nt, st);
         return go_rows2<OP, W, DefaultU<W>::value, 256>(d, op, blocks, nt, st);
     }
 }
@@ -632,10 +691,15 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     if (kind == KK_AUTO) kind = ((int64_t)d.nvec <= tn.flat_max_nvec) ? KK_FLAT : KK_ROWS;
     // the (U, BS) the dispatcher will pick -- chunking must agree with it
     const bool tunable = (op == kOpCopy || op == 38 || op == 41);
-    int U = unroll_for(W, 1), BS = 256;
+    // rows kernels: 128-thread blocks by default.  Small blocks retire and free
+    // their CU slots independently; on the headline shape 64/128/256/512/1024
+    // threads measured 6382/6307/6192/6046/5992 GB/s in a stand-alone probe
+    // (tools/h_shape_probe.hip) and 128 led 64 and 256 by 1-3 % in the library
+    // (profiles/r01/sweep_block*.jsonl).  512 only on the tunable 2-D path.
+    int U = unroll_for(W, 1), BS = (tn.block == 512) ? 256 : tn.block;
     if (kind == KK_ROWS && L <= 1 && W == 16 && tunable) {
         U = tn.unroll16;
-        if (tn.block == 512 && U <= 2) BS = 512;
+        BS = tn.block;
     }
     const uint32_t per_chunk = (uint32_t)BS * (uint32_t)U;
     d.align_mask = 0;

@@ -113,6 +113,7 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "cpol")) return &t.cpol;
     if (!strcmp(key, "xcd")) return &t.xcd;
     if (!strcmp(key, "order")) return &t.order;
+    if (!strcmp(key, "direct")) return &t.direct;
     return nullptr;
 }
 
@@ -128,7 +129,7 @@ int gaamd_set_tuning(const char *key, int value) {
     int *f = tuning_field(key);
     if (!f) return -1;
     if (!strcmp(key, "unroll16") && value != 1 && value != 2 && value != 4 && value != 8) return -1;
-    if (!strcmp(key, "block") && value != 256 && value != 512) return -1;
+    if (!strcmp(key, "block") && value != 64 && value != 128 && value != 256 && value != 512) return -1;
     const int old = *f;
     *f = value;
     return old;

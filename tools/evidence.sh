@@ -3,7 +3,9 @@
 #   1. PMC HBM traffic of the H kernel (two separate rocprofv3 --pmc passes)
 #   2. bench.py default line (N=1, workload H, CPU baseline included)
 #   3. bench lines for the other single-GPU configs (C2, C3, C4, H8200)
-#   4. rocprofv3 --kernel-trace --stats of the same bench command (no CPU leg)
+#   4. rocprofv3 --kernel-trace --stats of the same bench command (no CPU leg);
+#      merged per-launch busy time from the trace (tools/kernel_union.py), and
+#      the same profile with one library stream
 # Each GPU step has its own time limit; the first failure ends the script.
 # Summaries land in gpurun_out/evidence/ (copy into profiles/<TAG>/ afterwards).
 set -euo pipefail
@@ -22,4 +24,10 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
     python3 bench.py --no-cpu > "$OUT/bench_H_prof.json" 2> "$OUT/bench_H_prof.err"
 find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/rocprofv3_kernel_stats_H.csv" \;
+find "$OUT/prof" -name '*kernel_trace.csv' -exec cp {} "$OUT/rocprofv3_kernel_trace_H.csv" \;
+python3 tools/kernel_union.py "$OUT/rocprofv3_kernel_trace_H.csv" --json "$OUT/kernel_union_H.json"
+# the same with one library stream: per-dispatch AverageNs is then the launch time
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof1" -o bench -- \
+    python3 bench.py --no-cpu --tune streams=1 > "$OUT/bench_H_prof_1stream.json" 2> "$OUT/bench_H_prof_1stream.err"
+find "$OUT/prof1" -name '*kernel_stats.csv' -exec cp {} "$OUT/rocprofv3_kernel_stats_H_1stream.csv" \;
 echo done
