@@ -99,6 +99,29 @@ static void check_remote(int owner, const void *p, int64_t lo, int64_t hi) {
         fatal("address %p [%ld,%ld) of rank %d is not inside a comex_malloc segment", p, (long)lo, (long)hi, owner);
 }
 
+// Map a same-node peer's HBM (IPC handle).  A failure is not fatal here: a job
+// that never touches that peer's memory (owner-aligned accumulates, the weak-
+// scaling bench) runs on; the first operation that needs the mapping aborts with
+// this diagnosis (remote_view / the progress thread).
+static void *ipc_open(hipIpcMemHandle_t h, int q, const char *what) {
+    void *p = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        fprintf(stderr, "ga_amd rank %d: cannot map rank %d's %s over IPC (%s); operations that need it will "
+                "abort (HSA_ENABLE_IPC_MODE_LEGACY=0 is required for dmabuf IPC)\n", rt().rank, q, what,
+                hipGetErrorString(e));
+        return nullptr;
+    }
+    return p;
+}
+
+static const char *peer_staging_or_die(int src) {
+    const char *p = rt().peer_staging[src];
+    if (!p) fatal("rank %d's staging buffer is not mapped here (IPC open failed at comex_init)", src);
+    return p;
+}
+
 // address of rank `owner`'s byte `p` (owner's address space) in this process
 static char *remote_view(int owner, const void *p, int64_t lo, int64_t hi) {
     Runtime &r = rt();
@@ -108,7 +131,8 @@ static char *remote_view(int owner, const void *p, int64_t lo, int64_t hi) {
         if (!s.live) continue;
         const PeerMap &m = s.peer[owner];
         if (m.bytes && a + lo >= m.base && a + hi <= m.base + m.bytes) {
-            if (!m.mapped) fatal("rank %d is on another node: its memory is not mapped here", owner);
+            if (!m.mapped)
+                fatal("rank %d's segment is not mapped here (another node, or its IPC open failed)", owner);
             return m.mapped + (a - m.base);
         }
     }
@@ -393,7 +417,7 @@ static void progress_loop() {
         if (q.state.load(std::memory_order_acquire) == 2 && q.kind == 1) {
             // io-vector accumulate (the _acc_iov_handler analogue, comex.c:4284-4397)
             const int src = q.src_rank;
-            const char *packed = r.peer_staging[src] + q.staging_off;
+            const char *packed = peer_staging_or_die(src) + q.staging_off;
             IovDesc d;
             memset(&d, 0, sizeof(d));
             d.src_base = packed;
@@ -419,7 +443,7 @@ static void progress_loop() {
             worked = true;
         } else if (q.state.load(std::memory_order_acquire) == 2) {
             const int src = q.src_rank;
-            const char *packed = r.peer_staging[src] + q.staging_off;
+            const char *packed = peer_staging_or_die(src) + q.staging_off;
             const uint64_t rb = q.seq >> 32, re = q.seq & 0xffffffffull;
             int pstride[8];
             {
@@ -888,9 +912,7 @@ int comex_init() {
         for (int q = 0; q < r.size; ++q) {
             if (q == r.rank) { r.peer_staging[q] = r.staging; continue; }
             if (!r.same_node(q)) continue;   // another node: reached through wire.cpp
-            void *p = nullptr;
-            GA_HIP(hipIpcOpenMemHandle(&p, all[q].h, hipIpcMemLazyEnablePeerAccess));
-            r.peer_staging[q] = (char *)p;
+            r.peer_staging[q] = (char *)ipc_open(all[q].h, q, "staging buffer");
         }
         r.posted.assign(r.size, 0);
         r.stage_head.assign(r.size, 0);
@@ -1155,9 +1177,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
             s.peer[q].mapped = (char *)p;
         } else if (all[q].bytes && r.same_node(q)) {
             if (!device) fatal("host-memory segments are rank-private (use device segments for remote access)");
-            void *m = nullptr;
-            GA_HIP(hipIpcOpenMemHandle(&m, all[q].h, hipIpcMemLazyEnablePeerAccess));
-            s.peer[q].mapped = (char *)m;
+            s.peer[q].mapped = (char *)ipc_open(all[q].h, q, "segment");
         }
     }
     {
