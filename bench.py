@@ -61,6 +61,13 @@ WORKLOADS = {
     "C4": (DCP, [4096, 256, 256], [4096, 1048576], [4224, 1115136],
            "3-D double-complex 256^3 patch, dst in 264x264x256 (256 MiB)"),
 }
+# C5: GA_Acc into a block-distributed 32768^2 f64 array (GA's REGULAR
+# distribution, NGA_Create).  M1 (default): every rank NGA_Acc's its own block
+# from a device-resident local buffer (owner-aligned, no exchange).  --exchange
+# (M2): every rank NGA_Acc's the WHOLE array, so (p-1)/p of its patch goes to
+# the other owners (pack -> owner's unpack-acc over xGMI).  SURVEY.md 8(d) C5.
+GA_DIMS = [32768, 32768]
+C_DBL = 1004
 ESZ = {DBL: 8, DCP: 16}
 SCALE = {DBL: 0.7071067811865476, DCP: 0.6 - 0.8j}
 
@@ -129,14 +136,89 @@ class Dist:
 
 
 # ---------------------------------------------------------------- GPU leg
-def run_gpu(args, dist):
-    import ga_amd
-    L = ga_amd.lib()
+def bootstrap(L, dist):
     if dist.size > 1:
         ag, bar = dist.hooks()
         rc = L.gaamd_set_bootstrap(dist.rank, dist.size, dist.local_rank, ctypes.cast(ag, ctypes.c_void_p),
                                    ctypes.cast(bar, ctypes.c_void_p), None)
         assert rc == 0, rc
+
+
+def run_ga(args, dist):
+    """C5: NGA_Acc (include/ga.h; reference capi.c:2079 -> ngai_acc_common,
+    global/src/onesided.c:1334) on a 32768^2 f64 GA."""
+    import ga_amd
+    L = ga_amd.lib()
+    bootstrap(L, dist)
+    assert L.GA_Initialize() == 0
+    ia = ga_amd.int_array
+    g = L.NGA_Create(C_DBL, 2, ia(GA_DIMS), b"C5", None)
+    assert g > 0
+    blo, bhi = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
+    L.NGA_Distribution(g, dist.rank, blo, bhi)
+    exchange = args.exchange and dist.size > 1
+    lo, hi = ([0, 0], [GA_DIMS[0] - 1, GA_DIMS[1] - 1]) if exchange else (list(blo), list(bhi))
+    rows, cols = hi[0] - lo[0] + 1, hi[1] - lo[1] + 1
+    payload = rows * cols * 8
+    src = ga_amd.DeviceBuffer(payload)
+    ga_amd.fill(src.ptr, rows * cols, 0, 0x5EED0000 + dist.rank)
+    # the local block: fill through NGA_Access (its HBM address)
+    ptr, ld = ctypes.c_void_p(), (ctypes.c_int * 1)()
+    L.NGA_Access(g, blo, bhi, ctypes.byref(ptr), ld)
+    ga_amd.fill(ptr.value, (bhi[0] - blo[0] + 1) * (bhi[1] - blo[1] + 1), 0, 0x5EED0001 + dist.rank)
+    L.NGA_Release_update(g, blo, bhi)
+    ga_amd.sync()
+    L.GA_Sync()
+    grid = (ctypes.c_int * 2)()
+    L.GA_Get_proc_grid(g, grid)
+    alpha = ctypes.c_double(SCALE[DBL])
+    clo, chi, cld = ia(lo), ia(hi), ia([cols])
+    stream = L.gaamd_stream()
+
+    def step():
+        L.NGA_Acc(g, clo, chi, ctypes.c_void_p(src.ptr), cld, ctypes.byref(alpha))
+
+    for _ in range(args.warmup):
+        step()
+    ga_amd.sync()
+    L.GA_Sync()
+    launch = ga_amd.last_launch()
+    ev0, ev1 = L.gaamd_event_create(), L.gaamd_event_create()
+    dist.barrier()
+    ga_amd.sync()
+    t0 = time.perf_counter()
+    L.gaamd_event_record(ev0, stream)
+    L.gaamd_join()
+    for _ in range(args.steps):
+        step()
+    L.gaamd_join()
+    L.gaamd_event_record(ev1, stream)
+    ga_amd.sync()
+    if exchange:
+        L.GA_Sync()                     # every owner has applied every contribution
+    t1 = time.perf_counter()
+    dist.barrier()
+    elapsed = dist.max(t1 - t0)
+    region_ms = L.gaamd_event_elapsed_ms(ev0, ev1)
+    L.gaamd_event_destroy(ev0)
+    L.gaamd_event_destroy(ev1)
+    avg_kernel_s = dist.max(region_ms / 1e3 / args.steps) if not exchange else elapsed / args.steps
+    src.free()
+    L.GA_Sync()
+    L.GA_Destroy(g)
+    L.GA_Terminate()
+    desc = (f"GA_Acc, 32768^2 f64 GA on a {grid[0]}x{grid[1]} grid, "
+            + ("every rank the whole array (M2)" if exchange else f"own {rows}x{cols} block (M1)"))
+    return dict(op=DBL, desc=desc, payload=payload, alg_bytes=3 * payload, elems=rows * cols, elapsed=elapsed,
+                avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), exchange=exchange)
+
+
+def run_gpu(args, dist):
+    import ga_amd
+    L = ga_amd.lib()
+    if args.workload == "C5":
+        return run_ga(args, dist)
+    bootstrap(L, dist)
     assert ga_amd.comex_init() == 0
     for kv in args.tune or []:
         k, v = kv.split("=")
@@ -333,7 +415,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", default="H", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="H", choices=sorted(WORKLOADS) + ["C5"])
     ap.add_argument("--sets", type=int, default=8, help="rotating buffer sets (MALL defeat)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=8, help="host workers of the CPU baseline")
@@ -354,7 +436,7 @@ def main():
     achieved = alg / r["avg_kernel_s"] / 1e9
     traffic = load_traffic(args.workload, alg)
     cpu = None
-    if not args.no_cpu and n == 1:
+    if not args.no_cpu and n == 1 and args.workload != "C5":
         cpu = run_cpu_baseline(args.workload, args.cpu_seconds, args.cpu_threads)
     line = {
         "metric": METRIC,
@@ -371,7 +453,9 @@ def main():
         "data": "synthetic (splitmix64, SURVEY.md 8(d)); device-resident src+dst, %d rotating buffer sets" % args.sets,
         "config": {"workload": args.workload, "patch": r["desc"], "payload_bytes": r["payload"],
                    "algorithmic_bytes_per_step": alg,
-                   "parallelism": (f"exchange x{n}: rank r -> rank r+1, pack + owner unpack-acc over xGMI"
+                   "parallelism": (("GA_Acc of the whole array by every rank: pack + owner unpack-acc over xGMI"
+                                    if args.workload == "C5" else
+                                    f"exchange x{n}: rank r -> rank r+1, pack + owner unpack-acc over xGMI")
                                    if r["exchange"] else f"owner-aligned x{n} (no collective)"),
                    "kernel": r["launch"]},
         "payload_GiB_per_s": round(value / 3, 2),

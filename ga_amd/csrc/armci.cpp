@@ -45,6 +45,18 @@ static int contiguous_bytes(int *count, int stride_levels) {
     return (int)lcount;   // the reference's int product (armci.c:231-233)
 }
 
+// The reference collapses a contiguous patch to one comex_acc/put/get of
+// (int)prod(count) bytes (armci.c:231-233); above 2 GiB that product wraps and
+// the call moves the wrong number of bytes.  Patches
+// that large -- a whole 8 GiB GA block of a 32768^2 f64 array on one GPU -- keep
+// the strided path instead, which computes what the collapse means.
+static bool collapse(int *ss, int *ds, int *count, int levels) {
+    if (!armci_check_contiguous(ss, ds, count, levels)) return false;
+    long lcount = 1;
+    for (int i = 0; i <= levels; ++i) lcount *= count[i];
+    return lcount <= 2147483647L;
+}
+
 int PARMCI_Init() { return comex_init(); }
 int PARMCI_Init_args(int *argc, char ***argv) { return comex_init_args(argc, argv); }
 int PARMCI_Initialized() { return comex_initialized(); }
@@ -58,7 +70,7 @@ int PARMCI_Put(void *src, void *dst, int bytes, int proc) {
     return comex_put(src, dst, bytes, proc, COMEX_GROUP_WORLD);
 }
 int PARMCI_PutS(void *src, int *ss, void *dst, int *ds, int *count, int levels, int proc) {
-    if (armci_check_contiguous(ss, ds, count, levels))
+    if (collapse(ss, ds, count, levels))
         return comex_put(src, dst, contiguous_bytes(count, levels), proc, COMEX_GROUP_WORLD);
     return comex_puts(src, ss, dst, ds, count, levels, proc, COMEX_GROUP_WORLD);
 }
@@ -66,7 +78,7 @@ int PARMCI_Acc(int op, void *scale, void *src, void *dst, int bytes, int proc) {
     return comex_acc(op, scale, src, dst, bytes, proc, COMEX_GROUP_WORLD);
 }
 int PARMCI_AccS(int op, void *scale, void *src, int *ss, void *dst, int *ds, int *count, int levels, int proc) {
-    if (armci_check_contiguous(ss, ds, count, levels))
+    if (collapse(ss, ds, count, levels))
         return comex_acc(op, scale, src, dst, contiguous_bytes(count, levels), proc, COMEX_GROUP_WORLD);
     return comex_accs(op, scale, src, ss, dst, ds, count, levels, proc, COMEX_GROUP_WORLD);
 }
@@ -74,7 +86,7 @@ int PARMCI_Get(void *src, void *dst, int bytes, int proc) {
     return comex_get(src, dst, bytes, proc, COMEX_GROUP_WORLD);
 }
 int PARMCI_GetS(void *src, int *ss, void *dst, int *ds, int *count, int levels, int proc) {
-    if (armci_check_contiguous(ss, ds, count, levels))
+    if (collapse(ss, ds, count, levels))
         return comex_get(src, dst, contiguous_bytes(count, levels), proc, COMEX_GROUP_WORLD);
     return comex_gets(src, ss, dst, ds, count, levels, proc, COMEX_GROUP_WORLD);
 }
@@ -108,13 +120,13 @@ int PARMCI_NbPut(void *src, void *dst, int bytes, int proc, armci_hdl_t *h) {
     return comex_nbput(src, dst, bytes, proc, COMEX_GROUP_WORLD, h);
 }
 int PARMCI_NbPutS(void *src, int *ss, void *dst, int *ds, int *count, int levels, int proc, armci_hdl_t *h) {
-    if (armci_check_contiguous(ss, ds, count, levels))
+    if (collapse(ss, ds, count, levels))
         return comex_nbput(src, dst, contiguous_bytes(count, levels), proc, COMEX_GROUP_WORLD, h);
     return comex_nbputs(src, ss, dst, ds, count, levels, proc, COMEX_GROUP_WORLD, h);
 }
 int PARMCI_NbAccS(int op, void *scale, void *src, int *ss, void *dst, int *ds, int *count, int levels, int proc,
                   armci_hdl_t *h) {
-    if (armci_check_contiguous(ss, ds, count, levels))
+    if (collapse(ss, ds, count, levels))
         return comex_nbacc(op, scale, src, dst, contiguous_bytes(count, levels), proc, COMEX_GROUP_WORLD, h);
     return comex_nbaccs(op, scale, src, ss, dst, ds, count, levels, proc, COMEX_GROUP_WORLD, h);
 }
@@ -122,7 +134,7 @@ int PARMCI_NbGet(void *src, void *dst, int bytes, int proc, armci_hdl_t *h) {
     return comex_nbget(src, dst, bytes, proc, COMEX_GROUP_WORLD, h);
 }
 int PARMCI_NbGetS(void *src, int *ss, void *dst, int *ds, int *count, int levels, int proc, armci_hdl_t *h) {
-    if (armci_check_contiguous(ss, ds, count, levels))
+    if (collapse(ss, ds, count, levels))
         return comex_nbget(src, dst, contiguous_bytes(count, levels), proc, COMEX_GROUP_WORLD, h);
     return comex_nbgets(src, ss, dst, ds, count, levels, proc, COMEX_GROUP_WORLD, h);
 }

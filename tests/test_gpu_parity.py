@@ -246,6 +246,35 @@ def test_full_size_integer_roundtrip(gpu_lib):
     assert mid != before and after == before
 
 
+def test_armci_contiguous_patch_over_2GiB(gpu_lib):
+    """ARMCI_AccS on a contiguous patch of 2 GiB + 8 KiB: the reference's
+    collapse to one comex_acc of (int)prod(count) bytes would wrap (armci.c:231-233,
+    SURVEY appendix A.8); the library keeps the strided path.  int64 data, checked
+    exactly on the first, middle and last rows against the oracle."""
+    L = gpu_lib
+    rows, row = 8193, 262144                  # 8193 * 256 KiB = 2 GiB + 256 KiB
+    nbytes = rows * row
+    sb, db = ga_amd.DeviceBuffer(nbytes), ga_amd.DeviceBuffer(nbytes)
+    try:
+        _fill_device(sb, C.LNG, nbytes, 3)
+        _fill_device(db, C.LNG, nbytes, 4)
+        ga_amd.sync()
+        probe = [0, rows // 2, rows - 1]
+        s_rows = {r: sb.download(np.int64, row // 8, r * row) for r in probe}
+        d_rows = {r: db.download(np.int64, row // 8, r * row) for r in probe}
+        keep, sp = ga_amd.scale_buffer(C.LNG, -5)
+        rc = L.ARMCI_AccS(C.LNG, sp, ctypes.c_void_p(sb.ptr), ga_amd.int_array([row]), ctypes.c_void_p(db.ptr),
+                          ga_amd.int_array([row]), ga_amd.int_array([row, rows]), 1, 0)
+        assert rc == 0
+        ga_amd.comex_fence_all()
+        for r in probe:
+            want = (d_rows[r].astype(np.uint64) + s_rows[r].astype(np.uint64) * np.uint64(2 ** 64 - 5)).view(np.int64)
+            assert np.array_equal(db.download(np.int64, row // 8, r * row), want), r
+    finally:
+        sb.free()
+        db.free()
+
+
 def test_empty_patches_are_noops(gpu_lib):
     """count[j]=0 (j>=1) -> n1dim = 0 -> the reference loop runs zero times."""
     b = ga_amd.DeviceBuffer(64)
