@@ -152,12 +152,13 @@ def run_ga(args, dist):
     bootstrap(L, dist)
     assert L.GA_Initialize() == 0
     ia = ga_amd.int_array
-    g = L.NGA_Create(C_DBL, 2, ia(GA_DIMS), b"C5", None)
+    dims = [args.ga_dims, args.ga_dims] if args.ga_dims else GA_DIMS
+    g = L.NGA_Create(C_DBL, 2, ia(dims), b"C5", None)
     assert g > 0
     blo, bhi = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
     L.NGA_Distribution(g, dist.rank, blo, bhi)
     exchange = args.exchange and dist.size > 1
-    lo, hi = ([0, 0], [GA_DIMS[0] - 1, GA_DIMS[1] - 1]) if exchange else (list(blo), list(bhi))
+    lo, hi = ([0, 0], [dims[0] - 1, dims[1] - 1]) if exchange else (list(blo), list(bhi))
     rows, cols = hi[0] - lo[0] + 1, hi[1] - lo[1] + 1
     payload = rows * cols * 8
     src = ga_amd.DeviceBuffer(payload)
@@ -177,6 +178,8 @@ def run_ga(args, dist):
 
     def step():
         L.NGA_Acc(g, clo, chi, ctypes.c_void_p(src.ptr), cld, ctypes.byref(alpha))
+        if args.verbose:
+            print(f"rank {dist.rank}: NGA_Acc done", file=sys.stderr, flush=True)
 
     for _ in range(args.warmup):
         step()
@@ -207,7 +210,7 @@ def run_ga(args, dist):
     L.GA_Sync()
     L.GA_Destroy(g)
     L.GA_Terminate()
-    desc = (f"GA_Acc, 32768^2 f64 GA on a {grid[0]}x{grid[1]} grid, "
+    desc = (f"GA_Acc, {dims[0]}x{dims[1]} f64 GA on a {grid[0]}x{grid[1]} grid, "
             + ("every rank the whole array (M2)" if exchange else f"own {rows}x{cols} block (M1)"))
     return dict(op=DBL, desc=desc, payload=payload, alg_bytes=3 * payload, elems=rows * cols, elapsed=elapsed,
                 avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), exchange=exchange)
@@ -424,6 +427,8 @@ def main():
     ap.add_argument("--exchange", action="store_true",
                     help="N>1: rank r accumulates into rank r+1's partition (remote path, SURVEY 8(d) M2)")
     ap.add_argument("--tune", action="append", help="key=value tuning knob (gaamd_set_tuning)")
+    ap.add_argument("--ga-dims", type=int, default=0, help="C5: square GA of this size instead of 32768^2")
+    ap.add_argument("--verbose", action="store_true", help="progress lines on stderr")
     args = ap.parse_args()
 
     dist = Dist(args.gpus)

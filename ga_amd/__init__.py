@@ -139,6 +139,13 @@ def last_launch():
             "launches": n.value, "blocks": b.value}
 
 
+def kernel_counts():
+    """launches so far by kind (this process): {'rows': n, 'flat': n, 'serial': n}"""
+    c = (ctypes.c_ulonglong * 4)()
+    lib().gaamd_kernel_counts(c)
+    return {"rows": c[1], "flat": c[2], "serial": c[3]}
+
+
 def set_tuning(key, value):
     return lib().gaamd_set_tuning(key.encode(), int(value))
 

@@ -637,6 +637,11 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
                       kind == X_ACC ? "acc" : (kind == X_PUT ? "put" : "get"), rc);
         if (host_side || r.blocking_sync) sched_sync_all();
     }
+    if (r.debug)
+        fprintf(stderr, "[ga_amd %d] %s -> %d levels %d count0 %d rows %d: src %s dst %s stream %d\n", r.rank,
+                kind == X_ACC ? "acc" : (kind == X_PUT ? "put" : "get"), world, levels, count[0],
+                levels ? count[levels] : 1, sv.registered ? "registered" : (sv.staged ? "staged" : "device"),
+                dv.registered ? "registered" : (dv.staged ? "staged" : "device"), si);
     if (host_side) {
         release_view(sv);
         release_view(dv);
@@ -896,6 +901,8 @@ int comex_init() {
     for (int i = 0; i < kMaxNb; ++i) GA_HIP(hipEventCreateWithFlags(&r.nb_ev[i], hipEventDisableTiming));
     const char *bs = getenv("COMEX_AMD_BLOCKING_SYNC");
     r.blocking_sync = bs && atoi(bs) != 0;
+    const char *dbg = getenv("COMEX_AMD_DEBUG");
+    r.debug = dbg ? atoi(dbg) : 0;
     if (r.size > 1) {
         // staging HBM for remote accumulates, exported to every local rank
         const char *mb = getenv("COMEX_AMD_STAGING_MB");
@@ -1154,6 +1161,13 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     if (bytes) {
         if (device) {
             GA_HIP(hipMalloc(&p, bytes));
+            if (r.debug) {
+                void *base = nullptr;
+                size_t sz = 0;
+                (void)hipMemGetAddressRange((hipDeviceptr_t *)&base, &sz, (hipDeviceptr_t)p);
+                fprintf(stderr, "[ga_amd %d] segment %p (%zu B): allocation base %p size %zu\n", r.rank, p,
+                        bytes, base, sz);
+            }
             if (r.size > 1) GA_HIP(hipIpcGetMemHandle(&mine.h, p));
         } else {
             GA_HIP(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));

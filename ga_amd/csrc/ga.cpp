@@ -510,9 +510,11 @@ void GA_Zero(int g_a) {
     Runtime &r = rt();
     long lo[GA_MAX_DIM], hi[GA_MAX_DIM];
     const long n = block_elems(a, r.rank, lo, hi);
-    comex_fence_all(COMEX_GROUP_WORLD);
-    if (n) GA_HIP(hipMemsetAsync(a.ptr[r.rank], 0, (size_t)n * a.elemsize, r.stream));
+    // pnga_zero (global.nalg.c:60-90) is collective and syncs first: no rank may
+    // zero its block while another still reads or writes it
     comex_barrier(COMEX_GROUP_WORLD);
+    if (n) GA_HIP(hipMemsetAsync(a.ptr[r.rank], 0, (size_t)n * a.elemsize, r.stream));
+    comex_barrier(COMEX_GROUP_WORLD);   // fences (syncs every library stream) + barrier
 }
 
 void NGA_Distribution(int g_a, int iproc, int lo[], int hi[]) {

@@ -93,6 +93,7 @@ void side_span_host(const int *stride, const int *count, int stride_levels, int6
 
 int elem_size(int op);            // bytes per element for op; 1 for copy; 0 if unknown
 LaunchInfo *last_launch_info();   // most recent launch_strided (any caller)
+unsigned long long kernel_count(int kind);   // launch_strided launches so far, by KernelKind
 
 // I/O-vector descriptor: n pairs of `bytes`; a side is a device array of n
 // addresses (list) or, when the list is null, base + i*bytes (packed)

@@ -31,6 +31,7 @@
 #include <string.h>
 #include <algorithm>
 #include <type_traits>
+#include <atomic>
 
 namespace gaamd {
 
@@ -48,6 +49,8 @@ FastDiv make_fastdiv(uint32_t d) {
 
 static Tuning g_tuning;
 Tuning &tuning() { return g_tuning; }
+static std::atomic<unsigned long long> g_kind_count[4];
+unsigned long long kernel_count(int kind) { return (kind >= 0 && kind < 4) ? g_kind_count[kind].load() : 0; }
 
 int elem_size(int op) {
     switch (op) {
@@ -581,6 +584,39 @@ static void side_span(const int64_t *str, const uint32_t *cnt, int L, int64_t ro
     }
 }
 
+// Byte span [lo, hi) of rows [rb, re) of one side (re > rb).  Digits of the
+// levels above the highest level k where rb and re-1 differ are fixed; the
+// level-k digit runs monotonically from digit_k(rb) to digit_k(re-1); the
+// levels below k may take any value.  Exact for one level, a tight bound above.
+static void range_span(const int64_t *str, const uint32_t *cnt, int L, int64_t row_bytes, uint64_t rb, uint64_t re,
+                       int64_t &lo, int64_t &hi) {
+    uint32_t da[kMaxLevels], db[kMaxLevels];
+    uint64_t a = rb, b = re - 1;
+    for (int j = 0; j < L; ++j) {
+        const uint32_t c = cnt[j] ? cnt[j] : 1;
+        da[j] = (uint32_t)(a % c);
+        db[j] = (uint32_t)(b % c);
+        a /= c;
+        b /= c;
+    }
+    int k = -1;
+    for (int j = L - 1; j >= 0; --j)
+        if (da[j] != db[j]) { k = j; break; }
+    int64_t base = 0;
+    for (int j = k + 1; j < L; ++j) base += (int64_t)da[j] * str[j];
+    lo = base;
+    hi = base + row_bytes;
+    if (k >= 0) {
+        const int64_t e0 = (int64_t)da[k] * str[k], e1 = (int64_t)db[k] * str[k];
+        lo += std::min(e0, e1);
+        hi += std::max(e0, e1);
+        for (int j = 0; j < k; ++j) {
+            const int64_t e = str[j] * (int64_t)(cnt[j] ? cnt[j] - 1 : 0);
+            if (e < 0) lo += e; else hi += e;
+        }
+    }
+}
+
 void side_span_host(const int *stride, const int *count, int stride_levels, int64_t row_bytes,
                     int64_t *lo, int64_t *hi) {
     int64_t str[kMaxLevels];
@@ -632,9 +668,13 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     const bool dst_overlap = rows_may_overlap(ds, cn, L, row_bytes);
     bool src_dst_overlap = false;
     {
+        // spans of the rows this call touches: a chunked caller (remote pack /
+        // unpack-acc) passes a row range and a packed base rebased so that row
+        // row_begin lands at its slice -- the full-range span of such a side
+        // reaches far outside the slice and would falsely overlap the other side
         int64_t slo, shi, dlo, dhi;
-        side_span(ss, cn, L, row_bytes, slo, shi);
-        side_span(ds, cn, L, row_bytes, dlo, dhi);
+        range_span(ss, cn, L, row_bytes, row_begin, row_end, slo, shi);
+        range_span(ds, cn, L, row_bytes, row_begin, row_end, dlo, dhi);
         const int64_t sb = (int64_t)(uintptr_t)src, db = (int64_t)(uintptr_t)dst;
         const bool same_layout = (src == dst) && !memcmp(ss, ds, sizeof(int64_t) * L);
         if (!same_layout && sb + slo < db + dhi && db + dlo < sb + shi) src_dst_overlap = true;
@@ -744,6 +784,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         ++launches;
         total_blocks += blocks;
     }
+    g_kind_count[kind] += (unsigned long long)launches;
     if (info) {
         info->kind = kind;
         info->width = W;

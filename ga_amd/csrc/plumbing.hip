@@ -101,6 +101,11 @@ int gaamd_last_launch(int *kind, int *width, int *unroll, int *launches, unsigne
     return 0;
 }
 
+int gaamd_kernel_counts(unsigned long long counts[4]) {
+    for (int k = 0; k < 4; ++k) counts[k] = kernel_count(k);
+    return 0;
+}
+
 static int *tuning_field(const char *key) {
     Tuning &t = tuning();
     if (!strcmp(key, "kind")) return &t.kind;

@@ -113,6 +113,7 @@ struct Runtime {
     hipStream_t stream = nullptr;              // primary stream (= streams[0])
     std::vector<hipStream_t> streams;          // COMEX_AMD_STREAMS streams (sched.cpp)
     bool blocking_sync = false;     // COMEX_AMD_BLOCKING_SYNC
+    int debug = 0;                  // COMEX_AMD_DEBUG: trace transfers on stderr
     // bootstrap
     gaamd_allgather_fn ag = nullptr;
     gaamd_barrier_fn bar = nullptr;

@@ -64,6 +64,9 @@ int gaamd_unpack_acc(int op, const void *scale, const void *packed, void *dst,
 /* kind / vector width / unroll / launches / blocks of the last kernel-level call */
 int gaamd_last_launch(int *kind, int *width, int *unroll, int *launches,
                       unsigned long long *blocks);
+/* kernel launches since start, by kind: counts[0..3] = {unused, rows, flat,
+ * serial}, every caller of this process (user calls, progress thread, wire) */
+int gaamd_kernel_counts(unsigned long long counts[4]);
 /* keys: "kind" (0 auto,1 rows,2 flat,3 serial), "unroll16", "nontemporal",
  * "flat_max_nvec", "max_grid"; returns the previous value or -1 */
 int gaamd_set_tuning(const char *key, int value);

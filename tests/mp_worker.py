@@ -79,6 +79,10 @@ def main():
     print(f"RANK {rank} OK", flush=True)
 
 
+def say(rank, msg):
+    print(f"rank {rank}: {msg}", file=sys.stderr, flush=True)
+
+
 def remote_test(L, rank, size):
     import ga_amd
     from oracle import Oracle
@@ -107,6 +111,7 @@ def remote_test(L, rank, size):
         rc = ga_amd.comex_accs(DBL, float(rank + 1), src.ctypes.data, [src_ld * 8], seg[t] + off, [ld * 8],
                                count, 1, t)
         assert rc == 0
+    say(rank, "remote accs posted")
     # a strided put into the next rank and a get from the previous one
     nxt, prv = (rank + 1) % size, (rank - 1) % size
     patch = np.full((20, 16), 1e6 + rank, dtype=np.float64)
@@ -130,6 +135,7 @@ def remote_test(L, rank, size):
         bad = np.nonzero(got != want.view(np.float64))[0]
         raise SystemExit(f"rank {rank}: {bad.size} elements differ, first {bad[:5]}")
 
+    say(rank, "block checked")
     # remote strided get of the previous rank's patch
     out = np.zeros((90, 120), dtype=np.float64)
     assert ga_amd.comex_gets(seg[prv] + (7 + 11 * ld) * 8, [ld * 8], out.ctypes.data, [120 * 8], count, 1,
@@ -139,6 +145,7 @@ def remote_test(L, rank, size):
     exp = pb[11:101, 7:127] + total * src[:, :120]
     assert np.array_equal(out, exp), f"rank {rank}: remote get mismatch"
 
+    say(rank, "remote get checked")
     # many small remote accumulates in flight (inbox wrap, staging reuse)
     for it in range(300):
         t = (rank + 1 + it) % size
@@ -154,6 +161,7 @@ def remote_test(L, rank, size):
     exp2[:, 3:7] += cnt_into_me * src[:3, :4]
     assert np.array_equal(got2.reshape(3, ld), exp2), f"rank {rank}: many-small mismatch"
 
+    say(rank, "many-small checked")
     # remote io-vector accumulate (scatter-acc with duplicates) into the next rank
     ga_amd.comex_barrier()
     vsrc = np.arange(64, dtype=np.float64) + 1.0 + rank
@@ -183,6 +191,7 @@ def remote_test(L, rank, size):
     for i, j in enumerate(idx):
         exp_n[j] += 2.0 * vsrc[i]
     assert np.array_equal(gb.download(np.float64, 40)[::-1], exp_n), f"rank {rank}: remote getv mismatch"
+    say(rank, "accv/getv checked")
     # remote io-vector put of 8 singles into the next rank's tail slots 32..39
     ga_amd.comex_barrier()
     pv = ga_amd.DeviceBuffer(64)
@@ -195,7 +204,38 @@ def remote_test(L, rank, size):
     ga_amd.comex_fence_all()
     assert np.array_equal(tail[32:], np.arange(8, dtype=np.float64) - 100.0 * prv), f"rank {rank}: putv"
 
+    say(rank, "putv checked")
+    # a remote accumulate larger than the staging sub-ring travels as row ranges
+    # (pack -> staging slice -> owner's unpack-acc with a rebased packed base);
+    # no chunk may fall back to the one-lane serial kernel, which a full-range
+    # span of the rebased side once triggered (gaamd_kernels.hip range_span)
     ga_amd.comex_barrier()
+    rows, rowb, ldb = 1024, 16384, 20480          # 16 MiB of payload per rank
+    seg2 = ga_amd.comex_malloc(ldb * rows, size)
+    ga_amd.lib().gaamd_memset(ctypes.c_void_p(seg2[rank]), 0, ldb * rows)
+
+    def big_src(r):
+        return (np.arange(rows * ldb // 8, dtype=np.float64) % 251 - 125 + r).reshape(rows, ldb // 8)
+    bs = ga_amd.DeviceBuffer(ldb * rows)
+    bs.upload(big_src(rank))
+    ga_amd.sync()
+    serial0 = ga_amd.kernel_counts()["serial"]
+    ga_amd.comex_barrier()
+    assert ga_amd.comex_accs(DBL, 2.0, bs.ptr, [ldb], seg2[nxt], [ldb], [rowb, rows], 1, nxt) == 0
+    say(rank, "chunked remote acc posted")
+    ga_amd.comex_barrier()
+    mine = np.zeros((rows, ldb // 8), dtype=np.float64)
+    assert ga_amd.lib().comex_get(ctypes.c_void_p(seg2[rank]), mine.ctypes.data_as(ctypes.c_void_p), ldb * rows,
+                                  rank, 0) == 0
+    ga_amd.comex_fence_all()
+    exp3 = np.zeros_like(mine)
+    exp3[:, :rowb // 8] = 2.0 * big_src(prv)[:, :rowb // 8]
+    assert np.array_equal(mine, exp3), f"rank {rank}: chunked remote acc mismatch"
+    assert ga_amd.kernel_counts()["serial"] == serial0, f"rank {rank}: a chunk ran on the serial kernel"
+    bs.free()
+
+    ga_amd.comex_barrier()
+    assert ga_amd.comex_free(seg2[rank]) == 0
     assert ga_amd.comex_free(seg[rank]) == 0
     ga_amd.comex_finalize()
 
@@ -229,6 +269,7 @@ def ga_test(L, rank, size):
     alpha = ctypes.c_double(rank + 1)
     L.NGA_Acc(g, ia(lo), ia(hi), buf.ctypes.data_as(ctypes.c_void_p), ia([ldc]), ctypes.byref(alpha))
     L.GA_Sync()
+    say(rank, "ga sync 1")
     if rank == 0:
         got = np.zeros(dims, dtype=np.float64)
         L.NGA_Get(g, ia([0, 0]), ia([dims[0] - 1, dims[1] - 1]), got.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]))
@@ -240,6 +281,7 @@ def ga_test(L, rank, size):
             want[lo_r[0]:hi[0] + 1, lo_r[1]:hi[1] + 1] += (r + 1) * b[:, :cols]
         assert np.array_equal(got, want), "NGA_Acc result differs"
     L.GA_Sync()
+    say(rank, "ga sync 2")
 
     # testc.c:69-89: everybody accumulates buf[i] = i into the same row, alpha 1
     L.GA_Zero(g)
@@ -249,11 +291,13 @@ def ga_test(L, rank, size):
     L.NGA_Acc(g, ia([row, 0]), ia([row, dims[1] - 1]), b.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]),
               ctypes.byref(one))
     L.GA_Sync()
+    say(rank, "ga sync 3")
     if rank == 0:
         out = np.zeros(dims[1])
         L.NGA_Get(g, ia([row, 0]), ia([row, dims[1] - 1]), out.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]))
         assert np.array_equal(out, size * np.arange(dims[1], dtype=np.float64)), "testc.c KAT failed"
     L.GA_Sync()
+    say(rank, "ga sync 4")
 
     # put / get round trip of a patch owned by several ranks
     p = (np.arange(40 * 50, dtype=np.float64) + 1e5 * (rank + 1)).reshape(40, 50)
@@ -261,10 +305,23 @@ def ga_test(L, rank, size):
     if phi[0] < dims[0]:
         L.NGA_Put(g, ia(plo), ia(phi), p.ctypes.data_as(ctypes.c_void_p), ia([50]))
     L.GA_Sync()
+    say(rank, "ga sync 5")
     q = np.zeros((40, 50))
     if phi[0] < dims[0]:
         L.NGA_Get(g, ia(plo), ia(phi), q.ctypes.data_as(ctypes.c_void_p), ia([50]))
-        assert np.array_equal(p, q), "put/get round trip"
+        if not np.array_equal(p, q):
+            # diagnostics: the same get again into host memory, and into HBM
+            q2 = np.zeros((40, 50))
+            L.NGA_Get(g, ia(plo), ia(phi), q2.ctypes.data_as(ctypes.c_void_p), ia([50]))
+            qd = ga_amd.DeviceBuffer(q2.nbytes)
+            L.NGA_Get(g, ia(plo), ia(phi), ctypes.c_void_p(qd.ptr), ia([50]))
+            q3 = qd.download(np.float64, 2000).reshape(40, 50)
+            say(rank, f"retry host get ok={np.array_equal(p, q2)}, device get ok={np.array_equal(p, q3)}")
+            bad = np.argwhere(p != q)
+            rows_bad = sorted(set(int(x) for x in bad[:, 0]))
+            raise AssertionError(f"put/get round trip: {len(bad)} differ, rows {rows_bad[:10]}.., cols "
+                                 f"{sorted(set(int(x) for x in bad[:, 1]))[:10]}.., first got {q[tuple(bad[0])]} "
+                                 f"want {p[tuple(bad[0])]}")
 
     # gather / scatter / scatter-acc (gai_gatscat, onesided.c:2747): random
     # subscripts over every owner, repeated ones included
@@ -279,6 +336,7 @@ def ga_test(L, rank, size):
     two = ctypes.c_double(2.0)
     L.NGA_Scatter_acc(g, vals.ctypes.data_as(ctypes.c_void_p), ptrs, nv, ctypes.byref(two))
     L.GA_Sync()
+    say(rank, "ga sync 6")
     full = np.zeros(dims)
     L.NGA_Get(g, ia([0, 0]), ia([dims[0] - 1, dims[1] - 1]), full.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]))
     want = np.zeros(dims)
@@ -298,6 +356,7 @@ def ga_test(L, rank, size):
     L.NGA_Gather(g, got2.ctypes.data_as(ctypes.c_void_p), ptrs, nv)
     assert np.array_equal(got2, got), "NGA_Gather"
     L.GA_Sync()
+    say(rank, "ga sync 7")
     # rank 0 alone: non-integer values with repeated subscripts, applied in input
     # order per owner -> bit-exact against the sequential _acc order
     L.GA_Zero(g)
@@ -316,6 +375,7 @@ def ga_test(L, rank, size):
         want3 = np.array([exp[(int(subs[k, 0]), int(subs[k, 1]))] for k in range(nv)])
         assert np.array_equal(got3.view(np.int64), want3.view(np.int64)), "NGA_Scatter_acc order"
     L.GA_Sync()
+    say(rank, "ga sync 8")
     # scatter (put) of unique subscripts
     L.GA_Zero(g)
     rs = np.random.default_rng(77)                              # same subscripts on every rank
@@ -326,11 +386,13 @@ def ga_test(L, rank, size):
         L.NGA_Scatter_flat(g, uv.ctypes.data_as(ctypes.c_void_p),
                            np.ascontiguousarray(uniq).ravel().ctypes.data_as(ctypes.POINTER(ctypes.c_int)), len(uniq))
     L.GA_Sync()
+    say(rank, "ga sync 9")
     L.NGA_Get(g, ia([0, 0]), ia([dims[0] - 1, dims[1] - 1]), full.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]))
     want = np.zeros(dims)
     want[uniq[:, 0], uniq[:, 1]] = np.arange(1, len(uniq) + 1) * 1.5
     assert np.array_equal(full, want), "NGA_Scatter"
     L.GA_Sync()
+    say(rank, "ga sync 10")
 
     # local block through NGA_Access is an HBM address
     lo_m, hi_m = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
@@ -347,6 +409,7 @@ def ga_test(L, rank, size):
         assert np.array_equal(mine.reshape(nr, nc), ref)
         L.NGA_Release(g, lo_m, hi_m)
     L.GA_Sync()
+    say(rank, "ga sync 11")
     L.GA_Destroy(g)
 
     # 3-D int array, accumulate with alpha 3 (integer arithmetic, exact)
@@ -357,12 +420,14 @@ def ga_test(L, rank, size):
     L.NGA_Acc(g3, ia([3, 5, 7]), ia([12, 16, 20]), v.ctypes.data_as(ctypes.c_void_p), ia([12, 14]),
               ctypes.byref(three))
     L.GA_Sync()
+    say(rank, "ga sync 12")
     out3 = np.zeros(d3, dtype=np.int32)
     L.NGA_Get(g3, ia([0, 0, 0]), ia([16, 22, 28]), out3.ctypes.data_as(ctypes.c_void_p), ia([23, 29]))
     w3 = np.zeros(d3, dtype=np.int32)
     w3[3:13, 5:17, 7:21] = 3 * size * v
     assert np.array_equal(out3, w3), "3-D int NGA_Acc"
     L.GA_Sync()
+    say(rank, "ga sync 13")
     L.GA_Destroy(g3)
     if rank == 0:
         L.GA_Print_stats()

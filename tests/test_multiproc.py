@@ -44,6 +44,12 @@ def launch(mode, n=2, timeout=240, nodes=None, extra_env=None):
         for p in procs:
             out, _ = p.communicate(timeout=timeout)
             outs.append((p.returncode, out))
+    except subprocess.TimeoutExpired:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        tails = [f"--- rank {r} ---\n" + (p.communicate()[0] or "")[-2000:] for r, p in enumerate(procs)]
+        raise AssertionError(f"{mode}: ranks did not finish in {timeout} s\n" + "\n".join(tails))
     finally:
         for p in procs:
             if p.poll() is None:
@@ -72,12 +78,12 @@ def test_bootstrap_several_nodes_and_wire(nodes):
 
 @pytest.mark.gpu
 def test_remote_acc_put_get_two_ranks_one_gpu():
-    launch("remote", n=2, timeout=300)
+    launch("remote", n=2, timeout=120)
 
 
 @pytest.mark.gpu
 def test_remote_three_ranks_gloo_hooks():
-    launch("remote-gloo", n=3, timeout=300)
+    launch("remote-gloo", n=3, timeout=120)
 
 
 @pytest.mark.gpu
@@ -85,22 +91,22 @@ def test_remote_three_ranks_gloo_hooks():
 def test_remote_across_nodes_wire(nodes):
     """Ranks on different (simulated) nodes: acc/put/get/accv/getv/putv through the
     MPI-PR message protocol over TCP (wire.cpp); [0,0,1,1] mixes IPC and wire."""
-    launch("remote-gloo", n=len(nodes), timeout=300, nodes=nodes)
+    launch("remote-gloo", n=len(nodes), timeout=120, nodes=nodes)
 
 
 @pytest.mark.gpu
 def test_remote_across_nodes_wire_small_chunks():
     """Payloads cut into many row-range frames (1 MiB pinned chunks)."""
-    launch("remote-gloo", n=2, timeout=300, nodes=[0, 1], extra_env={"COMEX_AMD_WIRE_MB": "1"})
+    launch("remote-gloo", n=2, timeout=120, nodes=[0, 1], extra_env={"COMEX_AMD_WIRE_MB": "1"})
 
 
 @pytest.mark.gpu
 def test_ga_layer_across_nodes():
-    launch("ga-gloo", n=3, timeout=300, nodes=[0, 0, 1])
+    launch("ga-gloo", n=3, timeout=120, nodes=[0, 0, 1])
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [1, 2, 4])
 def test_ga_layer_nga_acc(n):
     """NGA_Create/NGA_Acc/NGA_Put/NGA_Get/NGA_Access over n ranks on one GPU."""
-    launch("ga", n=n, timeout=300)
+    launch("ga", n=n, timeout=120)
