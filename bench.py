@@ -266,11 +266,21 @@ def run_gpu(args, dist):
         ptrs = [(ctypes.c_void_p(s.ptr), ctypes.c_void_p(d.ptr)) for s, d in sets]
     stream = L.gaamd_stream()
 
+    pipeline = args.pipeline and not exchange
+    packed = [ga_amd.DeviceBuffer(payload) for _ in sets] if pipeline else []
+
     def step(i):
         sp_, dp_ = ptrs[i % len(ptrs)]
-        rc = L.comex_accs(op, sp, sp_, ss, dp_, ds, cnt, levels, target, 0)
+        if pipeline:
+            # the remote path's two kernels back to back on one GPU: pack (comex.c:1267)
+            # then the owner's unpack-acc (comex.c:4238-4268)
+            pk = ctypes.c_void_p(packed[i % len(packed)].ptr)
+            rc = L.gaamd_pack(sp_, ss, cnt, levels, pk, None) or \
+                L.gaamd_unpack_acc(op, sp, pk, dp_, ds, cnt, levels, None)
+        else:
+            rc = L.comex_accs(op, sp, sp_, ss, dp_, ds, cnt, levels, target, 0)
         if rc:
-            raise RuntimeError(f"comex_accs returned {rc}")
+            raise RuntimeError(f"step returned {rc}")
 
     for i in range(args.warmup):
         step(i)
@@ -305,7 +315,9 @@ def run_gpu(args, dist):
         avg_kernel_s = elapsed / args.steps   # the work runs on the owners' streams
 
     res = dict(op=op, desc=desc, payload=payload, alg_bytes=alg_bytes, elems=elems, elapsed=elapsed,
-               avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams())
+               avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), pipeline=pipeline)
+    for b in packed:
+        b.free()
     if args.host_rates and dist.rank == 0:
         res["host"] = host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_bytes)
     for s, d in sets:
@@ -426,6 +438,8 @@ def main():
     ap.add_argument("--host-rates", action="store_true", help="also measure host-inclusive rates")
     ap.add_argument("--exchange", action="store_true",
                     help="N>1: rank r accumulates into rank r+1's partition (remote path, SURVEY 8(d) M2)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="step = pack + unpack-acc (the remote path's two kernels) instead of the fused acc")
     ap.add_argument("--tune", action="append", help="key=value tuning knob (gaamd_set_tuning)")
     ap.add_argument("--ga-dims", type=int, default=0, help="C5: square GA of this size instead of 32768^2")
     ap.add_argument("--verbose", action="store_true", help="progress lines on stderr")
@@ -472,6 +486,14 @@ def main():
                      "streams": r["streams"]},
         "cpu_baseline": cpu,
     }
+    if r.get("pipeline"):
+        # two kernels per step on one stream: pack moves 2x payload, unpack-acc 3x
+        moved = 5 * r["payload"]
+        line["config"]["step"] = "gaamd_pack + gaamd_unpack_acc on one stream (pack-buffer traffic not credited in value)"
+        line["roofline"]["achieved"] = round(moved / r["avg_kernel_s"] / 1e9, 1)
+        line["roofline"]["frac"] = round(moved / r["avg_kernel_s"] / 1e9 / HBM_PEAK_GBS, 4)
+        line["roofline"]["traffic"] = None
+        line["roofline"]["timing"] = "bytes both kernels move (5 x payload) / (event-pair region / steps)"
     if r["exchange"]:
         # the kernels run on the owners' streams: no single-kernel roofline; the
         # per-step time is the whole exchange (pack, hand-off, unpack-acc)
