@@ -60,7 +60,7 @@ struct Tuning {
     int kind = KK_AUTO;     // force a kernel family
     int unroll16 = 1;       // vectors per thread for the W=16 rows kernels {1,2,4,8}
     int nontemporal = 1;    // nt loads/stores on the rows kernels (streamed once)
-    int block = 128;        // threads per block of the rows kernels {64, 128, 256, 512}
+    int block = 0;          // threads per block of the rows kernels {64, 128, 256, 512}; 0 = auto
     int flat_max_nvec = 127;// rows with at most this many vectors use the flat kernel
     int max_grid = 0;       // cap on blocks (0 = one block per work item)
     int align = 0;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses

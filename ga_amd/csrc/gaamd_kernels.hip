@@ -279,6 +279,42 @@ __global__ __launch_bounds__(BS) void k_rows2d(const Desc2D d, const OP op) {
     vstore<W, true>(dp, op.template apply<W>(b, a));
 }
 
+// DIRECT N-D kernel (2 or 3 stride levels, every row whole chunks): as
+// k_rows2d, with the row decoded by LV compile-time FastDiv digits from a
+// compact argument block (C4: 3-D double complex, 4 KiB rows).
+template <int LV>
+struct DescND {
+    const char *src;
+    char *dst;
+    int64_t s_str[LV], d_str[LV];
+    FastDiv cnt[LV];
+    FastDiv chunk_div;
+    uint32_t row0;
+};
+
+template <class OP, int W, int BS, int LV>
+__global__ __launch_bounds__(BS) void k_rowsnd(const DescND<LV> d, const OP op) {
+    const uint32_t w = blockIdx.x;
+    const uint32_t rl = d.chunk_div.div(w);
+    const uint32_t chunk = w - rl * d.chunk_div.d;
+    uint32_t r = d.row0 + rl;
+    int64_t so = 0, dof = 0;
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+        const uint32_t q = d.cnt[j].div(r);
+        const uint32_t dig = r - q * d.cnt[j].d;
+        so += (int64_t)dig * d.s_str[j];
+        dof += (int64_t)dig * d.d_str[j];
+        r = q;
+    }
+    const int64_t v = (int64_t)chunk * BS + threadIdx.x;
+    const char *sp = d.src + so + v * W;
+    char *dp = d.dst + dof + v * W;
+    typename Vec<W>::T a = vload<W, true>(sp), b = a;
+    if constexpr (OP::kReadsDst) b = vload<W, true>(dp);
+    vstore<W, true>(dp, op.template apply<W>(b, a));
+}
+
 // ROWS2 with a different block -> (row, chunk) order (tuning experiment on the
 // f64 2-D kernel; which rows are in flight together decides how the traffic
 // spreads over HBM channels):
@@ -471,6 +507,22 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
 template <class OP, int W, int LV, int BS>
 static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, int nt, hipStream_t st) {
     constexpr int U = DefaultU<W>::value;
+    if constexpr (U == 1 && (LV == 2 || LV == 3)) {
+        if (g_tuning.direct && nt && blocks == d.items && d.nvec % (uint32_t)BS == 0) {
+            DescND<LV> f;
+            f.src = d.src;
+            f.dst = d.dst;
+            for (int j = 0; j < LV; ++j) {
+                f.s_str[j] = d.s_str[j];
+                f.d_str[j] = d.d_str[j];
+                f.cnt[j] = d.cnt[j];
+            }
+            f.chunk_div = d.chunk_div;
+            f.row0 = d.row0;
+            hipLaunchKernelGGL((k_rowsnd<OP, W, BS, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
+            return hipGetLastError();
+        }
+    }
     if (nt) hipLaunchKernelGGL((k_rows<OP, W, U, BS, true, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, d, op);
     else hipLaunchKernelGGL((k_rows<OP, W, U, BS, false, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, d, op);
     return hipGetLastError();
@@ -731,15 +783,24 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     if (kind == KK_AUTO) kind = ((int64_t)d.nvec <= tn.flat_max_nvec) ? KK_FLAT : KK_ROWS;
     // the (U, BS) the dispatcher will pick -- chunking must agree with it
     const bool tunable = (op == kOpCopy || op == 38 || op == 41);
-    // rows kernels: 128-thread blocks by default.  Small blocks retire and free
-    // their CU slots independently; on the headline shape 64/128/256/512/1024
-    // threads measured 6382/6307/6192/6046/5992 GB/s in a stand-alone probe
-    // (tools/h_shape_probe.hip) and 128 led 64 and 256 by 1-3 % in the library
-    // (profiles/r01/sweep_block*.jsonl).  512 only on the tunable 2-D path.
-    int U = unroll_for(W, 1), BS = (tn.block == 512) ? 256 : tn.block;
+    // rows kernels: small blocks retire and free their CU slots independently;
+    // on the headline shape 64/128/256/512/1024 threads measured
+    // 6338/6268/6171/6020/5951 GB/s in a stand-alone probe (tools/h_shape_probe.hip).
+    // 512 only on the tunable 2-D path.
+    int block = tn.block;
+    if (block == 0) {
+        // auto: one-wave blocks when every row starts 4 KiB-aligned on both sides,
+        // 128 threads otherwise (H-shape ld sweep, profiles/r01/sweep_ld_block.jsonl:
+        // 64 leads by 1-6 % at ld 8192/8704/12288 and C3 by 4 %, 128 leads by 5-10 %
+        // at ld 8194..8320, whose rows start off 4 KiB boundaries)
+        uint64_t al = (uint64_t)(uintptr_t)src | (uint64_t)(uintptr_t)dst;
+        for (int j = 0; j < L; ++j) al |= (uint64_t)ss[j] | (uint64_t)ds[j];
+        block = (al & 4095) ? 128 : 64;
+    }
+    int U = unroll_for(W, 1), BS = (block == 512) ? 256 : block;
     if (kind == KK_ROWS && L <= 1 && W == 16 && tunable) {
         U = tn.unroll16;
-        BS = tn.block;
+        BS = block;
     }
     const uint32_t per_chunk = (uint32_t)BS * (uint32_t)U;
     d.align_mask = 0;

@@ -134,7 +134,7 @@ int gaamd_set_tuning(const char *key, int value) {
     int *f = tuning_field(key);
     if (!f) return -1;
     if (!strcmp(key, "unroll16") && value != 1 && value != 2 && value != 4 && value != 8) return -1;
-    if (!strcmp(key, "block") && value != 64 && value != 128 && value != 256 && value != 512) return -1;
+    if (!strcmp(key, "block") && value != 0 && value != 64 && value != 128 && value != 256 && value != 512) return -1;
     const int old = *f;
     *f = value;
     return old;

@@ -67,7 +67,7 @@ def test_golden_cases_armci_and_nb(gpu_lib, manifest, golden):
 
 
 @pytest.mark.parametrize("knob", [("kind", 1), ("kind", 2), ("kind", 3), ("unroll16", 2), ("unroll16", 4),
-                                  ("unroll16", 8), ("nontemporal", 0), ("max_grid", 7), ("block", 512), ("block", 256), ("block", 64),
+                                  ("unroll16", 8), ("nontemporal", 0), ("max_grid", 7), ("block", 512), ("block", 256), ("block", 128), ("block", 64),
                                   ("align", 1), ("cpol", 2 | 2 << 8), ("cpol", 16 | 2 << 8), ("xcd", 1), ("order", 1), ("order", 2),
                                   ("direct", 0)])
 def test_kernel_variants_identical(gpu_lib, manifest, golden, knob):
@@ -321,28 +321,32 @@ def test_wide_rows_odd_strides_all_knobs(gpu_lib, oracle, knobs):
 
 @pytest.mark.parametrize("direct", [1, 0])
 def test_whole_chunk_rows_every_op(gpu_lib, oracle, direct):
-    """Rows that are whole 4 KiB chunks (the loop-free direct 2-D kernel when
-    `direct` is on, k_rows2 when off), 1-D and 2-D, every op, odd leading
-    dimensions and offsets (16-byte aligned), bit-exact vs the oracle."""
+    """Rows that are whole 4 KiB chunks (the loop-free direct kernels k_rows2d /
+    k_rowsnd when `direct` is on, k_rows2 / k_rows when off), 1-D to 4-D, every
+    op, odd leading dimensions and offsets (16-byte aligned), bit-exact vs the
+    oracle."""
     old = ga_amd.set_tuning("direct", direct)
     try:
         rng = np.random.default_rng(7 + direct)
         for op in (C.INT, C.DBL, C.FLT, C.CPL, C.DCP, C.LNG):
-            esz = C.ESZ[op]
-            for levels in (0, 1):
+            for levels in (0, 1, 2, 3):
                 wbytes = 4096 * int(rng.integers(1, 4))
-                rows = int(rng.integers(2, 9)) if levels else 1
-                lds = wbytes + 16 * int(rng.integers(0, 40)) if levels else wbytes
-                ldd = wbytes + 16 * int(rng.integers(0, 40)) if levels else wbytes
+                count = [wbytes] + [int(rng.integers(2, 6)) for _ in range(levels)]
+                st, dt = [], []
+                sx, dx = wbytes, wbytes
+                for j in range(levels):
+                    sx += 16 * int(rng.integers(0, 40))
+                    dx += 16 * int(rng.integers(0, 40))
+                    st.append(sx)
+                    dt.append(dx)
+                    sx *= count[j + 1]
+                    dx *= count[j + 1]
                 so, do = 16 * int(rng.integers(0, 5)), 16 * int(rng.integers(0, 5))
-                count = [wbytes, rows] if levels else [wbytes]
-                src = C.fill_bytes(op, so + lds * rows, 21)
-                dst = C.fill_bytes(op, do + ldd * rows, 22)
+                src = C.fill_bytes(op, so + C.span(st, count, levels)[1], 21)
+                dst = C.fill_bytes(op, do + C.span(dt, count, levels)[1], 22)
                 sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
                 sb.upload(src)
                 db.upload(dst)
-                st = [lds] if levels else []
-                dt = [ldd] if levels else []
                 assert ga_amd.comex_accs(op, C.SCALE[op], sb.ptr + so, st, db.ptr + do, dt, count, levels, 0) == 0
                 ga_amd.comex_fence_all()
                 info = ga_amd.last_launch()
@@ -350,7 +354,7 @@ def test_whole_chunk_rows_every_op(gpu_lib, oracle, direct):
                 want = dst.copy()
                 oracle.accs(op, C.SCALE[op], src, so, st, want, do, dt, count, levels)
                 got = db.download(np.uint8, dst.size)
-                assert np.array_equal(got, want), (op, levels, wbytes, rows, lds, ldd, so, do)
+                assert np.array_equal(got, want), (op, levels, count, st, dt, so, do)
     finally:
         ga_amd.set_tuning("direct", old)
 

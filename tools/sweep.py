@@ -51,7 +51,10 @@ def main():
     ss, ds, cnt = ga_amd.int_array(sstr), ga_amd.int_array(dstr), ga_amd.int_array(count)
     stream = L.gaamd_stream()
     variants = [v for v in args.variants.split(";") if v]
-    defaults = {k: ga_amd.get_tuning(k) for k in ("kind", "unroll16", "nontemporal", "flat_max_nvec", "max_grid")}
+    # every knob is reset to its default before each variant (a variant sets only its own keys)
+    defaults = {k: ga_amd.get_tuning(k) for k in ("kind", "unroll16", "nontemporal", "flat_max_nvec", "max_grid",
+                                                   "block", "align", "cpol", "xcd", "order", "direct")}
+    defaults["streams"] = L.gaamd_num_streams()
     res = {v: [] for v in variants}
     wall = {v: [] for v in variants}
     enq = {v: [] for v in variants}
