@@ -548,6 +548,12 @@ static void fence_target(int t) {
 // ---- the one transfer routine ---------------------------------------------
 enum Xfer { X_ACC, X_PUT, X_GET };
 
+static uint64_t payload_bytes(int64_t row_bytes, const int *count, int levels) {
+    uint64_t n = (uint64_t)row_bytes;
+    for (int j = 1; j <= levels; ++j) n *= (uint64_t)count[j];
+    return n;
+}
+
 static int64_t row_bytes_of(int op, int count0) {
     const int esz = elem_size(op);
     return (op == kOpCopy) ? count0 : (int64_t)(count0 / esz) * esz;
@@ -630,7 +636,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
         if (host_side) sched_join();   // staged copies sit on stream 0: run there, after everything
-        else si = sched_pick(span_of(sv.dev, slo, shi), span_of(dv.dev, dlo, dhi));
+        else si = sched_pick(span_of(sv.dev, slo, shi), span_of(dv.dev, dlo, dhi), payload_bytes(rb, count, levels));
         const int rc = launch_strided(cop, scale, sv.dev, ss, dv.dev, ds, count, levels, r.streams[si],
                                       last_launch_info());
         if (rc) fatal("strided %s launch failed (code %d): misaligned elements or bad descriptor",

@@ -63,7 +63,7 @@ struct Tuning {
     int block = 0;          // threads per block of the rows kernels {64, 128, 256, 512}; 0 = auto
     int flat_max_nvec = 127;// rows with at most this many vectors use the flat kernel
     int max_grid = 0;       // cap on blocks (0 = one block per work item)
-    int align = 0;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses
+    int align = 1;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses (misaligned rows)
     int cpol = 0;           // f64 2-D kernel via buffer ops: load | store<<8 cache bits (0 = off)
     int xcd = 0;            // f64 2-D kernel: XCD-contiguous work ranges (experiment)
     int order = 0;          // f64 2-D kernel: 1 chunk-major, 2 scattered rows (experiment)

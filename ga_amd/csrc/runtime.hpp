@@ -151,7 +151,7 @@ void boot_finalize();
 void sched_init(int nstreams);
 void sched_fini();
 void sched_resize(int nstreams);
-int sched_pick(const Span &src, const Span &dst);   // stream index for an op
+int sched_pick(const Span &src, const Span &dst, uint64_t payload = 0);   // payload bytes of the op (0: unknown)   // stream index for an op
 void sched_join();
 void sched_sync_all();
 

@@ -89,7 +89,14 @@ void sched_sync_all() {
     g_hist.clear();
 }
 
-int sched_pick(const Span &src, const Span &dst) {
+// Launches that move at least this many payload bytes stay on the stream of the
+// previous operation even when independent: two such kernels running side by
+// side lost 3 % against running them back to back (C4, 256 MiB of double
+// complex per launch: profiles/r01/sweep_streams.jsonl), while the edge overlap
+// they would buy is < 1 % of their length.  Smaller launches alternate.
+constexpr uint64_t kBigPayload = 192ull << 20;
+
+int sched_pick(const Span &src, const Span &dst, uint64_t payload) {
     Runtime &r = rt();
     const int n = (int)r.streams.size();
     if (n <= 1) return 0;
@@ -104,7 +111,7 @@ int sched_pick(const Span &src, const Span &dst) {
     }
     int s;
     if (!mask) {
-        g_rr = (g_rr + 1) % n;
+        if (payload < kBigPayload) g_rr = (g_rr + 1) % n;
         s = g_rr;
     } else {
         s = last;   // the most recent dependency's stream; wait for the others
