@@ -54,7 +54,7 @@ def main():
     rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import ga_amd
     L = ga_amd.lib()
-    if mode in ("boot-gloo", "remote-gloo", "boot-nodes", "ga-gloo"):
+    if mode in ("boot-gloo", "remote-gloo", "boot-nodes", "ga-gloo", "stress-gloo"):
         ag, bar = torch_hooks(rank, size)
         keep = (ag, bar)  # noqa: F841
         assert L.gaamd_set_bootstrap(rank, size, rank, ctypes.cast(ag, ctypes.c_void_p),
@@ -74,6 +74,8 @@ def main():
         return
     if mode in ("ga", "ga-gloo"):
         ga_test(L, rank, size)
+    elif mode in ("stress", "stress-gloo"):
+        stress_test(L, rank, size)
     else:
         remote_test(L, rank, size)
     print(f"RANK {rank} OK", flush=True)
@@ -432,6 +434,149 @@ def ga_test(L, rank, size):
     if rank == 0:
         L.GA_Print_stats()
     L.GA_Terminate()
+
+
+# ---------------------------------------------------------------------------
+# stress: every rank runs a seeded random program of remote/local accumulates
+# (blocking, non-blocking, host or HBM source, 1-D..3-D, io-vector), puts into
+# its own zone of every segment, gets back from those zones, and fences at
+# random points.  Integer-valued f64, so concurrent accumulates from all ranks
+# sum exactly in any order; every rank regenerates every other rank's program
+# from its seed and checks its own segment at the end.
+ST_ACC = 96 * 1024          # f64 elements of the accumulate zone
+ST_ZONE = 4 * 1024          # f64 elements of one rank's put zone in every segment
+
+
+def stress_program(s, size, n_ops):
+    rng = np.random.default_rng(1000 + s)
+    ops = []
+    for _ in range(n_ops):
+        u = rng.random()
+        t = int(rng.integers(size))
+        if u < 0.55:
+            lv = int(rng.integers(0, 3))
+            cnt = [int(rng.integers(1, 300))] + [int(rng.integers(1, 9)) for _ in range(lv)]
+            st = []
+            x = cnt[0] + int(rng.integers(0, 40))
+            for j in range(lv):
+                st.append(x)
+                x = x * cnt[j + 1] + int(rng.integers(0, 7))
+            span = cnt[0] + sum(st[j] * (cnt[j + 1] - 1) for j in range(lv))
+            off = int(rng.integers(0, ST_ACC - span))
+            src = rng.integers(-50, 51, span).astype(np.float64)
+            ops.append(dict(kind="acc", t=t, count=cnt, st=st, off=off, src=src, alpha=float(rng.integers(-3, 4)),
+                            host=bool(rng.random() < 0.3), nb=bool(rng.random() < 0.25)))
+        elif u < 0.65:
+            n = int(rng.integers(1, 60))
+            idx = rng.integers(0, ST_ACC, n)
+            idx[n // 2:] = idx[: n - n // 2] if rng.random() < 0.5 else idx[n // 2:]     # duplicates sometimes
+            ops.append(dict(kind="accv", t=t, idx=idx, vals=rng.integers(-9, 10, n).astype(np.float64),
+                            alpha=float(rng.integers(1, 3))))
+        elif u < 0.85:
+            n = int(rng.integers(1, ST_ZONE))
+            off = int(rng.integers(0, ST_ZONE - n + 1))
+            ops.append(dict(kind="put", t=t, off=off, vals=rng.integers(-1000, 1000, n).astype(np.float64)))
+        elif u < 0.95:
+            ops.append(dict(kind="get", t=t))
+        else:
+            ops.append(dict(kind="fence", t=t))
+    return ops
+
+
+def stress_expected(me, size, n_ops):
+    acc = np.zeros(ST_ACC)
+    zones = np.zeros((size, ST_ZONE))
+    for s in range(size):
+        for op in stress_program(s, size, n_ops):
+            if op["t"] != me:
+                continue
+            if op["kind"] == "acc":
+                cnt, st = op["count"], op["st"]
+                rows = [0]
+                for j, c in enumerate(cnt[1:]):
+                    rows = [r + k * st[j] for k in range(c) for r in rows]
+                for r in rows:
+                    acc[op["off"] + r: op["off"] + r + cnt[0]] += op["alpha"] * op["src"][r: r + cnt[0]]
+            elif op["kind"] == "accv":
+                np.add.at(acc, op["idx"], op["alpha"] * op["vals"])
+            elif op["kind"] == "put":
+                zones[s, op["off"]: op["off"] + len(op["vals"])] = op["vals"]
+    return acc, zones
+
+
+def stress_test(L, rank, size):
+    import ga_amd
+    DBL = 38
+    n_ops = int(os.environ.get("STRESS_OPS", "400"))
+    assert ga_amd.comex_init() == 0
+    nbytes = (ST_ACC + size * ST_ZONE) * 8
+    seg = ga_amd.comex_malloc(nbytes, size)
+    L.gaamd_memset(ctypes.c_void_p(seg[rank]), 0, nbytes)
+    ga_amd.sync()
+    ga_amd.comex_barrier()
+    serial0 = ga_amd.kernel_counts()["serial"]
+    mine = np.zeros((size, ST_ZONE))            # what I have put into every target's zone for me
+    keep = []
+    pending = []
+    for k, op in enumerate(stress_program(rank, size, n_ops)):
+        t = op["t"]
+        if op["kind"] == "acc":
+            cnt, st = op["count"], op["st"]
+            if op["host"]:
+                buf = op["src"]
+                sp = buf.ctypes.data
+            else:
+                db = ga_amd.DeviceBuffer(op["src"].nbytes)
+                db.upload(op["src"])
+                keep.append(db)
+                sp = db.ptr
+            args = (DBL, op["alpha"], sp, [x * 8 for x in op["st"]], seg[t] + op["off"] * 8, [x * 8 for x in st],
+                    [cnt[0] * 8] + cnt[1:], len(st), t)
+            if op["nb"] and not op["host"]:
+                rc, h = ga_amd.comex_nbaccs(*args)
+                assert rc == 0
+                pending.append(h)
+            else:
+                assert ga_amd.comex_accs(*args) == 0
+        elif op["kind"] == "accv":
+            vb = ga_amd.DeviceBuffer(op["vals"].nbytes)
+            vb.upload(op["vals"])
+            keep.append(vb)
+            desc = [([vb.ptr + 8 * i for i in range(len(op["vals"]))],
+                     [seg[t] + 8 * int(i) for i in op["idx"]], 8)]
+            assert ga_amd.comex_accv(DBL, op["alpha"], desc, t) == 0
+        elif op["kind"] == "put":
+            v = op["vals"]
+            zone = seg[t] + (ST_ACC + rank * ST_ZONE + op["off"]) * 8
+            assert L.comex_put(v.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(zone), v.nbytes, t, 0) == 0
+            mine[t, op["off"]: op["off"] + len(v)] = v
+        elif op["kind"] == "get":
+            got = np.zeros(ST_ZONE)
+            zone = seg[t] + (ST_ACC + rank * ST_ZONE) * 8
+            assert L.comex_get(ctypes.c_void_p(zone), got.ctypes.data_as(ctypes.c_void_p), got.nbytes, t, 0) == 0
+            assert np.array_equal(got, mine[t]), f"rank {rank} op {k}: get of my zone at rank {t} differs"
+        else:
+            L.comex_fence_proc(t, 0)
+        if len(pending) > 8:
+            for h in pending:
+                assert ga_amd.comex_wait(h) == 0
+            pending = []
+    for h in pending:
+        assert ga_amd.comex_wait(h) == 0
+    say(rank, f"stress: {n_ops} ops issued")
+    ga_amd.comex_barrier()
+    out = np.zeros(ST_ACC + size * ST_ZONE)
+    assert L.comex_get(ctypes.c_void_p(seg[rank]), out.ctypes.data_as(ctypes.c_void_p), nbytes, rank, 0) == 0
+    acc, zones = stress_expected(rank, size, n_ops)
+    bad = np.nonzero(out[:ST_ACC] != acc)[0]
+    assert bad.size == 0, f"rank {rank}: {bad.size} accumulate-zone elements differ, first {bad[:5]}"
+    assert np.array_equal(out[ST_ACC:].reshape(size, ST_ZONE), zones), f"rank {rank}: put zones differ"
+    assert ga_amd.kernel_counts()["serial"] == serial0, f"rank {rank}: a serial kernel ran"
+    ga_amd.comex_barrier()
+    for b in keep:
+        b.free()
+    assert ga_amd.comex_free(seg[rank]) == 0
+    ga_amd.comex_finalize()
 
 
 if __name__ == "__main__":

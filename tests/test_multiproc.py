@@ -110,3 +110,15 @@ def test_ga_layer_across_nodes():
 def test_ga_layer_nga_acc(n):
     """NGA_Create/NGA_Acc/NGA_Put/NGA_Get/NGA_Access over n ranks on one GPU."""
     launch("ga", n=n, timeout=120)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,n,nodes,staging", [("stress", 3, None, "1"), ("stress-gloo", 4, None, "16"),
+                                                  ("stress-gloo", 3, [0, 0, 1], "1")])
+def test_stress_random_programs(mode, n, nodes, staging):
+    """Seeded random programs of remote/local accumulates (blocking, non-blocking,
+    host or HBM source, 1-D..3-D, io-vector), puts, gets and fences on every rank
+    at once; each rank checks its segment against all ranks' programs replayed
+    (integer-valued f64: exact in any order).  A 1 MiB staging ring forces
+    row-range chunking; nodes [0,0,1] mixes IPC and the wire protocol."""
+    launch(mode, n=n, timeout=150, nodes=nodes, extra_env={"COMEX_AMD_STAGING_MB": staging})
