@@ -29,6 +29,11 @@ struct Entry {
 std::vector<Entry> g_hist;
 std::vector<hipEvent_t> g_ev;   // one reusable event per stream for cross waits
 int g_rr = 0;
+// history dropped while every entry sat on one stream: the ops behind it are
+// ordered on g_base; a stream not yet in g_base_waited waits for g_base before
+// its first new op (cheaper than a full join for runs of one-stream work)
+int g_base = -1;
+unsigned g_base_waited = 0;
 
 inline bool overlap(const Span &a, const Span &b) { return a.lo < b.hi && b.lo < a.hi && a.lo < a.hi && b.lo < b.hi; }
 }  // namespace
@@ -47,6 +52,7 @@ void sched_init(int n) {
     for (int i = 0; i < n; ++i) GA_HIP(hipEventCreateWithFlags(&g_ev[i], hipEventDisableTiming));
     g_hist.clear();
     g_rr = 0;
+    g_base = -1;
 }
 
 // change the number of library streams at run time (all work drained first)
@@ -81,12 +87,14 @@ void sched_join() {
         for (int x = 1; x < n; ++x) wait_on(x, 0);   // everything after stream 0
     }
     g_hist.clear();
+    g_base = -1;
 }
 
 void sched_sync_all() {
     Runtime &r = rt();
     for (hipStream_t s : r.streams) GA_HIP(hipStreamSynchronize(s));
     g_hist.clear();
+    g_base = -1;
 }
 
 // Launches that move at least this many payload bytes stay on the stream of the
@@ -95,12 +103,27 @@ void sched_sync_all() {
 // complex per launch: profiles/r01/sweep_streams.jsonl), while the edge overlap
 // they would buy is < 1 % of their length.  Smaller launches alternate.
 constexpr uint64_t kBigPayload = 192ull << 20;
+// Below this, launches are host-bound (≈3 µs of enqueue against a shorter
+// kernel): alternating streams only added ≈1-2 µs per call up to 4 MiB and
+// gained from 16 MiB on (tools/perf_strided.cpp, profiles/r01/perf_strided.jsonl).
+constexpr uint64_t kSmallPayload = 8ull << 20;
 
 int sched_pick(const Span &src, const Span &dst, uint64_t payload) {
     Runtime &r = rt();
     const int n = (int)r.streams.size();
     if (n <= 1) return 0;
-    if ((int)g_hist.size() >= kHist) sched_join();
+    if ((int)g_hist.size() >= kHist) {
+        const int s0 = g_hist.front().stream;
+        bool one = g_base < 0 || g_base == s0;
+        for (const Entry &e : g_hist) one = one && e.stream == s0;
+        if (one) {   // drop the history; remember the stream it is ordered on
+            g_hist.clear();
+            if (g_base != s0) g_base_waited = 1u << s0;
+            g_base = s0;
+        } else {
+            sched_join();
+        }
+    }
     unsigned mask = 0;
     int last = -1;
     for (const Entry &e : g_hist) {
@@ -111,12 +134,17 @@ int sched_pick(const Span &src, const Span &dst, uint64_t payload) {
     }
     int s;
     if (!mask) {
-        if (payload < kBigPayload) g_rr = (g_rr + 1) % n;
+        if (payload == 0 || (payload >= kSmallPayload && payload < kBigPayload)) g_rr = (g_rr + 1) % n;
         s = g_rr;
     } else {
         s = last;   // the most recent dependency's stream; wait for the others
         for (int x = 0; x < n; ++x)
             if (x != s && (mask & (1u << x))) wait_on(s, x);
+    }
+    if (g_base >= 0 && !(g_base_waited & (1u << s))) {
+        wait_on(s, g_base);
+        g_base_waited |= 1u << s;
+        if (g_base_waited == (1u << n) - 1) g_base = -1;
     }
     g_hist.push_back({s, src, dst});
     return s;
