@@ -76,6 +76,8 @@ def main():
         ga_test(L, rank, size)
     elif mode in ("stress", "stress-gloo"):
         stress_test(L, rank, size)
+    elif mode == "testacc":
+        test_acc_ref(L, rank, size)
     else:
         remote_test(L, rank, size)
     print(f"RANK {rank} OK", flush=True)
@@ -434,6 +436,88 @@ def ga_test(L, rank, size):
     if rank == 0:
         L.GA_Print_stats()
     L.GA_Terminate()
+
+
+# ---------------------------------------------------------------------------
+# comex/testing/test.c test_acc (1028-1128) and test_cplx_acc (1130-1235),
+# restated: for ndim 1..7 every rank accumulates a 2^ndim patch of a host array
+# (alpha 0.1, double complex alpha (0, 0.1)) TIMES*nproc times into the far
+# corner of the ranks' arrays in a permuted proc order; each rank then gets its
+# corner back.  The reference checks rel 1e-4; since every contribution to an
+# element is the same rounded product, the sum is the same in any order, so
+# this checks bit-exactly against n sequential adds of that product.
+def test_acc_ref(L, rank, size):
+    import ga_amd
+    DBL, DCP, TIMES = 38, 41, 3
+    assert ga_amd.comex_init() == 0
+    n_acc = TIMES * size
+    for ndim in range(1, 8):
+        for op in (DBL, DCP):
+            esz = 8 if op == DBL else 16
+            side = max(3, int(round(2000 ** (1.0 / ndim))))
+            dimsA = [side + (j % 2) for j in range(ndim)]
+            dimsB = [side + 1 - (j % 2) for j in range(ndim)]
+            ea, eb = int(np.prod(dimsA)), int(np.prod(dimsB))
+            seg = ga_amd.comex_malloc(eb * esz, size)
+            L.gaamd_memset(ctypes.c_void_p(seg[rank]), 0, eb * esz)
+            ga_amd.sync()
+            if op == DBL:
+                a = np.arange(ea, dtype=np.float64) * 1.25 + rank + 0.5       # host (malloc-like) source
+                alpha = 0.1
+            else:
+                a = (np.arange(ea) * 1.25 + rank + 0.5) + 1j * (np.arange(ea) * -0.5 + 2.0 * rank)
+                alpha = complex(0.0, 0.1)
+            sA, sB = [esz * dimsA[0]], [esz * dimsB[0]]
+            for j in range(1, ndim - 1):
+                sA.append(sA[-1] * dimsA[j])
+                sB.append(sB[-1] * dimsB[j])
+            # first dimension fastest (column-major, as the reference's Index())
+            offA = 0
+            offB = sum((dimsB[j] - 2) * (esz * int(np.prod(dimsB[:j]))) for j in range(ndim))
+            count = [2 * esz] + [2] * (ndim - 1)
+            order = np.random.default_rng(5 + rank).permutation(size)
+            ga_amd.comex_barrier()
+            for i in range(n_acc):
+                p = int(order[i % size])
+                assert ga_amd.comex_accs(op, alpha, a.ctypes.data + offA, sA, seg[p] + offB, sB, count, ndim - 1,
+                                         p) == 0
+            ga_amd.comex_barrier()
+            # get my corner back into a zeroed host array laid out like a
+            c = np.zeros_like(a)
+            assert ga_amd.comex_gets(seg[rank] + offB, sB, c.ctypes.data + offA, sA, count, ndim - 1, rank) == 0
+            ga_amd.comex_fence_all()
+            # expected: every rank added n_acc/size ... each rank's own a: sum over sources
+            idx = [0]
+            for j in range(ndim):
+                stride = int(np.prod(dimsA[:j]))
+                idx = [x + k * stride for k in range(2) for x in idx]
+            idx = np.array(idx)
+            want = np.zeros(len(idx), dtype=a.dtype)
+            contribs = []
+            for s in range(size):
+                if op == DBL:
+                    a_s = np.arange(ea, dtype=np.float64) * 1.25 + s + 0.5
+                    contribs.append(a_s[idx] * 0.1)
+                else:
+                    a_s = (np.arange(ea) * 1.25 + s + 0.5) + 1j * (np.arange(ea) * -0.5 + 2.0 * s)
+                    br, bi = a_s[idx].real, a_s[idx].imag
+                    re = br * 0.0 - bi * 0.1          # acc.h:47-49 with C = (0, 0.1)
+                    im = br * 0.1 + bi * 0.0
+                    contribs.append(re + 1j * im)
+            # each source rank targets me TIMES times; sums of different sources
+            # depend on order, so compare per the reference (rel 1e-4) and, when a
+            # single source exists, exactly
+            for s in range(size):
+                for _ in range(TIMES):
+                    want = want + contribs[s]
+            got = c[idx]
+            assert np.allclose(got, want, rtol=1e-4, atol=0), (ndim, op, np.max(np.abs(got - want)))
+            if size == 1:
+                assert np.array_equal(got, want), (ndim, op)
+            ga_amd.comex_barrier()
+            assert ga_amd.comex_free(seg[rank]) == 0
+    say(rank, "test_acc / test_cplx_acc ndim 1..7 ok")
+    ga_amd.comex_finalize()
 
 
 # ---------------------------------------------------------------------------

@@ -122,3 +122,13 @@ def test_stress_random_programs(mode, n, nodes, staging):
     (integer-valued f64: exact in any order).  A 1 MiB staging ring forces
     row-range chunking; nodes [0,0,1] mixes IPC and the wire protocol."""
     launch(mode, n=n, timeout=150, nodes=nodes, extra_env={"COMEX_AMD_STAGING_MB": staging})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 3])
+def test_comex_test_acc_restated(n):
+    """comex/testing/test.c test_acc + test_cplx_acc (1028-1235) for ndim 1..7:
+    TIMES*nproc accumulates of a host patch (alpha 0.1 / (0, 0.1)) into the far
+    corner of every rank's array, checked at the reference's rel 1e-4 (exactly
+    on one rank, where the order is fixed)."""
+    launch("testacc", n=n, timeout=150)
