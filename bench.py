@@ -377,8 +377,8 @@ def host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_byt
 def run_cpu_baseline(workload, seconds, threads):
     """The reference's _acc per row (oracle/_ref), or the restatement if _ref is absent.
     SURVEY.md 8(d): P host workers, each on its own slab of the patch (oracle/mt_split.h),
-    for P = 1 and P = `threads`; each as many full steps as fit in ~seconds/2 (at least 2).
-    `value` is the P = `threads` rate; the single-core rate is reported beside it."""
+    for P = 1, 2, 4, 8 (up to `threads`); each as many full steps as fit in ~seconds/#P (at
+    least 2).  `value` is the P = `threads` rate; every P is reported beside it."""
     from oracle import Oracle, Ref, ref_available
     op, count, sstr, dstr, _ = WORKLOADS[workload]
     sbytes, dbytes = span_bytes(count, sstr), span_bytes(count, dstr)
@@ -393,19 +393,31 @@ def run_cpu_baseline(workload, seconds, threads):
         impl, kind = o, "port"
     levels = len(count) - 1
     rates, notes = {}, []
-    for p in sorted({1, max(1, threads)}):
+    ps = sorted({p for p in (1, 2, 4, 8) if p <= threads} | {max(1, threads)})
+    for p in ps:
         impl.accs_mt(op, SCALE[op], src, 0, sstr, dst, 0, dstr, count, levels, p)   # warm-up (page-in)
         n, t0 = 0, time.perf_counter()
         while True:
             impl.accs_mt(op, SCALE[op], src, 0, sstr, dst, 0, dstr, count, levels, p)
             n += 1
             el = time.perf_counter() - t0
-            if (el >= seconds / 2 and n >= 2) or n >= 10000:
+            if (el >= seconds / len(ps) and n >= 2) or n >= 10000:
                 break
         rates[p] = round(3 * patch_bytes(count) * n / el / 2 ** 30, 3)
         notes.append(f"P={p}: {n} full {workload} steps in {el:.1f} s")
     P = max(rates)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
     return {"value": rates[P], "unit": "GiB/s", "cores": P, "kind": kind, "single_core_value": rates[1],
+            "by_workers": {str(k): v for k, v in sorted(rates.items())},
+            "host": {"cpu": model, "nproc": os.cpu_count()},
             "sample": "; ".join(notes) + "; P host threads each on its own slab of the patch (outer level); "
                       + ("reference comex/src-common/acc.h _acc (HAVE_BLAS=0, gcc -O2) per row, "
                          "odometer of comex.c:6936-6961" if kind == "reference" else "oracle restatement")}
