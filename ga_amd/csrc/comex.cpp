@@ -252,6 +252,9 @@ static void release_view(View &v) {
 }
 
 // ---- non-blocking handles ------------------------------------------------
+static int g_nb_job[kMaxNb];   // nb handle -> its remote accumulate job (0: none; see progress_jobs)
+static void run_job(int id);
+
 static int nb_alloc() {
     Runtime &r = rt();
     for (int k = 0; k < kMaxNb; ++k) {
@@ -264,6 +267,8 @@ static int nb_alloc() {
     }
     // table full: complete the oldest like nb_wait_for_handle (comex.c:5653)
     const int i = r.nb_next;
+    if (g_nb_job[i]) run_job(g_nb_job[i]);
+    g_nb_job[i] = 0;
     GA_HIP(hipEventSynchronize(r.nb_ev[i]));
     r.nb_next = (i + 1) % kMaxNb;
     return i;
@@ -273,6 +278,7 @@ static int nb_alloc() {
 static void nb_complete_now(comex_request_t *h, int stream_idx = 0) {
     Runtime &r = rt();
     const int i = nb_alloc();
+    g_nb_job[i] = 0;
     GA_HIP(hipEventRecord(r.nb_ev[i], r.streams.empty() ? r.stream : r.streams[stream_idx]));
     *h = i;
 }
@@ -489,52 +495,203 @@ static void progress_loop() {
     for (hipEvent_t e : pool) (void)hipEventDestroy(e);
 }
 
-static void remote_acc(int t, int op, const void *scale, void *src, const int *ss, void *dst, const int *ds,
-                       const int *count, int levels) {
+// ---- asynchronous remote accumulate ---------------------------------------
+// Reference: nb_accs -> nb_accs_packed (comex.c:6890-7109) packs the patch and
+// sends it to the owner's progress rank, chunked.  Here a remote accumulate is
+// a job: row-range chunks are packed into the exported staging sub-ring for
+// the target as space allows, and each chunk is posted to the owner's inbox
+// once its pack kernel has finished.  Jobs advance whenever the caller is in
+// the library (any transfer, wait, test, fence), so the remote owners of one
+// GA patch -- one ARMCI_NbAccS each (onesided.c:1421-1438) -- progress side by
+// side instead of one owner after another.  Per target, chunks are posted in
+// the order their staging was allocated: ring release stays FIFO and the
+// owner's done counter matches the posted sequence.
+struct Chunk { int job; uint64_t off, len, rb, re; hipEvent_t ev; };
+struct RJob {
+    int id = 0, t = 0, op = 0, levels = 0;
+    unsigned char scale[16] = {};
+    View sv;
+    bool staged_src = false;
+    int ss[8] = {}, ds[8] = {}, count[8] = {}, pstride[8] = {};
+    char *dst = nullptr;
+    int64_t slo = 0, shi = 0;
+    uint64_t rows = 0, per_req = 0, next_rb = 0;
+    int outstanding = 0;
+};
+static std::deque<RJob> g_jobs;                 // unfinished jobs, creation order
+static std::vector<std::deque<Chunk>> g_out;    // per target: packed or packing, not yet posted
+static std::vector<hipEvent_t> g_chunk_ev;      // event pool
+static int g_job_next = 1;
+
+// stage_alloc without waiting: false when the ring has no room now
+static bool try_stage_alloc(int t, uint64_t len, uint64_t &off) {
+    Runtime &r = rt();
+    const uint64_t sub = sub_ring_bytes();
+    if (len > sub) fatal("staging request %lu exceeds ring %lu", (unsigned long)len, (unsigned long)sub);
+    reap(t);
+    std::deque<Pending> &q = g_pend[t];
+    uint64_t &head = r.stage_head[t];
+    if (q.empty()) { head = 0; off = 0; return true; }
+    const uint64_t tail = q.front().off;
+    if (head > tail) {
+        if (head + len <= sub) { off = head; return true; }
+        if (len <= tail) { off = 0; return true; }
+    } else if (head < tail) {
+        if (head + len <= tail) { off = head; return true; }
+    }
+    return false;
+}
+
+static RJob *find_job(int id) {
+    for (RJob &j : g_jobs) if (j.id == id) return &j;
+    return nullptr;
+}
+
+// one non-blocking pass over every job; true if anything moved
+static bool progress_jobs() {
+    Runtime &r = rt();
+    if (g_jobs.empty()) return false;
+    const uint64_t sub = sub_ring_bytes();
+    bool any = false;
+    // post chunks whose pack finished, per target in allocation order
+    for (int t = 0; t < (int)g_out.size(); ++t) {
+        std::deque<Chunk> &o = g_out[t];
+        while (!o.empty()) {
+            Chunk &c = o.front();
+            const hipError_t e = hipEventQuery(c.ev);
+            if (e == hipErrorNotReady) break;
+            if (e != hipSuccess) fatal("pack kernel failed: %s", hipGetErrorString(e));
+            RJob *j = find_job(c.job);
+            post_request(t, j->op, j->scale, (uint64_t)(uintptr_t)j->dst, j->ds, j->count, j->levels,
+                         (uint64_t)t * sub + c.off, c.len, c.rb, c.re);
+            --j->outstanding;
+            g_chunk_ev.push_back(c.ev);
+            o.pop_front();
+            any = true;
+        }
+    }
+    // pack new chunks where the target's ring has room
+    for (RJob &j : g_jobs) {
+        while (j.next_rb < j.rows) {
+            const uint64_t rb = j.next_rb, re = std::min(j.rows, rb + j.per_req);
+            const uint64_t len = (re - rb) * (uint64_t)j.count[0];
+            uint64_t off = 0;
+            if (!try_stage_alloc(j.t, len, off)) break;
+            const uint64_t seq = ++r.posted[j.t];
+            g_pend[j.t].push_back({seq, off, len});
+            r.stage_head[j.t] = off + len;
+            char *stage = r.staging + (size_t)j.t * sub + off;
+            hipEvent_t ev;
+            if (g_chunk_ev.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            else { ev = g_chunk_ev.back(); g_chunk_ev.pop_back(); }
+            {
+                std::lock_guard<std::mutex> g(r.launch_mu);
+                // a staged host src copy sits on stream 0 (ordered there at job start)
+                const int si = j.staged_src ? 0 : sched_pick(span_of(j.sv.dev, j.slo, j.shi),
+                                                             span_of(stage, 0, (int64_t)len), len);
+                // rows [rb, re) of src into the slice, rebased so row rb lands at `stage`
+                const int rc = launch_strided(kOpCopy, nullptr, j.sv.dev, j.ss, stage - (int64_t)rb * j.count[0],
+                                              j.pstride, j.count, j.levels, r.streams[si], nullptr, rb, re);
+                if (rc) fatal("pack launch failed (%d)", rc);
+                GA_HIP(hipEventRecord(ev, r.streams[si]));
+            }
+            g_out[j.t].push_back({j.id, off, len, rb, re, ev});
+            ++j.outstanding;
+            j.next_rb = re;
+            any = true;
+        }
+    }
+    // retire jobs whose every chunk is posted (the source is reusable)
+    for (auto it = g_jobs.begin(); it != g_jobs.end();) {
+        if (it->next_rb >= it->rows && it->outstanding == 0) {
+            release_view(it->sv);
+            it = g_jobs.erase(it);
+            any = true;
+        } else {
+            ++it;
+        }
+    }
+    return any;
+}
+
+static void backoff(unsigned &spins) {
+    if (++spins > 256) sched_yield();
+}
+
+static void run_job(int id) {
+    for (unsigned spins = 0; find_job(id); backoff(spins))
+        if (progress_jobs()) spins = 0;
+}
+
+static bool target_busy(int t) {
+    for (const RJob &j : g_jobs) if (j.t == t) return true;
+    return false;
+}
+
+static void drain_target(int t) {
+    for (unsigned spins = 0; target_busy(t); backoff(spins))
+        if (progress_jobs()) spins = 0;
+}
+
+static void drain_all_jobs() {
+    for (unsigned spins = 0; !g_jobs.empty(); backoff(spins))
+        if (progress_jobs()) spins = 0;
+}
+
+// start a remote accumulate; returns its job id (0: nothing to do)
+static int remote_acc_start(int t, int op, const void *scale, void *src, const int *ss, void *dst, const int *ds,
+                            const int *count, int levels) {
     Runtime &r = rt();
     const int esz = elem_size(op);
     const int64_t row_bytes = (int64_t)(count[0] / esz) * esz;
     uint64_t rows = 1;
     for (int j = 1; j <= levels; ++j) rows *= (uint64_t)count[j];
-    if (rows == 0 || row_bytes == 0) return;
-    int64_t slo = 0, shi = 0;
-    side_span_host(ss, count, levels, count[0], &slo, &shi);
-    View sv = local_view(src, slo, shi);
+    if (rows == 0 || row_bytes == 0) return 0;
+    RJob j;
+    j.id = g_job_next++;
+    if (g_job_next > (1 << 30)) g_job_next = 1;
+    j.t = t;
+    j.op = op;
+    j.levels = levels;
+    memcpy(j.scale, scale, (size_t)esz);
+    for (int k = 0; k <= levels; ++k) j.count[k] = count[k];
+    for (int k = 0; k < levels; ++k) { j.ss[k] = ss[k]; j.ds[k] = ds[k]; }
+    j.dst = (char *)dst;
+    side_span_host(ss, count, levels, count[0], &j.slo, &j.shi);
     // destination must be a registered segment of the owner (reg_cache_find)
     int64_t dlo = 0, dhi = 0;
     side_span_host(ds, count, levels, count[0], &dlo, &dhi);
     (void)remote_view(t, dst, dlo, dhi);
-
+    j.sv = local_view(src, j.slo, j.shi);
+    j.staged_src = j.sv.staged != nullptr;
+    if (j.staged_src) {
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        sched_join();
+    }
     const uint64_t sub = sub_ring_bytes();
-    uint64_t rows_per_req = std::max<uint64_t>(1, sub / (uint64_t)count[0]);
     if ((uint64_t)count[0] > sub) fatal("row of %d bytes exceeds staging ring", count[0]);
-    int pstride[8];
-    {
-        int64_t acc = count[0];
-        for (int j = 0; j < levels; ++j) { pstride[j] = (int)acc; acc *= count[j + 1]; }
+    j.per_req = std::max<uint64_t>(1, sub / (uint64_t)count[0]);
+    j.rows = rows;
+    int64_t acc = count[0];
+    for (int k = 0; k < levels; ++k) { j.pstride[k] = (int)acc; acc *= count[k + 1]; }
+    if (g_out.size() != (size_t)r.size) g_out.resize(r.size);
+    static const bool async_ok = [] {
+        const char *e = getenv("COMEX_AMD_ASYNC_ACC");   // 0: every remote accumulate completes in its call
+        return !e || atoi(e) != 0;
+    }();
+    const bool host_src = j.sv.registered || j.sv.staged || !async_ok;
+    g_jobs.push_back(j);
+    const int id = j.id;
+    progress_jobs();
+    if (host_src) {
+        // pageable host source: its pages are pinned (or copied) for this call
+        // only -- a view that outlived the call could be shadowed by another
+        // call's registration of the same pages and unmapped under it -- so
+        // the job completes before the call returns
+        run_job(id);
+        return 0;
     }
-    for (uint64_t rb = 0; rb < rows; rb += rows_per_req) {
-        const uint64_t re = std::min(rows, rb + rows_per_req);
-        const uint64_t len = (re - rb) * (uint64_t)count[0];
-        const uint64_t off = stage_alloc(t, len);
-        char *stage = r.staging + (size_t)t * sub + off;
-        int si = 0;
-        {
-            std::lock_guard<std::mutex> g(r.launch_mu);
-            if (needs_sync(sv)) sched_join();   // a staged src copy sits on stream 0
-            si = needs_sync(sv) ? 0 : sched_pick(span_of(sv.dev, slo, shi), span_of(stage, 0, (int64_t)len));
-            // pack rows [rb, re) of src into the staging slice (rebased so row rb lands at `stage`)
-            const int rc = launch_strided(kOpCopy, nullptr, sv.dev, ss, stage - (int64_t)rb * count[0], pstride,
-                                          count, levels, r.streams[si], nullptr, rb, re);
-            if (rc) fatal("pack launch failed (%d)", rc);
-        }
-        GA_HIP(hipStreamSynchronize(r.streams[si]));   // packed bytes complete before the owner reads them
-        const uint64_t seq = ++r.posted[t];
-        g_pend[t].push_back({seq, off, len});
-        r.stage_head[t] = off + len;
-        post_request(t, op, scale, (uint64_t)(uintptr_t)dst, ds, count, levels, (uint64_t)t * sub + off, len, rb, re);
-    }
-    release_view(sv);
+    return id;
 }
 
 static void fence_target(int t) {
@@ -542,6 +699,7 @@ static void fence_target(int t) {
     if (r.size == 1 || t == r.rank) return;
     if (!r.same_node(t)) { wire_fence(t); return; }
     if (r.posted.empty()) return;
+    drain_target(t);
     wait_done(t, r.posted[t]);
 }
 
@@ -563,6 +721,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
                 int levels, int proc, int group, comex_request_t *hdl) {
     ensure_init();
     Runtime &r = rt();
+    progress_jobs();   // pending remote accumulates advance on every call
     if (levels < 0 || levels >= COMEX_MAX_STRIDE_LEVEL) fatal("stride_levels %d out of range", levels);
     if (!count) fatal("count is NULL");
     uint64_t rows = 1;
@@ -608,8 +767,13 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     }
 
     if (world != r.rank && kind == X_ACC) {
-        remote_acc(world, op, scale, src, ss, dst, ds, count, levels);
-        if (hdl) nb_complete_now(hdl);
+        const int id = remote_acc_start(world, op, scale, src, ss, dst, ds, count, levels);
+        if (hdl) {
+            nb_complete_now(hdl);
+            g_nb_job[*hdl] = id;
+        } else if (id) {
+            run_job(id);
+        }
         return COMEX_SUCCESS;
     }
 
@@ -814,6 +978,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         }
         // remote io-vector accumulate: pack the sources + the owner addresses into
         // staging, the owner's progress thread applies them (k_iov)
+        drain_target(world);   // its staging ring is allocated and posted in order
         const uint64_t sub = sub_ring_bytes();
         const uint64_t per_pair = (uint64_t)bytes + 8;
         const int pairs_per_req = (int)std::max<uint64_t>(1, (sub - 32) / per_pair);
@@ -950,7 +1115,10 @@ int comex_initialized() { return rt().initialized ? 1 : 0; }
 int comex_finalize() {
     Runtime &r = rt();
     if (!r.initialized) return COMEX_SUCCESS;
-    comex_barrier(COMEX_GROUP_WORLD);
+    comex_barrier(COMEX_GROUP_WORLD);   // drains every remote accumulate job
+    for (hipEvent_t e : g_chunk_ev) (void)hipEventDestroy(e);
+    g_chunk_ev.clear();
+    g_out.clear();
     wire_finalize();
     if (r.progress.joinable()) {
         r.stop.store(true, std::memory_order_release);
@@ -1031,6 +1199,7 @@ int comex_fence_all(comex_group_t group) {
     ensure_init();
     (void)group;
     Runtime &r = rt();
+    drain_all_jobs();   // every target's chunks posted (side by side), then wait for each
     for (int t = 0; t < r.size; ++t) fence_target(t);
     std::lock_guard<std::mutex> g(r.launch_mu);
     sched_sync_all();
@@ -1119,6 +1288,8 @@ int comex_wait(comex_request_t *h) {
     Runtime &r = rt();
     if (!h || *h < 0 || *h >= kMaxNb) return COMEX_SUCCESS;
     if (r.nb_used[*h]) {
+        if (g_nb_job[*h]) run_job(g_nb_job[*h]);
+        g_nb_job[*h] = 0;
         GA_HIP(hipEventSynchronize(r.nb_ev[*h]));
         r.nb_used[*h] = false;
     }
@@ -1131,6 +1302,11 @@ int comex_test(comex_request_t *h, int *status) {
     Runtime &r = rt();
     *status = 0;   // 0 = complete (reference returns status 0 when done)
     if (!h || *h < 0 || *h >= kMaxNb || !r.nb_used[*h]) return COMEX_SUCCESS;
+    if (g_nb_job[*h]) {
+        progress_jobs();
+        if (find_job(g_nb_job[*h])) { *status = 1; return COMEX_SUCCESS; }
+        g_nb_job[*h] = 0;
+    }
     hipError_t e = hipEventQuery(r.nb_ev[*h]);
     if (e == hipErrorNotReady) { *status = 1; return COMEX_SUCCESS; }
     if (e != hipSuccess) fatal("request failed: %s", hipGetErrorString(e));
@@ -1143,6 +1319,8 @@ int comex_wait_all(comex_group_t group) {
     ensure_init();
     (void)group;
     Runtime &r = rt();
+    drain_all_jobs();
+    for (int i = 0; i < kMaxNb; ++i) g_nb_job[i] = 0;
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
         sched_sync_all();
