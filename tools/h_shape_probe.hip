@@ -20,7 +20,7 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 
 constexpr int64_t kLd = 65536, kRow = 16384, kRows = 4096;
 
-template <int BS, int U>
+template <int BS, int U, int POL = 3>   // POL bit0: nt loads, bit1: nt stores
 __global__ __launch_bounds__(BS) void k_h(const char *src, char *dst, double s) {
     constexpr uint32_t chunk_bytes = BS * U * 16;
     constexpr uint32_t cpr = kRow / chunk_bytes;   // chunks per row (power of two)
@@ -32,21 +32,27 @@ __global__ __launch_bounds__(BS) void k_h(const char *src, char *dst, double s) 
     v2d x[U], y[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-        x[k] = __builtin_nontemporal_load(sp + k * BS);
-        y[k] = __builtin_nontemporal_load(dp + k * BS);
+        if constexpr (POL & 1) {
+            x[k] = __builtin_nontemporal_load(sp + k * BS);
+            y[k] = __builtin_nontemporal_load(dp + k * BS);
+        } else {
+            x[k] = sp[k * BS];
+            y[k] = dp[k * BS];
+        }
     }
 #pragma unroll
     for (int k = 0; k < U; ++k) {
         v2d p = x[k] * s;
-        __builtin_nontemporal_store(y[k] + p, dp + k * BS);
+        if constexpr (POL & 2) __builtin_nontemporal_store(y[k] + p, dp + k * BS);
+        else dp[k * BS] = y[k] + p;
     }
 }
 
 typedef void (*Launch)(const char *, char *, hipStream_t);
-template <int BS, int U>
+template <int BS, int U, int POL = 3>
 static void launch(const char *s, char *d, hipStream_t st) {
     const uint32_t blocks = (uint32_t)(kRows * kRow / (BS * U * 16));
-    hipLaunchKernelGGL((k_h<BS, U>), dim3(blocks), dim3(BS), 0, st, s, d, 0.7071067811865476);
+    hipLaunchKernelGGL((k_h<BS, U, POL>), dim3(blocks), dim3(BS), 0, st, s, d, 0.7071067811865476);
 }
 
 struct Variant { std::string name; Launch fn; int nstreams; std::vector<double> gbs; };
@@ -75,6 +81,10 @@ int main(int argc, char **argv) {
         {"bs64_u4", launch<64, 4>, 1, {}}, {"bs128_u2", launch<128, 2>, 1, {}},
         {"bs256_u1_2streams", launch<256, 1>, 2, {}}, {"bs512_u1_2streams", launch<512, 1>, 2, {}},
         {"bs1024_u1_2streams", launch<1024, 1>, 2, {}},
+        {"bs64_u1_2streams", launch<64, 1>, 2, {}},
+        {"bs64_u1_2streams_plainloads", launch<64, 1, 2>, 2, {}},
+        {"bs64_u1_2streams_plainstores", launch<64, 1, 1>, 2, {}},
+        {"bs64_u1_2streams_plain", launch<64, 1, 0>, 2, {}},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
