@@ -139,6 +139,18 @@ def last_launch():
             "launches": n.value, "blocks": b.value}
 
 
+def plan_strided(op, src, src_stride, dst, dst_stride, count, stride_levels, row_begin=0, row_end=None):
+    """The launcher's plan for a strided op (no launch, no GPU): dict or raises on an error code."""
+    out = (ctypes.c_longlong * 8)()
+    rc = lib().gaamd_plan_strided(op, ctypes.c_void_p(src), int_array(src_stride), ctypes.c_void_p(dst),
+                                  int_array(dst_stride), int_array(count), stride_levels, row_begin,
+                                  (1 << 64) - 1 if row_end is None else row_end, out)
+    if rc:
+        raise ValueError(f"plan error {rc}")
+    return {"kind": KIND_NAME.get(out[0], out[0]), "width": out[1], "unroll": out[2], "block": out[3],
+            "launches": out[4], "blocks": out[5], "levels": out[6], "aligned": bool(out[7])}
+
+
 def kernel_counts():
     """launches so far by kind (this process): {'rows': n, 'flat': n, 'serial': n}"""
     c = (ctypes.c_ulonglong * 4)()

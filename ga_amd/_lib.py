@@ -130,6 +130,9 @@ SIGNATURES = {
     "gaamd_last_launch": (ctypes.c_int, [c_int_p, c_int_p, c_int_p, c_int_p,
                                          ctypes.POINTER(ctypes.c_ulonglong)]),
     "gaamd_kernel_counts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
+    "gaamd_plan_strided": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, c_int_p, ctypes.c_void_p, c_int_p, c_int_p,
+                                          ctypes.c_int, ctypes.c_ulonglong, ctypes.c_ulonglong,
+                                          ctypes.POINTER(ctypes.c_longlong)]),
     "gaamd_set_tuning": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     "gaamd_get_tuning": (ctypes.c_int, [ctypes.c_char_p]),
     "gaamd_device_count": (ctypes.c_int, []),

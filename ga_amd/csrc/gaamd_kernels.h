@@ -77,6 +77,9 @@ struct LaunchInfo {
     int unroll;
     int launches;
     uint64_t blocks;
+    int block;     // threads per block (rows kernels)
+    int levels;    // stride levels after dropping count-1 levels and merging contiguous ones
+    int aligned;   // 1: chunk grid shifted to chunk-aligned dst addresses
 };
 
 // Enqueue `op` (kOpCopy or COMEX_ACC_*) over the strided patch.  src/dst
@@ -85,7 +88,7 @@ struct LaunchInfo {
 int launch_strided(int op, const void *scale, const void *src, const int *src_stride,
                    void *dst, const int *dst_stride, const int *count, int stride_levels,
                    hipStream_t stream, LaunchInfo *info,
-                   uint64_t row_begin = 0, uint64_t row_end = ~0ull);
+                   uint64_t row_begin = 0, uint64_t row_end = ~0ull, bool plan_only = false);
 
 // byte span [lo, hi) of one side relative to its base pointer
 void side_span_host(const int *stride, const int *count, int stride_levels, int64_t row_bytes,

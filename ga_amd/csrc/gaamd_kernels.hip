@@ -682,7 +682,7 @@ void side_span_host(const int *stride, const int *count, int stride_levels, int6
 
 int launch_strided(int op, const void *scale, const void *src, const int *src_stride,
                    void *dst, const int *dst_stride, const int *count, int stride_levels,
-                   hipStream_t stream, LaunchInfo *info, uint64_t row_begin, uint64_t row_end) {
+                   hipStream_t stream, LaunchInfo *info, uint64_t row_begin, uint64_t row_end, bool plan_only) {
     const Tuning &tn = g_tuning;
     if (info) memset(info, 0, sizeof(*info));
     if (stride_levels < 0 || stride_levels > kMaxLevels) return -2;
@@ -763,7 +763,14 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     for (int j = 0; j < L; ++j) a |= (uint64_t)ss[j] | (uint64_t)ds[j];
     int W = (int)lowbit(a);
     if (W > 16) W = 16;
-    if (W < esz) return -8;   // elements not naturally aligned
+    // elements below their natural alignment (a Fortran complex*16 array is only
+    // 8-byte aligned): one element per vector, read and written with dword-
+    // aligned multi-dword accesses, which global memory serves at any dword
+    // alignment; below 4 bytes the launcher refuses
+    if (W < esz) {
+        if (W < 4) return -8;
+        W = esz;
+    }
     if (serial) W = esz;
 
     Desc d;
@@ -840,18 +847,23 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         }
         if (tn.max_grid > 0 && blocks > (uint64_t)tn.max_grid) blocks = (uint64_t)tn.max_grid;
         if (blocks > lim) blocks = lim;
-        hipError_t e = dispatch(op, scale, W, kind, U, BS, tn.nontemporal, d, blocks, stream);
-        if (e != hipSuccess) return -100 - (int)e;
+        if (!plan_only) {
+            hipError_t e = dispatch(op, scale, W, kind, U, BS, tn.nontemporal, d, blocks, stream);
+            if (e != hipSuccess) return -100 - (int)e;
+        }
         ++launches;
         total_blocks += blocks;
     }
-    g_kind_count[kind] += (unsigned long long)launches;
+    if (!plan_only) g_kind_count[kind] += (unsigned long long)launches;
     if (info) {
         info->kind = kind;
         info->width = W;
         info->unroll = (kind == KK_ROWS) ? U : 0;
         info->launches = launches;
         info->blocks = total_blocks;
+        info->block = (kind == KK_ROWS) ? BS : (kind == KK_FLAT ? 256 : 64);
+        info->levels = L;
+        info->aligned = d.align_mask ? 1 : 0;
     }
     return 0;
 }
@@ -945,7 +957,10 @@ int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool ser
     if (!d.dst_list) a |= (uint64_t)(uintptr_t)d.dst_base | (uint64_t)d.bytes;
     int W = (int)lowbit(a);
     if (W > 16) W = 16;
-    if (W < esz) return -8;
+    if (W < esz) {   // sub-natural element alignment: see launch_strided
+        if (W < 4) return -8;
+        W = esz;
+    }
     if (serial) W = esz;
     d.nvec = (uint32_t)(row / W);
     d.nvec_div = make_fastdiv(d.nvec);

@@ -50,6 +50,24 @@ int gaamd_strided(int op, const void *scale, const void *src, const int *src_str
                           &g_last);
 }
 
+int gaamd_plan_strided(int op, const void *src, const int *src_stride, const void *dst, const int *dst_stride,
+                       const int *count, int stride_levels, unsigned long long row_begin,
+                       unsigned long long row_end, long long plan[8]) {
+    LaunchInfo li;
+    const double one[2] = {1.0, 0.0};
+    const int rc = launch_strided(op, one, src, src_stride, (void *)dst, dst_stride, count, stride_levels, nullptr,
+                                  &li, row_begin, row_end, true);
+    plan[0] = li.kind;
+    plan[1] = li.width;
+    plan[2] = li.unroll;
+    plan[3] = li.block;
+    plan[4] = li.launches;
+    plan[5] = (long long)li.blocks;
+    plan[6] = li.levels;
+    plan[7] = li.aligned;
+    return rc;
+}
+
 long gaamd_packed_size(const int *count, int stride_levels) {
     long n = count[0];
     for (int j = 1; j <= stride_levels; ++j) n *= count[j];

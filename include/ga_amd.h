@@ -61,6 +61,13 @@ int gaamd_unpack(const void *packed, void *dst, const int *dst_stride, const int
                  int stride_levels, void *stream);
 int gaamd_unpack_acc(int op, const void *scale, const void *packed, void *dst,
                      const int *dst_stride, const int *count, int stride_levels, void *stream);
+/* The launch plan of a strided operation without launching anything (no GPU
+ * needed): plan[0..7] = {kind (1 rows, 2 flat, 3 serial), vector width, unroll,
+ * threads per block, launches, blocks, stride levels after merging, chunk grid
+ * aligned}; row_end = ~0 for all rows.  Returns 0 or the launcher's error code. */
+int gaamd_plan_strided(int op, const void *src, const int *src_stride, const void *dst, const int *dst_stride,
+                       const int *count, int stride_levels, unsigned long long row_begin,
+                       unsigned long long row_end, long long plan[8]);
 /* kind / vector width / unroll / launches / blocks of the last kernel-level call */
 int gaamd_last_launch(int *kind, int *width, int *unroll, int *launches,
                       unsigned long long *blocks);

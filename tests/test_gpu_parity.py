@@ -359,6 +359,28 @@ def test_whole_chunk_rows_every_op(gpu_lib, oracle, direct):
         ga_amd.set_tuning("direct", old)
 
 
+@pytest.mark.parametrize("op,off", [(C.DCP, 8), (C.CPL, 4), (C.DBL, 4), (C.LNG, 4)])
+def test_sub_natural_alignment(gpu_lib, oracle, op, off):
+    """Elements below their natural alignment (a Fortran complex*16 array is only
+    8-byte aligned): one element per dword-aligned vector, 1-D and 2-D, both sides
+    misaligned, bit-exact vs the oracle."""
+    esz = C.ESZ[op]
+    for count, st in (([esz * 777], []), ([esz * 301, 9], [esz * 333 + 8])):
+        levels = len(st)
+        src = C.fill_bytes(op, 64 + C.span(st, count, levels)[1], 31)
+        dst = C.fill_bytes(op, 64 + C.span(st, count, levels)[1], 32)
+        sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+        sb.upload(src)
+        db.upload(dst)
+        assert ga_amd.comex_accs(op, C.SCALE[op], sb.ptr + off, st, db.ptr + 16 + off, st, count, levels, 0) == 0
+        ga_amd.comex_fence_all()
+        info = ga_amd.last_launch()
+        assert info["width"] == esz, info
+        want = dst.copy()
+        oracle.accs(op, C.SCALE[op], src, off, st, want, 16 + off, st, count, levels)
+        assert np.array_equal(db.download(np.uint8, dst.size), want), (op, off, count)
+
+
 def test_stream_scheduler_random_dependencies(gpu_lib, oracle):
     """Random chains of accumulates and puts over a few buffers, with overlapping
     and disjoint ranges, issued back to back: independent ops may run on

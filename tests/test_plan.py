@@ -1,0 +1,103 @@
+"""Host logic of the strided launcher, on the CPU (no GPU): gaamd_plan_strided
+runs the launcher's planning -- level merging, ordering/aliasing checks, vector
+width, kernel family, block size, chunk alignment, row ranges -- and returns the
+plan without launching.  Addresses are synthetic (nothing is dereferenced)."""
+import pytest
+
+import ga_amd
+
+DBL, FLT, DCP = 38, 39, 41
+COPY = 0
+SRC, DST = 0x7F0000000000, 0x7F4000000000   # far apart, 64 KiB-aligned
+
+
+def plan(op, src, ss, dst, ds, count, levels, rb=0, re=None):
+    return ga_amd.plan_strided(op, src, ss, dst, ds, count, levels, rb, re)
+
+
+def test_headline_shape():
+    p = plan(DBL, SRC, [65536], DST, [65536], [16384, 4096], 1)
+    assert p["kind"] == "rows" and p["width"] == 16 and p["levels"] == 1
+    assert p["block"] == 64 and p["blocks"] == 4096 * 16 and p["launches"] == 1 and not p["aligned"]
+
+
+def test_misaligned_rows_take_128_threads_and_aligned_chunks():
+    p = plan(DBL, SRC, [65600], DST, [65600], [16384, 4096], 1)
+    assert p["block"] == 128 and p["aligned"]
+
+
+def test_contiguous_rows_collapse_to_one_run():
+    p = plan(DBL, SRC, [16384], DST, [16384], [16384, 4096], 1)
+    assert p["levels"] == 0 and p["kind"] == "rows"
+
+
+def test_continuing_levels_merge():
+    # level 2 continues level 1 on both sides (stride2 = stride1 * count1)
+    p = plan(DBL, SRC, [8192, 8192 * 10], DST, [4096 * 3, 4096 * 3 * 10], [4096, 10, 7], 2)
+    assert p["levels"] == 1
+
+
+def test_overlapping_destination_rows_are_serial():
+    p = plan(DBL, SRC, [64], DST, [32], [64, 100], 1)          # dst rows overlap each other
+    assert p["kind"] == "serial" and p["width"] == 8
+
+
+def test_src_overlapping_dst_is_serial_in_place_is_not():
+    assert plan(DBL, SRC, [64], SRC + 8, [64], [64, 100], 1)["kind"] == "serial"
+    assert plan(DBL, SRC, [64], SRC, [64], [64, 100], 1)["kind"] != "serial"
+
+
+def test_row_range_of_a_rebased_packed_side_is_not_serial():
+    """The remote unpack-acc of rows [1000, 1100): the packed side is rebased so
+    row 1000 lands at its staging slice; the full-range span of that rebased
+    pointer would reach across dst and force the one-lane serial kernel."""
+    row, rows = 16384, 4096
+    staging = DST + (1 << 30)
+    packed0 = staging - 1000 * row                # rebased base
+    dst = staging - (8 << 20)                     # inside the rebased side's full span
+    p = plan(DBL, packed0, [row], dst, [65536], [row, rows], 1, 1000, 1100)
+    assert p["kind"] == "rows", p
+    assert p["blocks"] == 100 * (row // 1024)
+    # the same rows but overlapping for real are serial
+    p2 = plan(DBL, packed0, [row], packed0 + 8, [row], [row, rows], 1, 1000, 1100)
+    assert p2["kind"] == "serial"
+
+
+@pytest.mark.parametrize("off,op,want", [(0, DBL, 16), (8, DBL, 8), (4, FLT, 4), (8, DCP, 16), (4, DBL, 8)])
+def test_vector_width_follows_alignment(off, op, want):
+    p = plan(op, SRC + off, [65536], DST, [65536], [4096, 64], 1)
+    assert p["width"] == want
+
+
+def test_sub_dword_alignment_is_rejected():
+    """Elements below natural alignment run one per (dword-aligned) vector; below 4 bytes: refused."""
+    with pytest.raises(ValueError):
+        plan(DBL, SRC + 2, [65536], DST, [65536], [4096, 64], 1)
+
+
+def test_short_rows_take_the_flat_kernel():
+    assert plan(DBL, SRC, [1024], DST, [1024], [512, 1000], 1)["kind"] == "flat"
+    assert plan(DBL, SRC, [4096], DST, [4096], [2048, 1000], 1)["kind"] == "rows"
+
+
+def test_empty_patch_launches_nothing():
+    p = plan(DBL, SRC, [64], DST, [64], [64, 0], 1)
+    assert p["launches"] == 0
+
+
+def test_eight_gib_block_is_one_launch():
+    p = plan(DBL, SRC, [262144], DST, [262144 + 4096], [262144, 32768], 1)
+    assert p["kind"] == "rows" and p["launches"] == 1 and p["blocks"] == 32768 * 256
+
+
+def test_too_many_rows_is_an_error():
+    with pytest.raises(ValueError):
+        plan(COPY, SRC, [16, 16 * 65536], DST, [16, 16 * 65536], [16, 65536, 65536], 2)
+
+
+def test_block_knob_overrides_auto():
+    old = ga_amd.set_tuning("block", 256)
+    try:
+        assert plan(DBL, SRC, [65536], DST, [65536], [16384, 4096], 1)["block"] == 256
+    finally:
+        ga_amd.set_tuning("block", old)
