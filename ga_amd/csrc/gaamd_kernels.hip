@@ -371,7 +371,7 @@ __global__ __launch_bounds__(BS) void k_rows2_buf(const Desc2 d, const OP op) {
 }
 
 // FLAT kernel: vectors of all rows flattened, each lane decodes its own row.
-template <class OP, int W, int U, int BS, int LV>
+template <class OP, int W, int U, int BS, int LV, bool NT = false>
 __global__ __launch_bounds__(BS) void k_flat(const Desc d, const OP op) {
     typedef typename Vec<W>::T V;
     const uint32_t span = (uint32_t)BS * U;
@@ -388,13 +388,13 @@ __global__ __launch_bounds__(BS) void k_flat(const Desc d, const OP op) {
                 int64_t so, dof;
                 row_offsets<LV>(d, d.row0 + rl, so, dof);
                 dps[k] = d.dst + dof + (size_t)v * W;
-                a[k] = vload<W, false>(d.src + so + (size_t)v * W);
-                if constexpr (OP::kReadsDst) b[k] = vload<W, false>(dps[k]);
+                a[k] = vload<W, NT>(d.src + so + (size_t)v * W);
+                if constexpr (OP::kReadsDst) b[k] = vload<W, NT>(dps[k]);
             }
         }
 #pragma unroll
         for (int k = 0; k < U; ++k)
-            if (dps[k]) vstore<W, false>(dps[k], op.template apply<W>(b[k], a[k]));
+            if (dps[k]) vstore<W, NT>(dps[k], op.template apply<W>(b[k], a[k]));
     }
 }
 
@@ -546,6 +546,15 @@ static hipError_t dispatch_w(int kind, int U, int BS, int nt, const Desc &d, con
         }
         if (kind == KK_FLAT) {
             constexpr int UF = (W == 16) ? 2 : 4;
+            if (g_tuning.flat_nt) {
+                if (d.levels == 1)
+                    hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 1, true>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+                else if (d.levels == 2)
+                    hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 2, true>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+                else
+                    hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 0, true>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+                return hipGetLastError();
+            }
             if (d.levels == 1)
                 hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 1>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
             else if (d.levels == 2)

@@ -137,6 +137,7 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "xcd")) return &t.xcd;
     if (!strcmp(key, "order")) return &t.order;
     if (!strcmp(key, "direct")) return &t.direct;
+    if (!strcmp(key, "flat_nt")) return &t.flat_nt;
     return nullptr;
 }
 
