@@ -140,6 +140,7 @@ def remote_test(L, rank, size):
         raise SystemExit(f"rank {rank}: {bad.size} elements differ, first {bad[:5]}")
 
     say(rank, "block checked")
+    ga_amd.comex_barrier()   # nobody accumulates into a block (many-small below) while its owner checks it
     # remote strided get of the previous rank's patch
     out = np.zeros((90, 120), dtype=np.float64)
     assert ga_amd.comex_gets(seg[prv] + (7 + 11 * ld) * 8, [ld * 8], out.ctypes.data, [120 * 8], count, 1,
