@@ -495,7 +495,11 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel_ms_avg": round(r["avg_kernel_s"] * 1e3, 4),
                      "timing": "HIP event pair around the timed launches (all library streams joined) / steps",
-                     "streams": r["streams"]},
+                     "streams": r["streams"],
+                     "rocprof_check": ("consecutive launches overlap on the library streams: compare kernel_ms_avg "
+                                       "with the merged busy time per dispatch of the rocprofv3 kernel trace "
+                                       "(tools/kernel_union.py), not with AverageNs"
+                                       if r["streams"] > 1 else "compare kernel_ms_avg with rocprofv3 AverageNs")},
         "cpu_baseline": cpu,
     }
     if r.get("pipeline"):
