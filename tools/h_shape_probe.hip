@@ -18,7 +18,10 @@
 
 typedef double v2d __attribute__((ext_vector_type(2)));
 
-constexpr int64_t kLd = 65536, kRow = 16384, kRows = 4096;
+#ifndef LD_BYTES
+#define LD_BYTES 65536
+#endif
+constexpr int64_t kLd = LD_BYTES, kRow = 16384, kRows = 4096;
 
 template <int BS, int U, int POL = 3>   // POL bit0: nt loads, bit1: nt stores
 __global__ __launch_bounds__(BS) void k_h(const char *src, char *dst, double s) {
