@@ -175,6 +175,14 @@ SIGNATURES = {
     "NGA_Put": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p]),
     "NGA_Get": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p]),
     "NGA_Access": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p]),
+    "NGA_NbAcc": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p, ctypes.c_void_p,
+                         ctypes.POINTER(ctypes.c_long)]),
+    "NGA_NbPut": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p, ctypes.POINTER(ctypes.c_long)]),
+    "NGA_NbGet": (None, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_void_p, c_int_p, ctypes.POINTER(ctypes.c_long)]),
+    "NGA_NbWait": (None, [ctypes.POINTER(ctypes.c_long)]),
+    "NGA_Strided_acc": (None, [ctypes.c_int, c_int_p, c_int_p, c_int_p, ctypes.c_void_p, c_int_p, ctypes.c_void_p]),
+    "NGA_Strided_put": (None, [ctypes.c_int, c_int_p, c_int_p, c_int_p, ctypes.c_void_p, c_int_p]),
+    "NGA_Strided_get": (None, [ctypes.c_int, c_int_p, c_int_p, c_int_p, ctypes.c_void_p, c_int_p]),
     "NGA_Scatter": (None, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "NGA_Scatter_flat": (None, [ctypes.c_int, ctypes.c_void_p, c_int_p, ctypes.c_int]),
     "NGA_Scatter_acc": (None, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),

@@ -251,7 +251,12 @@ static int allocate(GArray &a) {
 // ---- owner iteration + the per-owner ARMCI call (ngai_*_common) ---------------
 enum GaOp { GA_ACC, GA_PUT, GA_GET };
 
-static void patch_op(GaOp kind, int g_a, const long *lo, const long *hi, void *buf, const long *ld, void *alpha) {
+// skip != nullptr: the strided (every skip[d]-th element) variants,
+// pnga_strided_acc/put/get (onesided.c:4225-4470).  nb != nullptr: the
+// non-blocking variants (pnga_nbacc/nbput/nbget, onesided.c:685, 1300, 1481):
+// every owner's transfer is non-blocking and its handle is returned.
+static void patch_op(GaOp kind, int g_a, const long *lo, const long *hi, void *buf, const long *ld, void *alpha,
+                     const long *skip = nullptr, std::vector<armci_hdl_t> *nb = nullptr) {
     GArray &a = arr(g_a);
     Runtime &r = rt();
     const int nd = a.ndim, size = a.elemsize;
@@ -292,47 +297,92 @@ static void patch_op(GaOp kind, int g_a, const long *lo, const long *hi, void *b
         while (d < nd && ++bi[d] > b1[d]) { bi[d] = b0[d]; ++d; }
         if (d == nd) break;
     }
-    // remote owners first, then the local one (onesided.c:1387-1400)
-    std::stable_partition(owners.begin(), owners.end(), [&](const Owner &o) { return o.proc != r.rank; });
+    // remote owners first, then the local one (onesided.c:1387-1400); the
+    // strided variants keep the iterator's order (gai_iterator_next)
+    if (!skip)
+        std::stable_partition(owners.begin(), owners.end(), [&](const Owner &o) { return o.proc != r.rank; });
     std::vector<armci_hdl_t> hdl;
     for (size_t k = 0; k < owners.size(); ++k) {
         Owner &o = owners[k];
-        // gam_ComputePatchIndex (onesided.c:330-337)
-        long idx = o.plo[0] - lo[0], factor = 1;
-        for (int d = 0; d < nd - 1; d++) { factor *= ld[d]; idx += factor * (o.plo[d + 1] - lo[d + 1]); }
-        char *pbuf = (char *)buf + (long)size * idx;
-        // remote address: owner's block base + offset of plo in its column-major block
-        long roff = 0, rf = 1;
-        for (int d = 0; d < nd; d++) { roff += (o.plo[d] - o.blo[d]) * rf; rf *= o.ldrem[d]; }
-        char *prem = (char *)a.ptr[o.proc] + (long)size * roff;
-        int count[GA_MAX_DIM], stride_rem[GA_MAX_DIM], stride_loc[GA_MAX_DIM];
-        for (int d = 0; d < nd; d++) count[d] = (int)(o.phi[d] - o.plo[d] + 1);   // gam_ComputeCount
-        count[0] *= size;
-        stride_rem[0] = stride_loc[0] = size;                                       // gam_setstride
-        for (int d = 0; d < nd - 1; d++) {
-            stride_rem[d] *= (int)o.ldrem[d];
-            stride_loc[d] *= (int)ld[d];
-            stride_rem[d + 1] = stride_rem[d];
-            stride_loc[d + 1] = stride_loc[d];
+        int count[2 * GA_MAX_DIM], stride_rem[2 * GA_MAX_DIM], stride_loc[2 * GA_MAX_DIM];
+        int levels = nd - 1;
+        char *pbuf, *prem;
+        if (skip) {
+            // gai_correct_strided_patch (onesided.c:4051-4070): first/last selected element
+            bool empty = false;
+            for (int d = 0; d < nd; d++) {
+                long delta = o.plo[d] - lo[d];
+                if (delta % skip[d]) o.plo[d] = o.plo[d] - delta % skip[d] + skip[d];
+                delta = o.phi[d] - lo[d];
+                if (delta % skip[d]) o.phi[d] -= delta % skip[d];
+                if (o.phi[d] < o.plo[d]) empty = true;
+            }
+            if (empty) continue;
+            // gai_FindOffset(blo, plo, ldrem) (4204-4216): remote offset of plo
+            long roff = 0, rf = 1;
+            for (int d = 0; d < nd; d++) { roff += (o.plo[d] - o.blo[d]) * rf; if (d < nd - 1) rf *= o.ldrem[d]; }
+            prem = (char *)a.ptr[o.proc] + (long)size * roff;
+            // gai_ComputePatchIndexWithSkip (4178-4202): the local buffer holds only
+            // the selected elements
+            long idx = (o.plo[0] - lo[0]) / skip[0];
+            for (int d = 0; d < nd - 1; d++) idx += ld[d] * ((o.plo[d + 1] - lo[d + 1]) / skip[d + 1]);
+            pbuf = (char *)buf + (long)size * idx;
+            // gai_ComputeCountWithSkip (4077-4100, the "#if 1" form): one element per
+            // run, then the selected elements of every dimension as stride levels
+            count[0] = size;
+            for (int d = 0; d < nd; d++) count[d + 1] = (int)((o.phi[d] - o.plo[d]) / skip[d] + 1);
+            levels = nd;
+            // gai_SetStrideWithSkip (4135-4150, "#if 1"); the reference also reads
+            // ld[ndim-1], past the ndim-1 given, for a stride it never passes on
+            stride_rem[0] = stride_loc[0] = size;
+            for (int d = 0; d < nd; d++) {
+                stride_rem[d + 1] = stride_rem[d];
+                stride_rem[d] *= (int)skip[d];
+                stride_rem[d + 1] *= (int)o.ldrem[d];
+                stride_loc[d + 1] = stride_loc[d];
+                if (d < nd - 1) stride_loc[d + 1] *= (int)ld[d];
+            }
+        } else {
+            // gam_ComputePatchIndex (onesided.c:330-337)
+            long idx = o.plo[0] - lo[0], factor = 1;
+            for (int d = 0; d < nd - 1; d++) { factor *= ld[d]; idx += factor * (o.plo[d + 1] - lo[d + 1]); }
+            pbuf = (char *)buf + (long)size * idx;
+            // remote address: owner's block base + offset of plo in its column-major block
+            long roff = 0, rf = 1;
+            for (int d = 0; d < nd; d++) { roff += (o.plo[d] - o.blo[d]) * rf; rf *= o.ldrem[d]; }
+            prem = (char *)a.ptr[o.proc] + (long)size * roff;
+            for (int d = 0; d < nd; d++) count[d] = (int)(o.phi[d] - o.plo[d] + 1);   // gam_ComputeCount
+            count[0] *= size;
+            stride_rem[0] = stride_loc[0] = size;                                       // gam_setstride
+            for (int d = 0; d < nd - 1; d++) {
+                stride_rem[d] *= (int)o.ldrem[d];
+                stride_loc[d] *= (int)ld[d];
+                stride_rem[d + 1] = stride_rem[d];
+                stride_loc[d + 1] = stride_loc[d];
+            }
         }
         if (kind == GA_ACC && o.proc == r.rank) {
             long e = 1;
-            for (int d = 0; d < nd; d++) e *= o.phi[d] - o.plo[d] + 1;
+            for (int d = 0; d < nd; d++) e *= (o.phi[d] - o.plo[d]) / (skip ? skip[d] : 1) + 1;
             g_stat.accloc += (double)size * e;
         }
-        const bool last = (k + 1 == owners.size());
+        const bool last = !nb && (skip || k + 1 == owners.size());
         armci_hdl_t h = -1;
         if (kind == GA_ACC) {
-            if (last) ARMCI_AccS(a.optype, alpha, pbuf, stride_loc, prem, stride_rem, count, nd - 1, o.proc);
-            else ARMCI_NbAccS(a.optype, alpha, pbuf, stride_loc, prem, stride_rem, count, nd - 1, o.proc, &h);
+            if (last) ARMCI_AccS(a.optype, alpha, pbuf, stride_loc, prem, stride_rem, count, levels, o.proc);
+            else ARMCI_NbAccS(a.optype, alpha, pbuf, stride_loc, prem, stride_rem, count, levels, o.proc, &h);
         } else if (kind == GA_PUT) {
-            if (last) ARMCI_PutS(pbuf, stride_loc, prem, stride_rem, count, nd - 1, o.proc);
-            else ARMCI_NbPutS(pbuf, stride_loc, prem, stride_rem, count, nd - 1, o.proc, &h);
+            if (last) ARMCI_PutS(pbuf, stride_loc, prem, stride_rem, count, levels, o.proc);
+            else ARMCI_NbPutS(pbuf, stride_loc, prem, stride_rem, count, levels, o.proc, &h);
         } else {
-            if (last) ARMCI_GetS(prem, stride_rem, pbuf, stride_loc, count, nd - 1, o.proc);
-            else ARMCI_NbGetS(prem, stride_rem, pbuf, stride_loc, count, nd - 1, o.proc, &h);
+            if (last) ARMCI_GetS(prem, stride_rem, pbuf, stride_loc, count, levels, o.proc);
+            else ARMCI_NbGetS(prem, stride_rem, pbuf, stride_loc, count, levels, o.proc, &h);
         }
         if (h >= 0) hdl.push_back(h);
+    }
+    if (nb) {
+        nb->insert(nb->end(), hdl.begin(), hdl.end());
+        return;
     }
     for (armci_hdl_t &h : hdl) ARMCI_Wait(&h);   // nga_wait_internal
     if (kind == GA_GET) comex_fence_all(COMEX_GROUP_WORLD);   // data is in `buf` on return
@@ -549,6 +599,72 @@ static void c_patch(GaOp kind, int g_a, int lo[], int hi[], void *buf, int ld[],
     c2f_index(a.ndim, hi, fhi);
     if (a.ndim > 1) c2f(a.ndim - 1, ld, fld);
     patch_op(kind, g_a, flo, fhi, buf, fld, alpha);
+}
+
+// ---- strided (skip) and non-blocking variants: capi.c:1990-2060, 2103-2190 ----
+static void c_strided(GaOp kind, int g_a, int lo[], int hi[], int skip[], void *buf, int ld[], void *alpha) {
+    GArray &a = arr(g_a);
+    long flo[GA_MAX_DIM], fhi[GA_MAX_DIM], fld[GA_MAX_DIM] = {0}, fskip[GA_MAX_DIM];
+    c2f_index(a.ndim, lo, flo);
+    c2f_index(a.ndim, hi, fhi);
+    if (a.ndim > 1) c2f(a.ndim - 1, ld, fld);
+    c2f(a.ndim, skip, fskip);   // COPYC2F: reversed, no +1
+    for (int d = 0; d < a.ndim; d++)
+        if (fskip[d] < 1) fatal("nga_strided: invalid skip %ld along coordinate %d", fskip[d], d);
+    patch_op(kind, g_a, flo, fhi, buf, fld, alpha, fskip);
+}
+
+void NGA_Strided_acc(int g_a, int lo[], int hi[], int skip[], void *buf, int ld[], void *alpha) {
+    c_strided(GA_ACC, g_a, lo, hi, skip, buf, ld, alpha);
+}
+void NGA_Strided_put(int g_a, int lo[], int hi[], int skip[], void *buf, int ld[]) {
+    c_strided(GA_PUT, g_a, lo, hi, skip, buf, ld, nullptr);
+}
+void NGA_Strided_get(int g_a, int lo[], int hi[], int skip[], void *buf, int ld[]) {
+    c_strided(GA_GET, g_a, lo, hi, skip, buf, ld, nullptr);
+    comex_fence_all(COMEX_GROUP_WORLD);
+}
+
+// GA non-blocking handle -> the ARMCI handles of its owners (the reference's
+// gai_nbhdl agg lists, onesided.c:120-300); value = slot + 1, 0 = done
+struct GaNb { bool used = false; bool get = false; std::vector<armci_hdl_t> h; };
+static std::vector<GaNb> g_ga_nb;
+
+static void c_nb(GaOp kind, int g_a, int lo[], int hi[], void *buf, int ld[], void *alpha, ga_nbhdl_t *nbhandle) {
+    GArray &a = arr(g_a);
+    long flo[GA_MAX_DIM], fhi[GA_MAX_DIM], fld[GA_MAX_DIM] = {0};
+    c2f_index(a.ndim, lo, flo);
+    c2f_index(a.ndim, hi, fhi);
+    if (a.ndim > 1) c2f(a.ndim - 1, ld, fld);
+    size_t slot = 0;
+    while (slot < g_ga_nb.size() && g_ga_nb[slot].used) ++slot;
+    if (slot == g_ga_nb.size()) g_ga_nb.emplace_back();
+    GaNb &n = g_ga_nb[slot];
+    n.used = true;
+    n.get = kind == GA_GET;
+    n.h.clear();
+    patch_op(kind, g_a, flo, fhi, buf, fld, alpha, nullptr, &n.h);
+    *nbhandle = (ga_nbhdl_t)(slot + 1);
+}
+
+void NGA_NbAcc(int g_a, int lo[], int hi[], void *buf, int ld[], void *alpha, ga_nbhdl_t *nbhandle) {
+    c_nb(GA_ACC, g_a, lo, hi, buf, ld, alpha, nbhandle);
+}
+void NGA_NbPut(int g_a, int lo[], int hi[], void *buf, int ld[], ga_nbhdl_t *nbhandle) {
+    c_nb(GA_PUT, g_a, lo, hi, buf, ld, nullptr, nbhandle);
+}
+void NGA_NbGet(int g_a, int lo[], int hi[], void *buf, int ld[], ga_nbhdl_t *nbhandle) {
+    c_nb(GA_GET, g_a, lo, hi, buf, ld, nullptr, nbhandle);
+}
+void NGA_NbWait(ga_nbhdl_t *nbhandle) {   // pnga_nbwait -> nga_wait_internal (onesided.c:368)
+    if (!nbhandle || *nbhandle <= 0 || (size_t)*nbhandle > g_ga_nb.size()) return;
+    GaNb &n = g_ga_nb[(size_t)*nbhandle - 1];
+    if (!n.used) return;
+    for (armci_hdl_t &h : n.h) ARMCI_Wait(&h);
+    if (n.get) comex_fence_all(COMEX_GROUP_WORLD);   // data is in `buf` on return
+    n.h.clear();
+    n.used = false;
+    *nbhandle = 0;
 }
 
 void NGA_Acc(int g_a, int lo[], int hi[], void *buf, int ld[], void *alpha) { c_patch(GA_ACC, g_a, lo, hi, buf, ld, alpha); }

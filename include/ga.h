@@ -45,6 +45,19 @@ void NGA_Acc(int g_a, int lo[], int hi[], void *buf, int ld[], void *alpha);
 void NGA_Put(int g_a, int lo[], int hi[], void *buf, int ld[]);
 void NGA_Get(int g_a, int lo[], int hi[], void *buf, int ld[]);
 
+/* non-blocking patch operations (capi.c:2103-2190 -> pnga_nbacc/nbput/nbget,
+   onesided.c:685, 1300, 1481) and their wait (pnga_nbwait, onesided.c:368);
+   ga_nbhdl_t is GA's Integer (ga.h:18) */
+typedef long ga_nbhdl_t;
+void NGA_NbAcc(int g_a, int lo[], int hi[], void *buf, int ld[], void *alpha, ga_nbhdl_t *nbhandle);
+void NGA_NbPut(int g_a, int lo[], int hi[], void *buf, int ld[], ga_nbhdl_t *nbhandle);
+void NGA_NbGet(int g_a, int lo[], int hi[], void *buf, int ld[], ga_nbhdl_t *nbhandle);
+void NGA_NbWait(ga_nbhdl_t *nbhandle);
+/* every skip[d]-th element of the patch; buf holds only the selected elements
+   (capi.c:1990-2060 -> pnga_strided_acc/put/get, onesided.c:4225-4470) */
+void NGA_Strided_acc(int g_a, int lo[], int hi[], int skip[], void *buf, int ld[], void *alpha);
+void NGA_Strided_put(int g_a, int lo[], int hi[], int skip[], void *buf, int ld[]);
+void NGA_Strided_get(int g_a, int lo[], int hi[], int skip[], void *buf, int ld[]);
 /* direct access to the local block (an HBM address) */
 /* gather / scatter / scatter-accumulate of single elements: capi.c:3026-3160 ->
    gai_gatscat onesided.c:2747 (one ARMCI_GetV/PutV/AccV per owner).  subsArray[k]

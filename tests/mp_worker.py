@@ -328,6 +328,73 @@ def ga_test(L, rank, size):
                                  f"{sorted(set(int(x) for x in bad[:, 1]))[:10]}.., first got {q[tuple(bad[0])]} "
                                  f"want {p[tuple(bad[0])]}")
 
+    # strided (skip) accumulate / put / get (pnga_strided_*, onesided.c:4225-4470):
+    # every rank accumulates every 3rd row and 2nd column of [7..290] x [4..195]
+    L.GA_Zero(g)
+    slo, shi, skip = [7, 4], [290, 195], [3, 2]
+    n0, n1 = (shi[0] - slo[0]) // skip[0] + 1, (shi[1] - slo[1]) // skip[1] + 1
+    sld = n1 + 5
+    sbuf = (np.arange(n0 * sld, dtype=np.float64) % 29 - 14 + rank).reshape(n0, sld)
+    salpha = ctypes.c_double(rank + 2)
+    L.NGA_Strided_acc(g, ia(slo), ia(shi), ia(skip), sbuf.ctypes.data_as(ctypes.c_void_p), ia([sld]),
+                      ctypes.byref(salpha))
+    L.GA_Sync()
+    full = np.zeros(dims)
+    L.NGA_Get(g, ia([0, 0]), ia([dims[0] - 1, dims[1] - 1]), full.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]))
+    want = np.zeros(dims)
+    for r_ in range(size):
+        b_ = (np.arange(n0 * sld, dtype=np.float64) % 29 - 14 + r_).reshape(n0, sld)
+        want[slo[0]:shi[0] + 1:skip[0], slo[1]:shi[1] + 1:skip[1]] += (r_ + 2) * b_[:, :n1]
+    assert np.array_equal(full, want), "NGA_Strided_acc"
+    L.GA_Sync()
+    say(rank, "strided acc checked")
+    # rank 0 strided-puts every 2nd row/5th column, everybody strided-gets it back
+    L.GA_Zero(g)
+    plo2, phi2, pskip = [1, 0], [298, 199], [2, 5]
+    m0, m1 = (phi2[0] - plo2[0]) // pskip[0] + 1, (phi2[1] - plo2[1]) // pskip[1] + 1
+    pv = (np.arange(m0 * m1, dtype=np.float64) + 0.5).reshape(m0, m1)
+    if rank == 0:
+        L.NGA_Strided_put(g, ia(plo2), ia(phi2), ia(pskip), pv.ctypes.data_as(ctypes.c_void_p), ia([m1]))
+    L.GA_Sync()
+    gv = np.zeros((m0, m1))
+    L.NGA_Strided_get(g, ia(plo2), ia(phi2), ia(pskip), gv.ctypes.data_as(ctypes.c_void_p), ia([m1]))
+    assert np.array_equal(gv, pv), "NGA_Strided_put/get"
+    L.NGA_Get(g, ia([0, 0]), ia([dims[0] - 1, dims[1] - 1]), full.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]))
+    want = np.zeros(dims)
+    want[plo2[0]:phi2[0] + 1:pskip[0], plo2[1]:phi2[1] + 1:pskip[1]] = pv
+    assert np.array_equal(full, want), "NGA_Strided_put layout"
+    L.GA_Sync()
+    say(rank, "strided put/get checked")
+
+    # non-blocking acc / put / get (pnga_nbacc/nbput/nbget + pnga_nbwait)
+    L.GA_Zero(g)
+    nbh = ctypes.c_long(0)
+    L.NGA_NbAcc(g, ia(lo), ia(hi), buf.ctypes.data_as(ctypes.c_void_p), ia([ldc]), ctypes.byref(alpha),
+                ctypes.byref(nbh))
+    L.NGA_NbWait(ctypes.byref(nbh))
+    assert nbh.value == 0
+    L.GA_Sync()
+    L.NGA_Get(g, ia([0, 0]), ia([dims[0] - 1, dims[1] - 1]), full.ctypes.data_as(ctypes.c_void_p), ia([dims[1]]))
+    want = np.zeros(dims)
+    for r_ in range(size):
+        lo_r = [10 + r_, 5]
+        rr = hi[0] - lo_r[0] + 1
+        b_ = (np.arange(rr * (cols + 3), dtype=np.float64) % 37 - 18).reshape(rr, cols + 3)
+        want[lo_r[0]:hi[0] + 1, lo_r[1]:hi[1] + 1] += (r_ + 1) * b_[:, :cols]
+    assert np.array_equal(full, want), "NGA_NbAcc"
+    L.GA_Sync()
+    np_ = (np.arange(40 * 50, dtype=np.float64) - 7e4 * (rank + 1)).reshape(40, 50)
+    if phi[0] < dims[0]:
+        h1, h2 = ctypes.c_long(0), ctypes.c_long(0)
+        L.NGA_NbPut(g, ia(plo), ia(phi), np_.ctypes.data_as(ctypes.c_void_p), ia([50]), ctypes.byref(h1))
+        L.NGA_NbWait(ctypes.byref(h1))
+        nq = np.zeros((40, 50))
+        L.NGA_NbGet(g, ia(plo), ia(phi), nq.ctypes.data_as(ctypes.c_void_p), ia([50]), ctypes.byref(h2))
+        L.NGA_NbWait(ctypes.byref(h2))
+        assert np.array_equal(nq, np_), "NGA_NbPut/NbGet round trip"
+    L.GA_Sync()
+    say(rank, "nb acc/put/get checked")
+
     # gather / scatter / scatter-acc (gai_gatscat, onesided.c:2747): random
     # subscripts over every owner, repeated ones included
     L.GA_Zero(g)
