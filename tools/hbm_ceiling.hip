@@ -11,6 +11,9 @@
 #include <stdio.h>
 #include <stdint.h>
 #include <vector>
+#ifndef BS
+#define BS 256   // threads per block (-DBS=64 for the library's one-wave blocks)
+#endif
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
 
@@ -18,13 +21,13 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef double v2d __attribute__((ext_vector_type(2)));
 
 template <int U>
-__global__ __launch_bounds__(256) void k_read2(const v4u *a, const v4u *b, v4u *sink, uint32_t magic) {
-    const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+__global__ __launch_bounds__(BS) void k_read2(const v4u *a, const v4u *b, v4u *sink, uint32_t magic) {
+    const size_t base = (size_t)blockIdx.x * BS * U + threadIdx.x;
     v4u x[U], y[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-        x[k] = __builtin_nontemporal_load(a + base + k * 256);
-        y[k] = __builtin_nontemporal_load(b + base + k * 256);
+        x[k] = __builtin_nontemporal_load(a + base + k * BS);
+        y[k] = __builtin_nontemporal_load(b + base + k * BS);
     }
     uint32_t acc = 0;
 #pragma unroll
@@ -33,36 +36,36 @@ __global__ __launch_bounds__(256) void k_read2(const v4u *a, const v4u *b, v4u *
 }
 
 template <int U>
-__global__ __launch_bounds__(256) void k_write1(v4u *b, uint32_t v) {
-    const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+__global__ __launch_bounds__(BS) void k_write1(v4u *b, uint32_t v) {
+    const size_t base = (size_t)blockIdx.x * BS * U + threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < U; ++k) __builtin_nontemporal_store((v4u){v, v, v, (uint32_t)k}, b + base + k * 256);
+    for (int k = 0; k < U; ++k) __builtin_nontemporal_store((v4u){v, v, v, (uint32_t)k}, b + base + k * BS);
 }
 
 template <int U>
-__global__ __launch_bounds__(256) void k_copy(const v4u *a, v4u *b) {
-    const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+__global__ __launch_bounds__(BS) void k_copy(const v4u *a, v4u *b) {
+    const size_t base = (size_t)blockIdx.x * BS * U + threadIdx.x;
     v4u x[U];
 #pragma unroll
-    for (int k = 0; k < U; ++k) x[k] = __builtin_nontemporal_load(a + base + k * 256);
+    for (int k = 0; k < U; ++k) x[k] = __builtin_nontemporal_load(a + base + k * BS);
 #pragma unroll
-    for (int k = 0; k < U; ++k) __builtin_nontemporal_store(x[k], b + base + k * 256);
+    for (int k = 0; k < U; ++k) __builtin_nontemporal_store(x[k], b + base + k * BS);
 }
 
 #pragma clang fp contract(off)
 template <int U>
-__global__ __launch_bounds__(256) void k_axpy(const v2d *a, v2d *b, double s) {
-    const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+__global__ __launch_bounds__(BS) void k_axpy(const v2d *a, v2d *b, double s) {
+    const size_t base = (size_t)blockIdx.x * BS * U + threadIdx.x;
     v2d x[U], y[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-        x[k] = __builtin_nontemporal_load(a + base + k * 256);
-        y[k] = __builtin_nontemporal_load(b + base + k * 256);
+        x[k] = __builtin_nontemporal_load(a + base + k * BS);
+        y[k] = __builtin_nontemporal_load(b + base + k * BS);
     }
 #pragma unroll
     for (int k = 0; k < U; ++k) {
         v2d p = x[k] * s;
-        __builtin_nontemporal_store(y[k] + p, b + base + k * 256);
+        __builtin_nontemporal_store(y[k] + p, b + base + k * BS);
     }
 }
 
@@ -74,12 +77,12 @@ static const int streams_per_elem[] = {2, 1, 2, 3};
 
 template <int U>
 static void launch(Kind k, char *a, char *b, size_t bytes, hipStream_t st, v4u *sink) {
-    const uint32_t blocks = (uint32_t)(bytes / 16 / 256 / U);
+    const uint32_t blocks = (uint32_t)(bytes / 16 / BS / U);
     switch (k) {
-    case READ2: hipLaunchKernelGGL(k_read2<U>, dim3(blocks), dim3(256), 0, st, (const v4u *)a, (const v4u *)b, sink, 0x9e3779b9u); break;
-    case WRITE1: hipLaunchKernelGGL(k_write1<U>, dim3(blocks), dim3(256), 0, st, (v4u *)b, 7u); break;
-    case COPY: hipLaunchKernelGGL(k_copy<U>, dim3(blocks), dim3(256), 0, st, (const v4u *)a, (v4u *)b); break;
-    case AXPY: hipLaunchKernelGGL(k_axpy<U>, dim3(blocks), dim3(256), 0, st, (const v2d *)a, (v2d *)b, 0.7071067811865476); break;
+    case READ2: hipLaunchKernelGGL(k_read2<U>, dim3(blocks), dim3(BS), 0, st, (const v4u *)a, (const v4u *)b, sink, 0x9e3779b9u); break;
+    case WRITE1: hipLaunchKernelGGL(k_write1<U>, dim3(blocks), dim3(BS), 0, st, (v4u *)b, 7u); break;
+    case COPY: hipLaunchKernelGGL(k_copy<U>, dim3(blocks), dim3(BS), 0, st, (const v4u *)a, (v4u *)b); break;
+    case AXPY: hipLaunchKernelGGL(k_axpy<U>, dim3(blocks), dim3(BS), 0, st, (const v2d *)a, (v2d *)b, 0.7071067811865476); break;
     }
 }
 
@@ -118,9 +121,9 @@ static void run(Kind k, int U, size_t bytes, int nstreams, const Bufs &B, hipStr
         sum += gbs;
         if (gbs > best) best = gbs;
     }
-    printf("{\"kernel\": \"%s\", \"U\": %d, \"MiB_per_stream\": %zu, \"hip_streams\": %d, \"launches\": %d, "
+    printf("{\"kernel\": \"%s\", \"BS\": %d, \"U\": %d, \"MiB_per_stream\": %zu, \"hip_streams\": %d, \"launches\": %d, "
            "\"GBps_mean\": %.1f, \"GBps_best\": %.1f, \"us_per_launch\": %.2f}\n",
-           kname[k], U, bytes >> 20, nstreams, reps, sum / rounds, best,
+           kname[k], BS, U, bytes >> 20, nstreams, reps, sum / rounds, best,
            (double)bytes * streams_per_elem[k] / (sum / rounds * 1e9) * 1e6);
     fflush(stdout);
     CK(hipEventDestroy(e0));
