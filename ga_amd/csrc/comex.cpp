@@ -1101,6 +1101,21 @@ int comex_init() {
     }
     r.initialized = true;
     boot_barrier();
+    // the ARMCI_VERBOSE dump of the reference (comex.c:545-572): this run's configuration
+    const char *vb = getenv("COMEX_AMD_VERBOSE");
+    if (vb && atoi(vb) && r.rank == 0) {
+        hipDeviceProp_t prop;
+        const bool okp = hipGetDeviceProperties(&prop, r.device) == hipSuccess;
+        const char *async = getenv("COMEX_AMD_ASYNC_ACC");
+        const char *seg = getenv("COMEX_AMD_SEGMENT");
+        fprintf(stderr,
+                "ga_amd %s: ranks %d on %d node(s), device %d (%s, %d CUs), library streams %d, "
+                "staging %zu MiB/rank, remote acc %s, segments in %s, blocking sync %d\n",
+                gaamd_version(), r.size, r.nnodes, r.device, okp ? prop.gcnArchName : "?",
+                okp ? prop.multiProcessorCount : 0, (int)r.streams.size(), r.staging_bytes >> 20,
+                (async && !atoi(async)) ? "synchronous" : "asynchronous jobs", (seg && !strcmp(seg, "host")) ? "host" : "HBM",
+                r.blocking_sync ? 1 : 0);
+    }
     return COMEX_SUCCESS;
 }
 
