@@ -365,6 +365,15 @@ def host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_byt
             L.comex_fence_all(0)
             ts.append(time.perf_counter() - t0)
         out[f"zerocopy_{kind}_GiBps"] = alg_bytes / min(ts) / 2 ** 30
+        # the GA-typical case: the patch comes from host memory (MA), the array
+        # block (dst) lives in HBM -- only src crosses PCIe
+        ts = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            L.comex_accs(op, sp, ctypes.c_void_p(hsp), ss, ctypes.c_void_p(ddst.ptr), ds, cnt, levels, 0, 0)
+            L.comex_fence_all(0)
+            ts.append(time.perf_counter() - t0)
+        out[f"host_src_{kind}_hbm_dst_GiBps"] = alg_bytes / min(ts) / 2 ** 30
         if kind == "pinned":
             hs.free()
             hd.free()

@@ -1109,7 +1109,7 @@ int comex_init() {
         const char *async = getenv("COMEX_AMD_ASYNC_ACC");
         const char *seg = getenv("COMEX_AMD_SEGMENT");
         fprintf(stderr,
-                "ga_amd %s: ranks %d on %d node(s), device %d (%s, %d CUs), library streams %d, "
+                "%s: ranks %d on %d node(s), device %d (%s, %d CUs), library streams %d, "
                 "staging %zu MiB/rank, remote acc %s, segments in %s, blocking sync %d\n",
                 gaamd_version(), r.size, r.nnodes, r.device, okp ? prop.gcnArchName : "?",
                 okp ? prop.multiProcessorCount : 0, (int)r.streams.size(), r.staging_bytes >> 20,
