@@ -78,6 +78,8 @@ def main():
         stress_test(L, rank, size)
     elif mode == "testacc":
         test_acc_ref(L, rank, size)
+    elif mode == "testdim":
+        test_dim_ref(L, rank, size)
     else:
         remote_test(L, rank, size)
     print(f"RANK {rank} OK", flush=True)
@@ -728,6 +730,202 @@ def stress_test(L, rank, size):
     for b in keep:
         b.free()
     assert ga_amd.comex_free(seg[rank]) == 0
+    ga_amd.comex_finalize()
+
+
+# ---------------------------------------------------------------------------
+# comex/testing/test.c test_dim (526-609) and test_nbdim (667-802), restated:
+# strided put of a random patch of a host array (init(): value = sum idx[d]*100^d,
+# test.c:217-239) into a random position of rank proc's array (dims + 1 in every
+# dimension, test.c:38-45), strided get back into another random position of a
+# host array, exact comparison (compare_patches with eps 0).  test_dim targets
+# proc = nproc-1-me, LOOP times per ndim; test_nbdim posts all ndim 1..7 puts
+# non-blocking (nbput for ndim 1, nbputs otherwise) to get_next_RRproc's targets,
+# waits, then the gets likewise.  The reference draws ranges with rand(); here a
+# seeded numpy generator per rank.
+TD_DIMS_A = [5, 3, 8, 9, 7, 3, 2]       # DIM1..DIM7 (test.c:18-35, non-Solaris)
+TD_DIMS_B = [d + 1 for d in TD_DIMS_A]  # EDIM = DIM + OFF
+
+
+def td_index(sub, dims):                # Index(), test.c:275-283
+    idx, f = 0, 1
+    for s, d in zip(sub, dims):
+        idx += s * f
+        f *= d
+    return idx
+
+
+def td_init(ndim):                      # init(), test.c:217-239
+    dims = TD_DIMS_A[:ndim]
+    n = int(np.prod(dims))
+    i = np.arange(n)
+    val = np.zeros(n)
+    field = 1.0
+    for d in dims:
+        val += field * (i % d)
+        i = i // d
+        field *= 100.0
+    return val
+
+
+def td_get_range(rng, dims):            # get_range(), test.c:122-140
+    lo, hi = [], []
+    for d in dims:
+        t1, t2 = int(rng.integers(d)), int(rng.integers(d))
+        lo.append(min(t1, t2))
+        hi.append(max(t1, t2))
+    return lo, hi
+
+
+def td_new_range(rng, dims, lo, hi):    # new_range(), test.c:144-159
+    nlo, nhi = [], []
+    for d, l, h in zip(dims, lo, hi):
+        diff = h - l + 1
+        rng_ = d - diff
+        t = int(rng.integers(rng_)) if rng_ > 0 else l
+        nlo.append(t)
+        nhi.append(t + diff - 1)
+    return nlo, nhi
+
+
+def td_strides(ndim):
+    sA, sB = [8], [8]
+    for i in range(ndim):
+        sA[i] *= TD_DIMS_A[i]
+        sB[i] *= TD_DIMS_B[i]
+        if i < ndim - 1:
+            sA.append(sA[i])
+            sB.append(sB[i])
+    return sA, sB
+
+
+def td_patch(arr, lo, hi, dims):
+    """elements of arr (first index fastest) in the patch lo..hi, in odometer order."""
+    v = arr.reshape(list(reversed(dims)))
+    sl = tuple(slice(l, h + 1) for l, h in zip(reversed(lo), reversed(hi)))
+    return v[sl].copy()
+
+
+class RRProc:                           # get_next_RRproc(), test.c:615-665
+    def __init__(self, me, nproc):
+        self.me, self.nproc = me, nproc
+        self.distance = nproc // 2 + (nproc % 2)
+        if nproc == 1:
+            self.distance = 0
+
+    def next(self, ndim):
+        me, nproc = self.me, self.nproc
+        proc = me + self.distance if me <= ((nproc // 2 - 1) if nproc % 2 == 0 else nproc // 2) else \
+            me - self.distance
+        if nproc % 2 != 0 and me == nproc // 2:
+            proc = me
+        if self.distance != 0:
+            if me < nproc // 2:
+                self.distance += 1
+                if me + self.distance >= nproc:
+                    self.distance = nproc // 2 + (nproc % 2) - me
+            else:
+                self.distance -= 1
+                if me - self.distance >= nproc // 2:
+                    d = nproc // 2 + (nproc % 2)
+                    self.distance = d + (me - d)
+            if ndim != 1 and 7 > nproc and nproc // 2 and ndim % (nproc // 2) == 0:
+                self.distance = nproc // 2 + (nproc % 2)
+        return proc
+
+
+def test_dim_ref(L, rank, size, loop=40):
+    import ga_amd
+    assert ga_amd.comex_init() == 0
+    rng = np.random.default_rng(1234 + rank)
+    # ---- test_dim, ndim 1..7
+    for ndim in range(1, 8):
+        dA, dB = TD_DIMS_A[:ndim], TD_DIMS_B[:ndim]
+        sA, sB = td_strides(ndim)
+        b = ga_amd.comex_malloc(8 * int(np.prod(dB)), size)
+        a = td_init(ndim)
+        c = np.zeros_like(a)
+        ga_amd.comex_fence_all()
+        ga_amd.comex_barrier()
+        proc = size - 1 - rank
+        for _ in range(loop):
+            loA, hiA = td_get_range(rng, dA)
+            loB, hiB = td_new_range(rng, dB, loA, hiA)
+            loC, hiC = td_new_range(rng, dA, loA, hiA)
+            i1, i2, i3 = td_index(loA, dA), td_index(loB, dB), td_index(loC, dA)
+            count = [hiA[j] - loA[j] + 1 for j in range(ndim)]
+            count[0] *= 8
+            assert ga_amd.comex_puts(a.ctypes.data + 8 * i1, sA, b[proc] + 8 * i2, sB, count, ndim - 1, proc) == 0
+            # consecutive operations to one process are ordered (test.c:590-591)
+            assert ga_amd.comex_gets(b[proc] + 8 * i2, sB, c.ctypes.data + 8 * i3, sA, count, ndim - 1, proc) == 0
+            assert np.array_equal(td_patch(a, loA, hiA, dA), td_patch(c, loC, hiC, dA)), (ndim, loA, hiA)
+        ga_amd.comex_barrier()
+        assert ga_amd.comex_free(b[rank]) == 0
+    say(rank, "test_dim ndim 1..7 ok")
+    # ---- test_nbdim
+    bs, As, Cs, rngs = {}, {}, {}, {}
+    for ndim in range(1, 8):
+        bs[ndim] = ga_amd.comex_malloc(8 * int(np.prod(TD_DIMS_B[:ndim])), size)
+        As[ndim] = td_init(ndim)
+        Cs[ndim] = np.zeros_like(As[ndim])
+    ga_amd.comex_fence_all()
+    ga_amd.comex_barrier()
+    hput, hget = {}, {}
+    rr = RRProc(rank, size)
+    for ndim in range(1, 8):
+        dA, dB = TD_DIMS_A[:ndim], TD_DIMS_B[:ndim]
+        sA, sB = td_strides(ndim)
+        proc = rr.next(ndim)
+        loA, hiA = td_get_range(rng, dA)
+        loB, hiB = td_new_range(rng, dB, loA, hiA)
+        loC, hiC = td_new_range(rng, dA, loA, hiA)
+        rngs[ndim] = (proc, loA, hiA, loB, loC, hiC)
+        count = [hiA[j] - loA[j] + 1 for j in range(ndim)]
+        count[0] *= 8
+        h = ctypes.c_int(-1)
+        src, dst = ctypes.c_void_p(As[ndim].ctypes.data + 8 * td_index(loA, dA)), \
+            ctypes.c_void_p(bs[ndim][proc] + 8 * td_index(loB, dB))
+        if ndim == 1:
+            rc = L.comex_nbput(src, dst, count[0], proc, 0, ctypes.byref(h))
+        else:
+            rc = L.comex_nbputs(src, ga_amd.int_array(sA), dst, ga_amd.int_array(sB), ga_amd.int_array(count),
+                                ndim - 1, proc, 0, ctypes.byref(h))
+        assert rc == 0
+        hput[ndim] = h
+    ga_amd.comex_barrier()
+    for ndim in range(1, 8):
+        assert ga_amd.comex_wait(hput[ndim]) == 0
+    ga_amd.comex_barrier()
+    ga_amd.comex_fence_all()
+    rr = RRProc(rank, size)
+    for ndim in range(1, 8):
+        dA, dB = TD_DIMS_A[:ndim], TD_DIMS_B[:ndim]
+        sA, sB = td_strides(ndim)
+        proc = rr.next(ndim)
+        p0, loA, hiA, loB, loC, hiC = rngs[ndim]
+        assert proc == p0
+        count = [hiA[j] - loA[j] + 1 for j in range(ndim)]
+        count[0] *= 8
+        h = ctypes.c_int(-1)
+        src, dst = ctypes.c_void_p(bs[ndim][proc] + 8 * td_index(loB, dB)), \
+            ctypes.c_void_p(Cs[ndim].ctypes.data + 8 * td_index(loC, dA))
+        if ndim == 1:
+            rc = L.comex_nbget(src, dst, count[0], proc, 0, ctypes.byref(h))
+        else:
+            rc = L.comex_nbgets(src, ga_amd.int_array(sB), dst, ga_amd.int_array(sA), ga_amd.int_array(count),
+                                ndim - 1, proc, 0, ctypes.byref(h))
+        assert rc == 0
+        hget[ndim] = h
+    ga_amd.comex_barrier()
+    for ndim in range(1, 8):
+        assert ga_amd.comex_wait(hget[ndim]) == 0
+        p0, loA, hiA, loB, loC, hiC = rngs[ndim]
+        dA = TD_DIMS_A[:ndim]
+        assert np.array_equal(td_patch(As[ndim], loA, hiA, dA), td_patch(Cs[ndim], loC, hiC, dA)), ndim
+    ga_amd.comex_barrier()
+    for ndim in range(1, 8):
+        assert ga_amd.comex_free(bs[ndim][rank]) == 0
+    say(rank, "test_nbdim ok")
     ga_amd.comex_finalize()
 
 

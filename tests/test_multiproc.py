@@ -132,3 +132,13 @@ def test_comex_test_acc_restated(n):
     corner of every rank's array, checked at the reference's rel 1e-4 (exactly
     on one rank, where the order is fixed)."""
     launch("testacc", n=n, timeout=150)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_comex_test_dim_restated(n):
+    """comex/testing/test.c test_dim (526-609) + test_nbdim (667-802) for ndim
+    1..7: random strided patches of a host array put into rank proc's array and
+    got back into another random position, exact comparison; blocking to
+    nproc-1-me, then all ndim non-blocking to get_next_RRproc's targets."""
+    launch("testdim", n=n, timeout=150)
