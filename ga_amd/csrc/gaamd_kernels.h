@@ -69,6 +69,7 @@ struct Tuning {
     int order = 0;          // f64 2-D kernel: 1 chunk-major, 2 scattered rows (experiment)
     int direct = 1;         // 2-D rows of whole chunks: loop-free one-block-per-chunk kernel
     int flat_nt = 1;        // flat kernel (short rows): non-temporal loads/stores (+12-24 %)
+    int lds_pad = 0;        // rows kernels: dynamic LDS bytes per wave (caps resident blocks per CU; 0 = none)
 };
 Tuning &tuning();
 

@@ -437,6 +437,9 @@ static int unroll_for(int W, int u16) {
     }
 }
 template <int W> struct DefaultU { static constexpr int value = W == 16 ? 1 : (W == 8 ? 2 : (W == 4 ? 4 : 8)); };
+// dynamic LDS per block of the rows kernels: lds_pad bytes per wave.  The kernels use no
+// LDS; the allocation only caps how many blocks a CU holds at once (160 KiB / bytes).
+template <int BS> static inline uint32_t lds_bytes() { return (uint32_t)g_tuning.lds_pad * (BS / 64); }
 
 template <class OP, int W, int U, int BS>
 static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt, hipStream_t st) {
@@ -463,7 +466,7 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
             f.d_str = e.d_str;
             f.chunk_div = d.chunk_div;
             f.row0 = d.row0;
-            hipLaunchKernelGGL((k_rows2d<OP, W, BS>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
+            hipLaunchKernelGGL((k_rows2d<OP, W, BS>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, f, op);
             return hipGetLastError();
         }
     }
@@ -485,22 +488,22 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
         }
         if (g_tuning.xcd && nt && blocks == e.items && e.items % 8 == 0) {
             e.xcd_per = e.items / 8;
-            hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
+            hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true, true>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, e, op);
             return hipGetLastError();
         }
         const int cp = g_tuning.cpol;
         if (cp && !d.align_mask) {
 #define GAAMD_CPOL(LA, SA) \
     if (cp == ((LA) | ((SA) << 8))) { \
-        hipLaunchKernelGGL((k_rows2_buf<OP, U, BS, LA, SA>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op); \
+        hipLaunchKernelGGL((k_rows2_buf<OP, U, BS, LA, SA>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, e, op); \
         return hipGetLastError(); }
             GAAMD_CPOL(2, 2) GAAMD_CPOL(0, 2) GAAMD_CPOL(2, 0) GAAMD_CPOL(0, 0)
             GAAMD_CPOL(16, 2) GAAMD_CPOL(2, 16) GAAMD_CPOL(18, 18) GAAMD_CPOL(3, 3) GAAMD_CPOL(1, 2)
 #undef GAAMD_CPOL
         }
     }
-    if (nt) hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
-    else hipLaunchKernelGGL((k_rows2<OP, W, U, BS, false>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
+    if (nt) hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, e, op);
+    else hipLaunchKernelGGL((k_rows2<OP, W, U, BS, false>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, e, op);
     return hipGetLastError();
 }
 
@@ -519,12 +522,12 @@ static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, int n
             }
             f.chunk_div = d.chunk_div;
             f.row0 = d.row0;
-            hipLaunchKernelGGL((k_rowsnd<OP, W, BS, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
+            hipLaunchKernelGGL((k_rowsnd<OP, W, BS, LV>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, f, op);
             return hipGetLastError();
         }
     }
-    if (nt) hipLaunchKernelGGL((k_rows<OP, W, U, BS, true, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, d, op);
-    else hipLaunchKernelGGL((k_rows<OP, W, U, BS, false, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, d, op);
+    if (nt) hipLaunchKernelGGL((k_rows<OP, W, U, BS, true, LV>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, d, op);
+    else hipLaunchKernelGGL((k_rows<OP, W, U, BS, false, LV>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, d, op);
     return hipGetLastError();
 }
 template <class OP, int W, int LV>
