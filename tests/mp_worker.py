@@ -80,6 +80,8 @@ def main():
         test_acc_ref(L, rank, size)
     elif mode == "testdim":
         test_dim_ref(L, rank, size)
+    elif mode == "garef":
+        ga_ref_test(L, rank, size)
     else:
         remote_test(L, rank, size)
     print(f"RANK {rank} OK", flush=True)
@@ -927,6 +929,173 @@ def test_dim_ref(L, rank, size, loop=40):
         assert ga_amd.comex_free(bs[ndim][rank]) == 0
     say(rank, "test_nbdim ok")
     ga_amd.comex_finalize()
+
+
+
+# ---------------------------------------------------------------------------
+# GA-level accumulate tests of the reference, restated on the C API (row-major,
+# 0-based: Fortran (i, j) of an n x n array is C [j][i]):
+#  * test.F:596-658 disjoint ga_acc: the n x n array is tiled with inc x inc
+#    patches (inc = (n-1)/20 + 1, a patch ending at n-1 is stretched to n), tile
+#    ij is accumulated by rank ij mod nproc from b(i,j) = i+j with x = 10, and
+#    every rank checks the whole array against its local copy (reference:
+#    rel 1e-13; here exact: every element is accumulated once into 0);
+#    float/double complex variants (test.F:1567-1622, 2204-2259) and int;
+#  * test.F:700-725 overlapping accumulate: every rank adds 1.0 at (n/2, n/2),
+#    rank 0 checks nproc (reference |d| <= 1e-10; exact here);
+#  * ngatest_src/ndim_NGA_ACC.src for ndim 1..7 (the commented, smaller n set of
+#    ngatest.def): fill with val, then MAXLOOP times accumulate alpha = val times
+#    a random sub-range (random_range, ndim_util_comm.src:1-22) of rank
+#    nproc-1-me's block from the same position of a full local array, comparing
+#    the patch before/after (reference 1e-2; exact here, acc.h expression order).
+GA_TYPES = {1001: np.int32, 1003: np.float32, 1004: np.float64, 1007: np.complex128}
+
+
+def acc_expect(a, b, alpha):
+    """a + alpha*b in the order of acc.h:46-49 / 119-143 (no FMA, int wraps)."""
+    if np.iscomplexobj(a):
+        re = a.real + (b.real * alpha.real - b.imag * alpha.imag)
+        im = a.imag + (b.real * alpha.imag + b.imag * alpha.real)
+        return re + 1j * im
+    if a.dtype.kind == "i":
+        return (a.astype(np.int64) + np.int64(alpha) * b.astype(np.int64)).astype(np.uint32).view(np.int32)
+    return a + a.dtype.type(alpha) * b
+
+
+def typed_scalar(t, v):
+    if t == 1001:
+        return ctypes.c_int(int(v))
+    if t == 1003:
+        return ctypes.c_float(v)
+    if t == 1004:
+        return ctypes.c_double(v)
+    return (ctypes.c_double * 2)(v.real, v.imag)
+
+
+def ga_ref_test(L, rank, size):
+    ia = ga_amd_int_array()
+    assert L.GA_Initialize() == 0
+    P = ctypes.c_void_p
+    # ---- test.F:596-725
+    n = 100
+    inc = (n - 1) // 20 + 1
+    for t in (1004, 1007, 1003, 1001):
+        dt = GA_TYPES[t]
+        g = L.NGA_Create(t, 2, ia([n, n]), b"a", None)
+        assert g > 0
+        L.GA_Zero(g)
+        L.GA_Sync()
+        jj, ii = np.meshgrid(np.arange(1, n + 1), np.arange(1, n + 1), indexing="ij")
+        b = (ii + jj).astype(dt)                       # C b[j][i] = Fortran b(i, j) = i + j
+        if t == 1007:
+            b = b + 1j * (ii - 2 * jj)
+        x = {1001: 10, 1003: 10.0, 1004: 10.0, 1007: complex(10.0, -0.5)}[t]
+        alpha = typed_scalar(t, x)
+        a = np.zeros((n, n), dtype=dt)
+        ij = 0
+        for j in range(1, n + 1, inc):
+            for i in range(1, n + 1, inc):
+                ilo, ihi = i, min(i + inc - 1, n)
+                if ihi == n - 1:
+                    ihi = n
+                jlo, jhi = j, min(j + inc - 1, n)
+                if jhi == n - 1:
+                    jhi = n
+                if ij % size == rank:
+                    L.NGA_Acc(g, ia([jlo - 1, ilo - 1]), ia([jhi - 1, ihi - 1]),
+                              P(b.ctypes.data + b.itemsize * ((jlo - 1) * n + ilo - 1)), ia([n]), ctypes.byref(alpha))
+                ij += 1
+                sl = (slice(jlo - 1, jhi), slice(ilo - 1, ihi))
+                a[sl] = acc_expect(a[sl], b[sl], x)
+        L.GA_Sync()
+        got = np.zeros((n, n), dtype=dt)
+        L.NGA_Get(g, ia([0, 0]), ia([n - 1, n - 1]), P(got.ctypes.data), ia([n]))
+        assert np.array_equal(got, a), f"test.F disjoint ga_acc type {t}"
+        L.GA_Sync()
+        L.GA_Destroy(g)
+    say(rank, "test.F disjoint ga_acc (dbl, dcpl, float, int) ok")
+    g = L.NGA_Create(1004, 2, ia([n, n]), b"b", None)
+    L.GA_Zero(g)
+    one = ctypes.c_double(1.0)
+    e = np.ones(1)
+    L.NGA_Acc(g, ia([n // 2 - 1, n // 2 - 1]), ia([n // 2 - 1, n // 2 - 1]), P(e.ctypes.data), ia([1]),
+              ctypes.byref(one))
+    L.GA_Sync()
+    if rank == 0:
+        v = np.zeros(1)
+        L.NGA_Get(g, ia([n // 2 - 1, n // 2 - 1]), ia([n // 2 - 1, n // 2 - 1]), P(v.ctypes.data), ia([1]))
+        assert v[0] == float(size), ("overlapping ga_acc", v[0], size)
+    L.GA_Sync()
+    L.GA_Destroy(g)
+    say(rank, "test.F overlapping ga_acc ok")
+    # ---- ndim_NGA_ACC.src
+    n_of = {1: 2000, 2: 100, 3: 20, 4: 10, 5: 5, 6: 4, 7: 3}
+    rng = np.random.default_rng(77 + rank)
+    for t in (1001, 1004, 1007):
+        dt = GA_TYPES[t]
+        for ndim in range(1, 8):
+            nn = n_of[ndim]
+            dims = [nn] * ndim
+            g = L.NGA_Create(t, ndim, ia(dims), b"a", None)
+            assert g > 0
+            val = {1001: rank * 2 + 3, 1004: 0.5 + rank * 0.25, 1007: complex(0.5 + rank, -0.25)}[t]
+            # ga_fill(g_a, val): every rank puts val into its own block
+            blo, bhi = (ctypes.c_int * ndim)(), (ctypes.c_int * ndim)()
+            L.NGA_Distribution(g, rank, blo, bhi)
+            if all(bhi[k] >= blo[k] for k in range(ndim)):
+                ext = [bhi[k] - blo[k] + 1 for k in range(ndim)]
+                f = np.full(ext, val, dtype=dt)
+                L.NGA_Put(g, blo, bhi, P(f.ctypes.data), ia(ext[1:]))
+            L.GA_Sync()
+            proc = size - 1 - rank
+            lop, hip = (ctypes.c_int * ndim)(), (ctypes.c_int * ndim)()
+            L.NGA_Distribution(g, proc, lop, hip)
+            has = all(hip[k] >= lop[k] for k in range(ndim))
+            total = int(np.prod(dims))
+            if t == 1001:
+                b = rng.integers(-1000, 1000, total).astype(np.int32).reshape(dims)
+            else:
+                b = (rng.random(total) * 2 - 1).reshape(dims).astype(dt)
+                if t == 1007:
+                    b = b + 1j * (rng.random(total) - 0.5).reshape(dims)
+            alpha = typed_scalar(t, val)
+            ld = ia([nn] * (ndim - 1))
+            for loop in range(20):
+                lo, hi = [], []
+                for k in range(ndim):               # random_range(lop, hip, lo, hi)
+                    rg = hip[k] - lop[k] + 1
+                    l_ = lop[k] + int(rng.random() * rg) + 1
+                    h_ = hip[k] - (int(rng.random() * rg) + 1)
+                    if h_ < l_:
+                        l_, h_ = h_, l_
+                    lo.append(max(l_, lop[k]))
+                    hi.append(min(h_, hip[k]))
+                ok = has and all(hi[k] >= lo[k] for k in range(ndim))
+                L.GA_Sync()
+                ext = [hi[k] - lo[k] + 1 for k in range(ndim)] if ok else []
+                sl = tuple(slice(lo[k], hi[k] + 1) for k in range(ndim)) if ok else ()
+                if ok:
+                    before = np.zeros(ext, dtype=dt)
+                    L.NGA_Get(g, ia(lo), ia(hi), P(before.ctypes.data), ia(ext[1:]))
+                L.GA_Sync()
+                if ok:
+                    off = sum(lo[k] * int(np.prod(dims[k + 1:])) for k in range(ndim))
+                    L.NGA_Acc(g, ia(lo), ia(hi), P(b.ctypes.data + b.itemsize * off), ld, ctypes.byref(alpha))
+                L.GA_Sync()
+                if ok:
+                    after = np.zeros(ext, dtype=dt)
+                    L.NGA_Get(g, ia(lo), ia(hi), P(after.ctypes.data), ia(ext[1:]))
+                    want = acc_expect(before, b[sl], val)
+                    assert np.array_equal(after, want), ("ndim_NGA_ACC", t, ndim, loop, lo, hi)
+            L.GA_Sync()
+            L.GA_Destroy(g)
+    say(rank, "ndim_NGA_ACC (int, dbl, dcpl; ndim 1..7) ok")
+    L.GA_Terminate()
+
+
+def ga_amd_int_array():
+    import ga_amd
+    return ga_amd.int_array
 
 
 if __name__ == "__main__":

@@ -142,3 +142,13 @@ def test_comex_test_dim_restated(n):
     got back into another random position, exact comparison; blocking to
     nproc-1-me, then all ndim non-blocking to get_next_RRproc's targets."""
     launch("testdim", n=n, timeout=150)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 3, 4])
+def test_ga_reference_acc_tests_restated(n):
+    """global/testing/test.F:596-725 (disjoint and overlapping ga_acc; double,
+    double complex, float and int) and ngatest_src/ndim_NGA_ACC.src (random
+    sub-ranges of another rank's block, ndim 1..7; int, double, double complex)
+    on n ranks, exact against acc.h's expression order."""
+    launch("garef", n=n, timeout=150)
