@@ -80,6 +80,8 @@ def main():
         test_acc_ref(L, rank, size)
     elif mode == "testdim":
         test_dim_ref(L, rank, size)
+    elif mode == "testvec":
+        test_vector_ref(L, rank, size)
     elif mode == "garef":
         ga_ref_test(L, rank, size)
     else:
@@ -1096,6 +1098,98 @@ def ga_ref_test(L, rank, size):
 def ga_amd_int_array():
     import ga_amd
     return ga_amd.int_array
+
+
+
+# ---------------------------------------------------------------------------
+# comex/testing/test.c test_vector (1240-1386) and test_vector_acc (1394-1491),
+# restated.  test_vector: a random patch of a host 50x50 array goes to rank
+# nproc-1-me's 51x51 array as two comex_putv calls (lower triangle incl. the
+# diagonal: one descriptor per column of decreasing length; upper triangle: one
+# per column), then comes back whole with one comex_getv of `cols` runs into
+# another random position; exact.  test_vector_acc: every rank accumulates the
+# even and then the odd elements of a[i] = i (ELEMS = 200) into rank 0 with
+# alpha 0.1, one single-element run each, TIMES*nproc times; rank 0's array is
+# then a * alpha*TIMES*nproc*nproc at rel 1e-4 (exact on one rank against the
+# sequential sum).
+def test_vector_ref(L, rank, size, loop=60):
+    import ga_amd
+    assert ga_amd.comex_init() == 0
+    rng = np.random.default_rng(4321 + rank)
+    M = 50
+    dA, dB = [M, M], [M + 1, M + 1]
+    b = ga_amd.comex_malloc(8 * dB[0] * dB[1], size)
+    a = td_init_dims(dA)
+    c = np.zeros_like(a)
+    ga_amd.comex_barrier()
+    proc = size - 1 - rank
+    A, C = a.ctypes.data, c.ctypes.data
+    for _ in range(loop):
+        loA, hiA = td_get_range(rng, dA)
+        loB, hiB = td_new_range(rng, dB, loA, hiA)
+        loC, hiC = td_new_range(rng, dA, loA, hiA)
+        cols, rows = hiA[1] - loA[1] + 1, hiA[0] - loA[0] + 1
+        mrc = min(cols, rows)
+        descs = []
+        for i in range(mrc):               # lower triangle incl. diagonal
+            s_ = A + 8 * td_index([loA[0] + i, loA[1] + i], dA)
+            d_ = b[proc] + 8 * td_index([loB[0] + i, loB[1] + i], dB)
+            descs.append(([s_], [d_], (rows - i) * 8))
+        assert ga_amd.comex_putv(descs, proc) == 0
+        descs = []
+        for i in range(1, cols):           # upper triangle
+            s_ = A + 8 * td_index([loA[0], loA[1] + i], dA)
+            d_ = b[proc] + 8 * td_index([loB[0], loB[1] + i], dB)
+            descs.append(([s_], [d_], min(i, rows) * 8))
+        if cols - 1:
+            assert ga_amd.comex_putv(descs, proc) == 0
+        srcs = [b[proc] + 8 * td_index([loB[0], loB[1] + i], dB) for i in range(cols)]
+        dsts = [C + 8 * td_index([loC[0], loC[1] + i], dA) for i in range(cols)]
+        assert ga_amd.comex_getv([(srcs, dsts, rows * 8)], proc) == 0
+        assert np.array_equal(td_patch(a, loA, hiA, dA), td_patch(c, loC, hiC, dA)), (loA, hiA)
+    ga_amd.comex_barrier()
+    assert ga_amd.comex_free(b[rank]) == 0
+    say(rank, "test_vector ok")
+    # ---- test_vector_acc
+    ELEMS, TIMES, alpha = 200, 20, 0.1
+    b = ga_amd.comex_malloc(8 * ELEMS, size)
+    L.gaamd_memset(ctypes.c_void_p(b[rank]), 0, 8 * ELEMS)
+    ga_amd.sync()
+    a = np.arange(ELEMS, dtype=np.float64)
+    A = a.ctypes.data
+    ga_amd.comex_barrier()
+    for _ in range(TIMES * size):
+        for par in (0, 1):
+            idx = range(par, ELEMS, 2)
+            descs = [([A + 8 * j for j in idx], [b[0] + 8 * j for j in idx], 8)]
+            assert ga_amd.comex_accv(38, alpha, descs, 0) == 0
+    ga_amd.comex_fence_all()
+    ga_amd.comex_barrier()
+    cc = np.zeros(ELEMS)
+    assert L.comex_get(ctypes.c_void_p(b[0]), ctypes.c_void_p(cc.ctypes.data), 8 * ELEMS, 0, 0) == 0
+    want = a * (alpha * TIMES * size * size)
+    assert np.allclose(cc, want, rtol=1e-4, atol=0), np.max(np.abs(cc - want))
+    if size == 1:
+        seq = np.zeros(ELEMS)
+        for _ in range(TIMES):
+            seq = seq + a * alpha
+        assert np.array_equal(cc, seq)
+    ga_amd.comex_barrier()
+    assert ga_amd.comex_free(b[rank]) == 0
+    say(rank, "test_vector_acc ok")
+    ga_amd.comex_finalize()
+
+
+def td_init_dims(dims):                 # init() for arbitrary dims, test.c:217-239
+    n = int(np.prod(dims))
+    i = np.arange(n)
+    val = np.zeros(n)
+    field = 1.0
+    for d in dims:
+        val += field * (i % d)
+        i = i // d
+        field *= 100.0
+    return val
 
 
 if __name__ == "__main__":

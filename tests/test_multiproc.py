@@ -152,3 +152,13 @@ def test_ga_reference_acc_tests_restated(n):
     sub-ranges of another rank's block, ndim 1..7; int, double, double complex)
     on n ranks, exact against acc.h's expression order."""
     launch("garef", n=n, timeout=150)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_comex_test_vector_restated(n):
+    """comex/testing/test.c test_vector (1240-1386: triangular comex_putv pieces of
+    a random 2-D patch, comex_getv of the whole patch, exact) and test_vector_acc
+    (1394-1491: even/odd single-element comex_accv runs from every rank into rank
+    0, TIMES*nproc times, rel 1e-4; exact on one rank)."""
+    launch("testvec", n=n, timeout=150)
