@@ -97,7 +97,18 @@ class Dist:
             import torch
             import torch.distributed as td
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            td.init_process_group("gloo", rank=self.rank, world_size=self.size)
+            # gloo prints "[Gloo] Rank r is connected to ..." on stdout while it connects:
+            # send fd 1 to stderr meanwhile so stdout carries only the one JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                td.init_process_group("gloo", rank=self.rank, world_size=self.size)
+                td.barrier()
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.torch, self.td = torch, td
         if n_gpus != self.size and self.rank == 0:
             print(f"warning: --gpus {n_gpus} but WORLD_SIZE {self.size}", file=sys.stderr)
