@@ -82,6 +82,8 @@ def main():
         test_dim_ref(L, rank, size)
     elif mode == "testvec":
         test_vector_ref(L, rank, size)
+    elif mode == "armciacc":
+        armci_test_acc_ref(L, rank, size)
     elif mode == "garef":
         ga_ref_test(L, rank, size)
     else:
@@ -1190,6 +1192,70 @@ def td_init_dims(dims):                 # init() for arbitrary dims, test.c:217-
         i = i // d
         field *= 100.0
     return val
+
+
+
+# ---------------------------------------------------------------------------
+# armci/testing/test.c test_acc (896-976), restated through the ARMCI API
+# (ARMCI_Malloc, ARMCI_AccS, ARMCI_AllFence, ARMCI_Barrier, ARMCI_GetS): a
+# 2^ndim patch at the origin of a host array, alpha 0.1, accumulated TIMES*nproc
+# times into the far corner of the ranks' arrays in a permuted proc order
+# (GetPermutedProcList, test.c:993), then each rank gets its corner back and
+# compares with a * alpha*TIMES*nproc at rel 1e-4 (exact on one rank against the
+# sequential sum).  Odd ndim use ARMCI_NbAccS + ARMCI_WaitAll instead.
+def armci_test_acc_ref(L, rank, size, times=10):
+    import ga_amd
+    assert L.ARMCI_Init() == 0
+    P = ctypes.c_void_p
+    alpha = ctypes.c_double(0.1)
+    rng = np.random.default_rng(rank)
+    for ndim in range(1, 8):
+        dA, dB = TD_DIMS_A[:ndim], TD_DIMS_B[:ndim]
+        sA, sB = td_strides(ndim)
+        loA, loB = [0] * ndim, [d - 2 for d in dB]
+        count = [2 * 8] + [2] * (ndim - 1)
+        ptrs = (ctypes.c_void_p * size)()
+        nbytes = 8 * int(np.prod(dB))
+        assert L.ARMCI_Malloc(ptrs, nbytes) == 0
+        L.gaamd_memset(ctypes.c_void_p(ptrs[rank]), 0, nbytes)
+        ga_amd.sync()
+        a = td_init(ndim)
+        c = np.zeros_like(a)
+        plist = list(range(size))
+        for i in range(size):                  # random swapping, test.c:1013-1017
+            j = int(rng.integers(size))
+            plist[i], plist[j] = plist[j], plist[i]
+        i1, i2 = td_index(loA, dA), td_index(loB, dB)
+        L.ARMCI_AllFence()
+        L.ARMCI_Barrier()
+        for i in range(times * size):
+            proc = plist[i % size]
+            args = (P(a.ctypes.data + 8 * i1), ga_amd.int_array(sA), P(ptrs[proc] + 8 * i2), ga_amd.int_array(sB),
+                    ga_amd.int_array(count), ndim - 1, proc)
+            if ndim % 2:
+                h = ctypes.c_int(0)
+                assert L.ARMCI_NbAccS(38, ctypes.byref(alpha), *args, ctypes.byref(h)) == 0
+            else:
+                assert L.ARMCI_AccS(38, ctypes.byref(alpha), *args) == 0
+        if ndim % 2:
+            assert L.ARMCI_WaitAll() == 0
+        L.ARMCI_AllFence()
+        L.ARMCI_Barrier()
+        assert L.ARMCI_GetS(P(ptrs[rank] + 8 * i2), ga_amd.int_array(sB), P(c.ctypes.data + 8 * i1),
+                            ga_amd.int_array(sA), ga_amd.int_array(count), ndim - 1, rank) == 0
+        hi = [1] * ndim
+        got, base = td_patch(c, loA, hi, dA), td_patch(a, loA, hi, dA)
+        want = base * (0.1 * times * size)
+        assert np.allclose(got, want, rtol=1e-4, atol=0), (ndim, np.max(np.abs(got - want)))
+        if size == 1:
+            seq = np.zeros_like(base)
+            for _ in range(times):
+                seq = seq + base * 0.1
+            assert np.array_equal(got, seq), ndim
+        L.ARMCI_Barrier()
+        assert L.ARMCI_Free(ctypes.c_void_p(ptrs[rank])) == 0
+    say(rank, "armci test_acc ndim 1..7 ok")
+    L.ARMCI_Finalize()
 
 
 if __name__ == "__main__":

@@ -162,3 +162,12 @@ def test_comex_test_vector_restated(n):
     (1394-1491: even/odd single-element comex_accv runs from every rank into rank
     0, TIMES*nproc times, rel 1e-4; exact on one rank)."""
     launch("testvec", n=n, timeout=150)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 3])
+def test_armci_test_acc_restated(n):
+    """armci/testing/test.c test_acc (896-976) through ARMCI_Malloc/ARMCI_AccS
+    (ARMCI_NbAccS + ARMCI_WaitAll for odd ndim)/ARMCI_AllFence/ARMCI_GetS, ndim
+    1..7, rel 1e-4 as the reference (exact on one rank)."""
+    launch("armciacc", n=n, timeout=150)
