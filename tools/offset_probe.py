@@ -59,8 +59,10 @@ def main():
             for i in range(3):
                 L.comex_accs(op, sp, ptrs[i % len(ptrs)][0], ss, ptrs[i % len(ptrs)][1], ds, cnt, levels, 0, 0)
             L.gaamd_event_record(ev[0], stream)
+            L.gaamd_join()   # every library stream starts after ev[0]
             for i in range(args.steps):
                 L.comex_accs(op, sp, ptrs[i % len(ptrs)][0], ss, ptrs[i % len(ptrs)][1], ds, cnt, levels, 0, 0)
+            L.gaamd_join()   # ev[1] after the launches of every library stream
             L.gaamd_event_record(ev[1], stream)
             ga_amd.sync()
             ms = L.gaamd_event_elapsed_ms(ev[0], ev[1]) / args.steps

@@ -75,9 +75,11 @@ def main():
             import time
             t0 = time.perf_counter()
             L.gaamd_event_record(ev[0], stream)
+            L.gaamd_join()   # every library stream starts after ev[0]
             for i in range(args.steps):
                 s, d = sets[i % len(sets)]
                 L.comex_accs(op, sp, ctypes.c_void_p(s.ptr), ss, ctypes.c_void_p(d.ptr), ds, cnt, levels, 0, 0)
+            L.gaamd_join()   # ev[1] after the launches of every library stream
             L.gaamd_event_record(ev[1], stream)
             t_enq = time.perf_counter() - t0
             ga_amd.sync()
