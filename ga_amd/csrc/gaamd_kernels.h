@@ -69,6 +69,9 @@ struct Tuning {
     int order = 0;          // f64 2-D kernel: 1 chunk-major, 2 scattered rows (experiment)
     int direct = 1;         // 2-D rows of whole chunks: loop-free one-block-per-chunk kernel
     int flat_nt = 1;        // flat kernel (short rows): non-temporal loads/stores (+12-24 %)
+    int flat_shape = 1;     // flat kernel: 0 = 256 threads x 2 vectors, 1 = 64 threads x 1 vector (W=16, nt;
+                            // +3.5-5 % on 128 B-1 KiB rows, profiles/r01/sweep_flat_shape.jsonl)
+    int flat_line_min = 40; // rows off 128 B lines on both sides with at least this many vectors: rows kernel (0 = off)
     int lds_pad = 0;        // rows kernels: dynamic LDS bytes per wave (caps resident blocks per CU; 0 = none)
 };
 Tuning &tuning();

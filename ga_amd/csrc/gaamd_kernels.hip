@@ -427,6 +427,14 @@ template <> struct Tunable<AccDbl> { static constexpr bool value = true; };
 template <> struct Tunable<AccDcp> { static constexpr bool value = true; };
 template <> struct Tunable<CopyOp> { static constexpr bool value = true; };
 
+// flat kernel shape: 256 threads x 2 (W=16) or 4 vectors per thread, or with
+// flat_shape=1 (W=16, nt) one-wave blocks of one vector per lane
+static int flat_block_threads(int W, const Tuning &tn) { return (W == 16 && tn.flat_nt && tn.flat_shape == 1) ? 64 : 256; }
+static uint64_t flat_block_items(int W, const Tuning &tn) {
+    if (W == 16 && tn.flat_nt && tn.flat_shape == 1) return 64;
+    return 256ull * ((W == 16) ? 2 : 4);
+}
+
 // vectors per thread for the default shape: 16 B per thread per stream
 static int unroll_for(int W, int u16) {
     switch (W) {
@@ -549,6 +557,17 @@ static hipError_t dispatch_w(int kind, int U, int BS, int nt, const Desc &d, con
         }
         if (kind == KK_FLAT) {
             constexpr int UF = (W == 16) ? 2 : 4;
+            if constexpr (W == 16) {
+                if (g_tuning.flat_nt && g_tuning.flat_shape == 1) {   // one-wave blocks, one vector per lane
+                    if (d.levels == 1)
+                        hipLaunchKernelGGL((k_flat<OP, W, 1, 64, 1, true>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
+                    else if (d.levels == 2)
+                        hipLaunchKernelGGL((k_flat<OP, W, 1, 64, 2, true>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
+                    else
+                        hipLaunchKernelGGL((k_flat<OP, W, 1, 64, 0, true>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
+                    return hipGetLastError();
+                }
+            }
             if (g_tuning.flat_nt) {
                 if (d.levels == 1)
                     hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 1, true>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
@@ -799,7 +818,22 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     d.nvec_div = make_fastdiv(d.nvec);
 
     int kind = serial ? KK_SERIAL : tn.kind;
-    if (kind == KK_AUTO) kind = ((int64_t)d.nvec <= tn.flat_max_nvec) ? KK_FLAT : KK_ROWS;
+    if (kind == KK_AUTO) {
+        kind = ((int64_t)d.nvec <= tn.flat_max_nvec) ? KK_FLAT : KK_ROWS;
+        // rows that start off 128-byte lines on both sides: the flat kernel's waves cut rows
+        // (and their partial lines) at arbitrary vectors, the rows kernel keeps a row in one
+        // block: rows kernel from flat_line_min vectors up (+9-28 % at 640 B-2 KiB rows
+        // with ld = 2 x row + 16 B; line-aligned rows stay flat, which leads there by up to
+        // 18 %: profiles/r01/flat_vs_rows_grid.jsonl)
+        if (kind == KK_FLAT && tn.flat_line_min > 0 && (int64_t)d.nvec >= tn.flat_line_min) {
+            uint64_t sa = (uint64_t)(uintptr_t)src, da = (uint64_t)(uintptr_t)dst;
+            for (int j = 0; j < L; ++j) {
+                sa |= (uint64_t)ss[j];
+                da |= (uint64_t)ds[j];
+            }
+            if ((sa & 127) && (da & 127)) kind = KK_ROWS;
+        }
+    }
     // the (U, BS) the dispatcher will pick -- chunking must agree with it
     const bool tunable = (op == kOpCopy || op == 38 || op == 41);
     // rows kernels: small blocks retire and free their CU slots independently;
@@ -852,8 +886,8 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
             blocks = d.items;
         } else if (kind == KK_FLAT) {
             d.items = nr * d.nvec;
-            const int UF = (W == 16) ? 2 : 4;
-            blocks = (d.items + 256ull * UF - 1) / (256ull * UF);
+            const uint64_t per = flat_block_items(W, tn);
+            blocks = (d.items + per - 1) / per;
         } else {
             d.items = nr;
         }
@@ -873,7 +907,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         info->unroll = (kind == KK_ROWS) ? U : 0;
         info->launches = launches;
         info->blocks = total_blocks;
-        info->block = (kind == KK_ROWS) ? BS : (kind == KK_FLAT ? 256 : 64);
+        info->block = (kind == KK_ROWS) ? BS : (kind == KK_FLAT ? flat_block_threads(W, tn) : 64);
         info->levels = L;
         info->aligned = d.align_mask ? 1 : 0;
     }

@@ -139,6 +139,8 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "direct")) return &t.direct;
     if (!strcmp(key, "flat_nt")) return &t.flat_nt;
     if (!strcmp(key, "lds_pad")) return &t.lds_pad;
+    if (!strcmp(key, "flat_shape")) return &t.flat_shape;
+    if (!strcmp(key, "flat_line_min")) return &t.flat_line_min;
     return nullptr;
 }
 
@@ -154,6 +156,7 @@ int gaamd_set_tuning(const char *key, int value) {
     int *f = tuning_field(key);
     if (!f) return -1;
     if (!strcmp(key, "unroll16") && value != 1 && value != 2 && value != 4 && value != 8) return -1;
+    if (!strcmp(key, "flat_shape") && value != 0 && value != 1) return -1;
     if (!strcmp(key, "lds_pad") && (value < 0 || value > 40960)) return -1;
     if (!strcmp(key, "block") && value != 0 && value != 64 && value != 128 && value != 256 && value != 512) return -1;
     const int old = *f;

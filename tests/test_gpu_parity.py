@@ -69,7 +69,8 @@ def test_golden_cases_armci_and_nb(gpu_lib, manifest, golden):
 @pytest.mark.parametrize("knob", [("kind", 1), ("kind", 2), ("kind", 3), ("unroll16", 2), ("unroll16", 4),
                                   ("unroll16", 8), ("nontemporal", 0), ("max_grid", 7), ("block", 512), ("block", 256), ("block", 128), ("block", 64),
                                   ("align", 0), ("align", 1), ("cpol", 2 | 2 << 8), ("cpol", 16 | 2 << 8), ("xcd", 1), ("order", 1), ("order", 2),
-                                  ("direct", 0), ("flat_nt", 0)])
+                                  ("direct", 0), ("flat_nt", 0), ("flat_shape", 0),
+                                  ("flat_shape", 1), ("flat_line_min", 0)])
 def test_kernel_variants_identical(gpu_lib, manifest, golden, knob):
     """Every kernel family / tuning gives the same bits as the reference."""
     key, val = knob

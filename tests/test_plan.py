@@ -76,7 +76,16 @@ def test_sub_dword_alignment_is_rejected():
 
 
 def test_short_rows_take_the_flat_kernel():
-    assert plan(DBL, SRC, [1024], DST, [1024], [512, 1000], 1)["kind"] == "flat"
+    p = plan(DBL, SRC, [1024], DST, [1024], [512, 1000], 1)
+    assert p["kind"] == "flat"
+    # one-wave blocks of one 16-byte vector per lane (flat_shape=1): 32 vectors x 1000 rows
+    assert p["block"] == 64 and p["blocks"] == 32 * 1000 // 64
+    old = ga_amd.set_tuning("flat_shape", 0)
+    try:
+        p = plan(DBL, SRC, [1024], DST, [1024], [512, 1000], 1)
+        assert p["block"] == 256 and p["blocks"] == (32 * 1000 + 511) // 512
+    finally:
+        ga_amd.set_tuning("flat_shape", old)
     assert plan(DBL, SRC, [4096], DST, [4096], [2048, 1000], 1)["kind"] == "rows"
 
 
@@ -101,3 +110,19 @@ def test_block_knob_overrides_auto():
         assert plan(DBL, SRC, [65536], DST, [65536], [16384, 4096], 1)["block"] == 256
     finally:
         ga_amd.set_tuning("block", old)
+
+
+def test_rows_off_lines_on_both_sides_take_the_rows_kernel():
+    # 2032 B rows (127 vectors) at ld 4064: rows start off 128 B lines -> rows kernel
+    assert plan(DBL, SRC, [4064], DST, [4064], [2032, 1000], 1)["kind"] == "rows"
+    # line-aligned rows of the same length stay flat
+    assert plan(DBL, SRC, [4096], DST, [4096], [2032, 1000], 1)["kind"] == "flat"
+    # one side on lines: flat
+    assert plan(DBL, SRC, [4096], DST, [4064], [2032, 1000], 1)["kind"] == "flat"
+    # short rows (16 vectors) stay flat even off lines
+    assert plan(DBL, SRC, [528], DST, [528], [256, 1000], 1)["kind"] == "flat"
+    old = ga_amd.set_tuning("flat_line_min", 0)
+    try:
+        assert plan(DBL, SRC, [4064], DST, [4064], [2032, 1000], 1)["kind"] == "flat"
+    finally:
+        ga_amd.set_tuning("flat_line_min", old)

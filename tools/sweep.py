@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--sets", type=int, default=8)
     ap.add_argument("--ld", type=int, default=0, help="override the leading dimension (elements) of a 2-D workload")
     ap.add_argument("--rows", type=int, default=0, help="override the row count of a 2-D workload")
+    ap.add_argument("--row-bytes", type=int, default=0,
+                    help="2-D f64 shape with rows of this many bytes, ld = 2 x row, 64 MiB of payload")
+    ap.add_argument("--ld-bytes", type=int, default=0, help="with --row-bytes: leading dimension in bytes")
     ap.add_argument("--variants", default="default;unroll16=2;unroll16=8;nontemporal=1;unroll16=8,nontemporal=1")
     args = ap.parse_args()
     L = ga_amd.lib()
@@ -37,6 +40,11 @@ def main():
     if args.rows:
         count = [count[0], args.rows]
         desc += f" [rows overridden to {args.rows}]"
+    if args.row_bytes:
+        count = [args.row_bytes, (64 << 20) // args.row_bytes]
+        ldb = args.ld_bytes or 2 * args.row_bytes
+        sstr, dstr = [ldb], [ldb]
+        desc = f"2-D f64, {args.row_bytes} B rows x {count[1]}, ld {ldb} B"
     levels = len(count) - 1
     sb, db = bench.span_bytes(count, sstr), bench.span_bytes(count, dstr)
     alg = 3 * bench.patch_bytes(count)
@@ -53,7 +61,7 @@ def main():
     variants = [v for v in args.variants.split(";") if v]
     # every knob is reset to its default before each variant (a variant sets only its own keys)
     defaults = {k: ga_amd.get_tuning(k) for k in ("kind", "unroll16", "nontemporal", "flat_max_nvec", "max_grid",
-                                                   "block", "align", "cpol", "xcd", "order", "direct", "flat_nt", "lds_pad")}
+                                                   "block", "align", "cpol", "xcd", "order", "direct", "flat_nt", "lds_pad", "flat_shape", "flat_line_min")}
     defaults["streams"] = L.gaamd_num_streams()
     res = {v: [] for v in variants}
     wall = {v: [] for v in variants}
@@ -90,7 +98,7 @@ def main():
             res[v].append(alg / (ms / 1e3) / 1e9)
             wall[v].append(alg * args.steps / t_all / 1e9)
             enq[v].append(t_enq / args.steps * 1e6)
-    out = {"workload": args.workload + (f"@ld{args.ld}" if args.ld else "") + (f"@rows{args.rows}" if args.rows else ""),
+    out = {"workload": args.workload + (f"@ld{args.ld}" if args.ld else "") + (f"@row{args.row_bytes}B" if args.row_bytes else "") + (f"@ld{args.ld_bytes}B" if args.ld_bytes else "") + (f"@rows{args.rows}" if args.rows else ""),
            "desc": desc, "alg_bytes": alg,
            "GBps": {v: {"median": round(float(np.median(x)), 1), "min": round(float(np.min(x)), 1),
                         "max": round(float(np.max(x)), 1), "wall_median": round(float(np.median(wall[v])), 1),
