@@ -72,6 +72,7 @@ struct Tuning {
     int flat_shape = 1;     // flat kernel: 0 = 256 threads x 2 vectors, 1 = 64 threads x 1 vector (W=16, nt;
                             // +3.5-5 % on 128 B-1 KiB rows, profiles/r01/sweep_flat_shape.jsonl)
     int flat_line_min = 40; // rows off 128 B lines on both sides with at least this many vectors: rows kernel (0 = off)
+    int wide_unaligned = 0; // 16-byte vectors at 16-byte-misaligned (dword-aligned) bases when rows/strides allow
     int lds_pad = 0;        // rows kernels: dynamic LDS bytes per wave (caps resident blocks per CU; 0 = none)
 };
 Tuning &tuning();

@@ -802,6 +802,16 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         if (W < 4) return -8;
         W = esz;
     }
+    // base addresses below 16-byte alignment (a GA patch starting at an odd f64 column):
+    // when the row length and every stride are multiples of 16 bytes, 16-byte vectors at
+    // dword-aligned, 16-byte-misaligned addresses (global memory serves any dword
+    // alignment) instead of 8- or 4-byte vectors
+    if (tn.wide_unaligned && W < 16 && W >= 4) {
+        uint64_t g = (uint64_t)row_bytes | 16;
+        for (int j = 0; j < L; ++j) g |= (uint64_t)ss[j] | (uint64_t)ds[j];
+        const int Wg = (int)lowbit(g);
+        if (Wg > W) W = Wg > 16 ? 16 : Wg;
+    }
     if (serial) W = esz;
 
     Desc d;

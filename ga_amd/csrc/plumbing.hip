@@ -141,6 +141,7 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "lds_pad")) return &t.lds_pad;
     if (!strcmp(key, "flat_shape")) return &t.flat_shape;
     if (!strcmp(key, "flat_line_min")) return &t.flat_line_min;
+    if (!strcmp(key, "wide_unaligned")) return &t.wide_unaligned;
     return nullptr;
 }
 

@@ -38,8 +38,14 @@ def main():
     levels = len(count) - 1
     sb, db = bench.span_bytes(count, sstr), bench.span_bytes(count, dstr)
     alg = 3 * bench.patch_bytes(count)
-    variants = [tuple(int(x) for x in v.split(":")) for v in args.offsets.split(";") if v]
-    pad = max(max(a, b) for a, b in variants) + 4096
+    # a variant is "src_off:dst_off" or "src_off:dst_off:knob=val,knob=val" (knobs set for it only)
+    variants = [v for v in args.offsets.split(";") if v]
+
+    def parse(v):
+        f = v.split(":")
+        knobs = dict(kv.split("=") for kv in f[2].split(",")) if len(f) > 2 and f[2] else {}
+        return int(f[0]), int(f[1]), {k: int(x) for k, x in knobs.items()}
+    pad = max(max(parse(v)[0], parse(v)[1]) for v in variants) + 4096
     sets = []
     for i in range(args.sets):
         s, d = ga_amd.DeviceBuffer(sb + pad), ga_amd.DeviceBuffer(db + pad)
@@ -54,7 +60,8 @@ def main():
     res = {v: [] for v in variants}
     for rnd in range(args.rounds + 1):
         for v in variants:
-            so, do = v
+            so, do, knobs = parse(v)
+            old = {k: ga_amd.set_tuning(k, x) for k, x in knobs.items()}
             ptrs = [(ctypes.c_void_p(s.ptr + so), ctypes.c_void_p(d.ptr + do)) for s, d in sets]
             for i in range(3):
                 L.comex_accs(op, sp, ptrs[i % len(ptrs)][0], ss, ptrs[i % len(ptrs)][1], ds, cnt, levels, 0, 0)
@@ -66,12 +73,15 @@ def main():
             L.gaamd_event_record(ev[1], stream)
             ga_amd.sync()
             ms = L.gaamd_event_elapsed_ms(ev[0], ev[1]) / args.steps
+            for k, x in old.items():
+                ga_amd.set_tuning(k, x)
             if rnd:
                 res[v].append(alg / (ms / 1e3) / 1e9)
     addrs = [(hex(s.ptr), hex(d.ptr)) for s, d in sets[:2]]
     out = {"workload": args.workload, "desc": desc, "alg_bytes": alg, "bases": addrs,
-           "GBps": {f"src+{a}:dst+{b}": {"median": round(float(np.median(x)), 1), "min": round(float(np.min(x)), 1),
-                                         "max": round(float(np.max(x)), 1)} for (a, b), x in res.items()}}
+           "GBps": {"src+{}:dst+{}{}".format(*v.split(":")[:2], (":" + v.split(":")[2]) if v.count(":") > 1 else ""):
+                    {"median": round(float(np.median(x)), 1), "min": round(float(np.min(x)), 1),
+                     "max": round(float(np.max(x)), 1)} for v, x in res.items()}}
     print(json.dumps(out), flush=True)
     ga_amd.comex_finalize()
 
