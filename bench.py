@@ -244,7 +244,9 @@ def run_gpu(args, dist):
     sbytes, dbytes = span_bytes(count, sstr), span_bytes(count, dstr)
     payload = patch_bytes(count)
     elems = payload // esz
-    alg_bytes = 3 * payload            # src read + dst read + dst write
+    xfer = getattr(args, "xfer", "acc")
+    # src read + dst read + dst write; a strided put/get reads and writes once
+    alg_bytes = 3 * payload if xfer == "acc" else 2 * payload
     type_code = 0                      # f64 reals (dcpl = 2 f64 each)
 
     # --sets independent (src, dst) pairs; rotate so the MALL cannot hold them.
@@ -288,6 +290,10 @@ def run_gpu(args, dist):
             pk = ctypes.c_void_p(packed[i % len(packed)].ptr)
             rc = L.gaamd_pack(sp_, ss, cnt, levels, pk, None) or \
                 L.gaamd_unpack_acc(op, sp, pk, dp_, ds, cnt, levels, None)
+        elif xfer == "put":             # comex_puts (comex.c:6342): local src -> the target's patch
+            rc = L.comex_puts(sp_, ss, dp_, ds, cnt, levels, target, 0)
+        elif xfer == "get":             # comex_gets (comex.c:6617): the target's patch -> local buffer
+            rc = L.comex_gets(dp_, ds, sp_, ss, cnt, levels, target, 0)
         else:
             rc = L.comex_accs(op, sp, sp_, ss, dp_, ds, cnt, levels, target, 0)
         if rc:
@@ -326,7 +332,8 @@ def run_gpu(args, dist):
         avg_kernel_s = elapsed / args.steps   # the work runs on the owners' streams
 
     res = dict(op=op, desc=desc, payload=payload, alg_bytes=alg_bytes, elems=elems, elapsed=elapsed,
-               avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), pipeline=pipeline)
+               avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), pipeline=pipeline,
+               xfer=xfer)
     for b in packed:
         b.free()
     if args.host_rates and dist.rank == 0:
@@ -472,6 +479,8 @@ def main():
                     help="N>1: rank r accumulates into rank r+1's partition (remote path, SURVEY 8(d) M2)")
     ap.add_argument("--pipeline", action="store_true",
                     help="step = pack + unpack-acc (the remote path's two kernels) instead of the fused acc")
+    ap.add_argument("--xfer", default="acc", choices=["acc", "put", "get"],
+                    help="operation per step: strided accumulate (the metric), or strided put / get")
     ap.add_argument("--tune", action="append", help="key=value tuning knob (gaamd_set_tuning)")
     ap.add_argument("--ga-dims", type=int, default=0, help="C5: square GA of this size instead of 32768^2")
     ap.add_argument("--verbose", action="store_true", help="progress lines on stderr")
@@ -485,9 +494,9 @@ def main():
     alg = r["alg_bytes"]
     value = n * args.steps * alg / r["elapsed"] / 2 ** 30
     achieved = alg / r["avg_kernel_s"] / 1e9
-    traffic = load_traffic(args.workload, alg)
+    traffic = load_traffic(args.workload, alg) if r.get("xfer", "acc") == "acc" else None
     cpu = None
-    if not args.no_cpu and n == 1 and args.workload != "C5":
+    if not args.no_cpu and n == 1 and args.workload != "C5" and r.get("xfer", "acc") == "acc":
         cpu = run_cpu_baseline(args.workload, args.cpu_seconds, args.cpu_threads)
     line = {
         "metric": METRIC,
@@ -509,7 +518,7 @@ def main():
                                     f"exchange x{n}: rank r -> rank r+1, pack + owner unpack-acc over xGMI")
                                    if r["exchange"] else f"owner-aligned x{n} (no collective)"),
                    "kernel": r["launch"]},
-        "payload_GiB_per_s": round(value / 3, 2),
+        "payload_GiB_per_s": round(value / (3 if r.get("xfer", "acc") == "acc" else 2), 2),
         "hbm_peak_frac": round(value * 2 ** 30 / (dist.size * HBM_PEAK_GBS * 1e9), 4),   # per GPU
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -522,6 +531,9 @@ def main():
                                        if r["streams"] > 1 else "compare kernel_ms_avg with rocprofv3 AverageNs")},
         "cpu_baseline": cpu,
     }
+    if r.get("xfer", "acc") != "acc":
+        line["metric"] = f"GiB/s device-resident strided f64 {r['xfer']} (comex_{r['xfer']}s), not the headline metric"
+        line["config"]["step"] = f"comex_{r['xfer']}s of the patch; algorithmic bytes = 2 x payload (read + write)"
     if r.get("pipeline"):
         # two kernels per step on one stream: pack moves 2x payload, unpack-acc 3x
         moved = 5 * r["payload"]

@@ -30,6 +30,7 @@
 #include <unistd.h>
 #include <sched.h>
 #include <deque>
+#include <memory>
 #include <algorithm>
 
 namespace gaamd {
@@ -835,6 +836,17 @@ static int xfer_contig(Xfer kind, int op, void *scale, void *src, void *dst, int
 static char *g_iov_scratch = nullptr;
 static size_t g_iov_scratch_bytes = 0;
 
+static char *g_iov_host = nullptr;
+static size_t g_iov_host_bytes = 0;
+
+static char *iov_host_scratch(size_t bytes) {   // pinned upload staging; caller holds launch_mu
+    if (bytes <= g_iov_host_bytes) return g_iov_host;
+    if (g_iov_host) GA_HIP(hipHostFree(g_iov_host));
+    g_iov_host_bytes = std::max<size_t>(bytes, 1 << 20);
+    GA_HIP(hipHostMalloc((void **)&g_iov_host, g_iov_host_bytes, hipHostMallocDefault));
+    return g_iov_host;
+}
+
 static char *iov_scratch(size_t bytes) {   // caller holds launch_mu
     if (bytes <= g_iov_scratch_bytes) return g_iov_scratch;
     sched_sync_all();
@@ -862,42 +874,143 @@ static bool any_cross_overlap(std::vector<std::pair<uint64_t, uint64_t>> a, std:
     return false;
 }
 
-// one descriptor whose every address is device-accessible in this process
-static void iov_local(int cop, const void *scale, const std::vector<uint64_t> &src, const std::vector<uint64_t> &dst,
-                      int bytes) {
+// Device views of the listed addresses, resolved through a small cache of the
+// allocations already seen (one hipPointerGetAttributes per allocation instead of
+// per pair: a GA scatter-acc lists up to millions of addresses in a few buffers).
+struct ViewCache {
+    struct Range { uint64_t lo = 0, hi = 0; int64_t delta = 0; };
+    Range r[4];
+    uint64_t neg[4] = {~0ull, ~0ull, ~0ull, ~0ull};   // pages known not to be device-accessible
+    int next = 0, next_neg = 0;
+    bool view(void *p, int bytes, uint64_t *out) {
+        const uint64_t a = (uint64_t)(uintptr_t)p;
+        for (const Range &x : r)
+            if (a >= x.lo && a + (uint64_t)bytes <= x.hi) { *out = (uint64_t)((int64_t)a + x.delta); return true; }
+        const uint64_t pg = a & ~(uint64_t)(kPage - 1);
+        for (uint64_t q : neg)
+            if (q == pg && a + (uint64_t)bytes <= pg + kPage) return false;
+        char *d = nullptr;
+        if (!direct_view(p, &d)) {
+            neg[next_neg] = pg;
+            next_neg = (next_neg + 1) % 4;
+            return false;
+        }
+        *out = (uint64_t)(uintptr_t)d;
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)d) == hipSuccess && size) {
+            Range &x = r[next];
+            next = (next + 1) % 4;
+            x.delta = (int64_t)(uintptr_t)d - (int64_t)a;
+            x.lo = (uint64_t)((int64_t)(uintptr_t)base - x.delta);
+            x.hi = x.lo + size;
+        } else {
+            (void)hipGetLastError();
+        }
+        return true;
+    }
+};
+
+// io-vector pairs from this many up use the GPU-sorted run kernel (launch_iov_runs)
+// instead of a host-side overlap check
+constexpr int kIovRunsMin = 4096;
+
+// One descriptor on this GPU.  `src` lists device addresses, or is empty when
+// `host_src` holds the n source runs packed on the host (gathered from pageable
+// memory by the caller); `dst` lists device addresses, or is empty when the
+// results go packed to `host_dst` (getv into pageable memory: the caller
+// scatters them).  Reference: nb_accv / nb_putv / nb_getv to a self/SMP target,
+// comex.c:7327-7400 (one _acc / memcpy per pair, in order).
+static void iov_local(int cop, const void *scale, const uint64_t *src, const uint64_t *dst, int bytes, int n,
+                      const char *host_src = nullptr, char *host_dst = nullptr) {
     Runtime &r = rt();
-    const int n = (int)src.size();
-    std::vector<std::pair<uint64_t, uint64_t>> sr(n), dr(n);
+    const bool src_listed = src != nullptr, dst_listed = dst != nullptr;
     uint64_t align_or = 0, slo = ~0ull, shi = 0, dlo = ~0ull, dhi = 0;
     for (int i = 0; i < n; ++i) {
-        sr[i] = {src[i], src[i] + (uint64_t)bytes};
-        dr[i] = {dst[i], dst[i] + (uint64_t)bytes};
-        align_or |= src[i] | dst[i];
-        slo = std::min(slo, src[i]);
-        shi = std::max(shi, src[i] + (uint64_t)bytes);
-        dlo = std::min(dlo, dst[i]);
-        dhi = std::max(dhi, dst[i] + (uint64_t)bytes);
+        if (src_listed) {
+            align_or |= src[i];
+            slo = std::min(slo, src[i]);
+            shi = std::max(shi, src[i] + (uint64_t)bytes);
+        }
+        if (dst_listed) {
+            align_or |= dst[i];
+            dlo = std::min(dlo, dst[i]);
+            dhi = std::max(dhi, dst[i] + (uint64_t)bytes);
+        }
     }
-    const bool serial = ranges_overlap(dr) || any_cross_overlap(sr, dr);
-    std::vector<uint64_t> lists(2 * (size_t)n);
-    memcpy(lists.data(), src.data(), (size_t)n * 8);
-    memcpy(lists.data() + n, dst.data(), (size_t)n * 8);
+    bool serial = false, runs = false;
+    if (dst_listed) {
+        // a source inside a destination: the reference order matters across pairs
+        bool cross = false;
+        if (src_listed && slo < dhi && dlo < shi) {
+            std::vector<std::pair<uint64_t, uint64_t>> sr((size_t)n), dr((size_t)n);
+            for (int i = 0; i < n; ++i) {
+                sr[i] = {src[i], src[i] + (uint64_t)bytes};
+                dr[i] = {dst[i], dst[i] + (uint64_t)bytes};
+            }
+            cross = any_cross_overlap(sr, dr);
+        }
+        // every destination a whole number of pairs from dlo (no partial overlaps)
+        bool congruent = true;
+        if ((bytes & (bytes - 1)) == 0) {
+            uint64_t x = 0;
+            for (int i = 0; i < n; ++i) x |= dst[i] - dlo;
+            congruent = (x & (uint64_t)(bytes - 1)) == 0;
+        } else {
+            const FastDiv fd = make_fastdiv((uint32_t)bytes);   // no 64-bit divide per pair
+            for (int i = 0; i < n && congruent; ++i) {
+                const uint64_t off = dst[i] - dlo;
+                congruent = off < (1ull << 32) ? (uint64_t)fd.div((uint32_t)off) * (uint64_t)bytes == off
+                                               : off % (uint64_t)bytes == 0;
+            }
+        }
+        const uint64_t units = (dhi - dlo) / (uint64_t)bytes + 1;
+        if (cross) {
+            serial = true;
+        } else if (n >= kIovRunsMin && congruent && bytes <= kIovRunsMaxBytes && units <= (1ull << 32)) {
+            runs = true;   // repeated destinations are ordered on the GPU
+        } else {
+            std::vector<std::pair<uint64_t, uint64_t>> dr((size_t)n);
+            for (int i = 0; i < n; ++i) dr[i] = {dst[i], dst[i] + (uint64_t)bytes};
+            serial = ranges_overlap(dr);
+        }
+    }
+    // device scratch: [dst list | src list or packed sources | packed results | run-sort work]
+    const size_t nb = (size_t)n * 8, pk = ((size_t)n * (size_t)bytes + 15) & ~(size_t)15;
+    const size_t o_dst = 0, o_src = dst_listed ? nb : 0;
+    const size_t o_res = o_src + (src_listed ? nb : pk);
+    const size_t o_work = (o_res + (dst_listed ? 0 : pk) + 255) & ~(size_t)255;   // sort work: 256-aligned
+    const size_t work = runs ? iov_runs_work_bytes((uint32_t)n) : 0;
     std::lock_guard<std::mutex> g(r.launch_mu);
-    char *dev = iov_scratch((size_t)n * 16);
-    sched_sync_all();   // the previous io-vector kernel has finished reading the scratch lists
-    GA_HIP(hipMemcpy(dev, lists.data(), (size_t)n * 16, hipMemcpyHostToDevice));
+    char *dev = iov_scratch(o_work + work);
+    sched_sync_all();   // the previous io-vector kernel and its upload are done with both scratches
+    char *up = iov_host_scratch(o_res);   // pinned: one DMA upload, stream-ordered before the kernel
+    if (dst_listed) memcpy(up + o_dst, dst, nb);
+    if (src_listed) memcpy(up + o_src, src, nb);
+    else memcpy(up + o_src, host_src, (size_t)n * (size_t)bytes);
     IovDesc d;
     memset(&d, 0, sizeof(d));
-    d.src_list = (const uint64_t *)dev;
-    d.dst_list = (const uint64_t *)dev + n;
+    if (src_listed) d.src_list = (const uint64_t *)(dev + o_src);
+    else d.src_base = dev + o_src;
+    if (dst_listed) d.dst_list = (const uint64_t *)(dev + o_dst);
+    else d.dst_base = dev + o_res;
     d.bytes = bytes;
     d.n = (uint32_t)n;
     Span ss, ds;
-    ss.lo = (int64_t)slo; ss.hi = (int64_t)shi;
-    ds.lo = (int64_t)dlo; ds.hi = (int64_t)dhi;
+    ss.lo = src_listed ? (int64_t)slo : (int64_t)(uintptr_t)(dev + o_src);
+    ss.hi = src_listed ? (int64_t)shi : ss.lo + (int64_t)pk;
+    ds.lo = dst_listed ? (int64_t)dlo : (int64_t)(uintptr_t)(dev + o_res);
+    ds.hi = dst_listed ? (int64_t)dhi : ds.lo + (int64_t)pk;
     const int si = sched_pick(ss, ds);
-    const int rc = launch_iov(cop, scale, d, align_or, serial, r.streams[si]);
+    GA_HIP(hipMemcpyAsync(dev, up, o_res, hipMemcpyHostToDevice, r.streams[si]));
+    const int rc = runs ? launch_iov_runs(cop, scale, d, align_or, dlo, (dhi - dlo) / (uint64_t)bytes + 1,
+                                          dev + o_work, work, r.streams[si])
+                        : launch_iov(cop, scale, d, align_or, serial, r.streams[si]);
     if (rc) fatal("io-vector launch failed (%d): misaligned elements?", rc);
+    if (!dst_listed) {
+        GA_HIP(hipStreamSynchronize(r.streams[si]));
+        GA_HIP(hipMemcpy(host_dst, dev + o_res, (size_t)n * (size_t)bytes, hipMemcpyDeviceToHost));
+    }
     if (r.blocking_sync) sched_sync_all();
 }
 
@@ -913,7 +1026,9 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         if (n <= 0) continue;
         if (bytes <= 0) fatal("io-vector of %d bytes", bytes);
         const bool remote_side_is_dst = (kind != X_GET);
-        std::vector<uint64_t> sv((size_t)n), dv((size_t)n);
+        // address lists, uninitialised (every entry is written before it is read)
+        std::unique_ptr<uint64_t[]> svb(new uint64_t[(size_t)n]), dvb(new uint64_t[(size_t)n]);
+        uint64_t *sv = svb.get(), *dv = dvb.get();
         bool host_bounce = false;
         if (world != r.rank && !r.same_node(world)) {
             // another node: one io-vector message per descriptor chunk (wire.cpp)
@@ -936,35 +1051,64 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
                 for (int i = 0; i < n; ++i)
                     xfer_contig(kind, op, scale, darr[k].src[i], darr[k].dst[i], bytes, proc, group, nullptr);
             } else if (kind == X_GET) {
-                wire_get_iov(sv.data(), dv.data(), n, bytes, world);
+                wire_get_iov(sv, dv, n, bytes, world);
             } else {
                 std::vector<std::pair<uint64_t, uint64_t>> dr((size_t)n);
                 for (int i = 0; i < n; ++i) dr[i] = {dv[i], dv[i] + (uint64_t)bytes};
-                wire_send_iov(cop, scale, sv.data(), dv.data(), n, bytes, ranges_overlap(dr), world);
+                wire_send_iov(cop, scale, sv, dv, n, bytes, ranges_overlap(dr), world);
             }
             continue;
         }
-        for (int i = 0; i < n; ++i) {
+        ViewCache vc;
+        bool src_host = false, dst_host = false;   // a whole side in pageable host memory
+        for (int i = 0; i < n && !host_bounce; ++i) {
             void *sp = darr[k].src[i], *dp = darr[k].dst[i];
-            char *d = nullptr;
+            uint64_t v = 0;
             if (world != r.rank && !remote_side_is_dst) {
                 sv[i] = (uint64_t)(uintptr_t)remote_view(world, sp, 0, bytes);
-            } else if (direct_view(sp, &d)) {
-                sv[i] = (uint64_t)(uintptr_t)d;
+            } else if (vc.view(sp, bytes, &v)) {
+                if (src_host) host_bounce = true;   // mixed host and device sources
+                sv[i] = v;
+            } else if (i == 0 || src_host) {
+                src_host = true;
             } else {
                 host_bounce = true;
-                break;
             }
             if (world != r.rank && remote_side_is_dst) {
                 if (kind == X_ACC) dv[i] = (uint64_t)(uintptr_t)dp;   // owner's address, checked below
                 else dv[i] = (uint64_t)(uintptr_t)remote_view(world, dp, 0, bytes);
-            } else if (direct_view(dp, &d)) {
-                dv[i] = (uint64_t)(uintptr_t)d;
+            } else if (vc.view(dp, bytes, &v)) {
+                if (dst_host) host_bounce = true;
+                dv[i] = v;
+            } else if (i == 0 || dst_host) {
+                dst_host = true;
             } else {
                 host_bounce = true;
-                break;
             }
         }
+        // packed host side: sources of an accumulate/put (local or same-node put), or the
+        // results of a copy (get/put into host memory); an accumulate into host memory
+        // needs the old values and stays per pair
+        if (src_host && dst_host) host_bounce = true;
+        if (dst_host && cop != kOpCopy) host_bounce = true;
+        if (src_host && world != r.rank && kind == X_ACC) host_bounce = true;
+        if (!host_bounce && (src_host || dst_host)) {
+            // pageable host runs on one side (GA's MA buffer `v` of a scatter/gather): the
+            // sources are gathered on the host and uploaded packed, or the results come
+            // back packed and are scattered on the host, in pair order
+            if (world != r.rank) fence_target(world);
+            if (src_host) {
+                std::vector<char> packed((size_t)n * (size_t)bytes);
+                for (int i = 0; i < n; ++i) memcpy(packed.data() + (size_t)i * bytes, darr[k].src[i], (size_t)bytes);
+                iov_local(cop, scale, nullptr, dv, bytes, n, packed.data(), nullptr);
+            } else {
+                std::vector<char> packed((size_t)n * (size_t)bytes);
+                iov_local(cop, scale, sv, nullptr, bytes, n, nullptr, packed.data());
+                for (int i = 0; i < n; ++i) memcpy(darr[k].dst[i], packed.data() + (size_t)i * bytes, (size_t)bytes);
+            }
+            continue;
+        }
+        if (src_host || dst_host) host_bounce = true;
         if (host_bounce) {
             // pageable host pairs: per-pair transfers (each maps its pages)
             for (int i = 0; i < n; ++i)
@@ -973,7 +1117,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         }
         if (world == r.rank || kind != X_ACC) {
             if (world != r.rank) fence_target(world);
-            iov_local(cop, scale, sv, dv, bytes);
+            iov_local(cop, scale, sv, dv, bytes, n);
             continue;
         }
         // remote io-vector accumulate: pack the sources + the owner addresses into
@@ -1003,7 +1147,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
                 std::lock_guard<std::mutex> g(r.launch_mu);
                 char *dev = iov_scratch((size_t)m * 8);
                 sched_sync_all();
-                GA_HIP(hipMemcpy(dev, sv.data() + i0, (size_t)m * 8, hipMemcpyHostToDevice));
+                GA_HIP(hipMemcpy(dev, sv + i0, (size_t)m * 8, hipMemcpyHostToDevice));
                 uint64_t salign = 0;
                 for (int i = 0; i < m; ++i) salign |= sv[(size_t)i0 + i];
                 IovDesc d;
@@ -1015,7 +1159,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
                 sched_join();
                 const int rc = launch_iov(kOpCopy, nullptr, d, salign, false, r.streams[0]);
                 if (rc) fatal("io-vector pack failed (%d)", rc);
-                GA_HIP(hipMemcpyAsync(stage + loff, dv.data() + i0, (size_t)m * 8, hipMemcpyHostToDevice,
+                GA_HIP(hipMemcpyAsync(stage + loff, dv + i0, (size_t)m * 8, hipMemcpyHostToDevice,
                                       r.streams[0]));
                 GA_HIP(hipStreamSynchronize(r.streams[0]));
             }
@@ -1159,6 +1303,9 @@ int comex_finalize() {
     sched_fini();
     if (g_iov_scratch) (void)hipFree(g_iov_scratch);
     g_iov_scratch = nullptr;
+    if (g_iov_host) (void)hipHostFree(g_iov_host);
+    g_iov_host = nullptr;
+    g_iov_host_bytes = 0;
     g_iov_scratch_bytes = 0;
     (void)hipStreamDestroy(r.stream);
     r.stream = nullptr;

@@ -115,9 +115,22 @@ struct IovDesc {
     uint32_t n;
     uint32_t nvec, items;   // filled by launch_iov
     FastDiv nvec_div;
+    const uint32_t *run_key;   // launch_iov_runs: destinations sorted ((dst - dlo) / bytes)
+    const uint32_t *run_perm;  //   and the pair index of each sorted position
 };
 // `align_or` = OR of every listed address (the launcher cannot read device lists);
 // `serial` applies the pairs one by one in order (overlapping destinations)
 int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool serial, hipStream_t stream);
+// Pairs whose destinations may repeat (GA scatter-accumulate with repeated
+// subscripts), without a host-side overlap check: the destinations are sorted on
+// the GPU (stable radix sort of (dst - dlo) / bytes, so equal destinations keep
+// their input order) and one lane per distinct destination applies its pairs in
+// input order -- the reference's pair order wherever it matters.  Requires a
+// device dst list, every dst - dlo a multiple of d.bytes, (dhi - dlo) / bytes
+// < 2^32, d.bytes <= kIovRunsMaxBytes, and no source inside a destination.
+constexpr int kIovRunsMaxBytes = 256;
+size_t iov_runs_work_bytes(uint32_t n);
+int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
+                    void *work, size_t work_bytes, hipStream_t stream);
 
 }  // namespace gaamd

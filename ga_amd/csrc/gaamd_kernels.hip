@@ -28,6 +28,7 @@
 #pragma clang fp contract(off)
 
 #include "gaamd_kernels.h"
+#include <hipcub/device/device_radix_sort.hpp>
 #include <string.h>
 #include <algorithm>
 #include <type_traits>
@@ -973,12 +974,43 @@ __global__ __launch_bounds__(64) void k_iov_serial(const IovDesc d, const OP op)
     }
 }
 
+// launch_iov_runs: sort keys = destination index relative to dlo, values = pair index
+__global__ __launch_bounds__(256) void k_iov_keys(const uint64_t *dst_list, uint64_t dlo, uint32_t bytes, uint32_t n,
+                                                  uint32_t *keys, uint32_t *vals) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = (uint32_t)((dst_list[i] - dlo) / bytes);
+    vals[i] = i;
+}
+
+// one lane per distinct destination (the first sorted position of its run)
+// applies the run's pairs in input order
+template <class OP, int W>
+__global__ __launch_bounds__(256) void k_iov_runs(const IovDesc d, const OP op) {
+    const uint32_t j0 = blockIdx.x * 256u + threadIdx.x;
+    if (j0 >= d.n) return;
+    const uint32_t key = d.run_key[j0];
+    if (j0 > 0 && d.run_key[j0 - 1] == key) return;
+    for (uint32_t j = j0; j < d.n && d.run_key[j] == key; ++j) {
+        const uint32_t i = d.run_perm[j];
+        const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
+        char *dp = (char *)d.dst_list[i];
+        for (uint32_t v = 0; v < d.nvec; ++v) {
+            typename Vec<W>::T x = vload<W, false>(sp + (size_t)v * W), y = x;
+            if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
+            vstore<W, false>(dp + (size_t)v * W, op.template apply<W>(y, x));
+        }
+    }
+}
+
 template <class OP, int W>
 static hipError_t iov_w(const IovDesc &d, const OP &op, bool serial, hipStream_t st) {
     if constexpr (W < OP::kElem) {
         return hipErrorInvalidValue;
     } else {
-        if (serial) {
+        if (d.run_key) {
+            hipLaunchKernelGGL((k_iov_runs<OP, W>), dim3((d.n + 255u) / 256u), dim3(256), 0, st, d, op);
+        } else if (serial) {
             hipLaunchKernelGGL((k_iov_serial<OP, W>), dim3(1), dim3(64), 0, st, d, op);
         } else {
             constexpr int U = 2;
@@ -1002,6 +1034,8 @@ static hipError_t iov_op(int W, const IovDesc &d, const OP &op, bool serial, hip
     return hipErrorInvalidValue;
 }
 
+static int iov_dispatch(int op, const void *scale, int W, const IovDesc &d, bool serial, hipStream_t stream);
+
 int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool serial, hipStream_t stream) {
     const int esz = elem_size(op);
     if (!esz || d.bytes <= 0) return -4;
@@ -1022,6 +1056,60 @@ int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool ser
     d.nvec_div = make_fastdiv(d.nvec);
     if ((uint64_t)d.n * d.nvec >= (1ull << 31)) return -7;
     d.items = d.n * d.nvec;
+    return iov_dispatch(op, scale, W, d, serial, stream);
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static size_t iov_sort_temp_bytes(uint32_t n) {
+    size_t t = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                             (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0, 32);
+    return t;
+}
+
+size_t iov_runs_work_bytes(uint32_t n) { return 4 * align256((size_t)n * 4) + align256(iov_sort_temp_bytes(n)); }
+
+int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
+                    void *work, size_t work_bytes, hipStream_t stream) {
+    const int esz = elem_size(op);
+    if (!esz || d.bytes <= 0 || d.bytes > kIovRunsMaxBytes || !d.dst_list) return -4;
+    if (op != kOpCopy && !scale) return -5;
+    if (units > (1ull << 32)) return -7;
+    const int64_t row = (op == kOpCopy) ? d.bytes : (int64_t)(d.bytes / esz) * esz;   // acc.h:122
+    if (d.n == 0 || row == 0) return 0;
+    if (work_bytes < iov_runs_work_bytes(d.n)) return -6;
+    uint64_t a = align_or | (uint64_t)row | 16;
+    if (!d.src_list) a |= (uint64_t)(uintptr_t)d.src_base | (uint64_t)d.bytes;
+    int W = (int)lowbit(a);
+    if (W > 16) W = 16;
+    if (W < esz) {
+        if (W < 4) return -8;
+        W = esz;
+    }
+    d.nvec = (uint32_t)(row / W);
+    d.nvec_div = make_fastdiv(d.nvec);
+    d.items = d.n * d.nvec;
+    char *w = (char *)work;
+    const size_t q = align256((size_t)d.n * 4);
+    uint32_t *kin = (uint32_t *)w, *kout = (uint32_t *)(w + q), *vin = (uint32_t *)(w + 2 * q),
+             *vout = (uint32_t *)(w + 3 * q);
+    void *temp = w + 4 * q;
+    size_t temp_bytes = work_bytes - 4 * q;
+    int end_bit = 1;
+    while (end_bit < 32 && (1ull << end_bit) < units) ++end_bit;
+    hipLaunchKernelGGL(k_iov_keys, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, d.dst_list, dlo,
+                       (uint32_t)d.bytes, d.n, kin, vin);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return -100 - (int)e;
+    e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, kin, kout, vin, vout, (int)d.n, 0, end_bit, stream);
+    if (e != hipSuccess) return -100 - (int)e;
+    d.run_key = kout;
+    d.run_perm = vout;
+    return iov_dispatch(op, scale, W, d, false, stream);
+}
+
+static int iov_dispatch(int op, const void *scale, int W, const IovDesc &d, bool serial, hipStream_t stream) {
     hipError_t e;
     switch (op) {
     case kOpCopy: e = iov_op(W, d, CopyOp{}, serial, stream); break;

@@ -126,6 +126,8 @@ class Ref:
         L.ref_accs.argtypes = [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int]
         L.ref_accs_mt.restype = ctypes.c_int
         L.ref_accs_mt.argtypes = [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int, ctypes.c_int]
+        L.ref_accv.restype = ctypes.c_int
+        L.ref_accv.argtypes = [ctypes.c_int, _vp, _vp, _vp, ctypes.c_long, ctypes.c_int]
         self.L = L
 
     def accs(self, op, scale, src, src_off, src_stride, dst, dst_off, dst_stride, count, levels):
@@ -138,6 +140,12 @@ class Ref:
         rc = self.L.ref_accs_mt(op, _ptr(s), _vp(src.ctypes.data + src_off), _ints(src_stride),
                                 _vp(dst.ctypes.data + dst_off), _ints(dst_stride), _ints(count), levels, nthreads)
         assert rc == 0
+
+    def accv(self, op, scale, src_addrs, dst_addrs, nbytes):
+        """one _acc per (src, dst) pair; src_addrs/dst_addrs: uint64 arrays of host addresses."""
+        s = np.array([scale], dtype=_scale_dtype(op))
+        assert self.L.ref_accv(op, _ptr(s), _vp(src_addrs.ctypes.data), _vp(dst_addrs.ctypes.data),
+                               len(src_addrs), nbytes) == 0
 
 
 def ref_available():

@@ -92,3 +92,12 @@ int ref_accs_mt(int op, const void *scale, const char *src, const int *src_strid
     return mt_accs(ref_accs, ref_esize(op), op, scale, src, src_stride, dst, dst_stride, count,
                    stride_levels, nthreads);
 }
+
+/* io-vector accumulate to a self/SMP target: one _acc per (src[i], dst[i]) pair,
+ * as nb_accv does for such targets (comex.c:7327-7400 -> nb_acc 6228-6260) */
+int ref_accv(int op, const void *scale, void *const *src, void *const *dst, long n, int bytes)
+{
+    long i;
+    for (i = 0; i < n; i++) _acc(op, bytes, dst[i], src[i], scale);
+    return 0;
+}

@@ -504,3 +504,101 @@ def test_accv_host_source_pairs(gpu_lib, oracle):
     _oracle_acc_pairs(oracle, op, C.SCALE[op], src, want, [(i * nbytes, (n - 1 - i) * nbytes) for i in range(n)],
                       nbytes)
     assert np.array_equal(db.download(np.uint8, dst.size), want)
+
+
+def _giov_np(src_addrs, dst_addrs, nbytes):
+    """one comex_giov_t over numpy uint64 address arrays (large n without Python lists);
+    the arrays stay referenced by the returned descriptor."""
+    src_addrs = np.ascontiguousarray(src_addrs, dtype=np.uint64)
+    dst_addrs = np.ascontiguousarray(dst_addrs, dtype=np.uint64)
+    g = ga_amd.GIOV()
+    g._keep = (src_addrs, dst_addrs)
+    g.src = ctypes.cast(ctypes.c_void_p(src_addrs.ctypes.data), ctypes.POINTER(ctypes.c_void_p))
+    g.dst = ctypes.cast(ctypes.c_void_p(dst_addrs.ctypes.data), ctypes.POINTER(ctypes.c_void_p))
+    g.count, g.bytes = len(src_addrs), nbytes
+    return g
+
+
+@pytest.mark.parametrize("op,nbytes,slots,shift", [(C.DBL, 8, 3000, 0), (C.DBL, 8, 10 ** 6, 0), (C.FLT, 4, 500, 0),
+                                                   (C.DCP, 16, 2000, 0), (C.INT, 12, 700, 0), (C.LNG, 8, 100, 0),
+                                                   (C.CPL, 8 * 3, 5000, 0), (C.DBL, 48, 4000, 0),
+                                                   (C.DBL, 320, 300, 0), (C.DBL, 16, 3000, 8)])
+def test_accv_large_repeated_destinations(gpu_lib, oracle, op, nbytes, slots, shift):
+    """GA scatter-acc sizes: 40 000 pairs in one descriptor, destinations drawn from
+    `slots` (many repeats), bit-exact against the pairs applied one by one in order.
+    From 4096 pairs the launcher sorts destinations on the GPU and applies each
+    destination's pairs in input order (launch_iov_runs); 320-byte pairs and
+    destinations not congruent modulo the pair size (`shift`: some start half a
+    pair later) take the host-checked path instead."""
+    rng = np.random.default_rng(nbytes * 7 + slots)
+    n = 40000
+    src = C.fill_bytes(op, n * nbytes, 5)
+    dst = C.fill_bytes(op, slots * nbytes + 64, 6)
+    sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+    sb.upload(src)
+    db.upload(dst)
+    so = np.arange(n, dtype=np.uint64) * nbytes
+    do = rng.integers(0, slots, n).astype(np.uint64) * nbytes
+    if shift:
+        do[rng.random(n) < 0.01] += shift
+    g = _giov_np(so + np.uint64(sb.ptr), do + np.uint64(db.ptr), nbytes)
+    keep, sp = ga_amd.scale_buffer(op, C.SCALE[op])
+    assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
+    ga_amd.comex_fence_all()
+    want = dst.copy()
+    _oracle_acc_pairs(oracle, op, C.SCALE[op], src, want, list(zip(so.tolist(), do.tolist())), nbytes)
+    got = db.download(np.uint8, dst.size)
+    assert same_bits_nan_aware(got, want, op)
+
+
+@pytest.mark.parametrize("n", [50, 20000])
+def test_accv_host_sources_packed(gpu_lib, oracle, n):
+    """Pageable host sources (GA's MA buffer `v` of NGA_Scatter_acc) are gathered on the
+    host and uploaded packed (one kernel, not one transfer per pair); repeated
+    destinations still apply in order."""
+    op, nbytes = C.DBL, 8
+    rng = np.random.default_rng(n)
+    src = C.fill_bytes(op, n * nbytes, 3)
+    dst = C.fill_bytes(op, 1000 * nbytes, 4)
+    db = ga_amd.DeviceBuffer(dst.size)
+    db.upload(dst)
+    so = np.arange(n, dtype=np.uint64) * nbytes
+    do = rng.integers(0, 1000, n).astype(np.uint64) * nbytes
+    g = _giov_np(so + np.uint64(src.ctypes.data), do + np.uint64(db.ptr), nbytes)
+    keep, sp = ga_amd.scale_buffer(op, C.SCALE[op])
+    assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
+    ga_amd.comex_fence_all()
+    want = dst.copy()
+    _oracle_acc_pairs(oracle, op, C.SCALE[op], src, want, list(zip(so.tolist(), do.tolist())), nbytes)
+    assert np.array_equal(db.download(np.uint8, dst.size), want)
+
+
+def test_getv_putv_host_side_packed(gpu_lib):
+    """comex_getv into pageable host memory (results packed on the GPU, scattered on
+    the host in pair order: a repeated destination keeps the last pair's bytes) and
+    comex_putv from pageable host memory, 30 000 pairs of 24 bytes."""
+    rng = np.random.default_rng(11)
+    nbytes, n, slots = 24, 30000, 5000
+    dev = rng.integers(0, 256, slots * nbytes, dtype=np.uint8)
+    db = ga_amd.DeviceBuffer(dev.size)
+    db.upload(dev)
+    so = rng.integers(0, slots, n).astype(np.uint64) * nbytes
+    host = np.zeros(2000 * nbytes, dtype=np.uint8)
+    do = rng.integers(0, 2000, n).astype(np.uint64) * nbytes
+    g = _giov_np(so + np.uint64(db.ptr), do + np.uint64(host.ctypes.data), nbytes)
+    assert gpu_lib.comex_getv(ctypes.byref(g), 1, 0, 0) == 0
+    want = np.zeros_like(host)
+    for a, b in zip(so.tolist(), do.tolist()):
+        want[b:b + nbytes] = dev[a:a + nbytes]
+    assert np.array_equal(host, want)
+    # putv from host: repeated destinations, last pair wins
+    src = rng.integers(0, 256, n * nbytes, dtype=np.uint8)
+    s_off = np.arange(n, dtype=np.uint64) * nbytes
+    d_off = rng.integers(0, slots, n).astype(np.uint64) * nbytes
+    g = _giov_np(s_off + np.uint64(src.ctypes.data), d_off + np.uint64(db.ptr), nbytes)
+    assert gpu_lib.comex_putv(ctypes.byref(g), 1, 0, 0) == 0
+    ga_amd.comex_fence_all()
+    want = dev.copy()
+    for a, b in zip(s_off.tolist(), d_off.tolist()):
+        want[b:b + nbytes] = src[a:a + nbytes]
+    assert np.array_equal(db.download(np.uint8, dev.size), want)
