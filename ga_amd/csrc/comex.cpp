@@ -911,6 +911,31 @@ struct ViewCache {
     }
 };
 
+// host-side packing of pageable io-vector runs, in pair order (fixed-size copies
+// for the element sizes GA scatters, so the compiler emits plain loads/stores)
+template <int B> static void gather_fixed(char *out, void *const *p, int n) {
+    for (int i = 0; i < n; ++i) memcpy(out + (size_t)i * B, p[i], B);
+}
+template <int B> static void scatter_fixed(void *const *p, const char *in, int n) {
+    for (int i = 0; i < n; ++i) memcpy(p[i], in + (size_t)i * B, B);
+}
+static void gather_runs(char *out, void *const *p, int n, int bytes) {
+    switch (bytes) {
+    case 4: return gather_fixed<4>(out, p, n);
+    case 8: return gather_fixed<8>(out, p, n);
+    case 16: return gather_fixed<16>(out, p, n);
+    }
+    for (int i = 0; i < n; ++i) memcpy(out + (size_t)i * bytes, p[i], (size_t)bytes);
+}
+static void scatter_runs(void *const *p, const char *in, int n, int bytes) {
+    switch (bytes) {
+    case 4: return scatter_fixed<4>(p, in, n);
+    case 8: return scatter_fixed<8>(p, in, n);
+    case 16: return scatter_fixed<16>(p, in, n);
+    }
+    for (int i = 0; i < n; ++i) memcpy(p[i], in + (size_t)i * bytes, (size_t)bytes);
+}
+
 // io-vector pairs from this many up use the GPU-sorted run kernel (launch_iov_runs)
 // instead of a host-side overlap check
 constexpr int kIovRunsMin = 4096;
@@ -925,18 +950,43 @@ static void iov_local(int cop, const void *scale, const uint64_t *src, const uin
                       const char *host_src = nullptr, char *host_dst = nullptr) {
     Runtime &r = rt();
     const bool src_listed = src != nullptr, dst_listed = dst != nullptr;
+    // device scratch: [dst list | src list or packed sources | packed results | run-sort work],
+    // uploaded from pinned staging; the lists are copied there in the same pass that
+    // takes their spans
+    const size_t nb = (size_t)n * 8, pk = ((size_t)n * (size_t)bytes + 15) & ~(size_t)15;
+    const size_t o_dst = 0, o_src = dst_listed ? nb : 0;
+    const size_t o_res = o_src + (src_listed ? nb : pk);
+    std::unique_lock<std::mutex> g(r.launch_mu);
+    sched_sync_all();   // the previous io-vector kernel and its upload are done with both scratches
+    char *up = iov_host_scratch(o_res);
     uint64_t align_or = 0, slo = ~0ull, shi = 0, dlo = ~0ull, dhi = 0;
-    for (int i = 0; i < n; ++i) {
-        if (src_listed) {
-            align_or |= src[i];
-            slo = std::min(slo, src[i]);
-            shi = std::max(shi, src[i] + (uint64_t)bytes);
+    if (src_listed) {
+        uint64_t *u = (uint64_t *)(up + o_src), o = 0, lo = ~0ull, hi = 0;
+        for (int i = 0; i < n; ++i) {
+            const uint64_t a = src[i];
+            u[i] = a;
+            o |= a;
+            lo = a < lo ? a : lo;
+            hi = a > hi ? a : hi;
         }
-        if (dst_listed) {
-            align_or |= dst[i];
-            dlo = std::min(dlo, dst[i]);
-            dhi = std::max(dhi, dst[i] + (uint64_t)bytes);
+        align_or |= o;
+        slo = lo;
+        shi = hi + (uint64_t)bytes;
+    } else {
+        memcpy(up + o_src, host_src, (size_t)n * (size_t)bytes);
+    }
+    if (dst_listed) {
+        uint64_t *u = (uint64_t *)(up + o_dst), o = 0, lo = ~0ull, hi = 0;
+        for (int i = 0; i < n; ++i) {
+            const uint64_t a = dst[i];
+            u[i] = a;
+            o |= a;
+            lo = a < lo ? a : lo;
+            hi = a > hi ? a : hi;
         }
+        align_or |= o;
+        dlo = lo;
+        dhi = hi + (uint64_t)bytes;
     }
     bool serial = false, runs = false;
     if (dst_listed) {
@@ -975,19 +1025,9 @@ static void iov_local(int cop, const void *scale, const uint64_t *src, const uin
             serial = ranges_overlap(dr);
         }
     }
-    // device scratch: [dst list | src list or packed sources | packed results | run-sort work]
-    const size_t nb = (size_t)n * 8, pk = ((size_t)n * (size_t)bytes + 15) & ~(size_t)15;
-    const size_t o_dst = 0, o_src = dst_listed ? nb : 0;
-    const size_t o_res = o_src + (src_listed ? nb : pk);
     const size_t o_work = (o_res + (dst_listed ? 0 : pk) + 255) & ~(size_t)255;   // sort work: 256-aligned
     const size_t work = runs ? iov_runs_work_bytes((uint32_t)n) : 0;
-    std::lock_guard<std::mutex> g(r.launch_mu);
     char *dev = iov_scratch(o_work + work);
-    sched_sync_all();   // the previous io-vector kernel and its upload are done with both scratches
-    char *up = iov_host_scratch(o_res);   // pinned: one DMA upload, stream-ordered before the kernel
-    if (dst_listed) memcpy(up + o_dst, dst, nb);
-    if (src_listed) memcpy(up + o_src, src, nb);
-    else memcpy(up + o_src, host_src, (size_t)n * (size_t)bytes);
     IovDesc d;
     memset(&d, 0, sizeof(d));
     if (src_listed) d.src_list = (const uint64_t *)(dev + o_src);
@@ -1026,9 +1066,14 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         if (n <= 0) continue;
         if (bytes <= 0) fatal("io-vector of %d bytes", bytes);
         const bool remote_side_is_dst = (kind != X_GET);
-        // address lists, uninitialised (every entry is written before it is read)
-        std::unique_ptr<uint64_t[]> svb(new uint64_t[(size_t)n]), dvb(new uint64_t[(size_t)n]);
-        uint64_t *sv = svb.get(), *dv = dvb.get();
+        // address lists in buffers kept across calls: fresh ones cost a page fault per
+        // 512 entries, more than the classification itself at scatter-acc sizes
+        static std::vector<uint64_t> g_sv, g_dv;
+        if (g_sv.size() < (size_t)n) {
+            g_sv.resize((size_t)n);
+            g_dv.resize((size_t)n);
+        }
+        uint64_t *sv = g_sv.data(), *dv = g_dv.data();
         bool host_bounce = false;
         if (world != r.rank && !r.same_node(world)) {
             // another node: one io-vector message per descriptor chunk (wire.cpp)
@@ -1097,14 +1142,15 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             // sources are gathered on the host and uploaded packed, or the results come
             // back packed and are scattered on the host, in pair order
             if (world != r.rank) fence_target(world);
+            static std::vector<char> g_packed;   // kept across calls (no page faults per call)
+            if (g_packed.size() < (size_t)n * (size_t)bytes) g_packed.resize((size_t)n * (size_t)bytes);
+            char *packed = g_packed.data();
             if (src_host) {
-                std::vector<char> packed((size_t)n * (size_t)bytes);
-                for (int i = 0; i < n; ++i) memcpy(packed.data() + (size_t)i * bytes, darr[k].src[i], (size_t)bytes);
-                iov_local(cop, scale, nullptr, dv, bytes, n, packed.data(), nullptr);
+                gather_runs(packed, darr[k].src, n, bytes);
+                iov_local(cop, scale, nullptr, dv, bytes, n, packed, nullptr);
             } else {
-                std::vector<char> packed((size_t)n * (size_t)bytes);
-                iov_local(cop, scale, sv, nullptr, bytes, n, nullptr, packed.data());
-                for (int i = 0; i < n; ++i) memcpy(darr[k].dst[i], packed.data() + (size_t)i * bytes, (size_t)bytes);
+                iov_local(cop, scale, sv, nullptr, bytes, n, nullptr, packed);
+                scatter_runs(darr[k].dst, packed, n, bytes);
             }
             continue;
         }
