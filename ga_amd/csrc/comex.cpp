@@ -373,8 +373,9 @@ static void post_request(int t, int op, const void *scale, uint64_t dst_addr, co
 
 // io-vector request: staging holds n packed source runs, then the n owner
 // addresses (8-byte aligned)
+// mode: 0 parallel, 1 in order on one lane (destinations overlap), 2 GPU-sorted runs
 static void post_request_iov(int t, int op, const void *scale, int bytes, int n, uint64_t off, uint64_t len,
-                             uint64_t dlo, uint64_t dhi, uint64_t align_or, bool serial) {
+                             uint64_t dlo, uint64_t dhi, uint64_t align_or, int mode) {
     Runtime &r = rt();
     Inbox *ib = inbox_of(r.shm, t);
     const uint64_t ticket = ib->tail.fetch_add(1, std::memory_order_acq_rel);
@@ -401,7 +402,7 @@ static void post_request_iov(int t, int op, const void *scale, int bytes, int n,
     memset(q.scale, 0, sizeof(q.scale));
     if (scale) memcpy(q.scale, scale, (size_t)elem_size(op));
     q.kind = 1;
-    q.iov_serial = serial ? 1 : 0;
+    q.iov_serial = mode;
     q.iov_align = align_or;
     q.state.store(2, std::memory_order_release);
 }
@@ -416,6 +417,9 @@ static void progress_loop() {
     struct Inflight { hipEvent_t ev; int src; };
     std::deque<Inflight> inflight;
     std::vector<hipEvent_t> pool;
+    char *prog_work = nullptr;          // launch_iov_runs scratch of this thread
+    size_t prog_work_bytes = 0;
+    hipEvent_t prog_work_ev = nullptr;
     unsigned idle = 0;
     for (;;) {
         bool worked = false;
@@ -440,7 +444,25 @@ static void progress_loop() {
                 dsp.lo = (int64_t)q.dst_addr;
                 dsp.hi = (int64_t)q.dst_hi;
                 const int si = sched_pick(span_of(packed, 0, (int64_t)q.bytes), dsp);
-                const int rc = launch_iov(q.op, q.scale, d, q.iov_align, q.iov_serial != 0, r.streams[si]);
+                int rc;
+                if (q.iov_serial == 2) {
+                    // repeated destinations ordered on the GPU; the progress thread's own sort
+                    // scratch, free once the previous runs kernel has finished
+                    const size_t need = iov_runs_work_bytes(d.n);
+                    if (prog_work_ev) GA_HIP(hipEventSynchronize(prog_work_ev));
+                    if (need > prog_work_bytes) {
+                        if (prog_work) GA_HIP(hipFree(prog_work));
+                        prog_work_bytes = std::max<size_t>(need, 1 << 20);
+                        GA_HIP(hipMalloc((void **)&prog_work, prog_work_bytes));
+                    }
+                    if (!prog_work_ev) GA_HIP(hipEventCreateWithFlags(&prog_work_ev, hipEventDisableTiming));
+                    rc = launch_iov_runs(q.op, q.scale, d, q.iov_align, q.dst_addr,
+                                         (q.dst_hi - q.dst_addr) / (uint64_t)d.bytes + 1, prog_work, prog_work_bytes,
+                                         r.streams[si]);
+                    GA_HIP(hipEventRecord(prog_work_ev, r.streams[si]));
+                } else {
+                    rc = launch_iov(q.op, q.scale, d, q.iov_align, q.iov_serial != 0, r.streams[si]);
+                }
                 if (rc) fatal("io-vector accumulate launch failed (%d)", rc);
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
             }
@@ -494,6 +516,11 @@ static void progress_loop() {
         else sched_yield();
     }
     for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+    if (prog_work_ev) {
+        (void)hipEventSynchronize(prog_work_ev);
+        (void)hipEventDestroy(prog_work_ev);
+    }
+    if (prog_work) (void)hipFree(prog_work);
 }
 
 // ---- asynchronous remote accumulate ---------------------------------------
@@ -1136,8 +1163,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         // needs the old values and stays per pair
         if (src_host && dst_host) host_bounce = true;
         if (dst_host && cop != kOpCopy) host_bounce = true;
-        if (src_host && world != r.rank && kind == X_ACC) host_bounce = true;
-        if (!host_bounce && (src_host || dst_host)) {
+        if (!host_bounce && (src_host || dst_host) && (world == r.rank || kind != X_ACC)) {
             // pageable host runs on one side (GA's MA buffer `v` of a scatter/gather): the
             // sources are gathered on the host and uploaded packed, or the results come
             // back packed and are scattered on the host, in pair order
@@ -1154,7 +1180,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             }
             continue;
         }
-        if (src_host || dst_host) host_bounce = true;
+        if (dst_host) host_bounce = true;   // (a remote accumulate from host sources is gathered below)
         if (host_bounce) {
             // pageable host pairs: per-pair transfers (each maps its pages)
             for (int i = 0; i < n; ++i)
@@ -1174,37 +1200,57 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         const int pairs_per_req = (int)std::max<uint64_t>(1, (sub - 32) / per_pair);
         for (int i0 = 0; i0 < n; i0 += pairs_per_req) {
             const int m = std::min(pairs_per_req, n - i0);
-            std::vector<std::pair<uint64_t, uint64_t>> dr((size_t)m);
             uint64_t align_or = 0, dlo = ~0ull, dhi = 0;
             for (int i = 0; i < m; ++i) {
                 const uint64_t a = dv[(size_t)i0 + i];
                 (void)remote_view(world, (void *)(uintptr_t)a, 0, bytes);   // reg_cache_find
-                dr[i] = {a, a + (uint64_t)bytes};
                 align_or |= a;
                 dlo = std::min(dlo, a);
                 dhi = std::max(dhi, a + (uint64_t)bytes);
             }
-            const bool serial = ranges_overlap(dr);
+            // repeated destinations: the owner orders them on its GPU when every destination
+            // is a whole number of pairs from dlo, else a host check picks the serial kernel
+            int mode = 0;
+            bool congruent = m >= kIovRunsMin && bytes <= kIovRunsMaxBytes &&
+                             (dhi - dlo) / (uint64_t)bytes < (1ull << 32);
+            for (int i = 0; i < m && congruent; ++i) congruent = (dv[(size_t)i0 + i] - dlo) % (uint64_t)bytes == 0;
+            if (congruent) {
+                mode = 2;
+            } else {
+                std::vector<std::pair<uint64_t, uint64_t>> dr((size_t)m);
+                for (int i = 0; i < m; ++i) dr[i] = {dv[(size_t)i0 + i], dv[(size_t)i0 + i] + (uint64_t)bytes};
+                mode = ranges_overlap(dr) ? 1 : 0;
+            }
             const uint64_t loff = iov_list_off(m, bytes);
             const uint64_t len_b = loff + (uint64_t)m * 8;
             const uint64_t off = stage_alloc(world, len_b);
             char *stage = r.staging + (size_t)world * sub + off;
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
-                char *dev = iov_scratch((size_t)m * 8);
-                sched_sync_all();
-                GA_HIP(hipMemcpy(dev, sv + i0, (size_t)m * 8, hipMemcpyHostToDevice));
-                uint64_t salign = 0;
-                for (int i = 0; i < m; ++i) salign |= sv[(size_t)i0 + i];
-                IovDesc d;
-                memset(&d, 0, sizeof(d));
-                d.src_list = (const uint64_t *)dev;
-                d.dst_base = stage;
-                d.bytes = bytes;
-                d.n = (uint32_t)m;
-                sched_join();
-                const int rc = launch_iov(kOpCopy, nullptr, d, salign, false, r.streams[0]);
-                if (rc) fatal("io-vector pack failed (%d)", rc);
+                if (src_host) {
+                    // pageable sources (GA's MA buffer): gathered on the host, one upload
+                    static std::vector<char> g_rpacked;
+                    if (g_rpacked.size() < (size_t)m * (size_t)bytes) g_rpacked.resize((size_t)m * (size_t)bytes);
+                    gather_runs(g_rpacked.data(), darr[k].src + i0, m, bytes);
+                    sched_join();
+                    GA_HIP(hipMemcpyAsync(stage, g_rpacked.data(), (size_t)m * (size_t)bytes, hipMemcpyHostToDevice,
+                                          r.streams[0]));
+                } else {
+                    char *dev = iov_scratch((size_t)m * 8);
+                    sched_sync_all();
+                    GA_HIP(hipMemcpy(dev, sv + i0, (size_t)m * 8, hipMemcpyHostToDevice));
+                    uint64_t salign = 0;
+                    for (int i = 0; i < m; ++i) salign |= sv[(size_t)i0 + i];
+                    IovDesc d;
+                    memset(&d, 0, sizeof(d));
+                    d.src_list = (const uint64_t *)dev;
+                    d.dst_base = stage;
+                    d.bytes = bytes;
+                    d.n = (uint32_t)m;
+                    sched_join();
+                    const int rc = launch_iov(kOpCopy, nullptr, d, salign, false, r.streams[0]);
+                    if (rc) fatal("io-vector pack failed (%d)", rc);
+                }
                 GA_HIP(hipMemcpyAsync(stage + loff, dv + i0, (size_t)m * 8, hipMemcpyHostToDevice,
                                       r.streams[0]));
                 GA_HIP(hipStreamSynchronize(r.streams[0]));
@@ -1213,7 +1259,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             g_pend[world].push_back({seq, off, len_b});
             r.stage_head[world] = off + len_b;
             post_request_iov(world, op, scale, bytes, m, (uint64_t)world * sub + off, len_b, dlo, dhi, align_or,
-                             serial);
+                             mode);
         }
     }
     if (hdl) nb_complete_now(hdl);

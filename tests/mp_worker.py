@@ -54,7 +54,7 @@ def main():
     rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import ga_amd
     L = ga_amd.lib()
-    if mode in ("boot-gloo", "remote-gloo", "boot-nodes", "ga-gloo", "stress-gloo"):
+    if mode in ("boot-gloo", "remote-gloo", "boot-nodes", "ga-gloo", "stress-gloo", "scatremote-gloo"):
         ag, bar = torch_hooks(rank, size)
         keep = (ag, bar)  # noqa: F841
         assert L.gaamd_set_bootstrap(rank, size, rank, ctypes.cast(ag, ctypes.c_void_p),
@@ -82,6 +82,8 @@ def main():
         test_dim_ref(L, rank, size)
     elif mode == "testvec":
         test_vector_ref(L, rank, size)
+    elif mode in ("scatremote", "scatremote-gloo"):
+        scatter_remote_test(L, rank, size)
     elif mode == "armciacc":
         armci_test_acc_ref(L, rank, size)
     elif mode == "garef":
@@ -1256,6 +1258,75 @@ def armci_test_acc_ref(L, rank, size, times=10):
         assert L.ARMCI_Free(ctypes.c_void_p(ptrs[rank])) == 0
     say(rank, "armci test_acc ndim 1..7 ok")
     L.ARMCI_Finalize()
+
+
+
+# ---------------------------------------------------------------------------
+# remote io-vector accumulates at GA scatter-acc sizes: every rank sends one
+# comex_accv of n single-float pairs to every rank (itself included) into the
+# zone of the target's segment reserved for this source, destinations random in
+# the zone (many repeats); sources in HBM on even ranks, in pageable host memory
+# on odd ranks.  One source per zone, so the bits depend only on that source's
+# pair order: each target replays every source's pairs in order (np.add.at is
+# unbuffered, float32 multiply then add as acc.h) and compares bit for bit.
+SCAT_N, SCAT_ZONE = 20000, 3000
+
+
+def scat_pairs(src_rank, dst_rank):
+    rng = np.random.default_rng(1000 * src_rank + dst_rank)
+    idx = rng.integers(0, SCAT_ZONE, SCAT_N)
+    vals = (rng.random(SCAT_N) * 2 - 1).astype(np.float32)
+    return idx, vals
+
+
+def scatter_remote_test(L, rank, size):
+    import ga_amd
+    FLT, alpha = 39, np.float32(0.7071067811865476)
+    assert ga_amd.comex_init() == 0
+    zone_b = SCAT_ZONE * 4
+    seg = ga_amd.comex_malloc(zone_b * size, size)
+    init = (np.arange(SCAT_ZONE * size) % 97).astype(np.float32) * np.float32(0.25)
+    L.gaamd_memcpy(ctypes.c_void_p(seg[rank]), init.ctypes.data_as(ctypes.c_void_p), init.nbytes)
+    ga_amd.sync()
+    ga_amd.comex_barrier()
+    keep = []
+    for t in list(range(rank + 1, size)) + list(range(0, rank + 1)):
+        idx, vals = scat_pairs(rank, t)
+        if rank % 2 == 0:
+            vb = ga_amd.DeviceBuffer(vals.nbytes)
+            vb.upload(vals)
+            sbase = vb.ptr
+            keep.append(vb)
+        else:
+            sbase = vals.ctypes.data
+            keep.append(vals)
+        src = (np.uint64(sbase) + 4 * np.arange(SCAT_N, dtype=np.uint64)).astype(np.uint64)
+        dst = (np.uint64(seg[t] + zone_b * rank) + 4 * idx.astype(np.uint64)).astype(np.uint64)
+        g = ga_amd.GIOV()
+        g.src = ctypes.cast(ctypes.c_void_p(src.ctypes.data), ctypes.POINTER(ctypes.c_void_p))
+        g.dst = ctypes.cast(ctypes.c_void_p(dst.ctypes.data), ctypes.POINTER(ctypes.c_void_p))
+        g.count, g.bytes = SCAT_N, 4
+        ks, sp = ga_amd.scale_buffer(FLT, float(alpha))
+        assert L.comex_accv(FLT, sp, ctypes.byref(g), 1, t, 0) == 0
+        keep.append((src, dst))
+    ga_amd.comex_fence_all()
+    ga_amd.comex_barrier()
+    got = np.zeros(SCAT_ZONE * size, dtype=np.float32)
+    L.gaamd_memcpy(got.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(seg[rank]), got.nbytes)
+    want = init.copy()
+    for s_ in range(size):
+        idx, vals = scat_pairs(s_, rank)
+        z = want[SCAT_ZONE * s_:SCAT_ZONE * (s_ + 1)]
+        np.add.at(z, idx, alpha * vals)
+    bad = np.flatnonzero(got.view(np.uint32) != want.view(np.uint32))
+    assert bad.size == 0, f"rank {rank}: {bad.size} elements differ, first zone {bad[0] // SCAT_ZONE}"
+    ga_amd.comex_barrier()
+    for b in keep:
+        if isinstance(b, ga_amd.DeviceBuffer):
+            b.free()
+    assert ga_amd.comex_free(seg[rank]) == 0
+    say(rank, "remote scatter-acc ok")
+    ga_amd.comex_finalize()
 
 
 if __name__ == "__main__":

@@ -171,3 +171,15 @@ def test_armci_test_acc_restated(n):
     (ARMCI_NbAccS + ARMCI_WaitAll for odd ndim)/ARMCI_AllFence/ARMCI_GetS, ndim
     1..7, rel 1e-4 as the reference (exact on one rank)."""
     launch("armciacc", n=n, timeout=150)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,n,nodes", [("scatremote", 1, None), ("scatremote", 3, None),
+                                          ("scatremote-gloo", 3, [0, 0, 1])])
+def test_remote_scatter_acc_large(mode, n, nodes):
+    """comex_accv of 20 000 single-float pairs from every rank to every rank, many
+    repeated destinations, sources in HBM (even ranks) or pageable host memory (odd
+    ranks): the owner orders repeats on its GPU (launch_iov_runs) and host sources
+    are gathered into one upload; bit-exact against each source's pairs replayed in
+    order.  nodes [0,0,1] sends the third rank's traffic over the wire protocol."""
+    launch(mode, n=n, timeout=150, nodes=nodes)
