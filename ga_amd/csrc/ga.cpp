@@ -395,43 +395,58 @@ static void patch_op(GaOp kind, int g_a, const long *lo, const long *hi, void *b
 // within an owner -- and issue ONE ARMCI_GetV / PutV / AccV per owner with
 // `bytes = elemsize` and the (local, remote) address pairs (gam_Loc_ptr).
 // Repeated subscripts of a scatter-accumulate are applied in that order (the
-// io-vector kernel falls back to its in-order variant when destinations repeat).
+// io-vector path applies the pairs of a repeated destination in input order).
 enum GatScat { GS_GATHER, GS_SCATTER, GS_SCATTER_ACC };
 
-static int locate(const GArray &a, const long *sub, long *off) {
-    int proc = 0, mul = 1;
-    long blo[GA_MAX_DIM], bhi[GA_MAX_DIM];
-    int bi[GA_MAX_DIM];
-    for (int d = 0; d < a.ndim; d++) {
-        if (sub[d] < 1 || sub[d] > a.dims[d]) return -1;
-        const std::vector<long> &m = a.map[d];
-        bi[d] = (int)(std::upper_bound(m.begin(), m.end(), sub[d]) - m.begin()) - 1;
-        proc += bi[d] * mul;
-        mul *= a.nblock[d];
-    }
-    block_elems(a, proc, blo, bhi);
-    long o = 0, f = 1;   // gam_Loc_ptr: column-major offset inside the owner's block
-    for (int d = 0; d < a.ndim; d++) { o += (sub[d] - blo[d]) * f; f *= bhi[d] - blo[d] + 1; }
-    *off = o;
-    return proc;
+
+// per-call buffers kept across calls: a scatter of millions of elements would
+// otherwise page-fault its way through fresh arrays every call
+template <class T> static T *grow(std::vector<T> &v, size_t n) {
+    if (v.size() < n) v.resize(n);
+    return v.data();
 }
 
 static void gatscat(GatScat op, int g_a, void *v, const long *fsub, long nv, void *alpha) {
     if (nv < 1) return;   // pnga_gather / pnga_scatter: nv < 1 returns
     GArray &a = arr(g_a);
     Runtime &r = rt();
-    const int size = a.elemsize;
-    std::vector<int> proc(nv);
-    std::vector<long> off(nv);
+    const int size = a.elemsize, nd = a.ndim;
+    static std::vector<int> s_proc;
+    static std::vector<long> s_off;
+    static std::vector<void *> s_loc, s_rem;
+    int *proc = grow(s_proc, (size_t)nv);
+    long *off = grow(s_off, (size_t)nv);
+    // every owner's block: first index and extents (gam_Loc_ptr's column-major offset)
+    std::vector<long> blo((size_t)a.nproc_grid * nd), ext((size_t)a.nproc_grid * nd);
+    for (int p = 0; p < a.nproc_grid; ++p) {
+        long lo[GA_MAX_DIM], hi[GA_MAX_DIM];
+        block_elems(a, p, lo, hi);
+        for (int d = 0; d < nd; ++d) {
+            blo[(size_t)p * nd + d] = lo[d];
+            ext[(size_t)p * nd + d] = hi[d] - lo[d] + 1;
+        }
+    }
     std::vector<long> nelem(r.size, 0);
     for (long k = 0; k < nv; k++) {
-        proc[k] = locate(a, fsub + k * a.ndim, &off[k]);
-        if (proc[k] < 0) fatal("gather/scatter: invalid subscript of element %ld", k);
-        nelem[proc[k]]++;
+        const long *sub = fsub + k * nd;
+        int pr = 0, mul = 1;
+        for (int d = 0; d < nd; d++) {   // locate(): the owner's block along each dimension
+            if (sub[d] < 1 || sub[d] > a.dims[d]) fatal("gather/scatter: invalid subscript of element %ld", k);
+            const std::vector<long> &m = a.map[d];
+            const int bi = (int)(std::upper_bound(m.begin(), m.end(), sub[d]) - m.begin()) - 1;
+            pr += bi * mul;
+            mul *= a.nblock[d];
+        }
+        long o = 0, f = 1;
+        const long *bl = &blo[(size_t)pr * nd], *ex = &ext[(size_t)pr * nd];
+        for (int d = 0; d < nd; d++) { o += (sub[d] - bl[d]) * f; f *= ex[d]; }
+        proc[k] = pr;
+        off[k] = o;
+        nelem[pr]++;
     }
     std::vector<long> first(r.size, 0), fill(r.size, 0);
     for (int p = 1; p < r.size; p++) first[p] = first[p - 1] + nelem[p - 1];
-    std::vector<void *> loc(nv), rem(nv);
+    void **loc = grow(s_loc, (size_t)nv), **rem = grow(s_rem, (size_t)nv);
     for (long k = 0; k < nv; k++) {
         const long j = first[proc[k]] + fill[proc[k]]++;
         loc[j] = (char *)v + (long)size * k;
@@ -693,30 +708,31 @@ void NGA_Release(int g_a, int lo[], int hi[]) { (void)arr(g_a); (void)lo; (void)
 void NGA_Release_update(int g_a, int lo[], int hi[]) { (void)arr(g_a); (void)lo; (void)hi; }
 
 // capi.c:3026-3160 (NGA_Scatter*, NGA_Gather*): C subscripts -> Fortran order, +1
-static std::vector<long> c2f_subs(int g_a, int *const *subs, const int *flat, int n) {
+static const long *c2f_subs(int g_a, int *const *subs, const int *flat, int n) {
     const int nd = arr(g_a).ndim;
-    std::vector<long> f((size_t)std::max(n, 0) * nd);
-    for (int k = 0; k < n; k++) c2f_index(nd, subs ? subs[k] : flat + (long)k * nd, &f[(size_t)k * nd]);
-    return f;
+    static std::vector<long> f;   // kept across calls (see gatscat)
+    long *out = grow(f, (size_t)std::max(n, 0) * nd + 1);
+    for (int k = 0; k < n; k++) c2f_index(nd, subs ? subs[k] : flat + (long)k * nd, out + (size_t)k * nd);
+    return out;
 }
 
 void NGA_Scatter(int g_a, void *v, int *subsArray[], int n) {
-    gatscat(GS_SCATTER, g_a, v, c2f_subs(g_a, subsArray, nullptr, n).data(), n, nullptr);
+    gatscat(GS_SCATTER, g_a, v, c2f_subs(g_a, subsArray, nullptr, n), n, nullptr);
 }
 void NGA_Scatter_flat(int g_a, void *v, int subsArray[], int n) {
-    gatscat(GS_SCATTER, g_a, v, c2f_subs(g_a, nullptr, subsArray, n).data(), n, nullptr);
+    gatscat(GS_SCATTER, g_a, v, c2f_subs(g_a, nullptr, subsArray, n), n, nullptr);
 }
 void NGA_Scatter_acc(int g_a, void *v, int *subsArray[], int n, void *alpha) {
-    gatscat(GS_SCATTER_ACC, g_a, v, c2f_subs(g_a, subsArray, nullptr, n).data(), n, alpha);
+    gatscat(GS_SCATTER_ACC, g_a, v, c2f_subs(g_a, subsArray, nullptr, n), n, alpha);
 }
 void NGA_Scatter_acc_flat(int g_a, void *v, int subsArray[], int n, void *alpha) {
-    gatscat(GS_SCATTER_ACC, g_a, v, c2f_subs(g_a, nullptr, subsArray, n).data(), n, alpha);
+    gatscat(GS_SCATTER_ACC, g_a, v, c2f_subs(g_a, nullptr, subsArray, n), n, alpha);
 }
 void NGA_Gather(int g_a, void *v, int *subsArray[], int n) {
-    gatscat(GS_GATHER, g_a, v, c2f_subs(g_a, subsArray, nullptr, n).data(), n, nullptr);
+    gatscat(GS_GATHER, g_a, v, c2f_subs(g_a, subsArray, nullptr, n), n, nullptr);
 }
 void NGA_Gather_flat(int g_a, void *v, int subsArray[], int n) {
-    gatscat(GS_GATHER, g_a, v, c2f_subs(g_a, nullptr, subsArray, n).data(), n, nullptr);
+    gatscat(GS_GATHER, g_a, v, c2f_subs(g_a, nullptr, subsArray, n), n, nullptr);
 }
 
 void GA_Get_proc_grid(int g_a, int dims[]) {

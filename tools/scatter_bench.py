@@ -35,8 +35,12 @@ def main():
     ap.add_argument("--src", default="dev", choices=["dev", "host"])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--ga", action="store_true",
+                    help="NGA_Scatter_acc_flat / NGA_Gather_flat of n elements of a 16384^2 f64 GA (host v)")
     args = ap.parse_args()
     L = ga_amd.lib()
+    if args.ga:
+        return ga_main(L, args)
     assert ga_amd.comex_init() == 0
     region = 1 << 30
     dstb = ga_amd.DeviceBuffer(region)
@@ -100,6 +104,37 @@ def main():
         if vb is not None:
             vb.free()
     ga_amd.comex_finalize()
+
+
+def ga_main(L, args):
+    """GA caller layer: gai_gatscat owner grouping (onesided.c:2747) -> one ARMCI_AccV /
+    ARMCI_GetV per owner (one owner here), subscripts and `v` in host memory."""
+    assert L.GA_Initialize() == 0
+    side = 16384
+    g = L.NGA_Create(1004, 2, ga_amd.int_array([side, side]), b"scat", None)
+    assert g > 0
+    L.GA_Zero(g)
+    rng = np.random.default_rng(3)
+    alpha = ctypes.c_double(ALPHA)
+    for n in [int(x) for x in args.pairs.split(",")]:
+        subs = rng.integers(0, side, 2 * n).astype(np.int32)
+        v = rng.random(n)
+        out = np.zeros(n)
+        sp = subs.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+        for name, fn in (("NGA_Scatter_acc_flat",
+                          lambda: L.NGA_Scatter_acc_flat(g, ctypes.c_void_p(v.ctypes.data), sp, n, ctypes.byref(alpha))),
+                         ("NGA_Gather_flat", lambda: L.NGA_Gather_flat(g, ctypes.c_void_p(out.ctypes.data), sp, n))):
+            fn()
+            ga_amd.sync()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                fn()
+            ga_amd.sync()
+            el = (time.perf_counter() - t0) / args.steps
+            print(json.dumps({"tool": "scatter_bench", "api": name, "elements": n, "ga": f"{side}^2 f64, 1 rank",
+                              "steps": args.steps, "ms_per_call": round(el * 1e3, 3),
+                              "Melems_per_s": round(n / el / 1e6, 2)}), flush=True)
+    L.GA_Terminate()
 
 
 if __name__ == "__main__":
