@@ -433,6 +433,21 @@ def run_cpu_baseline(workload, seconds, threads):
         rates[p] = round(3 * patch_bytes(count) * n / el / 2 ** 30, 3)
         notes.append(f"P={p}: {n} full {workload} steps in {el:.1f} s")
     P = max(rates)
+    # the progress-rank path (ACC_SMP=0): pack (comex.c:1267-1328) then
+    # unpack-accumulate (4238-4268) on one core -- the restatement (oracle), as comex.c
+    # itself is not built here; no MPI copy in between, so an upper bound for that path
+    packed = None
+    o.accs_packed(op, SCALE[op], src, 0, sstr, dst, 0, dstr, count, levels)   # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        o.accs_packed(op, SCALE[op], src, 0, sstr, dst, 0, dstr, count, levels)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds / (len(ps) + 1) and n >= 2) or n >= 10000:
+            break
+    packed = {"value": round(3 * patch_bytes(count) * n / el / 2 ** 30, 3), "unit": "GiB/s", "cores": 1,
+              "kind": "port", "sample": f"{n} full {workload} steps in {el:.1f} s: oracle pack + unpack-acc "
+                                        "(comex.c:1267-1328, 4238-4268), one core, no MPI transfer"}
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -444,6 +459,7 @@ def run_cpu_baseline(workload, seconds, threads):
         pass
     return {"value": rates[P], "unit": "GiB/s", "cores": P, "kind": kind, "single_core_value": rates[1],
             "by_workers": {str(k): v for k, v in sorted(rates.items())},
+            "packed_path_single_core": packed,
             "host": {"cpu": model, "nproc": os.cpu_count()},
             "sample": "; ".join(notes) + "; P host threads each on its own slab of the patch (outer level); "
                       + ("reference comex/src-common/acc.h _acc (HAVE_BLAS=0, gcc -O2) per row, "
