@@ -84,6 +84,8 @@ def main():
         test_vector_ref(L, rank, size)
     elif mode in ("scatremote", "scatremote-gloo"):
         scatter_remote_test(L, rank, size)
+    elif mode == "ngags":
+        ngatest_gs(L, rank, size)
     elif mode == "armciacc":
         armci_test_acc_ref(L, rank, size)
     elif mode == "garef":
@@ -1327,6 +1329,68 @@ def scatter_remote_test(L, rank, size):
     assert ga_amd.comex_free(seg[rank]) == 0
     say(rank, "remote scatter-acc ok")
     ga_amd.comex_finalize()
+
+
+
+# ---------------------------------------------------------------------------
+# ngatest_src/ndim_NGA_SCATTER_ACC.src and ndim_NGA_GATHER.src restated (C API,
+# row-major subscripts): for ndim 1..7, every rank draws m = total/100 distinct
+# random elements from its own slice of the linear index space (me*total/nproc
+# onwards, so the slices of different ranks never collide but cross owner
+# blocks), scatter-accumulates random values with alpha = rand(me*2+1), and
+# checks every element against v*alpha + (value before) read back with
+# NGA_Get (reference 1e-5; exact here); then gathers the same elements and
+# compares with single-element gets.  int, double, double complex.
+def ngatest_gs(L, rank, size):
+    ia = ga_amd_int_array()
+    P = ctypes.c_void_p
+    assert L.GA_Initialize() == 0
+    n_of = {1: 2000, 2: 100, 3: 20, 4: 10, 5: 5, 6: 4, 7: 3}
+    rng = np.random.default_rng(300 + rank)
+    for t in (1001, 1004, 1007):
+        dt = GA_TYPES[t]
+        for ndim in range(1, 8):
+            dims = [n_of[ndim]] * ndim
+            total = int(np.prod(dims))
+            g = L.NGA_Create(t, ndim, ia(dims), b"a", None)
+            assert g > 0
+            L.GA_Zero(g)
+            m = max(1, total // 100)
+            lo_i, span = rank * total // size, max(1, total // size)
+            alpha = {1001: rank * 2 + 1, 1004: 0.25 + 0.5 * rank, 1007: complex(0.5, 0.25 * rank - 0.5)}[t]
+            for loop in range(3):
+                L.GA_Sync()
+                lin = lo_i + rng.choice(min(span, total - lo_i), size=min(m, span), replace=False)
+                k = len(lin)
+                subs = np.array(np.unravel_index(lin, dims)).T.astype(np.int32).copy()   # k x ndim, C order
+                if t == 1001:
+                    v = rng.integers(-50, 50, k).astype(np.int32)
+                else:
+                    v = (rng.random(k) * 2 - 1).astype(dt)
+                    if t == 1007:
+                        v = v + 1j * (rng.random(k) - 0.5)
+                before = np.zeros(k, dtype=dt)
+                for i in range(k):
+                    sub = ia(subs[i].tolist())
+                    L.NGA_Get(g, sub, sub, P(before.ctypes.data + i * before.itemsize), ia([1] * (ndim - 1)))
+                want = acc_expect(before, v, alpha)
+                L.GA_Sync()
+                al = typed_scalar(t, alpha)
+                L.NGA_Scatter_acc_flat(g, P(v.ctypes.data), subs.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), k,
+                                       ctypes.byref(al))
+                L.GA_Sync()
+                after = np.zeros(k, dtype=dt)
+                for i in range(k):
+                    sub = ia(subs[i].tolist())
+                    L.NGA_Get(g, sub, sub, P(after.ctypes.data + i * after.itemsize), ia([1] * (ndim - 1)))
+                assert np.array_equal(after, want), ("NGA_SCATTER_ACC", t, ndim, loop)
+                gat = np.zeros(k, dtype=dt)
+                L.NGA_Gather_flat(g, P(gat.ctypes.data), subs.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), k)
+                assert np.array_equal(gat, after), ("NGA_GATHER", t, ndim, loop)
+            L.GA_Sync()
+            L.GA_Destroy(g)
+    say(rank, "ndim_NGA_SCATTER_ACC / ndim_NGA_GATHER (int, dbl, dcpl; ndim 1..7) ok")
+    L.GA_Terminate()
 
 
 if __name__ == "__main__":

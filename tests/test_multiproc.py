@@ -183,3 +183,12 @@ def test_remote_scatter_acc_large(mode, n, nodes):
     are gathered into one upload; bit-exact against each source's pairs replayed in
     order.  nodes [0,0,1] sends the third rank's traffic over the wire protocol."""
     launch(mode, n=n, timeout=150, nodes=nodes)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 3])
+def test_ga_ndim_scatter_acc_gather_restated(n):
+    """global/testing/ngatest_src/ndim_NGA_SCATTER_ACC.src + ndim_NGA_GATHER.src:
+    distinct random elements per rank (crossing owner blocks), scatter-acc then
+    per-element get, gather vs get; ndim 1..7, int/double/double complex, exact."""
+    launch("ngags", n=n, timeout=150)
