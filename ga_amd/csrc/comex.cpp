@@ -936,6 +936,14 @@ struct ViewCache {
         }
         return true;
     }
+    // one allocation holding every byte of [lo, hi): its (uniform) device-view offset
+    bool span(uint64_t lo, uint64_t hi, int64_t *delta) {
+        uint64_t d = 0;
+        if (!view((void *)(uintptr_t)lo, 1, &d)) return false;
+        for (const Range &x : r)
+            if (lo >= x.lo && hi <= x.hi) { *delta = x.delta; return true; }
+        return false;
+    }
 };
 
 // host-side packing of pageable io-vector runs, in pair order (fixed-size copies
@@ -974,7 +982,8 @@ constexpr int kIovRunsMin = 4096;
 // scatters them).  Reference: nb_accv / nb_putv / nb_getv to a self/SMP target,
 // comex.c:7327-7400 (one _acc / memcpy per pair, in order).
 static void iov_local(int cop, const void *scale, const uint64_t *src, const uint64_t *dst, int bytes, int n,
-                      const char *host_src = nullptr, char *host_dst = nullptr) {
+                      const char *host_src = nullptr, char *host_dst = nullptr, int64_t sdelta = 0,
+                      int64_t ddelta = 0) {
     Runtime &r = rt();
     const bool src_listed = src != nullptr, dst_listed = dst != nullptr;
     // device scratch: [dst list | src list or packed sources | packed results | run-sort work],
@@ -990,7 +999,7 @@ static void iov_local(int cop, const void *scale, const uint64_t *src, const uin
     if (src_listed) {
         uint64_t *u = (uint64_t *)(up + o_src), o = 0, lo = ~0ull, hi = 0;
         for (int i = 0; i < n; ++i) {
-            const uint64_t a = src[i];
+            const uint64_t a = src[i] + (uint64_t)sdelta;
             u[i] = a;
             o |= a;
             lo = a < lo ? a : lo;
@@ -1005,7 +1014,7 @@ static void iov_local(int cop, const void *scale, const uint64_t *src, const uin
     if (dst_listed) {
         uint64_t *u = (uint64_t *)(up + o_dst), o = 0, lo = ~0ull, hi = 0;
         for (int i = 0; i < n; ++i) {
-            const uint64_t a = dst[i];
+            const uint64_t a = dst[i] + (uint64_t)ddelta;
             u[i] = a;
             o |= a;
             lo = a < lo ? a : lo;
@@ -1015,6 +1024,9 @@ static void iov_local(int cop, const void *scale, const uint64_t *src, const uin
         dlo = lo;
         dhi = hi + (uint64_t)bytes;
     }
+    // from here on the lists are the translated (device-view) copies in the staging
+    if (src_listed) src = (const uint64_t *)(up + o_src);
+    if (dst_listed) dst = (const uint64_t *)(up + o_dst);
     bool serial = false, runs = false;
     if (dst_listed) {
         // a source inside a destination: the reference order matters across pairs
@@ -1132,6 +1144,24 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             continue;
         }
         ViewCache vc;
+        if (world == r.rank && n >= 1024) {
+            // fast path: each side's addresses all inside one device-accessible allocation
+            // (GA's `v` buffer and array block): one range lookup per side, the lists go to
+            // the staging translated in the same pass that takes their spans
+            const uint64_t *rs = (const uint64_t *)darr[k].src, *rd = (const uint64_t *)darr[k].dst;
+            uint64_t smin = ~0ull, smax = 0, dmin = ~0ull, dmax = 0;
+            for (int i = 0; i < n; ++i) {
+                smin = rs[i] < smin ? rs[i] : smin;
+                smax = rs[i] > smax ? rs[i] : smax;
+                dmin = rd[i] < dmin ? rd[i] : dmin;
+                dmax = rd[i] > dmax ? rd[i] : dmax;
+            }
+            int64_t sdel = 0, ddel = 0;
+            if (vc.span(smin, smax + (uint64_t)bytes, &sdel) && vc.span(dmin, dmax + (uint64_t)bytes, &ddel)) {
+                iov_local(cop, scale, rs, rd, bytes, n, nullptr, nullptr, sdel, ddel);
+                continue;
+            }
+        }
         bool src_host = false, dst_host = false;   // a whole side in pageable host memory
         for (int i = 0; i < n && !host_bounce; ++i) {
             void *sp = darr[k].src[i], *dp = darr[k].dst[i];
