@@ -131,6 +131,10 @@ def cases():
     # (_acc processes bytes/sizeof(T) elements, acc.h:122)
     c = array_case("dbl_partial_elem", DBL, [10, 4], [12], [12])
     c["count"][0] = 10 * 8 + 5
+    # the buffers must hold the partial bytes too: pack/unpack/put/get move all
+    # count[0] bytes of every row (comex.c:1308-1325), only _acc stops at whole elements
+    c["src_bytes"] = c["src_off"] + span(c["src_stride"], c["count"], 1)[1]
+    c["dst_bytes"] = c["dst_off"] + span(c["dst_stride"], c["count"], 1)[1]
     out.append(c)
     # overlapping destination rows: reference order decides the result
     c = array_case("dbl_overlap_dst_rows", DBL, [6, 5], [8], [8])

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Host-side AddressSanitizer + UBSan run of the CPU test suite (no GPU; GPU
+# sanitizers are not available on the pool).  The g++ host objects of
+# libga_amd.so (comex, armci, ga, sched, bootstrap, wire) are rebuilt with
+# -fsanitize=address,undefined in a scratch tree, swapped in for the duration
+# of the run, and the in-tree library is restored afterwards.  The hipcc
+# objects stay uninstrumented (one ASan runtime per process: gcc's).
+#
+#   bash tools/host_sanitize.sh            # reports to /tmp/gaamd_asan/*.log
+set -euo pipefail
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+W=/tmp/gaamd_asan
+rm -rf "$W" && mkdir -p "$W/pkg"
+cp -r "$ROOT/include" "$W/" && cp -r "$ROOT/ga_amd/csrc" "$W/pkg/"
+rm -f "$W"/pkg/csrc/*.o
+make -s -C "$W/pkg/csrc" -j8 OUT="$W/libga_amd_asan.so" \
+  CXXFLAGS="-O1 -g -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -fsanitize=address,undefined -fno-omit-frame-pointer"
+cp "$ROOT/ga_amd/libga_amd.so" "$W/libga_amd.real.so"
+trap 'cp "$W/libga_amd.real.so" "$ROOT/ga_amd/libga_amd.so"' EXIT
+cp "$W/libga_amd_asan.so" "$ROOT/ga_amd/libga_amd.so"
+GCCLIB=$(dirname "$(gcc -print-file-name=libasan.so)")
+cd "$ROOT"
+# test_c_client_compiles_and_links links a plain C program against the library,
+# which an instrumented build cannot satisfy without the sanitizer runtimes
+LD_PRELOAD="$GCCLIB/libasan.so $GCCLIB/libubsan.so" \
+ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0:log_path=$W/asan \
+UBSAN_OPTIONS=print_stacktrace=1:log_path=$W/ubsan \
+  python -m pytest tests -q -m "not gpu" -p no:cacheprovider \
+    --deselect tests/test_abi.py::test_c_client_compiles_and_links
+if ls "$W"/asan* "$W"/ubsan* >/dev/null 2>&1; then
+  echo "sanitizer reports:"; ls "$W"/asan* "$W"/ubsan* 2>/dev/null; exit 1
+fi
+echo "host sanitizers: clean"
