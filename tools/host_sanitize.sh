@@ -22,7 +22,7 @@ GCCLIB=$(dirname "$(gcc -print-file-name=libasan.so)")
 cd "$ROOT"
 # test_c_client_compiles_and_links links a plain C program against the library,
 # which an instrumented build cannot satisfy without the sanitizer runtimes
-LD_PRELOAD="$GCCLIB/libasan.so $GCCLIB/libubsan.so" \
+LD_PRELOAD="$GCCLIB/libasan.so $GCCLIB/libubsan.so${LD_PRELOAD:+ $LD_PRELOAD}" \
 ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0:log_path=$W/asan \
 UBSAN_OPTIONS=print_stacktrace=1:log_path=$W/ubsan \
   python -m pytest tests -q -m "not gpu" -p no:cacheprovider \
