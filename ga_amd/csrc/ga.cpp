@@ -20,8 +20,11 @@
 #include "../../include/comex.h"
 #include "runtime.hpp"
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <functional>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -406,7 +409,56 @@ template <class T> static T *grow(std::vector<T> &v, size_t n) {
     return v.data();
 }
 
-static void gatscat(GatScat op, int g_a, void *v, const long *fsub, long nv, void *alpha) {
+// Subscripts arrive in C order (capi.c:3026-3160: row-major, 0-based, as an
+// array of pointers or one flat array); they are read in place, reversed and
+// made 1-based per element rather than copied into a Fortran array first.
+// Locating owners and grouping the pairs is a stable counting sort by owner,
+// split over host threads for large calls: every thread locates a contiguous
+// range of elements and counts per owner, the counts are prefix-summed owner
+// by owner in thread order, and every thread writes its range's pairs at its
+// own offsets -- owners ascending, input order within an owner, as with one
+// thread.
+static int gs_threads() {
+    static const int n = [] {
+        const char *e = getenv("COMEX_AMD_GS_THREADS");
+        const int v = e ? atoi(e) : 8;
+        return v < 1 ? 1 : (v > 64 ? 64 : v);
+    }();
+    return n;
+}
+
+struct GsCtx {
+    const GArray *a;
+    int *const *csubs;
+    const int *cflat;
+    const long *blo, *ext;   // every owner's block: first index and extents
+    char *v;
+    int size;
+};
+
+static inline void gs_locate(const GsCtx &c, long k, int *pr_out, long *off_out) {
+    const GArray &a = *c.a;
+    const int nd = a.ndim;
+    const int *cs = c.csubs ? c.csubs[k] : c.cflat + k * nd;
+    long sub[GA_MAX_DIM];
+    int pr = 0, mul = 1;
+    for (int d = 0; d < nd; d++) {   // locate(): the owner's block along each dimension
+        sub[d] = (long)cs[nd - 1 - d] + 1;
+        if (sub[d] < 1 || sub[d] > a.dims[d]) fatal("gather/scatter: invalid subscript of element %ld", k);
+        if (a.nblock[d] > 1) {
+            const std::vector<long> &m = a.map[d];
+            pr += (int)(std::upper_bound(m.begin(), m.end(), sub[d]) - m.begin() - 1) * mul;
+        }
+        mul *= a.nblock[d];
+    }
+    long o = 0, f = 1;
+    const long *bl = c.blo + (size_t)pr * nd, *ex = c.ext + (size_t)pr * nd;
+    for (int d = 0; d < nd; d++) { o += (sub[d] - bl[d]) * f; f *= ex[d]; }
+    *pr_out = pr;
+    *off_out = o;
+}
+
+static void gatscat(GatScat op, int g_a, void *v, int *const *csubs, const int *cflat, long nv, void *alpha) {
     if (nv < 1) return;   // pnga_gather / pnga_scatter: nv < 1 returns
     GArray &a = arr(g_a);
     Runtime &r = rt();
@@ -416,7 +468,6 @@ static void gatscat(GatScat op, int g_a, void *v, const long *fsub, long nv, voi
     static std::vector<void *> s_loc, s_rem;
     int *proc = grow(s_proc, (size_t)nv);
     long *off = grow(s_off, (size_t)nv);
-    // every owner's block: first index and extents (gam_Loc_ptr's column-major offset)
     std::vector<long> blo((size_t)a.nproc_grid * nd), ext((size_t)a.nproc_grid * nd);
     for (int p = 0; p < a.nproc_grid; ++p) {
         long lo[GA_MAX_DIM], hi[GA_MAX_DIM];
@@ -426,32 +477,54 @@ static void gatscat(GatScat op, int g_a, void *v, const long *fsub, long nv, voi
             ext[(size_t)p * nd + d] = hi[d] - lo[d] + 1;
         }
     }
-    std::vector<long> nelem(r.size, 0);
-    for (long k = 0; k < nv; k++) {
-        const long *sub = fsub + k * nd;
-        int pr = 0, mul = 1;
-        for (int d = 0; d < nd; d++) {   // locate(): the owner's block along each dimension
-            if (sub[d] < 1 || sub[d] > a.dims[d]) fatal("gather/scatter: invalid subscript of element %ld", k);
-            const std::vector<long> &m = a.map[d];
-            const int bi = (int)(std::upper_bound(m.begin(), m.end(), sub[d]) - m.begin()) - 1;
-            pr += bi * mul;
-            mul *= a.nblock[d];
-        }
-        long o = 0, f = 1;
-        const long *bl = &blo[(size_t)pr * nd], *ex = &ext[(size_t)pr * nd];
-        for (int d = 0; d < nd; d++) { o += (sub[d] - bl[d]) * f; f *= ex[d]; }
-        proc[k] = pr;
-        off[k] = o;
-        nelem[pr]++;
-    }
-    std::vector<long> first(r.size, 0), fill(r.size, 0);
-    for (int p = 1; p < r.size; p++) first[p] = first[p - 1] + nelem[p - 1];
+    const GsCtx c{&a, csubs, cflat, blo.data(), ext.data(), (char *)v, size};
     void **loc = grow(s_loc, (size_t)nv), **rem = grow(s_rem, (size_t)nv);
-    for (long k = 0; k < nv; k++) {
-        const long j = first[proc[k]] + fill[proc[k]]++;
-        loc[j] = (char *)v + (long)size * k;
-        rem[j] = (char *)a.ptr[proc[k]] + (long)size * off[k];
+    const int P = r.size;
+    // one thread per 128 Ki elements, at most gs_threads() (COMEX_AMD_GS_THREADS, default 8)
+    const int T = (int)std::max(1L, std::min<long>(gs_threads(), nv >> 17));
+    std::vector<long> cnt((size_t)T * P, 0);   // cnt[t*P + p]: elements of thread t owned by p
+    auto range = [&](int t, long *k0, long *k1) { *k0 = nv * t / T; *k1 = nv * (t + 1) / T; };
+    auto locate = [&](int t) {
+        long k0, k1;
+        range(t, &k0, &k1);
+        std::vector<long> ct(P, 0);   // thread-local: neighbours' counters share cache lines
+        for (long k = k0; k < k1; k++) {
+            gs_locate(c, k, &proc[k], &off[k]);
+            ct[proc[k]]++;
+        }
+        std::copy(ct.begin(), ct.end(), &cnt[(size_t)t * P]);
+    };
+    std::vector<long> pos((size_t)T * P);      // pos[t*P + p]: next slot of thread t's owner-p pairs
+    auto place = [&](int t) {
+        long k0, k1;
+        range(t, &k0, &k1);
+        std::vector<long> pt(&pos[(size_t)t * P], &pos[(size_t)t * P] + P);
+        for (long k = k0; k < k1; k++) {
+            const long j = pt[proc[k]]++;
+            loc[j] = c.v + (long)size * k;
+            rem[j] = (char *)a.ptr[proc[k]] + (long)size * off[k];
+        }
+    };
+    auto run = [&](const std::function<void(int)> &fn) {
+        if (T == 1) { fn(0); return; }
+        std::vector<std::thread> th;
+        th.reserve(T - 1);
+        for (int t = 1; t < T; t++) th.emplace_back(fn, t);
+        fn(0);
+        for (std::thread &x : th) x.join();
+    };
+    run(locate);
+    std::vector<long> nelem(P, 0), first(P, 0);
+    long acc = 0;
+    for (int p = 0; p < P; p++) {
+        first[p] = acc;
+        for (int t = 0; t < T; t++) {
+            pos[(size_t)t * P + p] = acc;
+            acc += cnt[(size_t)t * P + p];
+        }
+        nelem[p] = acc - first[p];
     }
+    run(place);
     double &tot = op == GS_GATHER ? g_stat.gattot : g_stat.scatot;
     double &lcl = op == GS_GATHER ? g_stat.gatloc : g_stat.scaloc;
     (op == GS_GATHER ? g_stat.numgat : g_stat.numsca)++;
@@ -707,32 +780,24 @@ void NGA_Access(int g_a, int lo[], int hi[], void *ptr, int ld[]) {
 void NGA_Release(int g_a, int lo[], int hi[]) { (void)arr(g_a); (void)lo; (void)hi; }
 void NGA_Release_update(int g_a, int lo[], int hi[]) { (void)arr(g_a); (void)lo; (void)hi; }
 
-// capi.c:3026-3160 (NGA_Scatter*, NGA_Gather*): C subscripts -> Fortran order, +1
-static const long *c2f_subs(int g_a, int *const *subs, const int *flat, int n) {
-    const int nd = arr(g_a).ndim;
-    static std::vector<long> f;   // kept across calls (see gatscat)
-    long *out = grow(f, (size_t)std::max(n, 0) * nd + 1);
-    for (int k = 0; k < n; k++) c2f_index(nd, subs ? subs[k] : flat + (long)k * nd, out + (size_t)k * nd);
-    return out;
-}
-
+// capi.c:3026-3160 (NGA_Scatter*, NGA_Gather*): C subscripts, converted per element in gatscat
 void NGA_Scatter(int g_a, void *v, int *subsArray[], int n) {
-    gatscat(GS_SCATTER, g_a, v, c2f_subs(g_a, subsArray, nullptr, n), n, nullptr);
+    gatscat(GS_SCATTER, g_a, v, subsArray, nullptr, n, nullptr);
 }
 void NGA_Scatter_flat(int g_a, void *v, int subsArray[], int n) {
-    gatscat(GS_SCATTER, g_a, v, c2f_subs(g_a, nullptr, subsArray, n), n, nullptr);
+    gatscat(GS_SCATTER, g_a, v, nullptr, subsArray, n, nullptr);
 }
 void NGA_Scatter_acc(int g_a, void *v, int *subsArray[], int n, void *alpha) {
-    gatscat(GS_SCATTER_ACC, g_a, v, c2f_subs(g_a, subsArray, nullptr, n), n, alpha);
+    gatscat(GS_SCATTER_ACC, g_a, v, subsArray, nullptr, n, alpha);
 }
 void NGA_Scatter_acc_flat(int g_a, void *v, int subsArray[], int n, void *alpha) {
-    gatscat(GS_SCATTER_ACC, g_a, v, c2f_subs(g_a, nullptr, subsArray, n), n, alpha);
+    gatscat(GS_SCATTER_ACC, g_a, v, nullptr, subsArray, n, alpha);
 }
 void NGA_Gather(int g_a, void *v, int *subsArray[], int n) {
-    gatscat(GS_GATHER, g_a, v, c2f_subs(g_a, subsArray, nullptr, n), n, nullptr);
+    gatscat(GS_GATHER, g_a, v, subsArray, nullptr, n, nullptr);
 }
 void NGA_Gather_flat(int g_a, void *v, int subsArray[], int n) {
-    gatscat(GS_GATHER, g_a, v, c2f_subs(g_a, nullptr, subsArray, n), n, nullptr);
+    gatscat(GS_GATHER, g_a, v, nullptr, subsArray, n, nullptr);
 }
 
 void GA_Get_proc_grid(int g_a, int dims[]) {

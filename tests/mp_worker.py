@@ -477,6 +477,31 @@ def ga_test(L, rank, size):
     assert np.array_equal(full, want), "NGA_Scatter"
     L.GA_Sync()
     say(rank, "ga sync 10")
+    # large calls: owners located and pairs grouped by several host threads
+    # (one per 128 Ki elements); rank 0 alone, 1 Mi non-integer values onto the
+    # 60 000 elements of every owner (~17 repeats each) -> bit-exact against
+    # the sequential mul-then-add order (np.add.at applies repeats in order)
+    L.GA_Zero(g)
+    if rank == 0:
+        nbig = 1 << 20
+        rb = np.random.default_rng(91)
+        bsub = np.stack([rb.integers(0, dims[0], nbig), rb.integers(0, dims[1], nbig)], axis=1).astype(np.int32)
+        bv = rb.standard_normal(nbig) * 1e3
+        alpha = 0.7071067811865476
+        L.NGA_Scatter_acc_flat(g, bv.ctypes.data_as(ctypes.c_void_p),
+                               bsub.ravel().ctypes.data_as(ctypes.POINTER(ctypes.c_int)), nbig,
+                               ctypes.byref(ctypes.c_double(alpha)))
+        wb = np.zeros(dims)
+        np.add.at(wb, (bsub[:, 0], bsub[:, 1]), bv * alpha)
+        L.NGA_Get(g, ia([0, 0]), ia([dims[0] - 1, dims[1] - 1]), full.ctypes.data_as(ctypes.c_void_p),
+                  ia([dims[1]]))
+        assert np.array_equal(full.view(np.int64), wb.view(np.int64)), "large NGA_Scatter_acc_flat"
+        gb = np.zeros(nbig)
+        L.NGA_Gather_flat(g, gb.ctypes.data_as(ctypes.c_void_p),
+                          bsub.ravel().ctypes.data_as(ctypes.POINTER(ctypes.c_int)), nbig)
+        assert np.array_equal(gb.view(np.int64), wb[bsub[:, 0], bsub[:, 1]].view(np.int64)), "large NGA_Gather_flat"
+    L.GA_Sync()
+    say(rank, "ga sync 10b")
 
     # local block through NGA_Access is an HBM address
     lo_m, hi_m = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
