@@ -946,6 +946,62 @@ struct ViewCache {
     }
 };
 
+// Host passes over io-vector lists (tens of MiB at GA scatter sizes) split into
+// contiguous ranges over a few threads: fn(t, i0, i1) for t < T, T = one thread
+// per 256 Ki pairs, at most 8.  Each range's results are combined by the caller
+// in range order, so the outcome does not depend on T.
+static int par_threads(long n) {
+    static const long cap = [] {   // COMEX_AMD_HOST_THREADS: at most this many (1..8, default 8)
+        const char *e = getenv("COMEX_AMD_HOST_THREADS");
+        const long v = e ? atol(e) : 8;
+        return v < 1 ? 1L : (v > 8 ? 8L : v);
+    }();
+    return (int)std::max(1L, std::min(cap, n >> 18));
+}
+template <class F> static void par_for(long n, int T, F fn) {
+    if (T <= 1) { fn(0, 0L, n); return; }
+    std::vector<std::thread> th;
+    th.reserve((size_t)T - 1);
+    for (int t = 1; t < T; ++t) th.emplace_back([&, t] { fn(t, n * t / T, n * (t + 1) / T); });
+    fn(0, 0L, n / T);
+    for (std::thread &x : th) x.join();
+}
+
+// Is every byte of [lo, hi) ordinary CPU memory of this process (one readable,
+// and if `write` writable, mapping that is not a device file)?  One lookup in
+// /proc/self/maps replaces a device-view query per page when a whole io-vector
+// side lies in pageable host memory (GA's MA buffer `v` of a scatter/gather):
+// device allocations are either PROT_NONE reservations or /dev/dri mappings, so
+// a side that passes is safe to gather/scatter on the host.  Any address not
+// covered (or a line that does not parse) answers false and the per-pair
+// classification decides as before.  COMEX_AMD_IOV_MAPS=0 disables it.
+static bool host_cpu_range(uint64_t lo, uint64_t hi, bool write) {
+    static const bool on = [] {
+        const char *e = getenv("COMEX_AMD_IOV_MAPS");
+        return !(e && atoi(e) == 0);
+    }();
+    if (!on || hi <= lo) return false;
+    FILE *f = fopen("/proc/self/maps", "r");
+    if (!f) return false;
+    char line[512];
+    bool ok = false;
+    while (fgets(line, sizeof(line), f)) {
+        const bool whole = strchr(line, '\n') != nullptr;
+        unsigned long long a = 0, b = 0;
+        char perms[8] = {0};
+        int path_at = 0;
+        if (sscanf(line, "%llx-%llx %7s %*s %*s %*s %n", &a, &b, perms, &path_at) < 3) break;
+        if (lo >= a && lo < b) {
+            const char *path = path_at > 0 ? line + path_at : "";
+            ok = hi <= b && perms[0] == 'r' && (!write || perms[1] == 'w') && strncmp(path, "/dev/", 5) != 0;
+            break;
+        }
+        while (!whole && fgets(line, sizeof(line), f) && !strchr(line, '\n')) {}   // rest of a long line
+    }
+    fclose(f);
+    return ok;
+}
+
 // host-side packing of pageable io-vector runs, in pair order (fixed-size copies
 // for the element sizes GA scatters, so the compiler emits plain loads/stores)
 template <int B> static void gather_fixed(char *out, void *const *p, int n) {
@@ -974,6 +1030,8 @@ static void scatter_runs(void *const *p, const char *in, int n, int bytes) {
 // io-vector pairs from this many up use the GPU-sorted run kernel (launch_iov_runs)
 // instead of a host-side overlap check
 constexpr int kIovRunsMin = 4096;
+// io-vectors from this many pairs try the whole-side host test (host_cpu_range)
+constexpr int kIovMapsMin = 65536;
 
 // One descriptor on this GPU.  `src` lists device addresses, or is empty when
 // `host_src` holds the n source runs packed on the host (gathered from pageable
@@ -983,7 +1041,7 @@ constexpr int kIovRunsMin = 4096;
 // comex.c:7327-7400 (one _acc / memcpy per pair, in order).
 static void iov_local(int cop, const void *scale, const uint64_t *src, const uint64_t *dst, int bytes, int n,
                       const char *host_src = nullptr, char *host_dst = nullptr, int64_t sdelta = 0,
-                      int64_t ddelta = 0) {
+                      int64_t ddelta = 0, void *const *gather_src = nullptr) {
     Runtime &r = rt();
     const bool src_listed = src != nullptr, dst_listed = dst != nullptr;
     // device scratch: [dst list | src list or packed sources | packed results | run-sort work],
@@ -996,33 +1054,44 @@ static void iov_local(int cop, const void *scale, const uint64_t *src, const uin
     sched_sync_all();   // the previous io-vector kernel and its upload are done with both scratches
     char *up = iov_host_scratch(o_res);
     uint64_t align_or = 0, slo = ~0ull, shi = 0, dlo = ~0ull, dhi = 0;
-    if (src_listed) {
-        uint64_t *u = (uint64_t *)(up + o_src), o = 0, lo = ~0ull, hi = 0;
-        for (int i = 0; i < n; ++i) {
-            const uint64_t a = src[i] + (uint64_t)sdelta;
-            u[i] = a;
-            o |= a;
-            lo = a < lo ? a : lo;
-            hi = a > hi ? a : hi;
+    // translate a list into the staging, taking its OR / min / max (per range, then combined)
+    auto translate = [&](const uint64_t *in, int64_t delta, uint64_t *u, uint64_t *lo_out, uint64_t *hi_out) {
+        const int T = par_threads(n);
+        uint64_t o[8] = {0}, lo[8], hi[8] = {0};
+        for (int t = 0; t < 8; ++t) lo[t] = ~0ull;
+        par_for(n, T, [&](int t, long i0, long i1) {
+            uint64_t ot = 0, lt = ~0ull, ht = 0;
+            for (long i = i0; i < i1; ++i) {
+                const uint64_t a = in[i] + (uint64_t)delta;
+                u[i] = a;
+                ot |= a;
+                lt = a < lt ? a : lt;
+                ht = a > ht ? a : ht;
+            }
+            o[t] = ot;
+            lo[t] = lt;
+            hi[t] = ht;
+        });
+        for (int t = 0; t < T; ++t) {
+            align_or |= o[t];
+            *lo_out = std::min(*lo_out, lo[t]);
+            *hi_out = std::max(*hi_out, hi[t]);
         }
-        align_or |= o;
-        slo = lo;
-        shi = hi + (uint64_t)bytes;
+    };
+    if (src_listed) {
+        translate(src, sdelta, (uint64_t *)(up + o_src), &slo, &shi);
+        shi += (uint64_t)bytes;
+    } else if (gather_src) {
+        // pageable sources gathered straight into the pinned staging, in pair order, on
+        // one thread: split over 8 threads it measured no faster on the boxes' shared
+        // host cores (profiles/r01/iov_host_threads.jsonl)
+        gather_runs(up + o_src, gather_src, n, bytes);
     } else {
         memcpy(up + o_src, host_src, (size_t)n * (size_t)bytes);
     }
     if (dst_listed) {
-        uint64_t *u = (uint64_t *)(up + o_dst), o = 0, lo = ~0ull, hi = 0;
-        for (int i = 0; i < n; ++i) {
-            const uint64_t a = dst[i] + (uint64_t)ddelta;
-            u[i] = a;
-            o |= a;
-            lo = a < lo ? a : lo;
-            hi = a > hi ? a : hi;
-        }
-        align_or |= o;
-        dlo = lo;
-        dhi = hi + (uint64_t)bytes;
+        translate(dst, ddelta, (uint64_t *)(up + o_dst), &dlo, &dhi);
+        dhi += (uint64_t)bytes;
     }
     // from here on the lists are the translated (device-view) copies in the staging
     if (src_listed) src = (const uint64_t *)(up + o_src);
@@ -1150,15 +1219,45 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             // the staging translated in the same pass that takes their spans
             const uint64_t *rs = (const uint64_t *)darr[k].src, *rd = (const uint64_t *)darr[k].dst;
             uint64_t smin = ~0ull, smax = 0, dmin = ~0ull, dmax = 0;
-            for (int i = 0; i < n; ++i) {
-                smin = rs[i] < smin ? rs[i] : smin;
-                smax = rs[i] > smax ? rs[i] : smax;
-                dmin = rd[i] < dmin ? rd[i] : dmin;
-                dmax = rd[i] > dmax ? rd[i] : dmax;
+            {
+                const int T = par_threads(n);
+                uint64_t mm[8][4];
+                par_for(n, T, [&](int t, long i0, long i1) {
+                    uint64_t a0 = ~0ull, a1 = 0, b0 = ~0ull, b1 = 0;
+                    for (long i = i0; i < i1; ++i) {
+                        a0 = rs[i] < a0 ? rs[i] : a0;
+                        a1 = rs[i] > a1 ? rs[i] : a1;
+                        b0 = rd[i] < b0 ? rd[i] : b0;
+                        b1 = rd[i] > b1 ? rd[i] : b1;
+                    }
+                    mm[t][0] = a0; mm[t][1] = a1; mm[t][2] = b0; mm[t][3] = b1;
+                });
+                for (int t = 0; t < T; ++t) {
+                    smin = std::min(smin, mm[t][0]);
+                    smax = std::max(smax, mm[t][1]);
+                    dmin = std::min(dmin, mm[t][2]);
+                    dmax = std::max(dmax, mm[t][3]);
+                }
             }
             int64_t sdel = 0, ddel = 0;
-            if (vc.span(smin, smax + (uint64_t)bytes, &sdel) && vc.span(dmin, dmax + (uint64_t)bytes, &ddel)) {
+            const bool sdev = vc.span(smin, smax + (uint64_t)bytes, &sdel);
+            const bool ddev = vc.span(dmin, dmax + (uint64_t)bytes, &ddel);
+            if (sdev && ddev) {
                 iov_local(cop, scale, rs, rd, bytes, n, nullptr, nullptr, sdel, ddel);
+                continue;
+            }
+            // one side wholly in pageable host memory (GA's `v`): packed on the host in
+            // pair order, as the per-pair classification below would, without it
+            if (n >= kIovMapsMin && ddev && !sdev && host_cpu_range(smin, smax + (uint64_t)bytes, false)) {
+                iov_local(cop, scale, nullptr, rd, bytes, n, nullptr, nullptr, 0, ddel, darr[k].src);
+                continue;
+            }
+            if (n >= kIovMapsMin && sdev && !ddev && cop == kOpCopy &&
+                host_cpu_range(dmin, dmax + (uint64_t)bytes, true)) {
+                static std::vector<char> g_hpack;
+                if (g_hpack.size() < (size_t)n * (size_t)bytes) g_hpack.resize((size_t)n * (size_t)bytes);
+                iov_local(cop, scale, rs, nullptr, bytes, n, nullptr, g_hpack.data(), sdel, 0);
+                scatter_runs(darr[k].dst, g_hpack.data(), n, bytes);
                 continue;
             }
         }
@@ -1198,15 +1297,13 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             // sources are gathered on the host and uploaded packed, or the results come
             // back packed and are scattered on the host, in pair order
             if (world != r.rank) fence_target(world);
-            static std::vector<char> g_packed;   // kept across calls (no page faults per call)
-            if (g_packed.size() < (size_t)n * (size_t)bytes) g_packed.resize((size_t)n * (size_t)bytes);
-            char *packed = g_packed.data();
-            if (src_host) {
-                gather_runs(packed, darr[k].src, n, bytes);
-                iov_local(cop, scale, nullptr, dv, bytes, n, packed, nullptr);
+            if (src_host) {   // gathered straight into the pinned upload staging
+                iov_local(cop, scale, nullptr, dv, bytes, n, nullptr, nullptr, 0, 0, darr[k].src);
             } else {
-                iov_local(cop, scale, sv, nullptr, bytes, n, nullptr, packed);
-                scatter_runs(darr[k].dst, packed, n, bytes);
+                static std::vector<char> g_packed;   // kept across calls (no page faults per call)
+                if (g_packed.size() < (size_t)n * (size_t)bytes) g_packed.resize((size_t)n * (size_t)bytes);
+                iov_local(cop, scale, sv, nullptr, bytes, n, nullptr, g_packed.data());
+                scatter_runs(darr[k].dst, g_packed.data(), n, bytes);
             }
             continue;
         }

@@ -551,11 +551,12 @@ def test_accv_large_repeated_destinations(gpu_lib, oracle, op, nbytes, slots, sh
     assert same_bits_nan_aware(got, want, op)
 
 
-@pytest.mark.parametrize("n", [50, 20000])
+@pytest.mark.parametrize("n", [50, 20000, 200000])
 def test_accv_host_sources_packed(gpu_lib, oracle, n):
     """Pageable host sources (GA's MA buffer `v` of NGA_Scatter_acc) are gathered on the
     host and uploaded packed (one kernel, not one transfer per pair); repeated
-    destinations still apply in order."""
+    destinations still apply in order. From 65 536 pairs a source side lying in one
+    host mapping is recognised with one /proc/self/maps lookup (host_cpu_range)."""
     op, nbytes = C.DBL, 8
     rng = np.random.default_rng(n)
     src = C.fill_bytes(op, n * nbytes, 3)
@@ -573,12 +574,14 @@ def test_accv_host_sources_packed(gpu_lib, oracle, n):
     assert np.array_equal(db.download(np.uint8, dst.size), want)
 
 
-def test_getv_putv_host_side_packed(gpu_lib):
+@pytest.mark.parametrize("n", [30000, 100000])
+def test_getv_putv_host_side_packed(gpu_lib, n):
     """comex_getv into pageable host memory (results packed on the GPU, scattered on
     the host in pair order: a repeated destination keeps the last pair's bytes) and
-    comex_putv from pageable host memory, 30 000 pairs of 24 bytes."""
+    comex_putv from pageable host memory, n pairs of 24 bytes (100 000: the whole-side
+    host test of the local fast path)."""
     rng = np.random.default_rng(11)
-    nbytes, n, slots = 24, 30000, 5000
+    nbytes, slots = 24, 5000
     dev = rng.integers(0, 256, slots * nbytes, dtype=np.uint8)
     db = ga_amd.DeviceBuffer(dev.size)
     db.upload(dev)
@@ -602,3 +605,29 @@ def test_getv_putv_host_side_packed(gpu_lib):
     for a, b in zip(s_off.tolist(), d_off.tolist()):
         want[b:b + nbytes] = src[a:a + nbytes]
     assert np.array_equal(db.download(np.uint8, dev.size), want)
+
+
+def test_accv_host_sources_in_two_buffers(gpu_lib, oracle):
+    """Host sources alternating between two separate pageable buffers: the span of the
+    source side is not one mapping (or is, if the allocator placed them adjacently);
+    either way the result equals the pairs applied in order."""
+    op, nbytes, n = C.DBL, 8, 70000
+    rng = np.random.default_rng(5)
+    a = C.fill_bytes(op, n * nbytes, 7)
+    b = C.fill_bytes(op, n * nbytes, 8)
+    dst = C.fill_bytes(op, 3000 * nbytes, 9)
+    db = ga_amd.DeviceBuffer(dst.size)
+    db.upload(dst)
+    idx = np.arange(n, dtype=np.uint64) * nbytes
+    pick = rng.random(n) < 0.5
+    sa = np.where(pick, idx + np.uint64(a.ctypes.data), idx + np.uint64(b.ctypes.data)).astype(np.uint64)
+    do = rng.integers(0, 3000, n).astype(np.uint64) * nbytes
+    g = _giov_np(sa, do + np.uint64(db.ptr), nbytes)
+    keep, sp = ga_amd.scale_buffer(op, C.SCALE[op])
+    assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
+    ga_amd.comex_fence_all()
+    both = np.concatenate([a, b])
+    so = np.where(pick, idx, idx + np.uint64(a.size)).astype(np.uint64)
+    want = dst.copy()
+    _oracle_acc_pairs(oracle, op, C.SCALE[op], both, want, list(zip(so.tolist(), do.tolist())), nbytes)
+    assert np.array_equal(db.download(np.uint8, dst.size), want)
