@@ -1262,7 +1262,22 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             }
         }
         bool src_host = false, dst_host = false;   // a whole side in pageable host memory
-        for (int i = 0; i < n && !host_bounce; ++i) {
+        bool classified = false;
+        if (world != r.rank && kind == X_ACC && n >= kIovMapsMin) {
+            // remote accumulate from GA's `v`: a source side in one ordinary host mapping is
+            // recognised with one lookup (host_cpu_range) instead of a query per page
+            const uint64_t *rs = (const uint64_t *)darr[k].src;
+            uint64_t smin = ~0ull, smax = 0;
+            for (int i = 0; i < n; ++i) {
+                smin = rs[i] < smin ? rs[i] : smin;
+                smax = rs[i] > smax ? rs[i] : smax;
+            }
+            if (host_cpu_range(smin, smax + (uint64_t)bytes, false)) {
+                src_host = classified = true;
+                memcpy(dv, darr[k].dst, (size_t)n * 8);   // owner addresses, checked per chunk below
+            }
+        }
+        for (int i = 0; i < n && !host_bounce && !classified; ++i) {
             void *sp = darr[k].src[i], *dp = darr[k].dst[i];
             uint64_t v = 0;
             if (world != r.rank && !remote_side_is_dst) {
@@ -1330,10 +1345,17 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             uint64_t align_or = 0, dlo = ~0ull, dhi = 0;
             for (int i = 0; i < m; ++i) {
                 const uint64_t a = dv[(size_t)i0 + i];
-                (void)remote_view(world, (void *)(uintptr_t)a, 0, bytes);   // reg_cache_find
                 align_or |= a;
                 dlo = std::min(dlo, a);
                 dhi = std::max(dhi, a + (uint64_t)bytes);
+            }
+            // reg_cache_find: one lookup when the chunk's destinations lie in one segment
+            // of the owner (a GA block), else one per pair (aborting on a stray address)
+            if (segment_of_rank(world, dlo, 0, (int64_t)(dhi - dlo))) {
+                (void)remote_view(world, (void *)(uintptr_t)dlo, 0, (int64_t)(dhi - dlo));
+            } else {
+                for (int i = 0; i < m; ++i)
+                    (void)remote_view(world, (void *)(uintptr_t)dv[(size_t)i0 + i], 0, bytes);
             }
             // repeated destinations: the owner orders them on its GPU when every destination
             // is a whole number of pairs from dlo, else a host check picks the serial kernel
