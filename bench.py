@@ -4,13 +4,20 @@
 Metric (BASELINE.json): GiB/s device-resident 2-D strided f64 accumulate,
 64 MiB patch; % HBM peak.
 
-A "step" is one comex_accs call (include/comex.h; reference comex_accs,
-comex/src-mpi-pr/comex.c:985) applying dst += alpha*src over the workload's
-patch, both sides resident in HBM.  Default workload "H": count = {2048*8 B,
-4096 rows}, src & dst leading dimension 8192 doubles (65 536 B) -- 64 MiB of
-payload, 192 MiB of algorithmic HBM traffic (src read + dst read + dst write,
-24 B per element).  Steps rotate over --sets independent buffer sets (default
-8 x 512 MiB) so the 256 MiB Infinity Cache cannot serve the working set.
+A "step" is one comex_nbaccs call (include/comex.h; reference comex_nbaccs,
+comex/src-mpi-pr/comex.c:1998-2027 -> nb_accs 6890) applying dst += alpha*src
+over the workload's patch, both sides resident in HBM; the handles are waited
+on (comex_wait, one 64 steps back) and comex_wait_all closes the timed region,
+so every step's kernel has finished inside it.  (A blocking comex_accs returns
+only after its kernel finished -- local completion, SURVEY.md 8(b) -- so a
+stream of them pays one host round trip per step: --api blocking measures that.)
+Default workload "H": count = {2048*8 B, 4096 rows}, src & dst leading
+dimension 8192 doubles (65 536 B) -- 64 MiB of payload, 192 MiB of algorithmic
+HBM traffic (src read + dst read + dst write, 24 B per element).  Steps rotate
+over --sets independent buffer sets (default 8 x 512 MiB) so the 256 MiB
+Infinity Cache cannot serve the working set.  Before the timed region the same
+step runs for --warmup steps and then for at least --warmup-ms of wall time,
+so the K timed steps do not start on a cold (clock-ramping) GPU.
 
 value = whole-job algorithmic traffic GiB/s = ranks * steps * bytes / max-over-
 ranks wall time.  roofline.achieved = the same algorithmic bytes per launch /
@@ -22,24 +29,34 @@ streams (ga_amd/csrc/sched.cpp), so consecutive launches overlap at their
 edges: the rocprofv3 --kernel-trace summary of the same command is committed
 under profiles/, and the per-launch time it agrees with is the merged busy time
 of the dispatches / dispatches (tools/kernel_union.py), not AverageNs, which
-counts shared time twice.  roofline.traffic = HBM bytes
-per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE (tools/pmc_traffic.py,
-profiles/pmc_latest.json).  cpu_baseline = the reference's own _acc
-(oracle/_ref, compiled from comex/src-common/acc.h) driven per row by P host
-threads, each on its own slab of the same workload, over a bounded sample
-(P = 1 reported beside it).
+counts shared time twice.  roofline.traffic = HBM bytes per launch from
+rocprofv3 FETCH_SIZE/WRITE_SIZE passes of the same workload (tools/pmc_traffic.py,
+profiles/pmc_latest.json) -- collected in separate profiled runs, not this one
+(roofline.traffic_source says so).  cpu_baseline = the reference's own _acc
+(oracle/_ref, compiled from comex/src-common/acc.h) driven per row by the
+restated nb_accs odometer (comex.c:6936-6961) on P host threads, each on its
+own slab of the same workload, over a bounded sample (P = 1 .. 16 reported).
 
-Multi-GPU: one process per GPU (torch.distributed.run); every rank accumulates
-into its own partition (GA owner-aligned patches) with no
-data-path collective -> "scaling": "weak".  torch.distributed (gloo, CPU) only
-carries the bootstrap allgather/barrier and the max-over-ranks reduction.
+Multi-GPU: one process per GPU.  Under torch.distributed.run (RANK/WORLD_SIZE
+set) every process is one rank; with --gpus N > 1 and no WORLD_SIZE, bench.py
+starts the N rank processes itself (before any HIP call) and forwards rank 0's
+line.  Every rank accumulates into its own partition (GA owner-aligned
+patches) with no data-path collective -> "scaling": "weak".
+torch.distributed (gloo, CPU) only carries the bootstrap allgather/barrier and
+the max-over-ranks reduction.  At N > 1 the line also carries C5 (GA_Acc into a
+block-distributed 32768^2 f64 GA): M1 (every rank its own
+block) and M2 (every rank the whole array: (p-1)/p of it through the remote
+path over xGMI), with per-GPU HBM fraction and per-GPU xGMI bytes/s.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
+from collections import deque
 
 import numpy as np
 
@@ -155,20 +172,59 @@ def bootstrap(L, dist):
         assert rc == 0, rc
 
 
-def run_ga(args, dist):
+class Handles:
+    """Non-blocking step handles: at most `depth` outstanding (comex_wait on the
+    oldest, which has long finished when the GPU keeps up), all drained by
+    comex_wait_all at the end of a region."""
+
+    def __init__(self, L, depth=64):
+        self.L, self.depth, self.q = L, depth, deque()
+
+    def new(self):
+        h = ctypes.c_int(-1)
+        self.q.append(h)
+        if len(self.q) > self.depth:
+            assert self.L.comex_wait(ctypes.byref(self.q.popleft())) == 0
+        return ctypes.byref(h)
+
+    def drain(self):
+        assert self.L.comex_wait_all(0) == 0
+        self.q.clear()
+
+
+def warm(step, args, first=0):
+    """W warm-up steps, then more of the same step until --warmup-ms have passed
+    (outside the timed region: a cold process reads 5-10 % low for its first
+    milliseconds).  Returns the index of the next step."""
+    i = first
+    for _ in range(args.warmup):
+        step(i)
+        i += 1
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.warmup_ms / 1e3:
+        step(i)
+        i += 1
+    return i
+
+
+def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True):
     """C5: NGA_Acc (include/ga.h; reference capi.c:2079 -> ngai_acc_common,
-    global/src/onesided.c:1334) on a 32768^2 f64 GA."""
+    global/src/onesided.c:1334) on a 32768^2 f64 GA.  NGA_Acc is GA's blocking
+    call: every owner but the last through ARMCI_NbAccS, the last ARMCI_AccS
+    (onesided.c:1421-1438)."""
     import ga_amd
     L = ga_amd.lib()
-    bootstrap(L, dist)
+    if not L.comex_initialized():
+        bootstrap(L, dist)
     assert L.GA_Initialize() == 0
     ia = ga_amd.int_array
     dims = [args.ga_dims, args.ga_dims] if args.ga_dims else GA_DIMS
+    exchange = (args.exchange if exchange is None else exchange) and dist.size > 1
+    steps = args.steps if steps is None else steps
     g = L.NGA_Create(C_DBL, 2, ia(dims), b"C5", None)
     assert g > 0
     blo, bhi = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
     L.NGA_Distribution(g, dist.rank, blo, bhi)
-    exchange = args.exchange and dist.size > 1
     lo, hi = ([0, 0], [dims[0] - 1, dims[1] - 1]) if exchange else (list(blo), list(bhi))
     rows, cols = hi[0] - lo[0] + 1, hi[1] - lo[1] + 1
     payload = rows * cols * 8
@@ -177,7 +233,8 @@ def run_ga(args, dist):
     # the local block: fill through NGA_Access (its HBM address)
     ptr, ld = ctypes.c_void_p(), (ctypes.c_int * 1)()
     L.NGA_Access(g, blo, bhi, ctypes.byref(ptr), ld)
-    ga_amd.fill(ptr.value, (bhi[0] - blo[0] + 1) * (bhi[1] - blo[1] + 1), 0, 0x5EED0001 + dist.rank)
+    block_bytes = (bhi[0] - blo[0] + 1) * (bhi[1] - blo[1] + 1) * 8
+    ga_amd.fill(ptr.value, block_bytes // 8, 0, 0x5EED0001 + dist.rank)
     L.NGA_Release_update(g, blo, bhi)
     ga_amd.sync()
     L.GA_Sync()
@@ -187,13 +244,16 @@ def run_ga(args, dist):
     clo, chi, cld = ia(lo), ia(hi), ia([cols])
     stream = L.gaamd_stream()
 
-    def step():
+    def step(_i):
         L.NGA_Acc(g, clo, chi, ctypes.c_void_p(src.ptr), cld, ctypes.byref(alpha))
         if args.verbose:
             print(f"rank {dist.rank}: NGA_Acc done", file=sys.stderr, flush=True)
 
-    for _ in range(args.warmup):
-        step()
+    saved = args.warmup_ms
+    if warmup_ms is not None:
+        args.warmup_ms = warmup_ms
+    nxt = warm(step, args)
+    args.warmup_ms = saved
     ga_amd.sync()
     L.GA_Sync()
     launch = ga_amd.last_launch()
@@ -203,8 +263,8 @@ def run_ga(args, dist):
     t0 = time.perf_counter()
     L.gaamd_event_record(ev0, stream)
     L.gaamd_join()
-    for _ in range(args.steps):
-        step()
+    for i in range(steps):
+        step(nxt + i)
     L.gaamd_join()
     L.gaamd_event_record(ev1, stream)
     ga_amd.sync()
@@ -216,22 +276,24 @@ def run_ga(args, dist):
     region_ms = L.gaamd_event_elapsed_ms(ev0, ev1)
     L.gaamd_event_destroy(ev0)
     L.gaamd_event_destroy(ev1)
-    avg_kernel_s = dist.max(region_ms / 1e3 / args.steps) if not exchange else elapsed / args.steps
+    avg_kernel_s = dist.max(region_ms / 1e3 / steps) if not exchange else elapsed / steps
     src.free()
     L.GA_Sync()
     L.GA_Destroy(g)
-    L.GA_Terminate()
+    if terminate:
+        L.GA_Terminate()
     desc = (f"GA_Acc, {dims[0]}x{dims[1]} f64 GA on a {grid[0]}x{grid[1]} grid, "
             + ("every rank the whole array (M2)" if exchange else f"own {rows}x{cols} block (M1)"))
     return dict(op=DBL, desc=desc, payload=payload, alg_bytes=3 * payload, elems=rows * cols, elapsed=elapsed,
-                avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), exchange=exchange)
+                avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), exchange=exchange,
+                steps=steps, block_bytes=block_bytes, array_bytes=dims[0] * dims[1] * 8)
 
 
-def run_gpu(args, dist):
+def run_gpu(args, dist, finalize=True):
     import ga_amd
     L = ga_amd.lib()
     if args.workload == "C5":
-        return run_ga(args, dist)
+        return run_ga(args, dist, terminate=finalize)
     bootstrap(L, dist)
     assert ga_amd.comex_init() == 0
     for kv in args.tune or []:
@@ -281,6 +343,8 @@ def run_gpu(args, dist):
 
     pipeline = args.pipeline and not exchange
     packed = [ga_amd.DeviceBuffer(payload) for _ in sets] if pipeline else []
+    hd = Handles(L)
+    nb = args.api == "nb"
 
     def step(i):
         sp_, dp_ = ptrs[i % len(ptrs)]
@@ -291,16 +355,19 @@ def run_gpu(args, dist):
             rc = L.gaamd_pack(sp_, ss, cnt, levels, pk, None) or \
                 L.gaamd_unpack_acc(op, sp, pk, dp_, ds, cnt, levels, None)
         elif xfer == "put":             # comex_puts (comex.c:6342): local src -> the target's patch
-            rc = L.comex_puts(sp_, ss, dp_, ds, cnt, levels, target, 0)
+            rc = (L.comex_nbputs(sp_, ss, dp_, ds, cnt, levels, target, 0, hd.new()) if nb else
+                  L.comex_puts(sp_, ss, dp_, ds, cnt, levels, target, 0))
         elif xfer == "get":             # comex_gets (comex.c:6617): the target's patch -> local buffer
-            rc = L.comex_gets(dp_, ds, sp_, ss, cnt, levels, target, 0)
+            rc = (L.comex_nbgets(dp_, ds, sp_, ss, cnt, levels, target, 0, hd.new()) if nb else
+                  L.comex_gets(dp_, ds, sp_, ss, cnt, levels, target, 0))
         else:
-            rc = L.comex_accs(op, sp, sp_, ss, dp_, ds, cnt, levels, target, 0)
+            rc = (L.comex_nbaccs(op, sp, sp_, ss, dp_, ds, cnt, levels, target, 0, hd.new()) if nb else
+                  L.comex_accs(op, sp, sp_, ss, dp_, ds, cnt, levels, target, 0))
         if rc:
             raise RuntimeError(f"step returned {rc}")
 
-    for i in range(args.warmup):
-        step(i)
+    nxt = warm(step, args)
+    hd.drain()
     ga_amd.sync()
     launch = ga_amd.last_launch()
 
@@ -315,9 +382,10 @@ def run_gpu(args, dist):
     L.gaamd_event_record(ev0, stream)
     L.gaamd_join()                      # every library stream starts after ev0
     for i in range(args.steps):
-        step(args.warmup + i)
+        step(nxt + i)
     L.gaamd_join()                      # the primary stream waits for the library's other streams
     L.gaamd_event_record(ev1, stream)
+    hd.drain()                          # every step's kernel has finished (comex_wait_all)
     ga_amd.sync()
     if exchange:
         L.comex_fence_all(0)            # remote completion: the owner has applied every request
@@ -333,7 +401,7 @@ def run_gpu(args, dist):
 
     res = dict(op=op, desc=desc, payload=payload, alg_bytes=alg_bytes, elems=elems, elapsed=elapsed,
                avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), pipeline=pipeline,
-               xfer=xfer)
+               xfer=xfer, warmup_steps=nxt)
     for b in packed:
         b.free()
     if args.host_rates and dist.rank == 0:
@@ -347,8 +415,33 @@ def run_gpu(args, dist):
         for seg in segs:
             ga_amd.comex_free(seg[dist.rank])
     res["exchange"] = exchange
-    ga_amd.comex_finalize()
+    if finalize:
+        ga_amd.comex_finalize()
     return res
+
+
+def c5_extras(args, dist):
+    """N > 1: C5 in the same job -- M1, every rank NGA_Acc's its
+    own block (owner-aligned, HBM-bound), and M2, every rank NGA_Acc's the whole
+    array, (p-1)/p of it through the remote path (pack into exported staging HBM,
+    the owner's unpack-acc reading it over xGMI).  Few steps: these are reported
+    beside the headline, not as `value`."""
+    out = {}
+    for mode, exchange, steps in (("M1", False, args.c5_steps), ("M2", True, max(1, args.c5_steps // 2))):
+        r = run_ga(args, dist, exchange=exchange, steps=steps, warmup_ms=0.0, terminate=(mode == "M2"))
+        p = dist.size
+        t = r["elapsed"] / steps
+        d = {"desc": r["desc"], "steps": steps, "ms_per_step": round(t * 1e3, 3),
+             "GiB_per_s_job": round(p * r["alg_bytes"] / t / 2 ** 30, 1)}
+        if exchange:
+            # each owner receives (p-1) blocks' worth of packed rows from its peers per step
+            xgmi = (p - 1) * r["block_bytes"]
+            d["xgmi_GBps_per_gpu"] = round(xgmi / t / 1e9, 1)
+            d["note"] = "whole-array accumulate by every rank; value counts 3 x payload of HBM-side traffic per rank"
+        else:
+            d["hbm_peak_frac_per_gpu"] = round(r["alg_bytes"] / t / (HBM_PEAK_GBS * 1e9), 4)
+        out[mode] = d
+    return out
 
 
 def host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_bytes, iters=5):
@@ -404,8 +497,11 @@ def host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_byt
 def run_cpu_baseline(workload, seconds, threads):
     """The reference's _acc per row (oracle/_ref), or the restatement if _ref is absent.
     SURVEY.md 8(d): P host workers, each on its own slab of the patch (oracle/mt_split.h),
-    for P = 1, 2, 4, 8 (up to `threads`); each as many full steps as fit in ~seconds/#P (at
-    least 2).  `value` is the P = `threads` rate; every P is reported beside it."""
+    for P = 1, 2, 4, 8, 16 (up to `threads`: the GPU box's CPU share per GPU is 16); each
+    as many full steps as fit in ~seconds/#P (at least 2).  `value` is the P = `threads`
+    rate; every P is reported beside it.  Provenance: the reference's own _acc (acc.h,
+    compiled into oracle/_ref) for the arithmetic, driven by the restated nb_accs
+    odometer (comex.c:6936-6961) -- comex.c itself is not built here."""
     from oracle import Oracle, Ref, ref_available
     op, count, sstr, dstr, _ = WORKLOADS[workload]
     sbytes, dbytes = span_bytes(count, sstr), span_bytes(count, dstr)
@@ -420,7 +516,7 @@ def run_cpu_baseline(workload, seconds, threads):
         impl, kind = o, "port"
     levels = len(count) - 1
     rates, notes = {}, []
-    ps = sorted({p for p in (1, 2, 4, 8) if p <= threads} | {max(1, threads)})
+    ps = sorted({p for p in (1, 2, 4, 8, 16) if p <= threads} | {max(1, threads)})
     for p in ps:
         impl.accs_mt(op, SCALE[op], src, 0, sstr, dst, 0, dstr, count, levels, p)   # warm-up (page-in)
         n, t0 = 0, time.perf_counter()
@@ -458,6 +554,8 @@ def run_cpu_baseline(workload, seconds, threads):
     except OSError:
         pass
     return {"value": rates[P], "unit": "GiB/s", "cores": P, "kind": kind, "single_core_value": rates[1],
+            "provenance": ("reference _acc (comex/src-common/acc.h compiled into oracle/_ref) + restated odometer "
+                           "(comex.c:6936-6961)") if kind == "reference" else "oracle restatement (oracle/comex_oracle.c)",
             "by_workers": {str(k): v for k, v in sorted(rates.items())},
             "packed_path_single_core": packed,
             "host": {"cpu": model, "nproc": os.cpu_count()},
@@ -480,15 +578,45 @@ def load_traffic(workload, launch_bytes):
     return None
 
 
+def free_port():
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    return port
+
+
+def spawn_ranks(n):
+    """--gpus N > 1 without a launcher: start N rank processes of this script
+    (one per GPU, LOCAL_RANK = GPU index) before this process touches HIP, wait
+    for all, forward rank 0's stdout line; exit status = the worst rank's."""
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup-ms", type=float, default=500.0,
+                    help="after --warmup steps, keep warming with the same step for this long (outside the timing)")
+    ap.add_argument("--api", default="nb", choices=["nb", "blocking"],
+                    help="nb: comex_nbaccs steps (handles waited 64 back, comex_wait_all at the end); "
+                         "blocking: comex_accs (returns after its kernel finished)")
     ap.add_argument("--workload", default="H", choices=sorted(WORKLOADS) + ["C5"])
     ap.add_argument("--sets", type=int, default=8, help="rotating buffer sets (MALL defeat)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=8, help="host workers of the CPU baseline")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host workers of the CPU baseline (the GPU box's CPU share is 16 per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--host-rates", action="store_true", help="also measure host-inclusive rates")
     ap.add_argument("--exchange", action="store_true",
@@ -499,11 +627,18 @@ def main():
                     help="operation per step: strided accumulate (the metric), or strided put / get")
     ap.add_argument("--tune", action="append", help="key=value tuning knob (gaamd_set_tuning)")
     ap.add_argument("--ga-dims", type=int, default=0, help="C5: square GA of this size instead of 32768^2")
+    ap.add_argument("--c5-steps", type=int, default=4, help="N>1: timed C5 M1 steps (M2: half as many)")
+    ap.add_argument("--no-extras", action="store_true", help="N>1: skip the C5 M1/M2 measurements")
     ap.add_argument("--verbose", action="store_true", help="progress lines on stderr")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+
     dist = Dist(args.gpus)
-    r = run_gpu(args, dist)
+    extras_on = dist.size > 1 and not args.no_extras and args.workload != "C5"
+    r = run_gpu(args, dist, finalize=not extras_on)
+    c5 = c5_extras(args, dist) if extras_on else None
     if dist.rank != 0:
         return
     n = dist.size
@@ -521,6 +656,8 @@ def main():
         "n_gpus": n,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_note": (f"{r.get('warmup_steps', args.warmup)} untimed steps: --warmup {args.warmup}, then the "
+                        f"same step until {args.warmup_ms:.0f} ms had passed"),
         "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
@@ -538,7 +675,11 @@ def main():
         "hbm_peak_frac": round(value * 2 ** 30 / (dist.size * HBM_PEAK_GBS * 1e9), 4),   # per GPU
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel_ms_avg": round(r["avg_kernel_s"] * 1e3, 4),
+                     "traffic": traffic,
+                     "traffic_source": ("profiles/pmc_latest.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "
+                                        "this workload's kernel (tools/pmc_traffic.py, gfx950 FETCH_SIZE x2), "
+                                        "collected in separate profiled runs, not this one") if traffic else None,
+                     "kernel_ms_avg": round(r["avg_kernel_s"] * 1e3, 4),
                      "timing": "HIP event pair around the timed launches (all library streams joined) / steps",
                      "streams": r["streams"],
                      "rocprof_check": ("consecutive launches overlap on the library streams: compare kernel_ms_avg "
@@ -546,7 +687,11 @@ def main():
                                        "(tools/kernel_union.py), not with AverageNs"
                                        if r["streams"] > 1 else "compare kernel_ms_avg with rocprofv3 AverageNs")},
         "cpu_baseline": cpu,
+        "api": ("comex_nbaccs per step, handles waited 64 back + comex_wait_all" if args.api == "nb"
+                else "comex_accs per step (blocking: returns after its kernel)"),
     }
+    if c5:
+        line["c5"] = c5
     if r.get("xfer", "acc") != "acc":
         line["metric"] = f"GiB/s device-resident strided f64 {r['xfer']} (comex_{r['xfer']}s), not the headline metric"
         line["config"]["step"] = f"comex_{r['xfer']}s of the patch; algorithmic bytes = 2 x payload (read + write)"

@@ -35,7 +35,7 @@ OP_DTYPE = {
 OP_NAME = {COMEX_ACC_INT: "int", COMEX_ACC_DBL: "dbl", COMEX_ACC_FLT: "flt", COMEX_ACC_CPL: "cpl",
            COMEX_ACC_DCP: "dcp", COMEX_ACC_LNG: "lng"}
 
-KIND_NAME = {0: "auto", 1: "rows", 2: "flat", 3: "serial"}
+KIND_NAME = {0: "auto", 1: "rows", 2: "flat", 3: "serial", 4: "ordered"}
 
 
 def lib():
@@ -152,10 +152,10 @@ def plan_strided(op, src, src_stride, dst, dst_stride, count, stride_levels, row
 
 
 def kernel_counts():
-    """launches so far by kind (this process): {'rows': n, 'flat': n, 'serial': n}"""
-    c = (ctypes.c_ulonglong * 4)()
+    """launches so far by kind (this process): {'rows': n, 'flat': n, 'serial': n, 'ordered': n}"""
+    c = (ctypes.c_ulonglong * 5)()
     lib().gaamd_kernel_counts(c)
-    return {"rows": c[1], "flat": c[2], "serial": c[3]}
+    return {"rows": c[1], "flat": c[2], "serial": c[3], "ordered": c[4]}
 
 
 def set_tuning(key, value):

@@ -116,6 +116,7 @@ SIGNATURES = {
     "gaamd_bootstrap_selftest": (ctypes.c_int, [ctypes.c_int]),
     "gaamd_rank": (ctypes.c_int, []),
     "gaamd_size": (ctypes.c_int, []),
+    "gaamd_device": (ctypes.c_int, []),
     "gaamd_node_info": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)] * 3),
     "gaamd_wire_selftest": (ctypes.c_int, [ctypes.c_int]),
     "gaamd_strided": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, c_int_p, ctypes.c_void_p,

@@ -123,15 +123,15 @@ void boot_init() {
         r.local_rank = env_int(lrank_env, r.rank);
     }
     if (r.size < 1 || r.rank < 0 || r.rank >= r.size) fatal("bad rank %d / size %d", r.rank, r.size);
-    if (r.size > kMaxRanks) fatal("world size %d exceeds %d ranks per node", r.size, kMaxRanks);
 
-    const size_t bytes = node_shm_bytes(r.size);
-    r.shm_bytes = bytes;
     r.node_of.assign(r.size, 0);
+    r.node_index.assign(r.size, 0);
     r.nnodes = 1;
     r.node = 0;
     r.node_size = r.size;
     if (r.size == 1) {
+        const size_t bytes = node_shm_bytes(1);
+        r.shm_bytes = bytes;
         void *p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
         if (p == MAP_FAILED) fatal("mmap(anon) failed");
         r.shm = reinterpret_cast<NodeShm *>(p);
@@ -164,10 +164,18 @@ void boot_init() {
         fatal("COMEX_AMD_NODE needs bootstrap hooks (gaamd_set_bootstrap): the node-shm rendezvous is per host");
     }
     r.node = r.node_of[r.rank];
-    r.node_size = 0;
+    // the node shm holds one inbox and one done[][] row/column per rank of the
+    // node, indexed by the rank's position on its node
     int leader = -1;
-    for (int q = 0; q < r.size; ++q)
-        if (r.node_of[q] == r.node) { if (leader < 0) leader = q; ++r.node_size; }
+    std::vector<int> seen_on(r.nnodes, 0);
+    for (int q = 0; q < r.size; ++q) {
+        r.node_index[q] = seen_on[r.node_of[q]]++;
+        if (r.node_of[q] == r.node && leader < 0) leader = q;
+    }
+    r.node_size = seen_on[r.node];
+    if (r.node_size > kMaxRanks) fatal("%d ranks on one node exceed %d", r.node_size, kMaxRanks);
+    const size_t bytes = node_shm_bytes(r.node_size);
+    r.shm_bytes = bytes;
 
     char name[128];
     if (r.hooks) {
@@ -221,7 +229,7 @@ void boot_allgather(const void *send, void *recv, size_t bytes) {
         if (r.ag(send, recv, bytes, r.ctx) != 0) fatal("bootstrap allgather hook failed");
         return;
     }
-    char *area = boot_area(r.shm, r.size);
+    char *area = boot_area(r.shm, r.node_size);   // one node: node_size == size
     for (size_t off = 0; off < bytes || (bytes == 0 && off == 0); off += kBootSlot) {
         const size_t n = bytes - off < kBootSlot ? bytes - off : kBootSlot;
         memcpy(area + (size_t)r.rank * kBootSlot, (const char *)send + off, n);
@@ -281,3 +289,4 @@ extern "C" int gaamd_bootstrap_selftest(int rounds) {
 
 extern "C" int gaamd_rank(void) { return rt().rank; }
 extern "C" int gaamd_size(void) { return rt().size; }
+extern "C" int gaamd_device(void) { return rt().device; }

@@ -300,15 +300,19 @@ static size_t sub_ring_bytes() {
     return (r.staging_bytes / (size_t)r.size) & ~(size_t)255;
 }
 
+// ring space of a request: every reservation is a multiple of 256 bytes, so
+// every request starts 256-byte aligned in the ring
+static uint64_t ring_len(uint64_t len) { return (len + 255) & ~255ull; }
+
 static void reap(int t) {
     Runtime &r = rt();
-    const uint64_t done = r.shm->done[r.rank][t].load(std::memory_order_acquire);
+    const uint64_t done = r.shm->done[r.li(r.rank)][r.li(t)].load(std::memory_order_acquire);
     while (!g_pend[t].empty() && g_pend[t].front().seq <= done) g_pend[t].pop_front();
 }
 
 static void wait_done(int t, uint64_t seq) {
     Runtime &r = rt();
-    for (unsigned spins = 0; r.shm->done[r.rank][t].load(std::memory_order_acquire) < seq; ++spins)
+    for (unsigned spins = 0; r.shm->done[r.li(r.rank)][r.li(t)].load(std::memory_order_acquire) < seq; ++spins)
         if (spins > 256) sched_yield();
     reap(t);
 }
@@ -340,7 +344,7 @@ static uint64_t stage_alloc(int t, uint64_t len) {
 static void post_request(int t, int op, const void *scale, uint64_t dst_addr, const int *dst_stride,
                          const int *count, int levels, uint64_t off, uint64_t len, uint64_t rb, uint64_t re) {
     Runtime &r = rt();
-    Inbox *ib = inbox_of(r.shm, t);
+    Inbox *ib = inbox_of(r.shm, r.li(t));
     const uint64_t ticket = ib->tail.fetch_add(1, std::memory_order_acq_rel);
     Request &q = ib->slot[ticket % kInboxSlots];
     // the slot belongs to our lap once the previous lap's ticket is consumed
@@ -377,7 +381,7 @@ static void post_request(int t, int op, const void *scale, uint64_t dst_addr, co
 static void post_request_iov(int t, int op, const void *scale, int bytes, int n, uint64_t off, uint64_t len,
                              uint64_t dlo, uint64_t dhi, uint64_t align_or, int mode) {
     Runtime &r = rt();
-    Inbox *ib = inbox_of(r.shm, t);
+    Inbox *ib = inbox_of(r.shm, r.li(t));
     const uint64_t ticket = ib->tail.fetch_add(1, std::memory_order_acq_rel);
     Request &q = ib->slot[ticket % kInboxSlots];
     for (unsigned spins = 0; ib->head.load(std::memory_order_acquire) + kInboxSlots <= ticket; ++spins)
@@ -413,7 +417,7 @@ static uint64_t iov_list_off(int n, int bytes) { return (((uint64_t)n * (uint64_
 static void progress_loop() {
     Runtime &r = rt();
     GA_HIP(hipSetDevice(r.device));
-    Inbox *ib = inbox_of(r.shm, r.rank);
+    Inbox *ib = inbox_of(r.shm, r.li(r.rank));
     struct Inflight { hipEvent_t ev; int src; };
     std::deque<Inflight> inflight;
     std::vector<hipEvent_t> pool;
@@ -503,7 +507,7 @@ static void progress_loop() {
             hipError_t e = hipEventQuery(inflight.front().ev);
             if (e == hipErrorNotReady) break;
             if (e != hipSuccess) fatal("unpack-acc failed: %s", hipGetErrorString(e));
-            r.shm->done[inflight.front().src][r.rank].fetch_add(1, std::memory_order_release);
+            r.shm->done[r.li(inflight.front().src)][r.li(r.rank)].fetch_add(1, std::memory_order_release);
             pool.push_back(inflight.front().ev);
             inflight.pop_front();
             worked = true;
@@ -604,10 +608,10 @@ static bool progress_jobs() {
             const uint64_t rb = j.next_rb, re = std::min(j.rows, rb + j.per_req);
             const uint64_t len = (re - rb) * (uint64_t)j.count[0];
             uint64_t off = 0;
-            if (!try_stage_alloc(j.t, len, off)) break;
+            if (!try_stage_alloc(j.t, ring_len(len), off)) break;
             const uint64_t seq = ++r.posted[j.t];
-            g_pend[j.t].push_back({seq, off, len});
-            r.stage_head[j.t] = off + len;
+            g_pend[j.t].push_back({seq, off, ring_len(len)});
+            r.stage_head[j.t] = off + ring_len(len);
             char *stage = r.staging + (size_t)j.t * sub + off;
             hipEvent_t ev;
             if (g_chunk_ev.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -675,6 +679,16 @@ static int remote_acc_start(int t, int op, const void *scale, void *src, const i
     uint64_t rows = 1;
     for (int j = 1; j <= levels; ++j) rows *= (uint64_t)count[j];
     if (rows == 0 || row_bytes == 0) return 0;
+    if (!r.direct_pending.empty() && r.direct_pending[t]) {
+        // an earlier put/get kernel writing or reading t's HBM through the IPC
+        // mapping may still run on one of our streams, while the owner applies
+        // this accumulate on its own stream: the pack below (and so the post,
+        // which waits for the pack) is ordered after it, as the reference's
+        // synchronous same-node put/acc are (comex.c:6084-6101, 6241-6260)
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        sched_join();
+        r.direct_pending[t] = 0;
+    }
     RJob j;
     j.id = g_job_next++;
     if (g_job_next > (1 << 30)) g_job_next = 1;
@@ -683,6 +697,9 @@ static int remote_acc_start(int t, int op, const void *scale, void *src, const i
     j.levels = levels;
     memcpy(j.scale, scale, (size_t)esz);
     for (int k = 0; k <= levels; ++k) j.count[k] = count[k];
+    // only whole elements travel (_acc applies bytes/sizeof(T) of them, acc.h:122):
+    // packed rows of row_bytes keep every row element-aligned in staging
+    j.count[0] = (int)row_bytes;
     for (int k = 0; k < levels; ++k) { j.ss[k] = ss[k]; j.ds[k] = ds[k]; }
     j.dst = (char *)dst;
     side_span_host(ss, count, levels, count[0], &j.slo, &j.shi);
@@ -697,10 +714,10 @@ static int remote_acc_start(int t, int op, const void *scale, void *src, const i
         sched_join();
     }
     const uint64_t sub = sub_ring_bytes();
-    if ((uint64_t)count[0] > sub) fatal("row of %d bytes exceeds staging ring", count[0]);
-    j.per_req = std::max<uint64_t>(1, sub / (uint64_t)count[0]);
+    if ((uint64_t)row_bytes > sub) fatal("row of %ld bytes exceeds staging ring", (long)row_bytes);
+    j.per_req = std::max<uint64_t>(1, sub / (uint64_t)row_bytes);
     j.rows = rows;
-    int64_t acc = count[0];
+    int64_t acc = row_bytes;
     for (int k = 0; k < levels; ++k) { j.pstride[k] = (int)acc; acc *= count[k + 1]; }
     if (g_out.size() != (size_t)r.size) g_out.resize(r.size);
     static const bool async_ok = [] {
@@ -825,16 +842,22 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     }
     const bool host_side = needs_sync(sv) || needs_sync(dv);
     int si = 0;
+    hipStream_t st;
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
         if (host_side) sched_join();   // staged copies sit on stream 0: run there, after everything
         else si = sched_pick(span_of(sv.dev, slo, shi), span_of(dv.dev, dlo, dhi), payload_bytes(rb, count, levels));
-        const int rc = launch_strided(cop, scale, sv.dev, ss, dv.dev, ds, count, levels, r.streams[si],
-                                      last_launch_info());
+        st = r.streams[si];
+        const int rc = launch_strided(cop, scale, sv.dev, ss, dv.dev, ds, count, levels, st, last_launch_info());
         if (rc) fatal("strided %s launch failed (code %d): misaligned elements or bad descriptor",
                       kind == X_ACC ? "acc" : (kind == X_PUT ? "put" : "get"), rc);
-        if (host_side || r.blocking_sync) sched_sync_all();
+        if (host_side) sched_sync_all();
     }
+    // blocking call: local completion before returning (src reusable, a get's
+    // dst filled) -- the stream the op went to holds it and its dependencies
+    const bool synced = host_side || (!hdl && r.blocking_sync);
+    if (!host_side && synced) GA_HIP(hipStreamSynchronize(st));
+    if (world != r.rank && !synced && !r.direct_pending.empty()) r.direct_pending[world] = 1;
     if (r.debug)
         fprintf(stderr, "[ga_amd %d] %s -> %d levels %d count0 %d rows %d: src %s dst %s stream %d\n", r.rank,
                 kind == X_ACC ? "acc" : (kind == X_PUT ? "put" : "get"), world, levels, count[0],
@@ -1159,7 +1182,7 @@ static void iov_local(int cop, const void *scale, const uint64_t *src, const uin
         GA_HIP(hipStreamSynchronize(r.streams[si]));
         GA_HIP(hipMemcpy(host_dst, dev + o_res, (size_t)n * (size_t)bytes, hipMemcpyDeviceToHost));
     }
-    if (r.blocking_sync) sched_sync_all();
+    // completion (blocking call) or the handle (non-blocking) is taken by xfer_vec
 }
 
 static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int proc, int group,
@@ -1372,7 +1395,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             }
             const uint64_t loff = iov_list_off(m, bytes);
             const uint64_t len_b = loff + (uint64_t)m * 8;
-            const uint64_t off = stage_alloc(world, len_b);
+            const uint64_t off = stage_alloc(world, ring_len(len_b));
             char *stage = r.staging + (size_t)world * sub + off;
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
@@ -1405,13 +1428,24 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
                 GA_HIP(hipStreamSynchronize(r.streams[0]));
             }
             const uint64_t seq = ++r.posted[world];
-            g_pend[world].push_back({seq, off, len_b});
-            r.stage_head[world] = off + len_b;
+            g_pend[world].push_back({seq, off, ring_len(len_b)});
+            r.stage_head[world] = off + ring_len(len_b);
             post_request_iov(world, op, scale, bytes, m, (uint64_t)world * sub + off, len_b, dlo, dhi, align_or,
                              mode);
         }
     }
-    if (hdl) nb_complete_now(hdl);
+    // io-vector kernels may sit on any library stream (sched_pick per descriptor):
+    // a handle is recorded after a join, so it covers all of them; a blocking call
+    // completes locally before returning
+    const bool blocking = !hdl && r.blocking_sync;
+    {
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        if (hdl) sched_join();
+        else if (blocking) sched_sync_all();
+    }
+    if (world != r.rank && r.same_node(world) && kind != X_ACC && !blocking && !r.direct_pending.empty())
+        r.direct_pending[world] = 1;
+    if (hdl) nb_complete_now(hdl, 0);
     return COMEX_SUCCESS;
 }
 
@@ -1456,7 +1490,7 @@ int comex_init() {
     }
     for (int i = 0; i < kMaxNb; ++i) GA_HIP(hipEventCreateWithFlags(&r.nb_ev[i], hipEventDisableTiming));
     const char *bs = getenv("COMEX_AMD_BLOCKING_SYNC");
-    r.blocking_sync = bs && atoi(bs) != 0;
+    r.blocking_sync = !bs || atoi(bs) != 0;
     const char *dbg = getenv("COMEX_AMD_DEBUG");
     r.debug = dbg ? atoi(dbg) : 0;
     if (r.size > 1) {
@@ -1479,6 +1513,7 @@ int comex_init() {
         }
         r.posted.assign(r.size, 0);
         r.stage_head.assign(r.size, 0);
+        r.direct_pending.assign(r.size, 0);
         g_pend.assign(r.size, {});
         r.stop.store(false);
         r.progress = std::thread(progress_loop);

@@ -54,26 +54,22 @@ struct Desc {
     Scale16 scale;
 };
 
-enum KernelKind { KK_AUTO = 0, KK_ROWS = 1, KK_FLAT = 2, KK_SERIAL = 3 };
+enum KernelKind { KK_AUTO = 0, KK_ROWS = 1, KK_FLAT = 2, KK_SERIAL = 3, KK_ORDERED = 4 };
+constexpr int kKinds = 5;
 
 struct Tuning {
     int kind = KK_AUTO;     // force a kernel family
-    int unroll16 = 1;       // vectors per thread for the W=16 rows kernels {1,2,4,8}
+    int unroll16 = 1;       // vectors per thread for the W=16 rows kernels {1,2,4}
     int nontemporal = 1;    // nt loads/stores on the rows kernels (streamed once)
-    int block = 0;          // threads per block of the rows kernels {64, 128, 256, 512}; 0 = auto
+    int block = 0;          // threads per block of the rows kernels {64, 128, 256}; 0 = auto
     int flat_max_nvec = 127;// rows with at most this many vectors use the flat kernel
-    int max_grid = 0;       // cap on blocks (0 = one block per work item)
     int align = 1;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses (misaligned rows)
-    int cpol = 0;           // f64 2-D kernel via buffer ops: load | store<<8 cache bits (0 = off)
-    int xcd = 0;            // f64 2-D kernel: XCD-contiguous work ranges (experiment)
-    int order = 0;          // f64 2-D kernel: 1 chunk-major, 2 scattered rows (experiment)
     int direct = 1;         // 2-D rows of whole chunks: loop-free one-block-per-chunk kernel
     int flat_nt = 1;        // flat kernel (short rows): non-temporal loads/stores (+12-24 %)
     int flat_shape = 1;     // flat kernel: 0 = 256 threads x 2 vectors, 1 = 64 threads x 1 vector (W=16, nt;
                             // +3.5-5 % on 128 B-1 KiB rows, profiles/r01/sweep_flat_shape.jsonl)
     int flat_line_min = 40; // rows off 128 B lines on both sides with at least this many vectors: rows kernel (0 = off)
     int wide_unaligned = 0; // 16-byte vectors at 16-byte-misaligned (dword-aligned) bases when rows/strides allow
-    int lds_pad = 0;        // rows kernels: dynamic LDS bytes per wave (caps resident blocks per CU; 0 = none)
 };
 Tuning &tuning();
 
@@ -102,7 +98,7 @@ void side_span_host(const int *stride, const int *count, int stride_levels, int6
 
 int elem_size(int op);            // bytes per element for op; 1 for copy; 0 if unknown
 LaunchInfo *last_launch_info();   // most recent launch_strided (any caller)
-unsigned long long kernel_count(int kind);   // launch_strided launches so far, by KernelKind
+unsigned long long kernel_count(int kind);   // launch_strided launches so far, by KernelKind (< kKinds)
 
 // I/O-vector descriptor: n pairs of `bytes`; a side is a device array of n
 // addresses (list) or, when the list is null, base + i*bytes (packed)

@@ -17,9 +17,13 @@
 //     global_load_dwordx4), all loads issued before the first FP op.
 //   * FLAT kernel (short rows, < 128 vectors): vectors of all rows are flattened
 //     so every lane of a wave has work; each lane decodes its own row.
-//   * SERIAL kernel: one lane walks rows and elements in reference order; used
-//     only when dst rows overlap each other or src overlaps dst, where the
-//     reference result depends on its sequential order.
+//   * ORDERED kernel: where rows truly share bytes (dst rows with each other,
+//     or a src row with a dst row: found exactly by classify_rows), one
+//     16-wave workgroup applies the rows in the reference's order, each row
+//     wave-parallel.
+//   * SERIAL kernel: one lane walks rows and elements in reference order; only
+//     for a src run that starts inside its own dst run below it (a recurrence
+//     inside one _acc loop).
 //   * Alpha travels in the kernel argument block (SGPRs), not LDS.
 //   * FP contraction is OFF (pragma below + -ffp-contract=off): the reference
 //     computes round(round(a*b)+c) with no FMA, so must we, bit for bit.
@@ -33,6 +37,8 @@
 #include <algorithm>
 #include <type_traits>
 #include <atomic>
+#include <vector>
+#include <utility>
 
 namespace gaamd {
 
@@ -50,8 +56,8 @@ FastDiv make_fastdiv(uint32_t d) {
 
 static Tuning g_tuning;
 Tuning &tuning() { return g_tuning; }
-static std::atomic<unsigned long long> g_kind_count[4];
-unsigned long long kernel_count(int kind) { return (kind >= 0 && kind < 4) ? g_kind_count[kind].load() : 0; }
+static std::atomic<unsigned long long> g_kind_count[kKinds];
+unsigned long long kernel_count(int kind) { return (kind >= 0 && kind < kKinds) ? g_kind_count[kind].load() : 0; }
 
 int elem_size(int op) {
     switch (op) {
@@ -90,11 +96,16 @@ __device__ __forceinline__ void vstore(char *p, typename Vec<W>::T v) {
 
 // ---------------------------------------------------------------------------
 // element operations on one W-byte vector
+// Each op also has serial_elem(dp, sp): one element through memory, for the
+// one-lane kernel (src element read whole, then the statements of acc.h:46-49:
+// the reference declares dst/src `restrict` and its compiled loop reads B once
+// per element, acc.h:106-122).
 struct CopyOp {
     static constexpr int kElem = 1;
     static constexpr bool kReadsDst = false;
     template <int W>
     __device__ __forceinline__ typename Vec<W>::T apply(typename Vec<W>::T, typename Vec<W>::T s) const { return s; }
+    __device__ __forceinline__ void serial_elem(char *dp, const char *sp) const { *dp = *sp; }
 };
 
 // dst += src*scale, acc.h:46 IADD_SCALE_REG; integers in unsigned arithmetic.
@@ -114,6 +125,12 @@ struct AccReal {
             a.t[i] = a.t[i] + prod;
         }
         return a.v;
+    }
+    __device__ __forceinline__ void serial_elem(char *dp, const char *sp) const {
+        A *it = reinterpret_cast<A *>(dp);
+        const A *v = reinterpret_cast<const A *>(sp);
+        A prod = *v * s;
+        *it = *it + prod;
     }
 };
 
@@ -143,6 +160,19 @@ struct AccCplx {
             a.t[2 * i + 1] = a.t[2 * i + 1] + im;
         }
         return a.v;
+    }
+    __device__ __forceinline__ void serial_elem(char *dp, const char *sp) const {
+        R *it = reinterpret_cast<R *>(dp);
+        const R *v = reinterpret_cast<const R *>(sp);
+        const R br = v[0], bi = v[1];
+        R p1 = br * sr;
+        R p2 = bi * si;
+        R re = p1 - p2;
+        it[0] = it[0] + re;
+        R p3 = br * si;
+        R p4 = bi * sr;
+        R im = p3 + p4;
+        it[1] = it[1] + im;
     }
 };
 
@@ -227,17 +257,11 @@ struct Desc2 {
     uint32_t row0, nvec, chunks, items;
     FastDiv chunk_div;
     uint32_t align_mask;   // != 0: chunk boundaries at dst addresses = 0 mod (mask+1)
-    uint32_t xcd_per;      // XCD-contiguous work (tuning experiment): items / 8, 0 = off
 };
 
-// XCD: blocks are dealt round-robin to the 8 XCDs (block b -> XCD b % 8); with
-// XCD set, XCD x takes the contiguous work range [x*items/8, (x+1)*items/8)
-// instead of every 8th chunk (launched with grid == items, items % 8 == 0).
-template <class OP, int W, int U, int BS, bool NT, bool XCD = false>
+template <class OP, int W, int U, int BS, bool NT>
 __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
-    uint32_t w0 = blockIdx.x;
-    if constexpr (XCD) w0 = (w0 & 7u) * d.xcd_per + (w0 >> 3);
-    for (uint32_t w = w0; w < d.items; w += gridDim.x) {
+    for (uint32_t w = blockIdx.x; w < d.items; w += gridDim.x) {
         const uint32_t rl = d.chunk_div.div(w);
         const uint32_t chunk = w - rl * d.chunks;
         const int64_t r = (int64_t)(d.row0 + rl);
@@ -316,61 +340,6 @@ __global__ __launch_bounds__(BS) void k_rowsnd(const DescND<LV> d, const OP op) 
     vstore<W, true>(dp, op.template apply<W>(b, a));
 }
 
-// ROWS2 with a different block -> (row, chunk) order (tuning experiment on the
-// f64 2-D kernel; which rows are in flight together decides how the traffic
-// spreads over HBM channels):
-//   ORD 1: chunk-major  -- w = chunk * rows + row
-//   ORD 2: row-scattered -- row = (w_row * mult) mod rows, mult coprime to rows
-template <class OP, int ORD>
-__global__ __launch_bounds__(256) void k_rows2_ord(const Desc2 d, const OP op, uint32_t rows, uint32_t mult) {
-    for (uint32_t w = blockIdx.x; w < d.items; w += gridDim.x) {
-        uint32_t rl, chunk;
-        if constexpr (ORD == 1) {
-            chunk = w / rows;
-            rl = w - chunk * rows;
-        } else {
-            const uint32_t q = d.chunk_div.div(w);
-            chunk = w - q * d.chunks;
-            rl = (uint32_t)(((uint64_t)q * mult) % rows);
-        }
-        const int64_t r = (int64_t)(d.row0 + rl);
-        const char *sp = d.src + r * d.s_str;
-        char *dp = d.dst + r * d.d_str;
-        const int64_t c0 = (int64_t)chunk * 256;
-        chunk_op<OP, 16, 1, 256, true>(sp, dp, c0 + threadIdx.x, d.nvec, c0 + 256 <= (int64_t)d.nvec, op);
-    }
-}
-
-// ROWS2 via buffer loads/stores: a per-row SRD whose num_records is the row
-// length, so lanes past the row (or before an aligned chunk start) read zeros
-// and their stores are dropped by the hardware range check -- no predicate.
-// LA/SA are the cache-policy bits of the loads/stores (sc0 = 1, nt = 2,
-// sc1 = 16): a tuning experiment on the headline kernel.
-template <class OP, int U, int BS, int LA, int SA>
-__global__ __launch_bounds__(BS) void k_rows2_buf(const Desc2 d, const OP op) {
-    typedef typename Vec<16>::T V;
-    const uint32_t row_bytes = d.nvec * 16u;
-    for (uint32_t w = blockIdx.x; w < d.items; w += gridDim.x) {
-        const uint32_t rl = d.chunk_div.div(w);
-        const uint32_t chunk = w - rl * d.chunks;
-        const int64_t r = (int64_t)(d.row0 + rl);
-        const char *sp = d.src + r * d.s_str;
-        char *dp = d.dst + r * d.d_str;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)sp, 0, row_bytes, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)dp, 0, row_bytes, 0x00020000);
-        const uint32_t off0 = (chunk * (uint32_t)(BS * U) + threadIdx.x) * 16u;
-        V a[U], b[U];
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            a[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off0 + k * BS * 16, 0, LA);
-            b[k] = __builtin_amdgcn_raw_buffer_load_b128(rd, off0 + k * BS * 16, 0, LA);
-        }
-#pragma unroll
-        for (int k = 0; k < U; ++k)
-            __builtin_amdgcn_raw_buffer_store_b128(op.template apply<16>(b[k], a[k]), rd, off0 + k * BS * 16, 0, SA);
-    }
-}
-
 // FLAT kernel: vectors of all rows flattened, each lane decodes its own row.
 template <class OP, int W, int U, int BS, int LV, bool NT = false>
 __global__ __launch_bounds__(BS) void k_flat(const Desc d, const OP op) {
@@ -400,18 +369,57 @@ __global__ __launch_bounds__(BS) void k_flat(const Desc d, const OP op) {
 }
 
 // SERIAL kernel: the reference's own order (row by row, element by element).
+// Only for a source run that reads bytes its own row wrote earlier in the same
+// _acc loop (src starting inside the row's dst, below it): a recurrence.
 template <class OP, int W>
 __global__ __launch_bounds__(64) void k_serial(const Desc d, const OP op) {
     if (threadIdx.x != 0) return;
     for (uint32_t r = 0; r < d.rows; ++r) {
         int64_t so, dof;
         row_offsets<0>(d, d.row0 + r, so, dof);
-        for (uint32_t v = 0; v < d.nvec; ++v) {
-            char *dp = d.dst + dof + (size_t)v * W;
-            typename Vec<W>::T a = vload<W, false>(d.src + so + (size_t)v * W);
-            typename Vec<W>::T b = a;
-            if constexpr (OP::kReadsDst) b = vload<W, false>(dp);
-            vstore<W, false>(dp, op.template apply<W>(b, a));
+        const uint64_t n = (uint64_t)d.nvec * W / OP::kElem;
+        for (uint64_t m = 0; m < n; ++m)
+            op.serial_elem(d.dst + dof + m * OP::kElem, d.src + so + m * OP::kElem);
+    }
+}
+
+// ORDERED kernel: rows whose bytes truly overlap (dst rows sharing bytes with
+// each other, or a src row sharing bytes with a dst row) in the reference's
+// row order (comex.c:6936-6961), each row wave-parallel.  One workgroup of 16
+// waves: a chunk of OB*U vectors is loaded completely (every load of the chunk
+// before any of its stores: a src run starting above its own dst run reads the
+// old bytes, as the reference's ascending _acc loop does), then stored; the
+// stores are drained (vmcnt(0)) and the workgroup synchronised before the next
+// chunk or row loads.  Loads are non-temporal, served by the XCD's L2 (not the
+// CU's L1), where the earlier stores of this workgroup have landed.
+constexpr int kOrderedBS = 1024;
+template <class OP, int W, int U>
+__global__ __launch_bounds__(kOrderedBS) void k_ordered(const Desc d, const OP op) {
+    typedef typename Vec<W>::T V;
+    for (uint32_t r = 0; r < d.rows; ++r) {
+        int64_t so, dof;
+        row_offsets<0>(d, d.row0 + r, so, dof);
+        const char *sp = d.src + so;
+        char *dp = d.dst + dof;
+        for (uint32_t c0 = 0; c0 < d.nvec; c0 += (uint32_t)(kOrderedBS * U)) {
+            V a[U], b[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const uint32_t v = c0 + (uint32_t)(k * kOrderedBS) + threadIdx.x;
+                if (v < d.nvec) {
+                    a[k] = vload<W, true>(sp + (size_t)v * W);
+                    b[k] = a[k];
+                    if constexpr (OP::kReadsDst) b[k] = vload<W, true>(dp + (size_t)v * W);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const uint32_t v = c0 + (uint32_t)(k * kOrderedBS) + threadIdx.x;
+                if (v < d.nvec) vstore<W, false>(dp + (size_t)v * W, op.template apply<W>(b[k], a[k]));
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
         }
     }
 }
@@ -420,9 +428,10 @@ __global__ __launch_bounds__(64) void k_serial(const Desc d, const OP op) {
 // host launch plumbing
 //
 // Instantiation policy: the 2-D kernel of the ops on the headline paths
-// (f64, double complex, byte copy) carries every tuning variant (U 1/2/4/8,
-// 512-thread blocks, nt on/off); every other (op, kernel) pair is built once
-// with the default shape (16 B per thread per stream) and nt on/off.
+// (f64, double complex, byte copy) carries the tuning variants (U 1/2/4
+// vectors per thread, 64/128/256-thread blocks, nt on/off); every other
+// (op, kernel) pair is built once with the default shape (16 B per thread per
+// stream) and nt on/off.
 template <class OP> struct Tunable { static constexpr bool value = false; };
 template <> struct Tunable<AccDbl> { static constexpr bool value = true; };
 template <> struct Tunable<AccDcp> { static constexpr bool value = true; };
@@ -446,9 +455,6 @@ static int unroll_for(int W, int u16) {
     }
 }
 template <int W> struct DefaultU { static constexpr int value = W == 16 ? 1 : (W == 8 ? 2 : (W == 4 ? 4 : 8)); };
-// dynamic LDS per block of the rows kernels: lds_pad bytes per wave.  The kernels use no
-// LDS; the allocation only caps how many blocks a CU holds at once (160 KiB / bytes).
-template <int BS> static inline uint32_t lds_bytes() { return (uint32_t)g_tuning.lds_pad * (BS / 64); }
 
 template <class OP, int W, int U, int BS>
 static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt, hipStream_t st) {
@@ -463,11 +469,9 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
     e.items = (uint32_t)d.items;
     e.chunk_div = d.chunk_div;
     e.align_mask = d.align_mask;
-    e.xcd_per = 0;
     if constexpr (U == 1) {
-        // whole chunks, one block each, nt on, no experiment knob active
-        if (g_tuning.direct && nt && !d.align_mask && blocks == e.items && d.nvec % (uint32_t)BS == 0 &&
-            !g_tuning.cpol && !g_tuning.xcd && !g_tuning.order) {
+        // whole chunks, one block each, nt on
+        if (g_tuning.direct && nt && !d.align_mask && blocks == e.items && d.nvec % (uint32_t)BS == 0) {
             Desc2D f;
             f.src = d.src;
             f.dst = d.dst;
@@ -475,44 +479,12 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
             f.d_str = e.d_str;
             f.chunk_div = d.chunk_div;
             f.row0 = d.row0;
-            hipLaunchKernelGGL((k_rows2d<OP, W, BS>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, f, op);
+            hipLaunchKernelGGL((k_rows2d<OP, W, BS>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
             return hipGetLastError();
         }
     }
-    if constexpr (W == 16 && U == 1 && BS == 256 && std::is_same<OP, AccDbl>::value) {
-        if ((g_tuning.order == 1 || g_tuning.order == 2) && nt && !d.align_mask && blocks == e.items) {
-            const uint32_t rows = e.items / e.chunks;
-            uint32_t mult = 1;
-            if (g_tuning.order == 2) {   // an odd multiplier near rows * 0.618 that is coprime to rows
-                auto gcd = [](uint64_t a, uint64_t b) { while (b) { uint64_t t = a % b; a = b; b = t; } return a; };
-                mult = (uint32_t)(rows * 0.6180339887) | 1u;
-                while (mult > 1 && gcd(mult, rows) != 1) mult += 2;
-                if (mult >= rows) mult = 1;
-            }
-            if (g_tuning.order == 1)
-                hipLaunchKernelGGL((k_rows2_ord<OP, 1>), dim3((uint32_t)blocks), dim3(256), 0, st, e, op, rows, mult);
-            else
-                hipLaunchKernelGGL((k_rows2_ord<OP, 2>), dim3((uint32_t)blocks), dim3(256), 0, st, e, op, rows, mult);
-            return hipGetLastError();
-        }
-        if (g_tuning.xcd && nt && blocks == e.items && e.items % 8 == 0) {
-            e.xcd_per = e.items / 8;
-            hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true, true>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, e, op);
-            return hipGetLastError();
-        }
-        const int cp = g_tuning.cpol;
-        if (cp && !d.align_mask) {
-#define GAAMD_CPOL(LA, SA) \
-    if (cp == ((LA) | ((SA) << 8))) { \
-        hipLaunchKernelGGL((k_rows2_buf<OP, U, BS, LA, SA>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, e, op); \
-        return hipGetLastError(); }
-            GAAMD_CPOL(2, 2) GAAMD_CPOL(0, 2) GAAMD_CPOL(2, 0) GAAMD_CPOL(0, 0)
-            GAAMD_CPOL(16, 2) GAAMD_CPOL(2, 16) GAAMD_CPOL(18, 18) GAAMD_CPOL(3, 3) GAAMD_CPOL(1, 2)
-#undef GAAMD_CPOL
-        }
-    }
-    if (nt) hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, e, op);
-    else hipLaunchKernelGGL((k_rows2<OP, W, U, BS, false>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, e, op);
+    if (nt) hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
+    else hipLaunchKernelGGL((k_rows2<OP, W, U, BS, false>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
     return hipGetLastError();
 }
 
@@ -531,12 +503,12 @@ static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, int n
             }
             f.chunk_div = d.chunk_div;
             f.row0 = d.row0;
-            hipLaunchKernelGGL((k_rowsnd<OP, W, BS, LV>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, f, op);
+            hipLaunchKernelGGL((k_rowsnd<OP, W, BS, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
             return hipGetLastError();
         }
     }
-    if (nt) hipLaunchKernelGGL((k_rows<OP, W, U, BS, true, LV>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, d, op);
-    else hipLaunchKernelGGL((k_rows<OP, W, U, BS, false, LV>), dim3((uint32_t)blocks), dim3(BS), lds_bytes<BS>(), st, d, op);
+    if (nt) hipLaunchKernelGGL((k_rows<OP, W, U, BS, true, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, d, op);
+    else hipLaunchKernelGGL((k_rows<OP, W, U, BS, false, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, d, op);
     return hipGetLastError();
 }
 template <class OP, int W, int LV>
@@ -554,6 +526,11 @@ static hipError_t dispatch_w(int kind, int U, int BS, int nt, const Desc &d, con
     } else {
         if (kind == KK_SERIAL) {
             hipLaunchKernelGGL((k_serial<OP, W>), dim3(1), dim3(64), 0, st, d, op);
+            return hipGetLastError();
+        }
+        if (kind == KK_ORDERED) {
+            // 64 bytes per thread per stream: 64 KiB chunks, one load round trip each
+            hipLaunchKernelGGL((k_ordered<OP, W, 4 * DefaultU<W>::value>), dim3(1), dim3(kOrderedBS), 0, st, d, op);
             return hipGetLastError();
         }
         if (kind == KK_FLAT) {
@@ -595,13 +572,11 @@ static hipError_t dispatch_w(int kind, int U, int BS, int nt, const Desc &d, con
     case 1: return go_rows2<OP, W, 1, B>(d, op, blocks, nt, st); \
     case 2: return go_rows2<OP, W, 2, B>(d, op, blocks, nt, st); \
     case 4: return go_rows2<OP, W, 4, B>(d, op, blocks, nt, st); \
-    case 8: return go_rows2<OP, W, 8, B>(d, op, blocks, nt, st); \
     }
             switch (BS) {
             case 64: GAAMD_U(64) break;
             case 128: GAAMD_U(128) break;
             case 256: GAAMD_U(256) break;
-            case 512: GAAMD_U(512) break;
             }
 #undef GAAMD_U
         }
@@ -701,6 +676,85 @@ static void range_span(const int64_t *str, const uint32_t *cnt, int L, int64_t r
     }
 }
 
+// Byte offset of row r of one side (odometer digits over the levels).
+static int64_t row_start(const int64_t *str, const uint32_t *cnt, int L, uint64_t r) {
+    int64_t o = 0;
+    for (int j = 0; j < L; ++j) {
+        const uint32_t c = cnt[j] ? cnt[j] : 1;
+        o += (int64_t)(r % c) * str[j];
+        r /= c;
+    }
+    return o;
+}
+
+// How the rows of one call may be scheduled.  The reference applies them
+// strictly in odometer order, each row in ascending element order (comex.c:
+// 6936-6961 -> acc.h:137-143), so where bytes are shared the order decides the
+// result:
+//   OV_NONE     no byte of a dst row is touched by any other row (src or dst):
+//               any order gives the reference's bytes -> the parallel kernels;
+//   OV_ORDERED  dst rows share bytes with each other, or a src row shares bytes
+//               with a dst row, but no src run starts inside its own dst run
+//               below it -> rows in order, each row wave-parallel (k_ordered);
+//   OV_SERIAL   some row's src run starts below its dst run and reaches into it
+//               (s < d < s + row): element m reads bytes the same _acc loop
+//               wrote at m' < m, a recurrence -> one lane in reference order.
+//               (acc.h's loop reads each src element whole before its
+//               statements -- restrict, acc.h:106-122 -- so a src run at or
+//               above its dst run, in place included, only ever reads bytes
+//               not yet written: no recurrence there.)
+// Exact (row intervals of both sides, sorted) up to kExactRows rows in the
+// call; above that a bound on spans and on the per-row dst - src distance.
+enum { OV_NONE = 0, OV_ORDERED = 1, OV_SERIAL = 2 };
+constexpr uint64_t kExactRows = 1ull << 18;
+
+static int classify_rows(int64_t sb, const int64_t *ss, int64_t db, const int64_t *ds, const uint32_t *cn, int L,
+                         int64_t rb, uint64_t r0, uint64_t r1) {
+    const uint64_t n = r1 - r0;
+    // spans of the rows this call touches: a chunked caller (remote pack /
+    // unpack-acc) passes a row range and a packed base rebased so that row r0
+    // lands at its slice -- the full-range span of such a side reaches far
+    // outside the slice and would falsely meet the other side
+    int64_t slo, shi, dlo, dhi;
+    range_span(ss, cn, L, rb, r0, r1, slo, shi);
+    range_span(ds, cn, L, rb, r0, r1, dlo, dhi);
+    const bool same_layout = sb == db && !memcmp(ss, ds, sizeof(int64_t) * L);
+    const bool spans_meet = !same_layout && sb + slo < db + dhi && db + dlo < sb + shi;
+    const bool dst_may = n > 1 && rows_may_overlap(ds, cn, L, rb);
+    if (!spans_meet && !dst_may) return OV_NONE;
+    if (n > kExactRows) {
+        // bound: dst - src of a row is (db - sb) + sum_j digit_j * (ds_j - ss_j)
+        int64_t lo = db - sb, hi = db - sb;
+        for (int j = 0; j < L; ++j) {
+            const int64_t e = (ds[j] - ss[j]) * (int64_t)(cn[j] ? cn[j] - 1 : 0);
+            if (e < 0) lo += e; else hi += e;
+        }
+        if (spans_meet && hi > 0 && lo < rb) return OV_SERIAL;
+        return OV_ORDERED;
+    }
+    std::vector<std::pair<int64_t, uint32_t>> S(spans_meet ? n : 0), D(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        const int64_t s = sb + row_start(ss, cn, L, r0 + i), d = db + row_start(ds, cn, L, r0 + i);
+        if (s < d && d < s + rb) return OV_SERIAL;
+        D[i] = {d, (uint32_t)i};
+        if (spans_meet) S[i] = {s, (uint32_t)i};
+    }
+    std::sort(D.begin(), D.end());
+    for (uint64_t k = 1; k < n; ++k)
+        if (D[k].first < D[k - 1].first + rb) return OV_ORDERED;
+    if (spans_meet) {
+        std::sort(S.begin(), S.end());
+        for (const auto &x : D) {
+            // src rows with a start in (d - rb, d + rb) share bytes with this dst row;
+            // only the row's own src at the same address (dst = dst + a*dst) is harmless
+            auto it = std::lower_bound(S.begin(), S.end(), std::make_pair(x.first - rb + 1, (uint32_t)0));
+            for (; it != S.end() && it->first < x.first + rb; ++it)
+                if (it->second != x.second || it->first != x.first) return OV_ORDERED;
+        }
+    }
+    return OV_NONE;
+}
+
 void side_span_host(const int *stride, const int *count, int stride_levels, int64_t row_bytes,
                     int64_t *lo, int64_t *hi) {
     int64_t str[kMaxLevels];
@@ -748,47 +802,36 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         cn[L] = (uint32_t)count[j + 1];
         ++L;
     }
-    // ordering / aliasing: the reference applies rows strictly in order
-    const bool dst_overlap = rows_may_overlap(ds, cn, L, row_bytes);
-    bool src_dst_overlap = false;
-    {
-        // spans of the rows this call touches: a chunked caller (remote pack /
-        // unpack-acc) passes a row range and a packed base rebased so that row
-        // row_begin lands at its slice -- the full-range span of such a side
-        // reaches far outside the slice and would falsely overlap the other side
-        int64_t slo, shi, dlo, dhi;
-        range_span(ss, cn, L, row_bytes, row_begin, row_end, slo, shi);
-        range_span(ds, cn, L, row_bytes, row_begin, row_end, dlo, dhi);
-        const int64_t sb = (int64_t)(uintptr_t)src, db = (int64_t)(uintptr_t)dst;
-        const bool same_layout = (src == dst) && !memcmp(ss, ds, sizeof(int64_t) * L);
-        if (!same_layout && sb + slo < db + dhi && db + dlo < sb + shi) src_dst_overlap = true;
+    // merge level into the row when rows are back to back on both sides (only
+    // when the row is whole elements, so _acc truncation is unchanged), and level
+    // j+1 into level j when it continues it on both sides.  Both keep the
+    // reference's visiting order of every byte (a merged row is the rows it
+    // replaces, in order), so the ordering analysis below sees the same problem.
+    while (!partial && L > 0 && ss[0] == row_bytes && ds[0] == row_bytes && (count[0] % esz) == 0 &&
+           row_bytes * (int64_t)cn[0] < (1ll << 31)) {
+        row_bytes *= cn[0];
+        for (int j = 1; j < L; ++j) { ss[j - 1] = ss[j]; ds[j - 1] = ds[j]; cn[j - 1] = cn[j]; }
+        --L;
     }
-    const bool serial = dst_overlap || src_dst_overlap || tn.kind == KK_SERIAL;
-
-    if (!serial) {
-        // merge level into the row when rows are back to back on both sides
-        // (only when the row is whole elements, so _acc truncation is unchanged)
-        while (!partial && L > 0 && ss[0] == row_bytes && ds[0] == row_bytes && (count[0] % esz) == 0 &&
-               row_bytes * (int64_t)cn[0] < (1ll << 31)) {
-            row_bytes *= cn[0];
-            for (int j = 1; j < L; ++j) { ss[j - 1] = ss[j]; ds[j - 1] = ds[j]; cn[j - 1] = cn[j]; }
+    for (int j = 0; j + 1 < L;) {
+        if (ss[j + 1] == ss[j] * (int64_t)cn[j] && ds[j + 1] == ds[j] * (int64_t)cn[j] &&
+            (uint64_t)cn[j] * cn[j + 1] < (1ull << 31)) {
+            cn[j] *= cn[j + 1];
+            for (int k = j + 1; k + 1 < L; ++k) { ss[k] = ss[k + 1]; ds[k] = ds[k + 1]; cn[k] = cn[k + 1]; }
             --L;
-        }
-        // merge level j+1 into level j when it continues it on both sides
-        for (int j = 0; j + 1 < L;) {
-            if (ss[j + 1] == ss[j] * (int64_t)cn[j] && ds[j + 1] == ds[j] * (int64_t)cn[j] &&
-                (uint64_t)cn[j] * cn[j + 1] < (1ull << 31)) {
-                cn[j] *= cn[j + 1];
-                for (int k = j + 1; k + 1 < L; ++k) { ss[k] = ss[k + 1]; ds[k] = ds[k + 1]; cn[k] = cn[k + 1]; }
-                --L;
-            } else {
-                ++j;
-            }
+        } else {
+            ++j;
         }
     }
     rows = 1;
     for (int j = 0; j < L; ++j) rows *= cn[j];
     if (!partial) row_end = rows;
+
+    // ordering / aliasing: the reference applies rows strictly in order
+    const int ov = classify_rows((int64_t)(uintptr_t)src, ss, (int64_t)(uintptr_t)dst, ds, cn, L, row_bytes,
+                                 row_begin, row_end);
+    const bool serial = ov == OV_SERIAL || tn.kind == KK_SERIAL;
+    const bool ordered = !serial && (ov == OV_ORDERED || tn.kind == KK_ORDERED);
 
     // vector width: largest power of two <= 16 dividing every address and stride
     uint64_t a = (uint64_t)(uintptr_t)src | (uint64_t)(uintptr_t)dst | (uint64_t)row_bytes | 16;
@@ -828,7 +871,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     d.nvec = (uint32_t)(row_bytes / W);
     d.nvec_div = make_fastdiv(d.nvec);
 
-    int kind = serial ? KK_SERIAL : tn.kind;
+    int kind = serial ? KK_SERIAL : (ordered ? KK_ORDERED : tn.kind);
     if (kind == KK_AUTO) {
         kind = ((int64_t)d.nvec <= tn.flat_max_nvec) ? KK_FLAT : KK_ROWS;
         // rows that start off 128-byte lines on both sides: the flat kernel's waves cut rows
@@ -850,7 +893,6 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     // rows kernels: small blocks retire and free their CU slots independently;
     // on the headline shape 64/128/256/512/1024 threads measured
     // 6338/6268/6171/6020/5951 GB/s in a stand-alone probe (tools/h_shape_probe.hip).
-    // 512 only on the tunable 2-D path.
     int block = tn.block;
     if (block == 0) {
         // auto: one-wave blocks when every row starts 4 KiB-aligned on both sides,
@@ -861,7 +903,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         for (int j = 0; j < L; ++j) al |= (uint64_t)ss[j] | (uint64_t)ds[j];
         block = (al & 4095) ? 128 : 64;
     }
-    int U = unroll_for(W, 1), BS = (block == 512) ? 256 : block;
+    int U = unroll_for(W, 1), BS = block;
     if (kind == KK_ROWS && L <= 1 && W == 16 && tunable) {
         U = tn.unroll16;
         BS = block;
@@ -882,7 +924,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     uint64_t rows_per_launch = rows;
     if (kind == KK_ROWS) rows_per_launch = std::min<uint64_t>(rows, lim / d.chunks);
     if (kind == KK_FLAT) rows_per_launch = std::min<uint64_t>(rows, lim / d.nvec);
-    if (kind == KK_SERIAL) rows_per_launch = rows;
+    if (kind == KK_SERIAL || kind == KK_ORDERED) rows_per_launch = rows;
     if (rows_per_launch == 0) return -9;
 
     int launches = 0;
@@ -902,7 +944,6 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         } else {
             d.items = nr;
         }
-        if (tn.max_grid > 0 && blocks > (uint64_t)tn.max_grid) blocks = (uint64_t)tn.max_grid;
         if (blocks > lim) blocks = lim;
         if (!plan_only) {
             hipError_t e = dispatch(op, scale, W, kind, U, BS, tn.nontemporal, d, blocks, stream);
@@ -918,7 +959,8 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         info->unroll = (kind == KK_ROWS) ? U : 0;
         info->launches = launches;
         info->blocks = total_blocks;
-        info->block = (kind == KK_ROWS) ? BS : (kind == KK_FLAT ? flat_block_threads(W, tn) : 64);
+        info->block = (kind == KK_ROWS) ? BS
+                      : (kind == KK_FLAT ? flat_block_threads(W, tn) : (kind == KK_ORDERED ? kOrderedBS : 64));
         info->levels = L;
         info->aligned = d.align_mask ? 1 : 0;
     }

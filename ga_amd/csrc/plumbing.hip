@@ -119,8 +119,8 @@ int gaamd_last_launch(int *kind, int *width, int *unroll, int *launches, unsigne
     return 0;
 }
 
-int gaamd_kernel_counts(unsigned long long counts[4]) {
-    for (int k = 0; k < 4; ++k) counts[k] = kernel_count(k);
+int gaamd_kernel_counts(unsigned long long counts[5]) {
+    for (int k = 0; k < kKinds; ++k) counts[k] = kernel_count(k);
     return 0;
 }
 
@@ -130,15 +130,10 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "unroll16")) return &t.unroll16;
     if (!strcmp(key, "nontemporal")) return &t.nontemporal;
     if (!strcmp(key, "flat_max_nvec")) return &t.flat_max_nvec;
-    if (!strcmp(key, "max_grid")) return &t.max_grid;
     if (!strcmp(key, "block")) return &t.block;
     if (!strcmp(key, "align")) return &t.align;
-    if (!strcmp(key, "cpol")) return &t.cpol;
-    if (!strcmp(key, "xcd")) return &t.xcd;
-    if (!strcmp(key, "order")) return &t.order;
     if (!strcmp(key, "direct")) return &t.direct;
     if (!strcmp(key, "flat_nt")) return &t.flat_nt;
-    if (!strcmp(key, "lds_pad")) return &t.lds_pad;
     if (!strcmp(key, "flat_shape")) return &t.flat_shape;
     if (!strcmp(key, "flat_line_min")) return &t.flat_line_min;
     if (!strcmp(key, "wide_unaligned")) return &t.wide_unaligned;
@@ -156,10 +151,9 @@ int gaamd_set_tuning(const char *key, int value) {
     }
     int *f = tuning_field(key);
     if (!f) return -1;
-    if (!strcmp(key, "unroll16") && value != 1 && value != 2 && value != 4 && value != 8) return -1;
+    if (!strcmp(key, "unroll16") && value != 1 && value != 2 && value != 4) return -1;
     if (!strcmp(key, "flat_shape") && value != 0 && value != 1) return -1;
-    if (!strcmp(key, "lds_pad") && (value < 0 || value > 40960)) return -1;
-    if (!strcmp(key, "block") && value != 0 && value != 64 && value != 128 && value != 256 && value != 512) return -1;
+    if (!strcmp(key, "block") && value != 0 && value != 64 && value != 128 && value != 256) return -1;
     const int old = *f;
     *f = value;
     return old;

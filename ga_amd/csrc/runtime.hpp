@@ -75,7 +75,7 @@ struct alignas(64) NodeShm {
     std::atomic<uint64_t> bar_count;
     std::atomic<uint64_t> bar_gen;
     char pad[40];
-    // done[s][t]: requests from s applied by t (monotonic)
+    // done[s][t]: requests from s applied by t (monotonic); s, t = positions on the node
     std::atomic<uint64_t> done[kMaxRanks][kMaxRanks];
     Inbox inbox[1];                  // [size] follows; then boot data area
 };
@@ -109,10 +109,16 @@ struct Runtime {
     // nodes (hosts): ranks of one node share the node shm and map each other's HBM
     int nnodes = 1, node = 0, node_size = 1;
     std::vector<int> node_of;                  // node index of every rank
+    std::vector<int> node_index;               // every rank's position on its node (node shm slots)
+    int li(int q) const { return node_index.empty() ? q : node_index[q]; }
     bool same_node(int q) const { return node_of.empty() || node_of[q] == node; }
     hipStream_t stream = nullptr;              // primary stream (= streams[0])
     std::vector<hipStream_t> streams;          // COMEX_AMD_STREAMS streams (sched.cpp)
-    bool blocking_sync = false;     // COMEX_AMD_BLOCKING_SYNC
+    // COMEX_AMD_BLOCKING_SYNC (default 1): a blocking call returns once its kernel
+    // has finished, i.e. src is reusable and a get's dst holds the data, as the
+    // reference's blocking calls promise; 0 is the documented
+    // opt-out where blocking calls are only stream-ordered
+    bool blocking_sync = true;
     int debug = 0;                  // COMEX_AMD_DEBUG: trace transfers on stderr
     // bootstrap
     gaamd_allgather_fn ag = nullptr;
@@ -134,6 +140,10 @@ struct Runtime {
     std::vector<char *> peer_staging;   // mapped staging of every rank
     std::vector<uint64_t> posted;       // requests posted to each target
     std::vector<uint64_t> stage_head;   // per-target staging ring write cursor
+    // per target: a put/get kernel addressing that rank's HBM through its IPC
+    // mapping may still run on one of our streams; a following remote
+    // accumulate (applied by the owner's progress thread) must wait for it
+    std::vector<uint8_t> direct_pending;
     std::thread progress;
     std::atomic<bool> stop{false};
     std::mutex launch_mu;

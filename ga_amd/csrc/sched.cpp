@@ -97,6 +97,7 @@ void sched_sync_all() {
     // (polling hipStreamQuery instead measured the same ≈13 µs acc + fence
     // latency: the floor is the GPU's launch-to-completion, not the host wake-up)
     for (hipStream_t s : r.streams) GA_HIP(hipStreamSynchronize(s));
+    for (uint8_t &p : r.direct_pending) p = 0;   // every put/get kernel has finished
     g_hist.clear();
     g_base = -1;
 }

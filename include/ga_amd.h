@@ -43,6 +43,8 @@ int gaamd_set_bootstrap(int rank, int size, int local_rank,
 int gaamd_bootstrap_selftest(int rounds);
 int gaamd_rank(void);
 int gaamd_size(void);
+/* HIP device of this rank after comex_init (COMEX_AMD_DEVICE or local rank mod devices) */
+int gaamd_device(void);
 /* nodes: ranks sharing a host (or the same COMEX_AMD_NODE value) map each other's
    HBM; ranks on different nodes exchange the MPI-PR messages over TCP (wire.cpp).
    After bootstrap: this rank's node index, the node count, ranks on this node. */
@@ -62,7 +64,7 @@ int gaamd_unpack(const void *packed, void *dst, const int *dst_stride, const int
 int gaamd_unpack_acc(int op, const void *scale, const void *packed, void *dst,
                      const int *dst_stride, const int *count, int stride_levels, void *stream);
 /* The launch plan of a strided operation without launching anything (no GPU
- * needed): plan[0..7] = {kind (1 rows, 2 flat, 3 serial), vector width, unroll,
+ * needed): plan[0..7] = {kind (1 rows, 2 flat, 3 serial, 4 ordered), vector width, unroll,
  * threads per block, launches, blocks, stride levels after merging, chunk grid
  * aligned}; row_end = ~0 for all rows.  Returns 0 or the launcher's error code. */
 int gaamd_plan_strided(int op, const void *src, const int *src_stride, const void *dst, const int *dst_stride,
@@ -71,11 +73,13 @@ int gaamd_plan_strided(int op, const void *src, const int *src_stride, const voi
 /* kind / vector width / unroll / launches / blocks of the last kernel-level call */
 int gaamd_last_launch(int *kind, int *width, int *unroll, int *launches,
                       unsigned long long *blocks);
-/* kernel launches since start, by kind: counts[0..3] = {unused, rows, flat,
- * serial}, every caller of this process (user calls, progress thread, wire) */
-int gaamd_kernel_counts(unsigned long long counts[4]);
-/* keys: "kind" (0 auto,1 rows,2 flat,3 serial), "unroll16", "nontemporal",
- * "flat_max_nvec", "max_grid"; returns the previous value or -1 */
+/* kernel launches since start, by kind: counts[0..4] = {unused, rows, flat,
+ * serial, ordered}, every caller of this process (user calls, progress thread, wire) */
+int gaamd_kernel_counts(unsigned long long counts[5]);
+/* keys: "kind" (0 auto, 1 rows, 2 flat, 3 serial, 4 ordered), "unroll16" (1/2/4),
+ * "nontemporal", "block" (0 auto/64/128/256), "flat_max_nvec", "align", "direct",
+ * "flat_nt", "flat_shape", "flat_line_min", "wide_unaligned", "streams";
+ * returns the previous value or -1 */
 int gaamd_set_tuning(const char *key, int value);
 int gaamd_get_tuning(const char *key);
 

@@ -50,7 +50,13 @@ typedef struct { float real, imag; } ora_scpl;
 
 /* acc.h:106-154, HAVE_BLAS == 0.  A += B*C for real types;
  * A.real += (B.real*C.real) - (B.imag*C.imag);
- * A.imag += (B.real*C.imag) + (B.imag*C.real)   for complex (B = src, C = scale). */
+ * A.imag += (B.real*C.imag) + (B.imag*C.real)   for complex (B = src, C = scale).
+ * acc.h declares dst/src `restrict` (acc.h:106-110, 121-122): the compiled loop
+ * reads B once per element for both statements, so B is read into `b` first --
+ * the same bytes as acc.h whenever src and dst do not overlap, and the compiled
+ * reference's bytes (oracle/_ref, tests/golden alias cases) where a caller
+ * aliases them (a patch accumulated onto itself), which restrict leaves to the
+ * compiler. */
 int ora_acc(int op, int bytes, void *dst, const void *src, const void *scale)
 {
 #define ORA_REG(CT)                                                           \
@@ -66,8 +72,9 @@ int ora_acc(int op, int bytes, void *dst, const void *src, const void *scale)
         CT *it = (CT *)dst; const CT *v = (const CT *)src;                    \
         const CT s = *(const CT *)scale;                                      \
         for (m = 0; m < m_lim; ++m) {                                         \
-            it[m].real += (v[m].real * s.real) - (v[m].imag * s.imag);        \
-            it[m].imag += (v[m].real * s.imag) + (v[m].imag * s.real);        \
+            const CT b = v[m];                                                \
+            it[m].real += (b.real * s.real) - (b.imag * s.imag);              \
+            it[m].imag += (b.real * s.imag) + (b.imag * s.real);              \
         }                                                                     \
     }
     switch (op) {

@@ -145,10 +145,55 @@ def cases():
     c["dst_stride"] = [0]           # every row onto the same run
     c["dst_bytes"] = 5 * 4
     out.append(c)
+    out.extend(alias_cases())
+    return out
+
+
+def alias_case(name, op, count, src_stride, dst_stride, src_off, dst_off, nbytes):
+    """src and dst inside ONE buffer (the dst buffer): comex_accs on a patch of an
+    array into another patch of the same array, where the reference's row and
+    element order (comex.c:6936-6961, acc.h:137-143) decides the bytes wherever
+    the two share memory.  `alias` cases carry no src array: src = dst + src_off."""
+    L = len(count) - 1
+    return dict(name=name, op=op, count=list(count), levels=L, src_stride=list(src_stride),
+                dst_stride=list(dst_stride), src_off=src_off, dst_off=dst_off, src_bytes=0, dst_bytes=nbytes,
+                edge=None, alias=True)
+
+
+def alias_cases():
+    out = []
+    e = 8
+    ld = 64 * e
+    # columns 0..15 into columns 16..31 of one ld-64 array: interleaved spans, no byte shared
+    out.append(alias_case("dbl_alias_columns", DBL, [16 * e, 40], [ld], [ld], 0, 16 * e, ld * 40))
+    # src row i is dst row i+1 (written later) / dst row i-1 (written earlier)
+    out.append(alias_case("dbl_alias_next_row", DBL, [40 * e, 30], [ld], [ld], ld, 0, ld * 32))
+    out.append(alias_case("dbl_alias_prev_row", DBL, [40 * e, 30], [ld], [ld], 0, ld, ld * 32))
+    # a row's src run one element below its dst run: a recurrence inside one _acc loop
+    out.append(alias_case("dbl_alias_shift_down", DBL, [40 * e, 12], [ld], [ld], 0, e, ld * 13))
+    # one element above: element m reads element m+1's old value
+    out.append(alias_case("dbl_alias_shift_up", DBL, [40 * e, 12], [ld], [ld], e, 0, ld * 13))
+    # a 3-D patch onto itself shifted by one plane and one row
+    out.append(alias_case("flt_alias_3d_shift", FLT, [24 * 4, 6, 5], [32 * 4, 32 * 4 * 8], [32 * 4, 32 * 4 * 8],
+                          32 * 4 * 8 + 32 * 4, 0, 32 * 4 * 8 * 7))
+    # in place (src is dst): real forms are dst + a*dst; the complex forms' second
+    # statement reads the real part the first one wrote (acc.h:47-49)
+    for op in (DBL, CPL, DCP, INT):
+        es = ESZ[op]
+        out.append(alias_case(f"{NAMES[op]}_alias_inplace", op, [33 * es, 9], [48 * es], [48 * es], 0, 0,
+                              48 * es * 9))
+    # complex src half an element above / a quarter element above its dst run
+    out.append(alias_case("dcp_alias_half_up", DCP, [20 * 16, 7], [32 * 16], [32 * 16], 8, 0, 32 * 16 * 8))
+    out.append(alias_case("dcp_alias_quarter_up", DCP, [20 * 16, 7], [32 * 16], [32 * 16], 4 + 16, 16,
+                          32 * 16 * 8))
+    out.append(alias_case("cpl_alias_half_down", CPL, [20 * 8, 7], [32 * 8], [32 * 8], 0, 4, 32 * 8 * 8))
+    # dst rows overlapping each other AND the src rows (zero dst stride onto the first row)
+    out.append(alias_case("lng_alias_zero_dst_stride", LNG, [12 * 8, 9], [16 * 8], [0], 16 * 8, 0, 16 * 8 * 10))
     return out
 
 
 def make_inputs(case):
+    """(src, dst) byte buffers; an alias case has an empty src (its src is in dst)."""
     op = case["op"]
     src = fill_bytes(op, case["src_bytes"], SEED)
     dst = fill_bytes(op, case["dst_bytes"], SEED + 1)

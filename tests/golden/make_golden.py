@@ -49,6 +49,8 @@ def full_size_configs():
 
 
 def run_ref(ref, case, src, dst):
+    if case.get("alias"):
+        src = dst   # src = dst buffer + src_off: the reference's _acc on aliased memory
     ref.accs(case["op"], C.SCALE[case["op"]], src, case["src_off"], case["src_stride"], dst, case["dst_off"],
              case["dst_stride"], case["count"], case["levels"])
 
@@ -65,8 +67,8 @@ def main():
         run_ref(ref, case, src, out)
         # the restatement must agree bit for bit before anything is committed
         chk = dst.copy()
-        ora.accs(case["op"], C.SCALE[case["op"]], src, case["src_off"], case["src_stride"], chk, case["dst_off"],
-                 case["dst_stride"], case["count"], case["levels"])
+        ora.accs(case["op"], C.SCALE[case["op"]], chk if case.get("alias") else src, case["src_off"],
+                 case["src_stride"], chk, case["dst_off"], case["dst_stride"], case["count"], case["levels"])
         assert np.array_equal(chk, out), case["name"]
         n = case["name"]
         arrays[f"{n}/src"] = src

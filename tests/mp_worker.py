@@ -90,6 +90,8 @@ def main():
         armci_test_acc_ref(L, rank, size)
     elif mode == "garef":
         ga_ref_test(L, rank, size)
+    elif mode == "order":
+        order_test(L, rank, size)
     else:
         remote_test(L, rank, size)
     print(f"RANK {rank} OK", flush=True)
@@ -105,6 +107,9 @@ def remote_test(L, rank, size):
     ora = Oracle()
     DBL = 38
     assert ga_amd.comex_init() == 0
+    if os.environ.get("TEST_DISTINCT_DEVICES"):
+        # one rank per GPU: the peer segments are opened by IPC on another device (xGMI)
+        assert L.gaamd_device() == rank, (L.gaamd_device(), rank)
     # each rank owns a 300 x 260 f64 block (column-major, ld 300)
     ld, ncol = 300, 260
     nbytes = ld * ncol * 8
@@ -253,6 +258,49 @@ def remote_test(L, rank, size):
 
     ga_amd.comex_barrier()
     assert ga_amd.comex_free(seg2[rank]) == 0
+    assert ga_amd.comex_free(seg[rank]) == 0
+    ga_amd.comex_finalize()
+
+
+def order_test(L, rank, size):
+    """A non-blocking HBM-source put of 32 MiB into the next rank's segment, then --
+    with no fence -- a strided accumulate into the same patch.  The put kernel runs
+    on this rank's stream through the IPC mapping, the accumulate is applied by the
+    owner's progress thread on the owner's stream: the library must order the
+    accumulate's pack (and so its post) after the put, as the reference's
+    synchronous same-node put and accumulate are (comex.c:6084-6101, 6241-6260).
+    The owner checks dst == A + 2*B bit for bit (one fixed order: put, then acc)."""
+    import ga_amd
+    DBL = 38
+    assert ga_amd.comex_init() == 0
+    rows, rowb, ldb = 1024, 32768, 32768 + 4096   # 32 MiB of payload, strided rows
+    nbytes = rows * ldb
+    seg = ga_amd.comex_malloc(nbytes, size)
+    nxt, prv = (rank + 1) % size, (rank - 1) % size
+    a, b = ga_amd.DeviceBuffer(nbytes), ga_amd.DeviceBuffer(nbytes)
+    ss, cnt = ga_amd.int_array([ldb]), ga_amd.int_array([rowb, rows])
+    for it in range(3):
+        ga_amd.fill(a.ptr, nbytes // 8, 0, 7000 + 10 * rank + it)
+        ga_amd.fill(b.ptr, nbytes // 8, 0, 8000 + 10 * rank + it)
+        ga_amd.sync()
+        ga_amd.comex_barrier()
+        h = ctypes.c_int(-1)
+        assert L.comex_nbputs(ctypes.c_void_p(a.ptr), ss, ctypes.c_void_p(seg[nxt]), ss, cnt, 1, nxt, 0,
+                              ctypes.byref(h)) == 0
+        assert ga_amd.comex_accs(DBL, 2.0, b.ptr, [ldb], seg[nxt], [ldb], [rowb, rows], 1, nxt) == 0
+        assert L.comex_wait(ctypes.byref(h)) == 0
+        ga_amd.comex_barrier()
+        got = np.zeros(nbytes // 8, dtype=np.float64)
+        assert L.comex_get(ctypes.c_void_p(seg[rank]), got.ctypes.data_as(ctypes.c_void_p), nbytes, rank, 0) == 0
+        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+        import cases as C
+        A = C.fill_real(np.float64, nbytes // 8, 7000 + 10 * prv + it).reshape(rows, ldb // 8)
+        B = C.fill_real(np.float64, nbytes // 8, 8000 + 10 * prv + it).reshape(rows, ldb // 8)
+        g = got.reshape(rows, ldb // 8)[:, :rowb // 8]
+        want = A[:, :rowb // 8] + B[:, :rowb // 8] * 2.0
+        assert np.array_equal(g.view(np.uint64), want.view(np.uint64)), f"rank {rank}: round {it}: acc overtook put"
+        say(rank, f"order round {it} checked")
+    ga_amd.comex_barrier()
     assert ga_amd.comex_free(seg[rank]) == 0
     ga_amd.comex_finalize()
 

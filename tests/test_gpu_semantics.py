@@ -1,0 +1,280 @@
+"""ComEx completion semantics and the launcher's ordering analysis on the MI355X,
+through the C ABI, against the oracle (bit-exact).
+
+* Patches of one array accumulated into other patches of it: interleaved spans
+  with no shared byte run the parallel rows kernel at the headline size; rows
+  that truly share bytes keep the reference's order (comex.c:6936-6961).
+* Blocking calls complete locally before returning (SURVEY.md 8(b) "Ownership /
+  lifetime"): src is reusable, a get's destination holds the data.
+* Non-blocking io-vector handles cover every kernel of the call.
+* Pageable host sources are pinned for one call only (registration lifetime).
+"""
+import ctypes
+import time
+
+import numpy as np
+import pytest
+
+import cases as C
+import ga_amd
+
+pytestmark = pytest.mark.gpu
+HBM_PEAK_GBS = 8000.0
+
+
+def _host(buf, n, dtype=np.uint8):
+    return np.ctypeslib.as_array((ctypes.c_uint8 * (n * np.dtype(dtype).itemsize)).from_address(buf)).view(dtype)
+
+
+def test_interleaved_columns_of_one_array_full_size(gpu_lib, oracle):
+    """Columns 0..2047 of a 4096-row, ld-8192 f64 array accumulated into its
+    columns 2048..4095 (the spans interleave, no byte is shared): the rows kernel,
+    bit-exact against the oracle applying the same call to the same buffer, and
+    >= 0.75 of HBM peak over 40 launches rotating 4 such arrays (1 GiB: beyond the
+    256 MiB Infinity Cache)."""
+    L = gpu_lib
+    ld, rows, w = 8192, 4096, 2048
+    nbytes = ld * 8 * rows
+    count, stride = [w * 8, rows], [ld * 8]
+    host = C.fill_bytes(C.DBL, nbytes, 77)
+    arrays = [ga_amd.DeviceBuffer(nbytes) for _ in range(4)]
+    try:
+        arrays[0].upload(host)
+        assert ga_amd.comex_accs(C.DBL, C.SCALE[C.DBL], arrays[0].ptr, stride, arrays[0].ptr + w * 8, stride,
+                                 count, 1, 0) == 0
+        info = ga_amd.last_launch()
+        assert info["kind"] == "rows" and info["width"] == 16, info
+        got = arrays[0].download(np.uint8, nbytes)
+        want = host.copy()
+        oracle.accs(C.DBL, C.SCALE[C.DBL], want, 0, stride, want, w * 8, stride, count, 1)
+        assert np.array_equal(got, want)
+        for a in arrays[1:]:
+            ga_amd.fill(a.ptr, nbytes // 8, 0, 78)
+        ga_amd.sync()
+        keep, sp = ga_amd.scale_buffer(C.DBL, C.SCALE[C.DBL])
+        ss, cnt = ga_amd.int_array(stride), ga_amd.int_array(count)
+        handles = []
+
+        def launch(i):
+            a = arrays[i % 4]
+            h = ctypes.c_int(-1)
+            assert L.comex_nbaccs(C.DBL, sp, ctypes.c_void_p(a.ptr), ss, ctypes.c_void_p(a.ptr + w * 8), ss, cnt,
+                                  1, 0, 0, ctypes.byref(h)) == 0
+            handles.append(h)
+            if len(handles) > 16:   # keep the handle table short: wait for the launch 16 back
+                assert L.comex_wait(ctypes.byref(handles.pop(0))) == 0
+
+        t_end = time.perf_counter() + 0.3
+        i = 0
+        while time.perf_counter() < t_end:
+            launch(i)
+            i += 1
+        assert L.comex_wait_all(0) == 0
+        handles.clear()
+        ev0, ev1 = L.gaamd_event_create(), L.gaamd_event_create()
+        st = L.gaamd_stream()
+        L.gaamd_event_record(ev0, st)
+        L.gaamd_join()
+        n = 40
+        for i in range(n):
+            launch(i)
+        L.gaamd_join()
+        L.gaamd_event_record(ev1, st)
+        assert L.comex_wait_all(0) == 0
+        handles.clear()
+        ms = L.gaamd_event_elapsed_ms(ev0, ev1)
+        L.gaamd_event_destroy(ev0)
+        L.gaamd_event_destroy(ev1)
+        gbs = 3 * w * 8 * rows * n / (ms * 1e-3) / 1e9
+        print(f"interleaved columns: {gbs:.0f} GB/s = {gbs / HBM_PEAK_GBS:.3f} of HBM peak")
+        assert gbs >= 0.75 * HBM_PEAK_GBS, gbs
+    finally:
+        for a in arrays:
+            a.free()
+
+
+def _alias_configs(rng):
+    """(op, count, src_stride, dst_stride, src_off, dst_off, nbytes) of one buffer"""
+    out = []
+    for op in (C.DBL, C.DCP, C.FLT, C.LNG):
+        e = C.ESZ[op]
+        for _ in range(6):
+            w = int(rng.integers(1, 300)) * e
+            rows = int(rng.integers(2, 60))
+            ld = w + e * int(rng.integers(-w // e + 1, 40))   # rows may overlap each other
+            ld = max(e, ld)
+            dld = ld if rng.random() < 0.6 else max(e, ld + e * int(rng.integers(-3, 4)))
+            so = e * int(rng.integers(0, 80))
+            do = e * int(rng.integers(0, 80))
+            nbytes = max(so + ld * (rows - 1) + w, do + dld * (rows - 1) + w) + 64
+            out.append((op, [w, rows], [ld], [dld], so, do, nbytes))
+        # 3-D: a patch onto itself shifted by one plane
+        w, r1, r2 = 32 * e, 5, 4
+        s1, s2 = 40 * e, 40 * e * 6
+        out.append((op, [w, r1, r2], [s1, s2], [s1, s2], s2, 0, s2 * 5 + 64))
+    return out
+
+
+def test_patches_of_one_buffer_match_the_reference_order(gpu_lib, oracle):
+    """Random 2-D/3-D patches of ONE buffer accumulated into other patches of it
+    (rows overlapping each other, src rows meeting dst rows above or below, in
+    place): whichever class the launcher picks (parallel, ordered, one-lane
+    serial), the bytes equal the oracle's sequential row/element order
+    (restrict semantics of acc.h, pinned by the alias golden cases)."""
+    rng = np.random.default_rng(31337)
+    kinds = {}
+    for op, count, ss, ds, so, do, nbytes in _alias_configs(rng):
+        host = C.fill_bytes(op, nbytes, int(rng.integers(1, 1 << 30)))
+        b = ga_amd.DeviceBuffer(nbytes)
+        b.upload(host)
+        assert ga_amd.comex_accs(op, C.SCALE[op], b.ptr + so, ss, b.ptr + do, ds, count, len(ss), 0) == 0
+        kind = ga_amd.last_launch()["kind"]
+        kinds[kind] = kinds.get(kind, 0) + 1
+        want = host.copy()
+        oracle.accs(op, C.SCALE[op], want, so, ss, want, do, ds, count, len(ss))
+        got = b.download(np.uint8, nbytes)
+        b.free()
+        assert np.array_equal(got, want), (op, count, ss, ds, so, do, kind)
+    assert "ordered" in kinds, kinds
+
+
+def test_ordered_kernel_large_overlapping_rows(gpu_lib, oracle):
+    """Every row of a 2048-row f64 patch into the SAME 64 KiB run (zero dst
+    stride): rows in order, each row by the whole 16-wave workgroup -- not one
+    lane; bit-exact and at least 3 GB/s (the one-lane kernel ran ~0.06 GB/s)."""
+    rows, w = 2048, 8192
+    src = C.fill_bytes(C.LNG, rows * w * 8, 5)
+    dst = C.fill_bytes(C.LNG, w * 8, 6)
+    sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+    sb.upload(src)
+    db.upload(dst)
+    t0 = time.perf_counter()
+    assert ga_amd.comex_accs(C.LNG, -3, sb.ptr, [w * 8], db.ptr, [0], [w * 8, rows], 1, 0) == 0
+    dt = time.perf_counter() - t0
+    assert ga_amd.last_launch()["kind"] == "ordered"
+    want = dst.copy()
+    oracle.accs(C.LNG, -3, src, 0, [w * 8], want, 0, [0], [w * 8, rows], 1)
+    assert np.array_equal(db.download(np.uint8, dst.size), want)
+    gbs = 3 * rows * w * 8 / dt / 1e9
+    print(f"ordered kernel: {gbs:.1f} GB/s (whole blocking call)")
+    assert gbs > 3, gbs
+
+
+def test_blocking_accs_returns_after_src_is_consumed(gpu_lib, oracle):
+    """A blocking comex_accs with an HBM src returns only once src is reusable
+    (the reference's blocking contract): overwriting src at once from the user's
+    own HIP stream -- which is not ordered after the library's streams -- leaves
+    the accumulated result unchanged.  Headline-shaped patch, three rounds."""
+    L = gpu_lib
+    user = L.gaamd_stream_create()
+    ld, rows, w = 8192, 1024, 2048
+    sbytes = ld * 8 * (rows - 1) + w * 8
+    count, stride = [w * 8, rows], [ld * 8]
+    sb, db = ga_amd.DeviceBuffer(sbytes), ga_amd.DeviceBuffer(sbytes)
+    try:
+        ga_amd.fill(sb.ptr, sbytes // 8, 0, 500)
+        ga_amd.fill(db.ptr, sbytes // 8, 0, 600)
+        ga_amd.sync()
+        want = db.download(np.uint8, sbytes)
+        for it in range(3):
+            src_host = C.fill_real(np.float64, sbytes // 8, 500 + it).view(np.uint8)
+            assert ga_amd.comex_accs(C.DBL, C.SCALE[C.DBL], sb.ptr, stride, db.ptr, stride, count, 1, 0) == 0
+            assert L.gaamd_fill(ctypes.c_void_p(sb.ptr), sbytes // 8, 0, 501 + it, user) == 0   # src reused at once
+            oracle.accs(C.DBL, C.SCALE[C.DBL], src_host, 0, stride, want, 0, stride, count, 1)
+            assert L.gaamd_sync(user) == 0
+        ga_amd.sync()
+        assert np.array_equal(db.download(np.uint8, sbytes), want)
+    finally:
+        sb.free()
+        db.free()
+        L.gaamd_stream_destroy(user)
+
+
+def test_blocking_get_into_pinned_memory_is_complete_on_return(gpu_lib):
+    """comex_gets into pinned host memory (comex_malloc_local / ARMCI_Malloc_local,
+    used in place through its device mapping) holds the data when the call
+    returns -- read by the CPU with no fence in between."""
+    L = gpu_lib
+    ld, rows, w = 4096, 2048, 3000
+    nbytes = ld * 8 * rows
+    dev = ga_amd.DeviceBuffer(nbytes)
+    pin = L.comex_malloc_local(w * 8 * rows)
+    try:
+        for it in range(3):
+            ga_amd.fill(dev.ptr, nbytes // 8, 3, 900 + it)
+            ga_amd.sync()
+            ctypes.memset(pin, 0, w * 8 * rows)
+            assert ga_amd.comex_gets(dev.ptr, [ld * 8], pin, [w * 8], [w * 8, rows], 1, 0) == 0
+            got = _host(pin, w * rows, np.int64).reshape(rows, w).copy()   # no fence
+            full = C.fill_real(np.int64, nbytes // 8, 900 + it).reshape(rows, ld)
+            assert np.array_equal(got, full[:, :w]), it
+    finally:
+        L.comex_free_local(ctypes.c_void_p(pin))
+        dev.free()
+
+
+def test_nb_vector_handle_covers_every_kernel(gpu_lib):
+    """comex_nbgetv of two descriptors (their io-vector kernels may land on
+    different library streams) into pinned host memory: after comex_wait on the
+    one handle the CPU sees every pair, with no fence."""
+    L = gpu_lib
+    n, nbytes = 60000, 64
+    src = np.random.default_rng(3).integers(0, 256, n * nbytes, dtype=np.uint8)
+    sb = ga_amd.DeviceBuffer(src.size)
+    sb.upload(src)
+    pin = L.comex_malloc_local(src.size)
+    try:
+        ctypes.memset(pin, 0, src.size)
+        perm = np.random.default_rng(4).permutation(n).astype(np.uint64)
+        half = n // 2
+        s_addr = np.uint64(sb.ptr) + np.arange(n, dtype=np.uint64) * np.uint64(nbytes)
+        d_addr = np.uint64(pin) + perm * np.uint64(nbytes)
+        descs = (ga_amd.GIOV * 2)()
+        keep = []
+        for k, (a, b) in enumerate(((0, half), (half, n))):
+            sa, da = np.ascontiguousarray(s_addr[a:b]), np.ascontiguousarray(d_addr[a:b])
+            keep += [sa, da]
+            descs[k].src = ctypes.cast(ctypes.c_void_p(sa.ctypes.data), ctypes.POINTER(ctypes.c_void_p))
+            descs[k].dst = ctypes.cast(ctypes.c_void_p(da.ctypes.data), ctypes.POINTER(ctypes.c_void_p))
+            descs[k].count, descs[k].bytes = b - a, nbytes
+        h = ctypes.c_int(-1)
+        assert L.comex_nbgetv(ctypes.cast(descs, ctypes.c_void_p), 2, 0, 0, ctypes.byref(h)) == 0
+        assert L.comex_wait(ctypes.byref(h)) == 0
+        got = _host(pin, src.size).reshape(n, nbytes).copy()   # no fence
+        assert np.array_equal(got[perm.astype(np.int64)], src.reshape(n, nbytes))
+    finally:
+        L.comex_free_local(ctypes.c_void_p(pin))
+        sb.free()
+
+
+def test_pageable_sources_sharing_pages_back_to_back(gpu_lib, oracle):
+    """Two non-blocking accumulates whose pageable host sources share pages, issued
+    back to back with the first kernel possibly in flight: a source's pages are
+    pinned for its own call only (a registration that outlived its call could be
+    shadowed by the next call's and unmapped under the kernel -- the illegal access
+    round 1 fixed).  Both results bit-exact."""
+    L = gpu_lib
+    rows, w, ld = 512, 2048, 2048 + 64
+    host = C.fill_bytes(C.DBL, ld * 8 * (2 * rows + 8), 12)
+    count, stride = [w * 8, rows], [ld * 8]
+    off2 = ld * 8 * rows // 2 + 8 * 3                     # second source starts mid-way: pages shared
+    d1, d2 = ga_amd.DeviceBuffer(ld * 8 * rows), ga_amd.DeviceBuffer(ld * 8 * rows)
+    dh1 = C.fill_bytes(C.DBL, ld * 8 * rows, 13)
+    dh2 = C.fill_bytes(C.DBL, ld * 8 * rows, 14)
+    d1.upload(dh1)
+    d2.upload(dh2)
+    keep, sp = ga_amd.scale_buffer(C.DBL, C.SCALE[C.DBL])
+    ss, cnt = ga_amd.int_array(stride), ga_amd.int_array(count)
+    h1, h2 = ctypes.c_int(-1), ctypes.c_int(-1)
+    for _ in range(3):
+        assert L.comex_nbaccs(C.DBL, sp, ctypes.c_void_p(host.ctypes.data), ss, ctypes.c_void_p(d1.ptr), ss, cnt, 1,
+                              0, 0, ctypes.byref(h1)) == 0
+        assert L.comex_nbaccs(C.DBL, sp, ctypes.c_void_p(host.ctypes.data + off2), ss, ctypes.c_void_p(d2.ptr), ss,
+                              cnt, 1, 0, 0, ctypes.byref(h2)) == 0
+        assert L.comex_wait(ctypes.byref(h1)) == 0 and L.comex_wait(ctypes.byref(h2)) == 0
+        oracle.accs(C.DBL, C.SCALE[C.DBL], host, 0, stride, dh1, 0, stride, count, 1)
+        oracle.accs(C.DBL, C.SCALE[C.DBL], host, off2, stride, dh2, 0, stride, count, 1)
+    assert np.array_equal(d1.download(np.uint8, dh1.size), dh1)
+    assert np.array_equal(d2.download(np.uint8, dh2.size), dh2)
+    d1.free()
+    d2.free()

@@ -82,6 +82,25 @@ def test_remote_acc_put_get_two_ranks_one_gpu():
 
 
 @pytest.mark.gpu
+def test_remote_put_then_acc_same_patch_no_fence():
+    """A non-blocking put then an accumulate into the same remote patch with no
+    fence: the accumulate lands after the put (advisor finding, comex.cpp)."""
+    launch("order", n=2, timeout=120)
+
+
+@pytest.mark.gpu
+def test_remote_across_two_devices():
+    """Two ranks on two distinct MI355X: each opens the other's segment and
+    staging by IPC on another device and runs remote acc/put/get/accv/getv/putv
+    over xGMI.  Needs a box with at least two GPUs (skipped on one)."""
+    import ga_amd
+    if ga_amd.lib().gaamd_device_count() < 2:
+        pytest.skip("one GPU visible: the two-device case needs a multi-GPU node")
+    launch("remote", n=2, timeout=120, extra_env={"TEST_DISTINCT_DEVICES": "1"})
+    launch("order", n=2, timeout=120)
+
+
+@pytest.mark.gpu
 def test_remote_three_ranks_gloo_hooks():
     launch("remote-gloo", n=3, timeout=120)
 

@@ -23,9 +23,24 @@ def test_oracle_accs_matches_reference_golden(oracle, manifest, golden):
     for case in manifest["cases"]:
         n = case["name"]
         src, dst = golden[f"{n}/src"], golden[f"{n}/dst_in"].copy()
+        if case.get("alias"):
+            src = dst   # src and dst in one buffer
         oracle.accs(case["op"], C.SCALE[case["op"]], src, case["src_off"], case["src_stride"], dst,
                     case["dst_off"], case["dst_stride"], case["count"], case["levels"])
         assert np.array_equal(dst, golden[f"{n}/dst_out"]), n
+
+
+def test_alias_cases_exercise_every_ordering_class(manifest):
+    """The aliased golden cases (one buffer, reference outputs from oracle/_ref) reach
+    each of the launcher's ordering classes: parallel, ordered and one-lane serial."""
+    import ga_amd
+    kinds = set()
+    base = 0x7F0000000000
+    for c in manifest["cases"]:
+        if c.get("alias"):
+            kinds.add(ga_amd.plan_strided(c["op"], base + c["src_off"], c["src_stride"], base + c["dst_off"],
+                                          c["dst_stride"], c["count"], c["levels"])["kind"])
+    assert {"ordered", "serial"} <= kinds and kinds & {"rows", "flat"}, kinds
 
 
 def test_oracle_packed_route_matches_direct(oracle, manifest, golden):
@@ -33,7 +48,7 @@ def test_oracle_packed_route_matches_direct(oracle, manifest, golden):
     for every case whose dst rows do not overlap."""
     for case in manifest["cases"]:
         n = case["name"]
-        if "overlap" in n or "zero_dst_stride" in n:
+        if "overlap" in n or "zero_dst_stride" in n or case.get("alias"):
             continue
         src, dst = golden[f"{n}/src"], golden[f"{n}/dst_in"].copy()
         oracle.accs_packed(case["op"], C.SCALE[case["op"]], src, case["src_off"], case["src_stride"], dst,
@@ -144,7 +159,7 @@ def test_multi_worker_baseline_matches_single(oracle, manifest, golden, nthreads
     impls = [oracle] + ([Ref()] if ref_available() else [])
     for case in manifest["cases"]:
         n = case["name"]
-        if "overlap" in n or "zero_dst_stride" in n:   # slabs would race on shared dst bytes
+        if "overlap" in n or "zero_dst_stride" in n or case.get("alias"):   # slabs would race on shared bytes
             continue
         src = golden[f"{n}/src"]
         for impl in impls:

@@ -37,14 +37,52 @@ def test_continuing_levels_merge():
     assert p["levels"] == 1
 
 
-def test_overlapping_destination_rows_are_serial():
-    p = plan(DBL, SRC, [64], DST, [32], [64, 100], 1)          # dst rows overlap each other
-    assert p["kind"] == "serial" and p["width"] == 8
+def test_overlapping_destination_rows_are_ordered():
+    """dst rows sharing bytes with each other: rows in the reference's order, each
+    row wave-parallel (one 1024-thread workgroup), not one lane"""
+    p = plan(DBL, SRC, [64], DST, [32], [64, 100], 1)
+    assert p["kind"] == "ordered" and p["width"] == 16 and p["block"] == 1024 and p["blocks"] == 1
+    p = plan(DBL, SRC, [64], DST, [0], [64, 100], 1)           # zero stride: every row into one
+    assert p["kind"] == "ordered"
 
 
-def test_src_overlapping_dst_is_serial_in_place_is_not():
+def test_src_starting_inside_its_dst_row_below_it_is_serial_in_place_is_not():
+    # src run at d - 8: element m reads what element m-1 of the same _acc loop wrote
     assert plan(DBL, SRC, [64], SRC + 8, [64], [64, 100], 1)["kind"] == "serial"
-    assert plan(DBL, SRC, [64], SRC, [64], [64, 100], 1)["kind"] != "serial"
+    # src run at d + 8: element m reads element m+1's old value -> ordered, parallel rows
+    assert plan(DBL, SRC + 8, [64], SRC, [64], [64, 100], 1)["kind"] == "ordered"
+    p = plan(DBL, SRC, [64], SRC, [64], [64, 100], 1)
+    assert p["kind"] not in ("serial", "ordered")
+
+
+def test_interleaved_spans_without_shared_bytes_are_parallel():
+    """Columns 0..2047 accumulated into columns 2048..4095 of one ld-8192 f64 array:
+    the spans interleave but no byte is shared -> the full-speed rows kernel
+    (the round-1 span test sent this to the one-lane kernel)."""
+    a = SRC
+    p = plan(DBL, a, [65536], a + 16384, [65536], [16384, 4096], 1)
+    assert p["kind"] == "rows" and p["width"] == 16 and p["blocks"] == 4096 * 16, p
+    # 3-D with interleaved planes, still disjoint
+    p = plan(DBL, a, [65536, 65536 * 64], a + 8192, [65536, 65536 * 64], [8192, 32, 16], 2)
+    assert p["kind"] == "rows", p
+
+
+def test_rows_sharing_bytes_across_rows_are_ordered():
+    a = SRC
+    # src row i is dst row i+1 (written later) and dst row i is src row i-1 (written earlier)
+    assert plan(DBL, a, [65536], a + 65536, [65536], [16384, 4096], 1)["kind"] == "ordered"
+    assert plan(DBL, a + 65536, [65536], a, [65536], [16384, 4096], 1)["kind"] == "ordered"
+    # partial overlap of a neighbouring row
+    assert plan(DBL, a, [65536], a + 65536 - 64, [65536], [16384, 64], 1)["kind"] == "ordered"
+
+
+def test_many_rows_with_meeting_spans_take_the_conservative_bound():
+    """above 2^18 rows the analysis bounds spans and dst - src instead of sorting rows"""
+    a = SRC
+    n = (1 << 18) + 10
+    assert plan(DBL, a, [256], a + 64, [256], [64, n], 1)["kind"] == "ordered"
+    assert plan(DBL, a, [256], a + 32, [256], [64, n], 1)["kind"] == "serial"
+    assert plan(DBL, a, [256], a + 128, [256], [64, n], 1)["kind"] != "serial"
 
 
 def test_row_range_of_a_rebased_packed_side_is_not_serial():
@@ -58,7 +96,7 @@ def test_row_range_of_a_rebased_packed_side_is_not_serial():
     p = plan(DBL, packed0, [row], dst, [65536], [row, rows], 1, 1000, 1100)
     assert p["kind"] == "rows", p
     assert p["blocks"] == 100 * (row // 1024)
-    # the same rows but overlapping for real are serial
+    # the same rows but overlapping for real (src run starting 8 B below its dst run)
     p2 = plan(DBL, packed0, [row], packed0 + 8, [row], [row, rows], 1, 1000, 1100)
     assert p2["kind"] == "serial"
 

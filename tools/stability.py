@@ -7,6 +7,9 @@ import argparse
 import ctypes
 import json
 import os
+# kernel-timing probe: blocking comex_accs calls only stream-ordered (the documented
+# COMEX_AMD_BLOCKING_SYNC=0 opt-out), so back-to-back launches are not host round trips
+os.environ.setdefault("COMEX_AMD_BLOCKING_SYNC", "0")
 import sys
 import time
 
