@@ -20,11 +20,13 @@ step runs for --warmup steps and then for at least --warmup-ms of wall time,
 so the K timed steps do not start on a cold (clock-ramping) GPU.
 
 value = whole-job algorithmic traffic GiB/s = ranks * steps * bytes / max-over-
-ranks wall time.  roofline.achieved = the same algorithmic bytes per launch /
-the average launch duration, from ONE HIP event pair around the K timed
-launches (all library streams joined to it; per-launch event pairs slowed the
-kernels by ~8 %; profiles/r01/gapprobe_H.json), so it includes the
-kernel-boundary gap.  The library runs independent accumulates on two HIP
+ranks wall time of the K timed steps (barrier + synchronize on both sides, no
+timing events inside: their marker packets between kernels cost ~0.6 us per
+step, tools/edge_probe.py).  roofline.achieved = the same algorithmic bytes per
+launch / the average launch duration, from HIP events recorded at both ends of
+every library stream around K more launches of the same step right after the
+value region (per-launch event pairs slowed the kernels by ~8 %,
+profiles/r01/gapprobe_H.json), so it includes the kernel-boundary gap.  The library runs independent accumulates on two HIP
 streams (ga_amd/csrc/sched.cpp), so consecutive launches overlap at their
 edges: the rocprofv3 --kernel-trace summary of the same command is committed
 under profiles/, and the per-launch time it agrees with is the merged busy time
@@ -207,6 +209,29 @@ def warm(step, args, first=0):
     return i
 
 
+def event_region(L, run, steps, first):
+    """The roofline's per-launch time: the same `steps` steps once more, right
+    after the value region, bracketed by one HIP event per library stream at each
+    end (first start to last end over all streams).  Kept out of the value region:
+    marker packets between kernels cost ~0.6 us per step there (tools/edge_probe.py,
+    profiles/r02/edge_probe.jsonl).  Returns (ms, index of the next step)."""
+    n = L.gaamd_num_streams()
+    streams = [L.gaamd_stream_at(i) for i in range(n)]
+    ev0 = [L.gaamd_event_create() for _ in streams]
+    ev1 = [L.gaamd_event_create() for _ in streams]
+    for e, st in zip(ev0, streams):
+        L.gaamd_event_record(e, st)
+    for i in range(steps):
+        run(first + i)
+    for e, st in zip(ev1, streams):
+        L.gaamd_event_record(e, st)
+    assert L.comex_wait_all(0) == 0
+    ms = max(L.gaamd_event_elapsed_ms(a, b) for a in ev0 for b in ev1)
+    for e in ev0 + ev1:
+        L.gaamd_event_destroy(e)
+    return ms, first + steps
+
+
 def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True):
     """C5: NGA_Acc (include/ga.h; reference capi.c:2079 -> ngai_acc_common,
     global/src/onesided.c:1334) on a 32768^2 f64 GA.  NGA_Acc is GA's blocking
@@ -242,8 +267,6 @@ def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True
     L.GA_Get_proc_grid(g, grid)
     alpha = ctypes.c_double(SCALE[DBL])
     clo, chi, cld = ia(lo), ia(hi), ia([cols])
-    stream = L.gaamd_stream()
-
     def step(_i):
         L.NGA_Acc(g, clo, chi, ctypes.c_void_p(src.ptr), cld, ctypes.byref(alpha))
         if args.verbose:
@@ -257,26 +280,23 @@ def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True
     ga_amd.sync()
     L.GA_Sync()
     launch = ga_amd.last_launch()
-    ev0, ev1 = L.gaamd_event_create(), L.gaamd_event_create()
+    # value region: wall clock only (no marker packets between the steps)
     dist.barrier()
     ga_amd.sync()
     t0 = time.perf_counter()
-    L.gaamd_event_record(ev0, stream)
-    L.gaamd_join()
     for i in range(steps):
         step(nxt + i)
-    L.gaamd_join()
-    L.gaamd_event_record(ev1, stream)
     ga_amd.sync()
     if exchange:
         L.GA_Sync()                     # every owner has applied every contribution
     t1 = time.perf_counter()
     dist.barrier()
     elapsed = dist.max(t1 - t0)
-    region_ms = L.gaamd_event_elapsed_ms(ev0, ev1)
-    L.gaamd_event_destroy(ev0)
-    L.gaamd_event_destroy(ev1)
-    avg_kernel_s = dist.max(region_ms / 1e3 / steps) if not exchange else elapsed / steps
+    if exchange:
+        avg_kernel_s = elapsed / steps   # the work runs on the owners' streams
+    else:
+        region_ms, _ = event_region(L, step, steps, nxt + steps)
+        avg_kernel_s = dist.max(region_ms / 1e3 / steps)
     src.free()
     L.GA_Sync()
     L.GA_Destroy(g)
@@ -339,8 +359,6 @@ def run_gpu(args, dist, finalize=True):
         ptrs = [(ctypes.c_void_p(s.ptr), ctypes.c_void_p(seg[target])) for (s, _), seg in zip(sets, segs)]
     else:
         ptrs = [(ctypes.c_void_p(s.ptr), ctypes.c_void_p(d.ptr)) for s, d in sets]
-    stream = L.gaamd_stream()
-
     pipeline = args.pipeline and not exchange
     packed = [ga_amd.DeviceBuffer(payload) for _ in sets] if pipeline else []
     hd = Handles(L)
@@ -371,20 +389,13 @@ def run_gpu(args, dist, finalize=True):
     ga_amd.sync()
     launch = ga_amd.last_launch()
 
-    # one HIP event pair on the library stream brackets the K launches of the
-    # timed region: average launch duration = region / K.  (An event pair around
-    # every launch would put a release between kernels and slow them down.)
-    ev0, ev1 = L.gaamd_event_create(), L.gaamd_event_create()
+    # value region: barrier + sync on both sides, wall clock, no timing events
     L.comex_barrier(0)
     dist.barrier()
     ga_amd.sync()
     t0 = time.perf_counter()
-    L.gaamd_event_record(ev0, stream)
-    L.gaamd_join()                      # every library stream starts after ev0
     for i in range(args.steps):
         step(nxt + i)
-    L.gaamd_join()                      # the primary stream waits for the library's other streams
-    L.gaamd_event_record(ev1, stream)
     hd.drain()                          # every step's kernel has finished (comex_wait_all)
     ga_amd.sync()
     if exchange:
@@ -392,12 +403,12 @@ def run_gpu(args, dist, finalize=True):
     t1 = time.perf_counter()
     dist.barrier()
     elapsed = dist.max(t1 - t0)
-    region_ms = L.gaamd_event_elapsed_ms(ev0, ev1)
-    L.gaamd_event_destroy(ev0)
-    L.gaamd_event_destroy(ev1)
-    avg_kernel_s = dist.max(region_ms / 1e3 / args.steps)
     if exchange:
         avg_kernel_s = elapsed / args.steps   # the work runs on the owners' streams
+    else:
+        # roofline: the same K steps again inside per-stream HIP events
+        region_ms, _ = event_region(L, step, args.steps, nxt + args.steps)
+        avg_kernel_s = dist.max(region_ms / 1e3 / args.steps)
 
     res = dict(op=op, desc=desc, payload=payload, alg_bytes=alg_bytes, elems=elems, elapsed=elapsed,
                avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), pipeline=pipeline,
@@ -680,7 +691,8 @@ def main():
                                         "this workload's kernel (tools/pmc_traffic.py, gfx950 FETCH_SIZE x2), "
                                         "collected in separate profiled runs, not this one") if traffic else None,
                      "kernel_ms_avg": round(r["avg_kernel_s"] * 1e3, 4),
-                     "timing": "HIP event pair around the timed launches (all library streams joined) / steps",
+                     "timing": ("HIP events at both ends of every library stream around K more launches of the "
+                                "same step right after the value region (first start to last end) / K"),
                      "streams": r["streams"],
                      "rocprof_check": ("consecutive launches overlap on the library streams: compare kernel_ms_avg "
                                        "with the merged busy time per dispatch of the rocprofv3 kernel trace "

@@ -139,6 +139,7 @@ SIGNATURES = {
     "gaamd_device_count": (ctypes.c_int, []),
     "gaamd_set_device": (ctypes.c_int, [ctypes.c_int]),
     "gaamd_stream": (ctypes.c_void_p, []),
+    "gaamd_stream_at": (ctypes.c_void_p, [ctypes.c_int]),
     "gaamd_dev_malloc": (ctypes.c_void_p, [ctypes.c_size_t]),
     "gaamd_dev_free": (ctypes.c_int, [ctypes.c_void_p]),
     "gaamd_host_malloc": (ctypes.c_void_p, [ctypes.c_size_t]),

@@ -270,17 +270,20 @@ static int nb_alloc() {
     const int i = r.nb_next;
     if (g_nb_job[i]) run_job(g_nb_job[i]);
     g_nb_job[i] = 0;
-    GA_HIP(hipEventSynchronize(r.nb_ev[i]));
+    (void)sched_complete(r.nb_stream[i], r.nb_seq[i], true);
     r.nb_next = (i + 1) % kMaxNb;
     return i;
 }
 
-// handle = an event on the stream the operation went to (0: the primary)
-static void nb_complete_now(comex_request_t *h, int stream_idx = 0) {
+// handle of an op just enqueued on library stream `stream_idx` (`on_stream`),
+// or of one with nothing left on a stream (completed in the call, or a remote
+// accumulate job whose completion the handle's job id tracks)
+static void nb_complete_now(comex_request_t *h, int stream_idx = 0, bool on_stream = false) {
     Runtime &r = rt();
     const int i = nb_alloc();
     g_nb_job[i] = 0;
-    GA_HIP(hipEventRecord(r.nb_ev[i], r.streams.empty() ? r.stream : r.streams[stream_idx]));
+    r.nb_stream[i] = stream_idx;
+    r.nb_seq[i] = on_stream ? sched_track(stream_idx) : 0;
     *h = i;
 }
 
@@ -867,7 +870,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         release_view(sv);
         release_view(dv);
     }
-    if (hdl) nb_complete_now(hdl, si);
+    if (hdl) nb_complete_now(hdl, si, true);
     return COMEX_SUCCESS;
 }
 
@@ -1445,7 +1448,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
     }
     if (world != r.rank && r.same_node(world) && kind != X_ACC && !blocking && !r.direct_pending.empty())
         r.direct_pending[world] = 1;
-    if (hdl) nb_complete_now(hdl, 0);
+    if (hdl) nb_complete_now(hdl, 0, true);
     return COMEX_SUCCESS;
 }
 
@@ -1483,12 +1486,23 @@ int comex_init() {
     const char *dv = getenv("COMEX_AMD_DEVICE");
     r.device = dv ? atoi(dv) : r.local_rank % ndev;
     GA_HIP(hipSetDevice(r.device));
+    // COMEX_AMD_WAIT: how host waits (stream/event synchronisation) wait for the
+    // GPU -- spin (lowest wake-up latency, a busy core), yield, or blocking
+    // (sleep until the interrupt); unset: the HIP runtime's default
+    if (const char *w = getenv("COMEX_AMD_WAIT")) {
+        const unsigned f = !strcmp(w, "spin") ? hipDeviceScheduleSpin
+                         : !strcmp(w, "yield") ? hipDeviceScheduleYield
+                         : !strcmp(w, "blocking") ? hipDeviceScheduleBlockingSync : hipDeviceScheduleAuto;
+        if (hipSetDeviceFlags(f) != hipSuccess) {
+            (void)hipGetLastError();
+            fprintf(stderr, "ga_amd: COMEX_AMD_WAIT=%s not applied (device already active)\n", w);
+        }
+    }
     GA_HIP(hipStreamCreateWithFlags(&r.stream, hipStreamDefault));
     {
         const char *ns = getenv("COMEX_AMD_STREAMS");
         sched_init(ns ? atoi(ns) : 2);   // 2: independent ops overlap kernel edges
     }
-    for (int i = 0; i < kMaxNb; ++i) GA_HIP(hipEventCreateWithFlags(&r.nb_ev[i], hipEventDisableTiming));
     const char *bs = getenv("COMEX_AMD_BLOCKING_SYNC");
     r.blocking_sync = !bs || atoi(bs) != 0;
     const char *dbg = getenv("COMEX_AMD_DEBUG");
@@ -1574,7 +1588,6 @@ int comex_finalize() {
     boot_barrier();
     if (r.staging) (void)hipFree(r.staging);
     r.staging = nullptr;
-    for (int i = 0; i < kMaxNb; ++i) (void)hipEventDestroy(r.nb_ev[i]);
     sched_sync_all();
     sched_fini();
     if (g_iov_scratch) (void)hipFree(g_iov_scratch);
@@ -1728,7 +1741,7 @@ int comex_wait(comex_request_t *h) {
     if (r.nb_used[*h]) {
         if (g_nb_job[*h]) run_job(g_nb_job[*h]);
         g_nb_job[*h] = 0;
-        GA_HIP(hipEventSynchronize(r.nb_ev[*h]));
+        (void)sched_complete(r.nb_stream[*h], r.nb_seq[*h], true);
         r.nb_used[*h] = false;
     }
     *h = -1;
@@ -1745,9 +1758,7 @@ int comex_test(comex_request_t *h, int *status) {
         if (find_job(g_nb_job[*h])) { *status = 1; return COMEX_SUCCESS; }
         g_nb_job[*h] = 0;
     }
-    hipError_t e = hipEventQuery(r.nb_ev[*h]);
-    if (e == hipErrorNotReady) { *status = 1; return COMEX_SUCCESS; }
-    if (e != hipSuccess) fatal("request failed: %s", hipGetErrorString(e));
+    if (!sched_complete(r.nb_stream[*h], r.nb_seq[*h], false)) { *status = 1; return COMEX_SUCCESS; }
     r.nb_used[*h] = false;
     *h = -1;
     return COMEX_SUCCESS;

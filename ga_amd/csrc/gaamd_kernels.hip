@@ -39,6 +39,8 @@
 #include <atomic>
 #include <vector>
 #include <utility>
+#include <mutex>
+#include <cmath>
 
 namespace gaamd {
 
@@ -708,8 +710,8 @@ static int64_t row_start(const int64_t *str, const uint32_t *cnt, int L, uint64_
 enum { OV_NONE = 0, OV_ORDERED = 1, OV_SERIAL = 2 };
 constexpr uint64_t kExactRows = 1ull << 18;
 
-static int classify_rows(int64_t sb, const int64_t *ss, int64_t db, const int64_t *ds, const uint32_t *cn, int L,
-                         int64_t rb, uint64_t r0, uint64_t r1) {
+static int classify_rows_exact(int64_t sb, const int64_t *ss, int64_t db, const int64_t *ds, const uint32_t *cn,
+                               int L, int64_t rb, uint64_t r0, uint64_t r1) {
     const uint64_t n = r1 - r0;
     // spans of the rows this call touches: a chunked caller (remote pack /
     // unpack-acc) passes a row range and a packed base rebased so that row r0
@@ -722,6 +724,23 @@ static int classify_rows(int64_t sb, const int64_t *ss, int64_t db, const int64_
     const bool spans_meet = !same_layout && sb + slo < db + dhi && db + dlo < sb + shi;
     const bool dst_may = n > 1 && rows_may_overlap(ds, cn, L, rb);
     if (!spans_meet && !dst_may) return OV_NONE;
+    if (L == 1 && ss[0] == ds[0]) {
+        // 2-D with one stride S on both sides (every GA patch of one array into
+        // another patch of it): src row i is dst row i moved by delta = sb - db, and
+        // src row i meets dst row j iff |delta + (i - j) S| < rb -- closed form
+        const int64_t S = ss[0], delta = sb - db;
+        if (delta < 0 && -delta < rb) return OV_SERIAL;         // d - s in (0, rb) on every row
+        if (n > 1 && (S < 0 ? -S : S) < rb) return OV_ORDERED;  // dst rows share bytes
+        if (!spans_meet) return OV_NONE;
+        const int64_t kmax = (int64_t)n - 1;
+        const int64_t kc = S ? (int64_t)std::floor(-(double)delta / (double)S) : 0;
+        for (int64_t k = kc - 1; k <= kc + 2; ++k) {
+            if (k < -kmax || k > kmax) continue;
+            const int64_t diff = delta + k * S;
+            if (diff > -rb && diff < rb && !(k == 0 && diff == 0)) return OV_ORDERED;
+        }
+        return OV_NONE;
+    }
     if (n > kExactRows) {
         // bound: dst - src of a row is (db - sb) + sum_j digit_j * (ds_j - ss_j)
         int64_t lo = db - sb, hi = db - sb;
@@ -753,6 +772,54 @@ static int classify_rows(int64_t sb, const int64_t *ss, int64_t db, const int64_
         }
     }
     return OV_NONE;
+}
+
+// The sorted-interval analysis costs O(rows log rows) of host time (~0.1 ms at
+// 4096 rows) -- more than a headline launch -- and callers repeat geometries
+// (the same GA patches, rotating buffers): its answers are kept in a small
+// direct-mapped cache keyed by the whole geometry.
+struct ClassifyKey {
+    int64_t sb, db, rb;
+    uint64_t r0, r1;
+    int32_t L, pad;
+    int64_t ss[kMaxLevels], ds[kMaxLevels];
+    uint32_t cn[kMaxLevels];
+    bool operator==(const ClassifyKey &o) const { return !memcmp(this, &o, sizeof(*this)); }
+};
+static std::mutex g_cls_mu;
+static ClassifyKey g_cls_key[64];
+static int g_cls_val[64];
+static bool g_cls_used[64];
+
+static int classify_rows(int64_t sb, const int64_t *ss, int64_t db, const int64_t *ds, const uint32_t *cn, int L,
+                         int64_t rb, uint64_t r0, uint64_t r1) {
+    ClassifyKey k;
+    memset(&k, 0, sizeof(k));
+    k.sb = sb;
+    k.db = db;
+    k.rb = rb;
+    k.r0 = r0;
+    k.r1 = r1;
+    k.L = L;
+    for (int j = 0; j < L; ++j) {
+        k.ss[j] = ss[j];
+        k.ds[j] = ds[j];
+        k.cn[j] = cn[j];
+    }
+    uint64_t h = 1469598103934665603ull;
+    const unsigned char *p = reinterpret_cast<const unsigned char *>(&k);
+    for (size_t i = 0; i < sizeof(k); ++i) h = (h ^ p[i]) * 1099511628211ull;
+    const int slot = (int)(h & 63);
+    {
+        std::lock_guard<std::mutex> g(g_cls_mu);
+        if (g_cls_used[slot] && g_cls_key[slot] == k) return g_cls_val[slot];
+    }
+    const int v = classify_rows_exact(sb, ss, db, ds, cn, L, rb, r0, r1);
+    std::lock_guard<std::mutex> g(g_cls_mu);
+    g_cls_key[slot] = k;
+    g_cls_val[slot] = v;
+    g_cls_used[slot] = true;
+    return v;
 }
 
 void side_span_host(const int *stride, const int *count, int stride_levels, int64_t row_bytes,

@@ -176,6 +176,10 @@ int gaamd_device_count(void) {
 
 int gaamd_set_device(int dev) { return hipSetDevice(dev) == hipSuccess ? 0 : -1; }
 void *gaamd_stream(void) { return rt().stream; }
+void *gaamd_stream_at(int i) {
+    Runtime &r = rt();
+    return (i >= 0 && i < (int)r.streams.size()) ? (void *)r.streams[i] : nullptr;
+}
 
 void *gaamd_dev_malloc(size_t bytes) {
     void *p = nullptr;

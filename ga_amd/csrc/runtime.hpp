@@ -3,7 +3,7 @@
 // Reference counterparts (comex/src-mpi-pr/comex.c):
 //   g_state (rank/size/host table)        -> Runtime::{rank,size,local_rank}
 //   reg_cache (reg_cache.c:380-409)       -> Runtime::segs (owner base -> mapped ptr)
-//   nb_state[COMEX_MAX_NB_OUTSTANDING]    -> Runtime::nb (HIP events)
+//   nb_state[COMEX_MAX_NB_OUTSTANDING]    -> Runtime::nb_* (stream + sequence, sched.cpp marks)
 //   per-rank POSIX semaphores (2812-2908) -> none: every write into rank t's
 //       HBM is issued on rank t's stream (its own ops, or requests its progress
 //       thread drains), so stream order serialises accumulates per target.
@@ -130,8 +130,10 @@ struct Runtime {
     // memory
     std::vector<Segment> segs;
     std::mutex seg_mu;
-    // non-blocking handles
-    hipEvent_t nb_ev[kMaxNb] = {};
+    // non-blocking handles: the op's stream and its sequence number there (sched.cpp
+    // completion marks; seq 0 = nothing left on a stream)
+    int nb_stream[kMaxNb] = {};
+    uint64_t nb_seq[kMaxNb] = {};
     bool nb_used[kMaxNb] = {};
     int nb_next = 0;
     // remote (multi-rank) state
@@ -164,6 +166,10 @@ void sched_resize(int nstreams);
 int sched_pick(const Span &src, const Span &dst, uint64_t payload = 0);   // payload bytes of the op (0: unknown)   // stream index for an op
 void sched_join();
 void sched_sync_all();
+// completion marks (user thread): sequence number of an op just enqueued on
+// stream s; whether op `seq` of stream s has completed (waiting for it if `wait`)
+uint64_t sched_track(int s);
+bool sched_complete(int s, uint64_t seq, bool wait);
 
 // wire.cpp: the host fallback between nodes (MPI-PR message protocol over TCP)
 void wire_init();                                   // collective; no-op on one node

@@ -87,6 +87,8 @@ int gaamd_get_tuning(const char *key);
 int gaamd_device_count(void);
 int gaamd_set_device(int dev);
 void *gaamd_stream(void);
+/* library stream i (0 = gaamd_stream()), or NULL past gaamd_num_streams() */
+void *gaamd_stream_at(int i);
 void *gaamd_dev_malloc(size_t bytes);
 int gaamd_dev_free(void *p);
 void *gaamd_host_malloc(size_t bytes);   /* pinned, device-mapped */

@@ -76,13 +76,25 @@ def test_rows_sharing_bytes_across_rows_are_ordered():
     assert plan(DBL, a, [65536], a + 65536 - 64, [65536], [16384, 64], 1)["kind"] == "ordered"
 
 
+def test_one_stride_2d_closed_form_is_exact_at_any_size():
+    """2-D, one stride on both sides: src row i meets dst row j iff |delta + (i-j) S| < row
+    (closed form, any number of rows)"""
+    a = SRC
+    n = (1 << 20) + 10
+    assert plan(DBL, a, [256], a + 64, [256], [64, n], 1)["kind"] in ("rows", "flat")   # interleaved, disjoint
+    assert plan(DBL, a, [256], a + 32, [256], [64, n], 1)["kind"] == "serial"           # d - s = 32 < 64
+    assert plan(DBL, a + 32, [256], a, [256], [64, n], 1)["kind"] == "ordered"          # src 32 B above
+    assert plan(DBL, a, [256], a + 256 * 7, [256], [64, n], 1)["kind"] == "ordered"     # row i+7 = row i
+    assert plan(DBL, a, [256], a + 256 * n, [256], [64, n], 1)["kind"] in ("rows", "flat")
+
+
 def test_many_rows_with_meeting_spans_take_the_conservative_bound():
-    """above 2^18 rows the analysis bounds spans and dst - src instead of sorting rows"""
+    """above 2^18 rows (and not the one-stride 2-D form) the analysis bounds spans and
+    dst - src instead of sorting rows"""
     a = SRC
     n = (1 << 18) + 10
-    assert plan(DBL, a, [256], a + 64, [256], [64, n], 1)["kind"] == "ordered"
-    assert plan(DBL, a, [256], a + 32, [256], [64, n], 1)["kind"] == "serial"
-    assert plan(DBL, a, [256], a + 128, [256], [64, n], 1)["kind"] != "serial"
+    assert plan(DBL, a, [256], a + 64, [264], [64, n], 1)["kind"] == "ordered"
+    assert plan(DBL, a, [256], a + 32, [264], [64, n], 1)["kind"] == "serial"
 
 
 def test_row_range_of_a_rebased_packed_side_is_not_serial():
