@@ -45,11 +45,16 @@ void fatal(const char *fmt, ...) {
 }
 
 size_t node_shm_bytes(int size) {
-    return sizeof(NodeShm) + sizeof(Inbox) * (size_t)(size > 1 ? size - 1 : 0) + kBootSlot * (size_t)size;
+    return sizeof(NodeShm) + sizeof(Inbox) * (size_t)(size > 1 ? size - 1 : 0) + kBootSlot * (size_t)size +
+           sizeof(std::atomic<uint32_t>) * (size_t)kMaxMutexes * (size_t)size;
 }
 Inbox *inbox_of(NodeShm *s, int rank) { return &s->inbox[rank]; }
 char *boot_area(NodeShm *s, int size) {
     return reinterpret_cast<char *>(s) + sizeof(NodeShm) + sizeof(Inbox) * (size_t)(size > 1 ? size - 1 : 0);
+}
+std::atomic<uint32_t> *mutex_words(NodeShm *s, int size, int rank) {
+    char *base = boot_area(s, size) + kBootSlot * (size_t)size;
+    return reinterpret_cast<std::atomic<uint32_t> *>(base) + (size_t)kMaxMutexes * (size_t)rank;
 }
 
 static int env_int(const char *const *names, int dflt) {

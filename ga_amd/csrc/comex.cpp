@@ -44,6 +44,19 @@ static void ensure_init() {
 // ---- groups ---------------------------------------------------------------
 static std::vector<std::vector<int>> g_groups;   // group id - 1 -> world ranks
 
+// world ranks of a comex group, in group-rank order
+std::vector<int> group_members(int group) {
+    Runtime &r = rt();
+    std::vector<int> m;
+    if (group == COMEX_GROUP_WORLD) {
+        for (int q = 0; q < r.size; ++q) m.push_back(q);
+        return m;
+    }
+    if (group < 1 || group > (int)g_groups.size() || g_groups[group - 1].empty())
+        fatal("invalid comex group %d", group);
+    return g_groups[group - 1];
+}
+
 int translate_world(int group, int proc) {
     Runtime &r = rt();
     if (group == COMEX_GROUP_WORLD) {
@@ -421,7 +434,10 @@ static void progress_loop() {
     Runtime &r = rt();
     GA_HIP(hipSetDevice(r.device));
     Inbox *ib = inbox_of(r.shm, r.li(r.rank));
-    struct Inflight { hipEvent_t ev; int src; };
+    struct Inflight { hipEvent_t ev; int src; bool rmw; };
+    // comex_rmw results: the kernel writes the old value here (pinned, device-mapped),
+    // one slot per requester position on the node
+    uint64_t *rmw_host = nullptr, *rmw_dev = nullptr;
     std::deque<Inflight> inflight;
     std::vector<hipEvent_t> pool;
     char *prog_work = nullptr;          // launch_iov_runs scratch of this thread
@@ -473,7 +489,31 @@ static void progress_loop() {
                 if (rc) fatal("io-vector accumulate launch failed (%d)", rc);
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
             }
-            inflight.push_back({ev, src});
+            inflight.push_back({ev, src, false});
+            q.state.store(0, std::memory_order_release);
+            ib->head.store(h + 1, std::memory_order_release);
+            worked = true;
+        } else if (q.state.load(std::memory_order_acquire) == 2 && q.kind == 2) {
+            // comex_rmw from a rank of this node (the progress rank's OP_FETCH_AND_ADD /
+            // OP_SWAP): one lane on this GPU, after earlier operations on those bytes
+            const int src = q.src_rank;
+            if (!rmw_host) {
+                GA_HIP(hipHostMalloc((void **)&rmw_host, sizeof(uint64_t) * kMaxRanks, hipHostMallocMapped));
+                GA_HIP(hipHostGetDevicePointer((void **)&rmw_dev, rmw_host, 0));
+            }
+            uint64_t val = 0;
+            memcpy(&val, q.scale, 8);
+            hipEvent_t ev;
+            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            else { ev = pool.back(); pool.pop_back(); }
+            {
+                std::lock_guard<std::mutex> g(r.launch_mu);
+                const int si = sched_pick(Span(), span_of((void *)q.dst_addr, 0, (int64_t)q.bytes));
+                const int rc = launch_rmw(q.op, (void *)q.dst_addr, (int)q.bytes, val, rmw_dev + r.li(src), r.streams[si]);
+                if (rc) fatal("rmw launch failed (%d): misaligned word?", rc);
+                GA_HIP(hipEventRecord(ev, r.streams[si]));
+            }
+            inflight.push_back({ev, src, true});
             q.state.store(0, std::memory_order_release);
             ib->head.store(h + 1, std::memory_order_release);
             worked = true;
@@ -501,7 +541,7 @@ static void progress_loop() {
                 if (rc) fatal("unpack-acc launch failed (%d)", rc);
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
             }
-            inflight.push_back({ev, src});
+            inflight.push_back({ev, src, false});
             q.state.store(0, std::memory_order_release);
             ib->head.store(h + 1, std::memory_order_release);
             worked = true;
@@ -510,6 +550,11 @@ static void progress_loop() {
             hipError_t e = hipEventQuery(inflight.front().ev);
             if (e == hipErrorNotReady) break;
             if (e != hipSuccess) fatal("unpack-acc failed: %s", hipGetErrorString(e));
+            if (inflight.front().rmw) {
+                RmwReply &rp = r.shm->rmw[r.li(inflight.front().src)];
+                rp.value = rmw_host[r.li(inflight.front().src)];
+                rp.seq.fetch_add(1, std::memory_order_release);
+            }
             r.shm->done[r.li(inflight.front().src)][r.li(r.rank)].fetch_add(1, std::memory_order_release);
             pool.push_back(inflight.front().ev);
             inflight.pop_front();
@@ -528,6 +573,7 @@ static void progress_loop() {
         (void)hipEventDestroy(prog_work_ev);
     }
     if (prog_work) (void)hipFree(prog_work);
+    if (rmw_host) (void)hipHostFree(rmw_host);
 }
 
 // ---- asynchronous remote accumulate ---------------------------------------
@@ -1452,6 +1498,91 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
     return COMEX_SUCCESS;
 }
 
+// ---- read-modify-write and mutexes -----------------------------------------
+// comex_rmw (comex.h:670): the reference sends OP_FETCH_AND_ADD / OP_SWAP to the
+// target's progress rank (comex.c:2120-2200), which applies it after every earlier
+// message from that source.  Here: on this rank's own memory a one-lane kernel on
+// the library stream that last touched those bytes; on a rank of this node a
+// request in its inbox (after our earlier requests to it), applied by its progress
+// thread on its GPU, the old value coming back through the node shm; on another
+// node a wire frame.
+static void post_request_rmw(int t, int swap, uint64_t addr, int bytes, uint64_t val) {
+    Runtime &r = rt();
+    Inbox *ib = inbox_of(r.shm, r.li(t));
+    const uint64_t ticket = ib->tail.fetch_add(1, std::memory_order_acq_rel);
+    Request &q = ib->slot[ticket % kInboxSlots];
+    for (unsigned spins = 0; ib->head.load(std::memory_order_acquire) + kInboxSlots <= ticket; ++spins)
+        if (spins > 256) sched_yield();
+    for (unsigned spins = 0;; ++spins) {
+        uint32_t expect = 0;
+        if (q.state.compare_exchange_weak(expect, 1, std::memory_order_acq_rel)) break;
+        if (spins > 256) sched_yield();
+    }
+    q.src_rank = r.rank;
+    q.op = swap;
+    q.levels = 0;
+    memset(q.count, 0, sizeof(q.count));
+    memset(q.dst_stride, 0, sizeof(q.dst_stride));
+    q.dst_addr = addr;
+    q.staging_off = 0;
+    q.bytes = (uint64_t)bytes;
+    q.seq = 0;
+    memset(q.scale, 0, sizeof(q.scale));
+    memcpy(q.scale, &val, 8);
+    q.kind = 2;
+    q.iov_serial = 0;
+    q.iov_align = 0;
+    q.dst_hi = 0;
+    q.state.store(2, std::memory_order_release);
+}
+
+uint64_t rmw_local(int swap, void *addr, int bytes, uint64_t val) {
+    Runtime &r = rt();
+    // one pinned result word per calling thread (user thread, wire server thread)
+    static thread_local uint64_t *host = nullptr, *dev = nullptr;
+    if (!host) {
+        GA_HIP(hipHostMalloc((void **)&host, sizeof(uint64_t), hipHostMallocMapped));
+        GA_HIP(hipHostGetDevicePointer((void **)&dev, host, 0));
+    }
+    char *d = nullptr;
+    if (!direct_view(addr, &d)) fatal("comex_rmw: %p is not device-accessible memory", addr);
+    hipStream_t st;
+    {
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        const int si = sched_pick(Span(), span_of(d, 0, bytes));
+        st = r.streams[si];
+        const int rc = launch_rmw(swap, d, bytes, val, dev, st);
+        if (rc) fatal("comex_rmw: launch failed (%d): misaligned word?", rc);
+    }
+    GA_HIP(hipStreamSynchronize(st));
+    return *(volatile uint64_t *)host;
+}
+
+// comex_create_mutexes / lock / unlock (comex.h:607-643; the reference keeps the
+// lock queues at each node's progress rank, comex.c:2225-2357): every rank's
+// mutexes are words in its node's shm (kMaxMutexes per rank); a rank of the same
+// node takes one with a compare-and-swap, a rank of another node through a
+// try-lock frame served by the owner's wire thread.
+static std::vector<int> g_mutex_count;   // mutexes created by every rank
+
+bool mutex_try_local(int owner, int mutex) {
+    Runtime &r = rt();
+    std::atomic<uint32_t> &w = mutex_words(r.shm, r.node_size, r.li(owner))[mutex];
+    uint32_t expect = 0;
+    return w.compare_exchange_strong(expect, 1, std::memory_order_acquire);
+}
+
+void mutex_release_local(int owner, int mutex) {
+    Runtime &r = rt();
+    mutex_words(r.shm, r.node_size, r.li(owner))[mutex].store(0, std::memory_order_release);
+}
+
+static void check_mutex(int mutex, int proc) {
+    if (g_mutex_count.empty()) fatal("comex_lock/unlock before comex_create_mutexes");
+    if (mutex < 0 || mutex >= g_mutex_count[proc])
+        fatal("mutex %d out of range on rank %d (%d created)", mutex, proc, g_mutex_count[proc]);
+}
+
 }  // namespace gaamd
 
 using namespace gaamd;
@@ -1659,9 +1790,9 @@ int comex_fence_all(comex_group_t group) {
 
 int comex_barrier(comex_group_t group) {
     ensure_init();
-    if (group != COMEX_GROUP_WORLD) fatal("comex_barrier on a sub-group is not supported");
     comex_fence_all(group);
-    boot_barrier();
+    if (group == COMEX_GROUP_WORLD) boot_barrier();
+    else members_barrier(group_members(group), group);   // the group's members only (groups.c barrier)
     return COMEX_SUCCESS;
 }
 
@@ -1787,7 +1918,9 @@ int comex_wait_proc(int proc, comex_group_t group) {
 static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool device) {
     ensure_init();
     Runtime &r = rt();
-    if (group != COMEX_GROUP_WORLD) fatal("comex_malloc on a sub-group is not supported");
+    // collective over the group's members (comex.c comex_malloc): ptr_arr is
+    // indexed by group rank; non-members keep no view of the segment
+    const std::vector<int> members = group_members(group);
     struct Info { uint64_t base, bytes; hipIpcMemHandle_t h; int32_t device, pad; } mine;
     memset(&mine, 0, sizeof(mine));
     void *p = nullptr;
@@ -1809,8 +1942,14 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     mine.base = (uint64_t)(uintptr_t)p;
     mine.bytes = bytes;
     mine.device = r.device;
+    std::vector<Info> gathered(members.size());
+    members_allgather(members, group, &mine, gathered.data(), sizeof(Info));
     std::vector<Info> all(r.size);
-    boot_allgather(&mine, all.data(), sizeof(Info));
+    memset(all.data(), 0, sizeof(Info) * all.size());
+    for (size_t k = 0; k < members.size(); ++k) {
+        all[members[k]] = gathered[k];
+        ptr_arr[k] = (void *)(uintptr_t)gathered[k].base;
+    }
     Segment s;
     s.live = true;
     s.device = device;
@@ -1819,7 +1958,6 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     for (int q = 0; q < r.size; ++q) {
         s.peer[q].base = all[q].base;
         s.peer[q].bytes = all[q].bytes;
-        ptr_arr[q] = (void *)(uintptr_t)all[q].base;
         if (q == r.rank) {
             s.peer[q].mapped = (char *)p;
         } else if (all[q].bytes && r.same_node(q)) {
@@ -1831,7 +1969,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         std::lock_guard<std::mutex> g(r.seg_mu);
         r.segs.push_back(std::move(s));
     }
-    boot_barrier();
+    members_barrier(members, group);
     return COMEX_SUCCESS;
 }
 
@@ -1849,12 +1987,13 @@ int comex_malloc_mem_dev(void **ptr_arr, size_t bytes, comex_group_t group, cons
 int comex_free(void *ptr, comex_group_t group) {
     ensure_init();
     Runtime &r = rt();
-    (void)group;
-    comex_fence_all(COMEX_GROUP_WORLD);
-    std::vector<uint64_t> all(r.size);
+    const std::vector<int> members = group_members(group);
+    comex_fence_all(group);
+    std::vector<uint64_t> gathered(members.size()), all(r.size, 0);
     uint64_t mine = (uint64_t)(uintptr_t)ptr;
-    boot_allgather(&mine, all.data(), sizeof(mine));
-    boot_barrier();   // nobody still reads the segment
+    members_allgather(members, group, &mine, gathered.data(), sizeof(mine));
+    for (size_t k = 0; k < members.size(); ++k) all[members[k]] = gathered[k];
+    members_barrier(members, group);   // nobody still reads the segment
     std::lock_guard<std::mutex> g(r.seg_mu);
     for (Segment &s : r.segs) {
         if (!s.live) continue;
@@ -1884,6 +2023,135 @@ void *comex_malloc_local(size_t bytes) {
 int comex_free_local(void *ptr) {
     if (ptr) GA_HIP(hipHostFree(ptr));
     return COMEX_SUCCESS;
+}
+
+// ---- read-modify-write (comex.h:670) ----
+int comex_rmw(int op, void *ploc, void *prem, int extra, int proc, comex_group_t group) {
+    ensure_init();
+    Runtime &r = rt();
+    progress_jobs();
+    const int world = translate_world(group, proc);
+    int bytes, swap;
+    uint64_t val;
+    switch (op) {
+    case COMEX_FETCH_AND_ADD: bytes = 4; swap = 0; val = (uint64_t)(uint32_t)extra; break;
+    case COMEX_FETCH_AND_ADD_LONG: bytes = 8; swap = 0; val = (uint64_t)(int64_t)extra; break;
+    case COMEX_SWAP: { int v; memcpy(&v, ploc, 4); bytes = 4; swap = 1; val = (uint64_t)(uint32_t)v; break; }
+    case COMEX_SWAP_LONG: { int64_t v; memcpy(&v, ploc, 8); bytes = 8; swap = 1; val = (uint64_t)v; break; }
+    default: fatal("comex_rmw: unknown op %d", op);
+    }
+    if (!ploc || !prem) fatal("comex_rmw: NULL ploc or prem");
+    uint64_t old = 0;
+    if (world == r.rank) {
+        old = rmw_local(swap, prem, bytes, val);
+    } else if (!r.same_node(world)) {
+        check_remote(world, prem, 0, bytes);
+        old = wire_rmw(world, swap, (uint64_t)(uintptr_t)prem, bytes, val);
+    } else {
+        check_remote(world, prem, 0, bytes);
+        // behind our earlier traffic to that rank: pending accumulate chunks posted
+        // first (the owner applies its inbox in order), direct put/get kernels done
+        drain_target(world);
+        if (!r.direct_pending.empty() && r.direct_pending[world]) {
+            std::lock_guard<std::mutex> g(r.launch_mu);
+            sched_sync_all();
+        }
+        RmwReply &rp = r.shm->rmw[r.li(r.rank)];
+        const uint64_t seq0 = rp.seq.load(std::memory_order_acquire);
+        post_request_rmw(world, swap, (uint64_t)(uintptr_t)prem, bytes, val);
+        ++r.posted[world];
+        for (unsigned spins = 0; rp.seq.load(std::memory_order_acquire) == seq0; ++spins)
+            if (spins > 256) sched_yield();
+        old = rp.value;
+    }
+    if (bytes == 4) {
+        const uint32_t o = (uint32_t)old;
+        memcpy(ploc, &o, 4);
+    } else {
+        memcpy(ploc, &old, 8);
+    }
+    return COMEX_SUCCESS;
+}
+
+// ---- mutexes (comex.h:607-643) ----
+int comex_create_mutexes(int num) {
+    ensure_init();
+    Runtime &r = rt();
+    if (num < 0 || num > kMaxMutexes) fatal("comex_create_mutexes(%d): 0..%d per rank", num, kMaxMutexes);
+    if (!g_mutex_count.empty()) fatal("comex_create_mutexes: mutexes exist (comex_destroy_mutexes first)");
+    std::atomic<uint32_t> *w = mutex_words(r.shm, r.node_size, r.li(r.rank));
+    for (int i = 0; i < num; ++i) w[i].store(0, std::memory_order_relaxed);
+    g_mutex_count.assign(r.size, 0);
+    boot_allgather(&num, g_mutex_count.data(), sizeof(int));   // exchange of mutex counts
+    comex_barrier(COMEX_GROUP_WORLD);
+    return COMEX_SUCCESS;
+}
+
+int comex_destroy_mutexes() {
+    ensure_init();
+    if (g_mutex_count.empty()) fatal("comex_destroy_mutexes without comex_create_mutexes");
+    comex_barrier(COMEX_GROUP_WORLD);   // no lock request outstanding
+    g_mutex_count.clear();
+    return COMEX_SUCCESS;
+}
+
+int comex_lock(int mutex, int proc) {
+    ensure_init();
+    Runtime &r = rt();
+    const int world = translate_world(COMEX_GROUP_WORLD, proc);
+    check_mutex(mutex, world);
+    for (unsigned spins = 0;; ++spins) {
+        if (r.same_node(world) ? mutex_try_local(world, mutex) : wire_lock(world, mutex, true)) break;
+        progress_jobs();
+        if (spins > 64) usleep(spins > 4096 ? 200 : 10);
+        else sched_yield();
+    }
+    return COMEX_SUCCESS;
+}
+
+int comex_unlock(int mutex, int proc) {
+    ensure_init();
+    Runtime &r = rt();
+    const int world = translate_world(COMEX_GROUP_WORLD, proc);
+    check_mutex(mutex, world);
+    // the reference's OP_UNLOCK reaches the owner after this rank's earlier messages
+    // to it, so the critical section's operations land first: complete them here
+    fence_target(world);
+    {
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        sched_sync_all();
+    }
+    if (r.same_node(world)) mutex_release_local(world, mutex);
+    else (void)wire_lock(world, mutex, false);
+    return COMEX_SUCCESS;
+}
+
+// ---- groups (comex.h:147-172) ----
+int comex_group_translate_ranks(int n, comex_group_t group_from, int *ranks_from, comex_group_t group_to,
+                                int *ranks_to) {
+    ensure_init();
+    for (int i = 0; i < n; ++i) {
+        const int w = translate_world(group_from, ranks_from[i]);
+        int out = -32766;   // MPI_UNDEFINED (MPI_Group_translate_ranks, which the reference calls)
+        if (group_to == COMEX_GROUP_WORLD) {
+            out = w;
+        } else {
+            int sz = 0;
+            comex_group_size(group_to, &sz);
+            for (int k = 0; k < sz; ++k)
+                if (translate_world(group_to, k) == w) { out = k; break; }
+        }
+        ranks_to[i] = out;
+    }
+    return COMEX_SUCCESS;
+}
+
+// comex.h:147 returns the group's MPI_Comm.  This runtime bootstraps without MPI
+// (launcher hooks or the node-shm rendezvous), so there is no communicator to hand
+// out: the call fails loudly instead of returning an unusable handle.
+int comex_group_comm(comex_group_t group, void *comm) {
+    (void)comm;
+    fatal("comex_group_comm(%d): libga_amd has no MPI communicator (it bootstraps without MPI)", group);
 }
 
 }  // extern "C"

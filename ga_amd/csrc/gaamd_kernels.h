@@ -97,6 +97,10 @@ void side_span_host(const int *stride, const int *count, int stride_levels, int6
                     int64_t *lo, int64_t *hi);
 
 int elem_size(int op);            // bytes per element for op; 1 for copy; 0 if unknown
+
+// comex_rmw: fetch-and-add (swap == 0) or swap of one 4- or 8-byte word at
+// `addr` (device-accessible); the old value lands in *out_dev (8 bytes)
+int launch_rmw(int swap, void *addr, int bytes, uint64_t val, uint64_t *out_dev, hipStream_t stream);
 LaunchInfo *last_launch_info();   // most recent launch_strided (any caller)
 unsigned long long kernel_count(int kind);   // launch_strided launches so far, by KernelKind (< kKinds)
 

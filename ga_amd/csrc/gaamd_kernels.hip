@@ -1035,6 +1035,35 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
 }
 
 // ---------------------------------------------------------------------------
+// comex_rmw (comex.h:670; the progress rank's fetch-and-add / swap handlers,
+// comex/src-mpi-pr/comex.c OP_FETCH_AND_ADD / OP_SWAP): one lane reads the old
+// value, writes the new one and reports the old one.  Callers order it on the
+// owner's stream after every earlier operation on those bytes (sched_pick), as
+// the reference serialises it behind the target's earlier messages.
+__global__ __launch_bounds__(64) void k_rmw(void *addr, int swap, int bytes, uint64_t val, uint64_t *out) {
+    if (threadIdx.x != 0) return;
+    if (bytes == 4) {
+        uint32_t *p = reinterpret_cast<uint32_t *>(addr);
+        const uint32_t old = *p;
+        *p = swap ? (uint32_t)val : old + (uint32_t)val;   // int wraparound
+        *out = old;
+    } else {
+        uint64_t *p = reinterpret_cast<uint64_t *>(addr);
+        const uint64_t old = *p;
+        *p = swap ? val : old + val;
+        *out = old;
+    }
+}
+
+int launch_rmw(int swap, void *addr, int bytes, uint64_t val, uint64_t *out_dev, hipStream_t stream) {
+    if (bytes != 4 && bytes != 8) return -4;
+    if (((uintptr_t)addr & (uintptr_t)(bytes - 1)) != 0) return -8;
+    hipLaunchKernelGGL(k_rmw, dim3(1), dim3(64), 0, stream, addr, swap, bytes, val, out_dev);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+// ---------------------------------------------------------------------------
 // I/O-vector kernels: n (src[i], dst[i]) pairs of `bytes` each -- comex_accv /
 // putv / getv (comex/src-mpi-pr/comex.c:7327-7400; the server side
 // _acc_iov_handler 4284-4397).  A side is either a device array of n 64-bit

@@ -41,6 +41,7 @@ constexpr int kMaxNb = 256;          // COMEX_MAX_NB_OUTSTANDING default
 constexpr int kMaxRanks = 64;        // ranks per node
 constexpr int kInboxSlots = 256;     // requests in flight per target
 constexpr size_t kBootSlot = 64 * 1024;
+constexpr int kMaxMutexes = 4096;    // comex_create_mutexes: locks per rank (node shm words)
 
 // ---- node-shared memory (one mapping per node, created at init) ----------
 struct alignas(64) Request {
@@ -55,7 +56,7 @@ struct alignas(64) Request {
     uint64_t bytes;                  // packed bytes
     uint64_t seq;                    // strided: row range (begin << 32 | end)
     uint8_t scale[16];
-    int32_t kind;                    // 0 strided (count/dst_stride), 1 io-vector
+    int32_t kind;                    // 0 strided (count/dst_stride), 1 io-vector, 2 rmw
     int32_t iov_serial;              // io-vector: destinations overlap -> in order
     uint64_t iov_align;              // io-vector: OR of the destination addresses
     uint64_t dst_hi;                 // io-vector: [dst_addr, dst_hi) covers every pair
@@ -69,6 +70,12 @@ struct alignas(64) Inbox {
     Request slot[kInboxSlots];
 };
 
+// comex_rmw reply to one requester (requests are blocking: one in flight per rank)
+struct alignas(64) RmwReply {
+    std::atomic<uint64_t> seq;       // replies delivered so far
+    uint64_t value;                  // the old remote value (4 or 8 bytes)
+};
+
 struct alignas(64) NodeShm {
     std::atomic<uint32_t> magic;
     int32_t size;
@@ -77,12 +84,15 @@ struct alignas(64) NodeShm {
     char pad[40];
     // done[s][t]: requests from s applied by t (monotonic); s, t = positions on the node
     std::atomic<uint64_t> done[kMaxRanks][kMaxRanks];
+    RmwReply rmw[kMaxRanks];         // indexed by the requester's position on the node
     Inbox inbox[1];                  // [size] follows; then boot data area
 };
 
 size_t node_shm_bytes(int size);
 Inbox *inbox_of(NodeShm *s, int rank);
 char *boot_area(NodeShm *s, int size);
+// lock words of the comex mutexes of the rank at node position `rank`
+std::atomic<uint32_t> *mutex_words(NodeShm *s, int size, int rank);
 
 // a device-view byte range [lo, hi) touched by one operation (lo == hi: none)
 struct Span {
@@ -188,10 +198,26 @@ void wire_send_iov(int op, const void *scale, const uint64_t *src_dev, const uin
 // io-vector get: n addresses of rank t -> n local device destinations
 void wire_get_iov(const uint64_t *src, const uint64_t *dst_dev, int n, int bytes, int t);
 void wire_fence(int t);                             // remote completion of everything sent to t
+// armci_msg transport (every multi-rank job): tagged byte messages, in send order per sender
+void msg_send(int to, int tag, const void *buf, size_t len);
+size_t msg_recv(int from, int tag, void *buf, size_t buflen, int *src);   // from < 0: any sender
+// comex_rmw / comex_lock on a rank of another node
+uint64_t wire_rmw(int t, int swap, uint64_t addr, int bytes, uint64_t val);
+bool wire_lock(int t, int mutex, bool acquire);   // acquire: try once (true = held); else release
+// comex.cpp: operations on this rank's (or this node's) memory, for the wire server
+uint64_t rmw_local(int swap, void *addr, int bytes, uint64_t val);
+bool mutex_try_local(int owner, int mutex);
+void mutex_release_local(int owner, int mutex);
 bool segment_of_rank(int owner, uint64_t p, int64_t lo, int64_t hi);   // comex.cpp (reg_cache_find)
 bool segment_local(const void *p, int64_t lo, int64_t hi);              // comex.cpp
 
-// comex.cpp helpers shared with armci.cpp
+// comex.cpp helpers shared with armci.cpp / armci_msg.cpp
 int translate_world(int group, int proc);
+std::vector<int> group_members(int group);   // world ranks in group-rank order
+// armci_msg.cpp: collectives over a member list (world ranks), by messages
+// (msg_send/msg_recv); `key` separates the traffic of different groups
+void members_allgather(const std::vector<int> &members, int key, const void *send, void *recv, size_t bytes);
+void members_barrier(const std::vector<int> &members, int key);
+void members_bcast(const std::vector<int> &members, int key, void *buf, size_t bytes, int root_index);
 
 }  // namespace gaamd

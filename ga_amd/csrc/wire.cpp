@@ -53,7 +53,10 @@
 #include <sys/socket.h>
 #include <unistd.h>
 #include <algorithm>
+#include <condition_variable>
+#include <deque>
 #include <memory>
+#include <mutex>
 
 namespace gaamd {
 
@@ -66,8 +69,9 @@ enum : int32_t {
     W_ACC = 8,          // + COMEX_ACC_x - 37: INT DBL FLT CPL DCP LNG
     W_ACC_PACKED = 14,  // + ...
     W_ACC_IOV = 20,     // + ...
-    W_FENCE = 26, W_QUIT = 33,
-    W_PING = 1000       // bootstrap self-test (not a reference op)
+    W_FENCE = 26, W_FETCH_AND_ADD = 27, W_SWAP = 28, W_LOCK = 31, W_UNLOCK = 32, W_QUIT = 33,
+    W_PING = 1000,      // bootstrap self-test (not a reference op)
+    W_MSG = 1001        // armci_msg_snd payload (MPI_Send in the reference, message.c:354)
 };
 
 struct Frame {
@@ -118,6 +122,25 @@ Pinned g_srv[2];
 int g_srv_next = 0;
 size_t g_chunk = 64u << 20;
 constexpr size_t kSecret = 32;
+
+// armci_msg point-to-point messages received for this rank, in arrival order
+// (per sender in send order: one connection per sender)
+struct Msg {
+    int from, tag;
+    std::vector<char> data;
+};
+std::mutex g_msg_mu;
+std::mutex g_send_mu;   // initiator connections: messages may be sent from any user thread
+std::condition_variable g_msg_cv;
+std::deque<Msg> g_msgs;
+
+void msg_push(int from, int tag, std::vector<char> &&data) {
+    {
+        std::lock_guard<std::mutex> g(g_msg_mu);
+        g_msgs.push_back({from, tag, std::move(data)});
+    }
+    g_msg_cv.notify_all();
+}
 unsigned char g_secret[kSecret];
 
 void wait_pinned(Pinned &b) {
@@ -407,6 +430,21 @@ bool serve_frame(int fd) {
         return true;
     }
     if (op == W_QUIT) return false;
+    if (op == W_MSG) {
+        std::vector<char> buf(f.length);
+        if (f.length) recv_all(fd, buf.data(), f.length);
+        msg_push(f.src_rank, (int)(int64_t)f.remote_address, std::move(buf));
+        return true;
+    }
+    if (op == W_LOCK || op == W_UNLOCK) {
+        // mutex f.remote_address of this rank (comex_lock/unlock, comex.c OP_LOCK/OP_UNLOCK):
+        // a try-lock answered at once; the initiator retries
+        char ok = 1;
+        if (op == W_LOCK) ok = mutex_try_local(rt().rank, (int)f.remote_address) ? 1 : 0;
+        else mutex_release_local(rt().rank, (int)f.remote_address);
+        send_all(fd, &ok, 1);
+        return true;
+    }
     static thread_local bool dev_set = false;
     if (!dev_set) {
         GA_HIP(hipSetDevice(rt().device));
@@ -417,6 +455,16 @@ bool serve_frame(int fd) {
         wait_pinned(g_srv[1]);
         const char ack = 1;
         send_all(fd, &ack, 1);
+        return true;
+    }
+    if (op == W_FETCH_AND_ADD || op == W_SWAP) {
+        // after every earlier frame of this connection: their kernels were scheduled
+        // before this one, and the rmw kernel is ordered behind those touching its bytes
+        check_local(f.remote_address, 0, (int64_t)f.length, f.src_rank);
+        uint64_t val = 0;
+        memcpy(&val, f.scale, 8);
+        const uint64_t old = rmw_local(op == W_SWAP, (void *)(uintptr_t)f.remote_address, (int)f.length, val);
+        send_all(fd, &old, sizeof(old));
         return true;
     }
     if (op == W_PUT || op == W_PUT_PACKED || (op >= W_ACC && op < W_ACC_PACKED + 6)) {
@@ -547,8 +595,68 @@ bool wire_active() { return g_active; }
 
 void wire_init() {
     Runtime &r = rt();
-    if (r.nnodes <= 1 || g_active) return;
+    // every multi-rank job: the armci_msg messages travel here too, inside a node
+    // as between nodes (COMEX_AMD_MSG=0 keeps single-node jobs socket-free; then
+    // only the world-group collectives, which use the node shm, are available)
+    const char *m = getenv("COMEX_AMD_MSG");
+    const bool msg = !(m && atoi(m) == 0);
+    if (r.size <= 1 || g_active || (r.nnodes <= 1 && !msg)) return;
     start_sockets();
+}
+
+void msg_send(int to, int tag, const void *buf, size_t len) {
+    Runtime &r = rt();
+    if (to < 0 || to >= r.size) fatal("armci_msg_snd: rank %d out of range", to);
+    if (to == r.rank) {
+        std::vector<char> d((const char *)buf, (const char *)buf + len);
+        msg_push(r.rank, tag, std::move(d));
+        return;
+    }
+    if (!g_active) fatal("armci_msg_snd needs the message transport (COMEX_AMD_MSG=0 disabled it)");
+    Frame f = make_frame(W_MSG, to, (uint64_t)(int64_t)tag, nullptr, nullptr, 0);
+    f.length = len;
+    std::lock_guard<std::mutex> g(g_send_mu);
+    send_frame(to, f, buf, len);
+}
+
+size_t msg_recv(int from, int tag, void *buf, size_t buflen, int *src) {
+    std::unique_lock<std::mutex> g(g_msg_mu);
+    for (;;) {
+        for (auto it = g_msgs.begin(); it != g_msgs.end(); ++it) {
+            if (it->tag != tag || (from >= 0 && it->from != from)) continue;
+            if (it->data.size() > buflen)
+                fatal("armci_msg_rcv: message of %zu bytes from rank %d, buffer holds %zu", it->data.size(), it->from,
+                      buflen);
+            const size_t n = it->data.size();
+            if (n) memcpy(buf, it->data.data(), n);
+            if (src) *src = it->from;
+            g_msgs.erase(it);
+            return n;
+        }
+        g_msg_cv.wait(g);
+    }
+}
+
+uint64_t wire_rmw(int t, int swap, uint64_t addr, int bytes, uint64_t val) {
+    Frame f = make_frame(swap ? W_SWAP : W_FETCH_AND_ADD, t, addr, nullptr, nullptr, 0);
+    f.length = (uint64_t)bytes;
+    memcpy(f.scale, &val, 8);
+    std::lock_guard<std::mutex> g(g_send_mu);
+    Peer &p = connect_to(t);
+    send_all(p.fd, &f, sizeof(f));
+    uint64_t old = 0;
+    recv_all(p.fd, &old, sizeof(old));
+    return old;
+}
+
+bool wire_lock(int t, int mutex, bool acquire) {
+    Frame f = make_frame(acquire ? W_LOCK : W_UNLOCK, t, (uint64_t)mutex, nullptr, nullptr, 0);
+    std::lock_guard<std::mutex> g(g_send_mu);
+    Peer &p = connect_to(t);
+    send_all(p.fd, &f, sizeof(f));
+    char ok = 0;
+    recv_all(p.fd, &ok, 1);
+    return ok != 0;
 }
 
 void wire_finalize() {

@@ -64,12 +64,19 @@ extern int comex_initialized();
 extern int comex_finalize();
 extern void comex_error(const char *msg, int code);
 
-/* groups: comex.h:107-186 (world group only, plus rank translation) */
+/* groups: comex.h:107-186 */
 extern int comex_group_create(int n, int *pid_list, comex_group_t group, comex_group_t *new_group);
 extern int comex_group_free(comex_group_t group);
 extern int comex_group_rank(comex_group_t group, int *rank);
 extern int comex_group_size(comex_group_t group, int *size);
 extern int comex_group_translate_world(comex_group_t group, int group_rank, int *world_rank);
+/* comex.h:159: ranks of group_from in group_to (MPI_UNDEFINED = -32766 if absent) */
+extern int comex_group_translate_ranks(int n, comex_group_t group_from, int *ranks_from,
+                                       comex_group_t group_to, int *ranks_to);
+#ifdef MPI_VERSION
+/* comex.h:147: aborts -- libga_amd bootstraps without MPI, there is no communicator */
+extern int comex_group_comm(comex_group_t group, MPI_Comm *comm);
+#endif
 extern int comex_barrier(comex_group_t group);
 
 /* put: comex.h:199-302 */
@@ -125,6 +132,15 @@ extern int comex_free(void *ptr, comex_group_t group);
 extern int comex_free_dev(void *ptr, comex_group_t group);
 extern void *comex_malloc_local(size_t bytes);
 extern int comex_free_local(void *ptr);
+
+/* atomics and mutexes: comex.h:607-670.  comex_rmw is applied by the owner of
+ * prem (its GPU, behind every earlier operation on those bytes); mutexes are
+ * words in the owner node's shared memory (at most 4096 per rank). */
+extern int comex_create_mutexes(int num);
+extern int comex_destroy_mutexes();
+extern int comex_lock(int mutex, int proc);
+extern int comex_unlock(int mutex, int proc);
+extern int comex_rmw(int op, void *ploc, void *prem, int extra, int proc, comex_group_t group);
 
 /* completion: comex.h:588-709 */
 extern int comex_fence_proc(int proc, comex_group_t group);

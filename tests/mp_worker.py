@@ -54,7 +54,8 @@ def main():
     rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import ga_amd
     L = ga_amd.lib()
-    if mode in ("boot-gloo", "remote-gloo", "boot-nodes", "ga-gloo", "stress-gloo", "scatremote-gloo"):
+    if mode in ("boot-gloo", "remote-gloo", "boot-nodes", "ga-gloo", "stress-gloo", "scatremote-gloo",
+                "armcimisc-gloo"):
         ag, bar = torch_hooks(rank, size)
         keep = (ag, bar)  # noqa: F841
         assert L.gaamd_set_bootstrap(rank, size, rank, ctypes.cast(ag, ctypes.c_void_p),
@@ -92,6 +93,8 @@ def main():
         ga_ref_test(L, rank, size)
     elif mode == "order":
         order_test(L, rank, size)
+    elif mode in ("armcimisc", "armcimisc-gloo"):
+        armci_misc_test(L, rank, size)
     else:
         remote_test(L, rank, size)
     print(f"RANK {rank} OK", flush=True)
@@ -303,6 +306,240 @@ def order_test(L, rank, size):
     ga_amd.comex_barrier()
     assert ga_amd.comex_free(seg[rank]) == 0
     ga_amd.comex_finalize()
+
+
+class MemInfo(ctypes.Structure):   # armci_meminfo_t (include/armci.h)
+    _fields_ = [("armci_addr", ctypes.c_void_p), ("addr", ctypes.c_void_p), ("size", ctypes.c_size_t),
+                ("cpid", ctypes.c_int), ("idlist", ctypes.c_long * 128)]
+
+
+def armci_misc_test(L, rank, size):
+    """The rest of the ARMCI surface GA calls: the message
+    layer (message.c), processor groups (groups.c), rmw and mutexes (armci.c:
+    282-292, 755-771), single values, flagged puts, domains, Memget and
+    armci_read/write_strided -- each checked for its reference result."""
+    import ga_amd
+    c_int, byref, vp = ctypes.c_int, ctypes.byref, ctypes.c_void_p
+    assert L.ARMCI_Init() == 0
+    assert (L.armci_msg_me(), L.armci_msg_nproc()) == (rank, size)
+    nxt, prv = (rank + 1) % size, (rank - 1) % size
+
+    # point to point: a ring, then everybody to rank 0 through rcvany
+    out = (c_int * 4)(*[100 * rank + i for i in range(4)])
+    inp, ln = (c_int * 4)(), c_int()
+    L.armci_msg_snd(77, out, 16, nxt)
+    L.armci_msg_rcv(77, inp, 16, byref(ln), prv)
+    assert ln.value == 16 and list(inp) == [100 * prv + i for i in range(4)], list(inp)
+    if rank:
+        L.armci_msg_snd(78, out, 8, 0)
+    else:
+        seen = set()
+        for _ in range(size - 1):
+            src = L.armci_msg_rcvany(78, inp, 16, byref(ln))
+            assert ln.value == 8 and inp[0] == 100 * src and inp[1] == 100 * src + 1
+            seen.add(src)
+        assert seen == set(range(1, size))
+    say(rank, "snd/rcv/rcvany")
+
+    # gops (message.c:188-225)
+    x = (c_int * 3)(rank + 1, rank, -rank)
+    L.armci_msg_igop(x, 3, b"+")
+    n1 = size * (size + 1) // 2
+    assert list(x) == [n1, n1 - size, -(n1 - size)], list(x)
+    x = (c_int * 2)(rank, -rank)
+    L.armci_msg_igop(x, 2, b"max")
+    assert list(x) == [size - 1, 0]
+    lx = (ctypes.c_long * 1)(1 << rank)
+    L.armci_msg_lgop(lx, 1, b"or")
+    assert lx[0] == (1 << size) - 1
+    llx = (ctypes.c_longlong * 1)(rank + 2)
+    L.armci_msg_llgop(llx, 1, b"*")
+    assert llx[0] == int(np.prod([r + 2 for r in range(size)]))
+    fx = (ctypes.c_float * 1)(float(rank) + 0.5)
+    L.armci_msg_fgop(fx, 1, b"min")
+    assert fx[0] == 0.5
+    dx = (ctypes.c_double * 2)(-(rank + 1.5), rank * 0.25)
+    L.armci_msg_dgop(dx, 2, b"absmax")
+    assert list(dx) == [size + 0.5, (size - 1) * 0.25], list(dx)
+    dx = (ctypes.c_double * 1)(rank + 1.0)
+    L.armci_msg_gop_scope(333, dx, 1, b"+", -307)
+    assert dx[0] == float(n1)
+    say(rank, "gops")
+
+    # bcast from the last rank, sel by max / min of the leading value
+    b = (ctypes.c_double * 3)(*([rank * 1.5] * 3))
+    L.armci_msg_bcast(b, 24, size - 1)
+    assert list(b) == [(size - 1) * 1.5] * 3
+    sel = (c_int * 3)((rank * 7) % size, rank, 1000 + rank)
+    L.armci_msg_sel_scope(333, sel, 12, b"max", -99, 1)
+    winner = max(range(size), key=lambda r: ((r * 7) % size, -r))
+    assert list(sel) == [(winner * 7) % size, winner, 1000 + winner], (list(sel), winner)
+    sel = (c_int * 3)((rank * 7) % size, rank, 1000 + rank)
+    L.armci_msg_sel_scope(333, sel, 12, b"min", -99, 1)
+    winner = min(range(size), key=lambda r: ((r * 7) % size, r))
+    assert list(sel) == [(winner * 7) % size, winner, 1000 + winner], (list(sel), winner)
+    root, up, left, right = c_int(), c_int(), c_int(), c_int()
+    L.armci_msg_bintree(333, byref(root), byref(up), byref(left), byref(right))
+    want_l = 2 * rank + 1 if 2 * rank + 1 < size else -1
+    want_r = 2 * rank + 2 if 2 * rank + 2 < size else -1
+    assert (root.value, up.value, left.value, right.value) == (0, (rank - 1) // 2 if rank else -1, want_l, want_r)
+    addrs = (vp * size)()
+    addrs[rank] = 0x1000 * (rank + 1)
+    L.armci_exchange_address(addrs, size)
+    assert [a or 0 for a in addrs] == [0x1000 * (r + 1) for r in range(size)]
+    L.armci_msg_barrier()
+    say(rank, "bcast/sel/bintree/exchange")
+
+    # segments: values, rmw, mutexes, flagged puts
+    seg = (vp * size)()
+    nbytes = 1 << 20
+    assert L.ARMCI_Malloc(seg, nbytes) == 0
+    zero = np.zeros(nbytes // 8, dtype=np.int64)
+    assert L.ARMCI_Put(zero.ctypes.data_as(vp), vp(seg[rank]), nbytes, rank) == 0
+    L.ARMCI_Barrier()
+    assert L.ARMCI_PutValueInt(1000 + rank, vp(seg[nxt] + 0), nxt) == 0
+    assert L.ARMCI_PutValueLong(-(1 << 40) - rank, vp(seg[nxt] + 8), nxt) == 0
+    assert L.ARMCI_PutValueFloat(0.25 + rank, vp(seg[nxt] + 16), nxt) == 0
+    assert L.ARMCI_PutValueDouble(1e300 * (rank + 1), vp(seg[nxt] + 24), nxt) == 0
+    h = c_int(-1)
+    assert L.ARMCI_NbPutValueInt(7 + rank, vp(seg[nxt] + 32), nxt, byref(h)) == 0
+    assert L.ARMCI_Wait(byref(h)) == 0
+    L.ARMCI_Barrier()
+    assert L.ARMCI_GetValueInt(vp(seg[rank] + 0), rank) == 1000 + prv
+    assert L.ARMCI_GetValueLong(vp(seg[rank] + 8), rank) == -(1 << 40) - prv
+    assert L.ARMCI_GetValueFloat(vp(seg[rank] + 16), rank) == 0.25 + prv
+    assert L.ARMCI_GetValueDouble(vp(seg[rank] + 24), rank) == 1e300 * (prv + 1)
+    assert L.ARMCI_GetValueInt(vp(seg[nxt] + 32), nxt) == 7 + rank
+    say(rank, "put/get values")
+
+    # fetch-and-add: every rank adds (rank+1) 50 times to rank 0's int and long
+    FETCH_AND_ADD, FETCH_AND_ADD_LONG, SWAP, SWAP_LONG = 12, 13, 10, 11
+    olds = []
+    for _ in range(50):
+        old = c_int()
+        assert L.ARMCI_Rmw(FETCH_AND_ADD, byref(old), vp(seg[0] + 64), rank + 1, 0) == 0
+        olds.append(old.value)
+        oldl = ctypes.c_long()
+        assert L.ARMCI_Rmw(FETCH_AND_ADD_LONG, byref(oldl), vp(seg[0] + 72), (rank + 1) << 33, 0) == 0
+    assert len(set(olds)) == 50 and all(0 <= o < 50 * n1 for o in olds)
+    L.ARMCI_Barrier()
+    assert L.ARMCI_GetValueInt(vp(seg[0] + 64), 0) == 50 * n1
+    assert L.ARMCI_GetValueLong(vp(seg[0] + 72), 0) == 50 * (n1 << 33)
+    # swap: a token passes through every rank; the values seen are a permutation
+    if rank == 0:
+        assert L.ARMCI_PutValueInt(-1, vp(seg[0] + 80), 0) == 0
+    L.ARMCI_Barrier()
+    v = c_int(rank)
+    assert L.ARMCI_Rmw(SWAP, byref(v), vp(seg[0] + 80), 0, 0) == 0
+    got = (c_int * 1)(v.value)
+    L.armci_msg_igop(got, 1, b"+")
+    L.ARMCI_Barrier()
+    last = L.ARMCI_GetValueInt(vp(seg[0] + 80), 0)
+    assert got[0] + last == -1 + n1 - size, (got[0], last)
+    vl = ctypes.c_long(5 << 40)
+    if rank == size - 1:
+        assert L.ARMCI_Rmw(SWAP_LONG, byref(vl), vp(seg[1 % size] + 88), 0, 1 % size) == 0
+        assert vl.value == 0
+    L.ARMCI_Barrier()
+    assert L.ARMCI_GetValueLong(vp(seg[1 % size] + 88), 1 % size) == 5 << 40
+    say(rank, "rmw")
+
+    # mutexes: a get / +1 / put critical section on rank (size-1)'s counter
+    assert L.ARMCI_Create_mutexes(3) == 0
+    owner = size - 1
+    for it in range(20):
+        L.ARMCI_Lock(it % 3, owner)
+        cur = L.ARMCI_GetValueLong(vp(seg[owner] + 128 + 8 * (it % 3)), owner)
+        assert L.ARMCI_PutValueLong(cur + 1, vp(seg[owner] + 128 + 8 * (it % 3)), owner) == 0
+        L.ARMCI_Unlock(it % 3, owner)
+    L.ARMCI_Barrier()
+    tot = sum(L.ARMCI_GetValueLong(vp(seg[owner] + 128 + 8 * k), owner) for k in range(3))
+    assert tot == 20 * size, tot
+    assert L.ARMCI_Destroy_mutexes() == 0
+    say(rank, "mutexes")
+
+    # flagged put: a strided patch then the flag; the receiver spins on its flag
+    rows, rowb = 64, 512
+    pat = np.arange(rows * rowb // 8, dtype=np.float64) + 1e6 * rank
+    ss, ds, cnt = ga_amd.int_array([rowb]), ga_amd.int_array([2 * rowb]), ga_amd.int_array([rowb, rows])
+    flag_off, data_off = 4096, 8192
+    assert L.ARMCI_PutS_flag(pat.ctypes.data_as(vp), ss, vp(seg[nxt] + data_off), ds, cnt, 1,
+                             ctypes.cast(vp(seg[nxt] + flag_off), ctypes.POINTER(c_int)), 1 + rank, nxt) == 0
+    while L.ARMCI_GetValueInt(vp(seg[rank] + flag_off), rank) != 1 + prv:
+        pass
+    back = np.zeros(rows * 2 * rowb // 8, dtype=np.float64)
+    assert L.ARMCI_Get(vp(seg[rank] + data_off), back.ctypes.data_as(vp), rows * 2 * rowb, rank) == 0
+    want = np.arange(rows * rowb // 8, dtype=np.float64) + 1e6 * prv
+    assert np.array_equal(back.reshape(rows, -1)[:, :rowb // 8].ravel(), want)
+    L.ARMCI_Barrier()
+    say(rank, "PutS_flag")
+
+    # domains: one node here (or COMEX_AMD_NODE's binning)
+    nd, nn, ns = c_int(), c_int(), c_int()
+    L.gaamd_node_info(byref(nd), byref(nn), byref(ns))
+    if nn.value == 1:
+        assert L.armci_domain_count(0) == 1 and L.armci_domain_nprocs(0, 0) == size
+        assert L.armci_domain_my_id(0) == 0 and L.armci_domain_id(0, prv) == 0
+        assert all(L.armci_domain_same_id(0, q) for q in range(size))
+        assert L.armci_domain_glob_proc_id(0, 0, size - 1) == size - 1
+    assert L.ARMCI_Same_node(nxt) == 0 and L.ARMCI_Uses_shm() == 0
+
+    # groups: the even ranks (groups.c); every rank creates it, members use it
+    evens = [q for q in range(size) if q % 2 == 0]
+    g = c_int()
+    L.ARMCI_Group_create(len(evens), ga_amd.int_array(evens), byref(g))
+    w = c_int()
+    L.ARMCI_Group_get_world(byref(w))
+    assert w.value == 0
+    if rank % 2 == 0:
+        gr, gs = c_int(), c_int()
+        L.ARMCI_Group_rank(byref(g), byref(gr))
+        L.ARMCI_Group_size(byref(g), byref(gs))
+        assert (gr.value, gs.value) == (rank // 2, len(evens))
+        assert L.ARMCI_Absolute_id(byref(g), gs.value - 1) == evens[-1]
+        gx = (ctypes.c_double * 1)(rank + 1.0)
+        L.armci_msg_group_dgop(gx, 1, b"+", byref(g))
+        assert gx[0] == float(sum(q + 1 for q in evens))
+        gi = (c_int * 1)(rank)
+        L.armci_msg_group_igop(gi, 1, b"max", byref(g))
+        assert gi[0] == evens[-1]
+        gb = (c_int * 2)(rank, rank)
+        L.armci_msg_group_bcast_scope(333, gb, 8, evens[-1], byref(g))
+        assert list(gb) == [evens[-1]] * 2
+        gseg = (vp * len(evens))()
+        assert L.ARMCI_Malloc_group(gseg, 4096, byref(g)) == 0
+        peer = evens[(gr.value + 1) % len(evens)]
+        assert L.ARMCI_PutValueInt(500 + rank, vp(gseg[(gr.value + 1) % len(evens)]), peer) == 0
+        L.ARMCI_GroupFence(byref(g))
+        L.armci_msg_group_barrier(byref(g))
+        src_r = evens[(gr.value - 1) % len(evens)]
+        assert L.ARMCI_GetValueInt(vp(gseg[gr.value]), rank) == 500 + src_r
+        L.armci_msg_group_barrier(byref(g))
+        assert L.ARMCI_Free_group(vp(gseg[gr.value]), byref(g)) == 0
+    L.ARMCI_Barrier()
+    L.ARMCI_Group_free(byref(g))
+    say(rank, "groups")
+
+    # Memget (armci.c:460-538) and armci_write/read_strided (iterator.c:158-193)
+    mi = MemInfo()
+    L.ARMCI_Memget(4096, byref(mi), 0)
+    assert mi.size == 4096 and mi.cpid == rank and L.ARMCI_Memat(byref(mi), 0) == mi.addr
+    ctypes.memset(mi.addr, 7, 4096)
+    L.ARMCI_Memctl(byref(mi))
+    patch = np.zeros((6, 10), dtype=np.float64)
+    packed = np.arange(4 * 3, dtype=np.float64) + rank
+    L.armci_write_strided(patch[1:, 2:].ctypes.data_as(vp), 1, ga_amd.int_array([80]), ga_amd.int_array([24, 4]),
+                          packed.ctypes.data_as(vp))
+    assert np.array_equal(patch[1:5, 2:5].ravel(), packed) and patch.sum() == packed.sum()
+    back = np.zeros(12, dtype=np.float64)
+    L.armci_read_strided(patch[1:, 2:].ctypes.data_as(vp), 1, ga_amd.int_array([80]), ga_amd.int_array([24, 4]),
+                         back.ctypes.data_as(vp))
+    assert np.array_equal(back, packed)
+    say(rank, "memget/strided")
+
+    L.ARMCI_Barrier()
+    assert L.ARMCI_Free(vp(seg[rank])) == 0
+    L.ARMCI_Finalize()
 
 
 def ga_test(L, rank, size):

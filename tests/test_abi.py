@@ -12,7 +12,7 @@ import ga_amd
 from ga_amd._lib import LIB_PATH, SIGNATURES
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("comex.h", "armci.h", "ga_amd.h", "ga.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("comex.h", "armci.h", "message.h", "ga_amd.h", "ga.h")]
 
 
 def declared_functions(path):
@@ -168,3 +168,17 @@ def test_c_client_runs(tmp_path):
     exe = _build_c_client(tmp_path)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "abi_client OK" in r.stdout, (r.returncode, r.stdout, r.stderr[-2000:])
+
+
+def test_global_src_armci_calls_link(tmp_path):
+    """Every ARMCI_* / armci_msg_* function the reference GA layer calls in its
+    default build (global/src) resolves in the library (tests/c/global_src_link.c
+    holds the list); only addresses are taken, nothing runs on a GPU."""
+    exe = tmp_path / "global_src_link"
+    cmd = ["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "c", "global_src_link.c"), "-L", os.path.join(ROOT, "ga_amd"), "-lga_amd",
+           "-Wl,-rpath," + os.path.join(ROOT, "ga_amd"), "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "global_src_link OK" in r.stdout, (r.stdout, r.stderr)

@@ -211,3 +211,12 @@ def test_ga_ndim_scatter_acc_gather_restated(n):
     distinct random elements per rank (crossing owner blocks), scatter-acc then
     per-element get, gather vs get; ndim 1..7, int/double/double complex, exact."""
     launch("ngags", n=n, timeout=150)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,nodes", [(1, None), (2, None), (3, None), (3, [0, 0, 1]), (2, [0, 1])])
+def test_armci_message_groups_rmw_mutexes(n, nodes):
+    """message.c / groups.c / rmw / mutexes / values / flags / domains / Memget /
+    armci_read/write_strided over n ranks; with `nodes` the cross-node cases go
+    through the wire protocol's FETCH_AND_ADD / SWAP / LOCK / UNLOCK frames."""
+    launch("armcimisc-gloo" if nodes else "armcimisc", n=n, timeout=120, nodes=nodes)
