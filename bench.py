@@ -253,8 +253,13 @@ def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True
     lo, hi = ([0, 0], [dims[0] - 1, dims[1] - 1]) if exchange else (list(blo), list(bhi))
     rows, cols = hi[0] - lo[0] + 1, hi[1] - lo[1] + 1
     payload = rows * cols * 8
-    src = ga_amd.DeviceBuffer(payload)
-    ga_amd.fill(src.ptr, rows * cols, 0, 0x5EED0000 + dist.rank)
+    if args.src_seg:   # the local buffer in this rank's segment: the direct-source route
+        src_seg = ga_amd.comex_malloc(payload, dist.size)
+        src, src_ptr = None, src_seg[dist.rank]
+    else:
+        src_seg, src = None, ga_amd.DeviceBuffer(payload)
+        src_ptr = src.ptr
+    ga_amd.fill(src_ptr, rows * cols, 0, 0x5EED0000 + dist.rank)
     # the local block: fill through NGA_Access (its HBM address)
     ptr, ld = ctypes.c_void_p(), (ctypes.c_int * 1)()
     L.NGA_Access(g, blo, bhi, ctypes.byref(ptr), ld)
@@ -268,7 +273,7 @@ def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True
     alpha = ctypes.c_double(SCALE[DBL])
     clo, chi, cld = ia(lo), ia(hi), ia([cols])
     def step(_i):
-        L.NGA_Acc(g, clo, chi, ctypes.c_void_p(src.ptr), cld, ctypes.byref(alpha))
+        L.NGA_Acc(g, clo, chi, ctypes.c_void_p(src_ptr), cld, ctypes.byref(alpha))
         if args.verbose:
             print(f"rank {dist.rank}: NGA_Acc done", file=sys.stderr, flush=True)
 
@@ -297,8 +302,12 @@ def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True
     else:
         region_ms, _ = event_region(L, step, steps, nxt + steps)
         avg_kernel_s = dist.max(region_ms / 1e3 / steps)
-    src.free()
+    routes = ga_amd.route_counts()
+    if src is not None:
+        src.free()
     L.GA_Sync()
+    if src_seg is not None:
+        ga_amd.comex_free(src_seg[dist.rank])
     L.GA_Destroy(g)
     if terminate:
         L.GA_Terminate()
@@ -306,7 +315,7 @@ def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True
             + ("every rank the whole array (M2)" if exchange else f"own {rows}x{cols} block (M1)"))
     return dict(op=DBL, desc=desc, payload=payload, alg_bytes=3 * payload, elems=rows * cols, elapsed=elapsed,
                 avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), exchange=exchange,
-                steps=steps, block_bytes=block_bytes, array_bytes=dims[0] * dims[1] * 8)
+                steps=steps, block_bytes=block_bytes, array_bytes=dims[0] * dims[1] * 8, routes=routes)
 
 
 def run_gpu(args, dist, finalize=True):
@@ -336,29 +345,41 @@ def run_gpu(args, dist, finalize=True):
     # r+1's (the remote path, pack -> owner's unpack-acc).
     exchange = args.exchange and dist.size > 1
     target = (dist.rank + 1) % dist.size if exchange else dist.rank
-    sets, segs = [], []
+    # --self-packed (N=1): accumulates to this rank take the packed route (pack ->
+    # staging -> progress thread unpack-acc), forced as COMEX_ENABLE_ACC_SELF=0 /
+    # COMEX_ENABLE_ACC_SMP=0 force it in the reference (comex.c:450-471)
+    self_packed = args.self_packed and not exchange
+    seg_dst = exchange or self_packed      # the packed and direct routes need a registered dst
+    sets, segs, src_segs = [], [], []
     for i in range(args.sets):
-        s = ga_amd.DeviceBuffer(sbytes)
-        ga_amd.fill(s.ptr, sbytes // 8, type_code, 0x5EED0000 + dist.rank)
-        if exchange:
+        if args.src_seg:                   # the source patch in this rank's own segment
+            sseg = ga_amd.comex_malloc(sbytes, dist.size)
+            s = None
+            src_segs.append(sseg)
+            sptr = sseg[dist.rank]
+        else:
+            s = ga_amd.DeviceBuffer(sbytes)
+            sptr = s.ptr
+        ga_amd.fill(sptr, sbytes // 8, type_code, 0x5EED0000 + dist.rank)
+        if seg_dst:
             seg = ga_amd.comex_malloc(dbytes, dist.size)
             ga_amd.fill(seg[dist.rank], dbytes // 8, type_code, 0x5EED0001 + dist.rank + 977 * i)
             segs.append(seg)
-            sets.append((s, None))
+            sets.append((s, None, sptr))
         else:
             d = ga_amd.DeviceBuffer(dbytes)
             ga_amd.fill(d.ptr, dbytes // 8, type_code, 0x5EED0001 + dist.rank + 977 * i)
-            sets.append((s, d))
+            sets.append((s, d, sptr))
     ga_amd.sync()
-    if exchange:
+    if seg_dst or args.src_seg:
         L.comex_barrier(0)
 
     keep, sp = ga_amd.scale_buffer(op, SCALE[op])
     ss, ds, cnt = ga_amd.int_array(sstr), ga_amd.int_array(dstr), ga_amd.int_array(count)
-    if exchange:
-        ptrs = [(ctypes.c_void_p(s.ptr), ctypes.c_void_p(seg[target])) for (s, _), seg in zip(sets, segs)]
+    if seg_dst:
+        ptrs = [(ctypes.c_void_p(sp), ctypes.c_void_p(seg[target])) for (_, _, sp), seg in zip(sets, segs)]
     else:
-        ptrs = [(ctypes.c_void_p(s.ptr), ctypes.c_void_p(d.ptr)) for s, d in sets]
+        ptrs = [(ctypes.c_void_p(sp), ctypes.c_void_p(d.ptr)) for _, d, sp in sets]
     pipeline = args.pipeline and not exchange
     packed = [ga_amd.DeviceBuffer(payload) for _ in sets] if pipeline else []
     hd = Handles(L)
@@ -385,6 +406,7 @@ def run_gpu(args, dist, finalize=True):
             raise RuntimeError(f"step returned {rc}")
 
     nxt = warm(step, args)
+    warmup_steps = nxt
     hd.drain()
     ga_amd.sync()
     launch = ga_amd.last_launch()
@@ -393,39 +415,62 @@ def run_gpu(args, dist, finalize=True):
     L.comex_barrier(0)
     dist.barrier()
     ga_amd.sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(nxt + i)
-    hd.drain()                          # every step's kernel has finished (comex_wait_all)
-    ga_amd.sync()
-    if exchange:
-        L.comex_fence_all(0)            # remote completion: the owner has applied every request
-    t1 = time.perf_counter()
+    def value_region(first):
+        t0 = time.perf_counter()
+        step(first)
+        t_first = time.perf_counter()
+        for i in range(1, args.steps):
+            step(first + i)
+        t_enq = time.perf_counter()
+        hd.drain()                          # every step's kernel has finished (comex_wait_all)
+        ga_amd.sync()
+        if seg_dst:
+            L.comex_fence_all(0)            # remote completion: the owner has applied every request
+        t1 = time.perf_counter()
+        return t1 - t0, {"first_call_us": round((t_first - t0) * 1e6, 1),
+                         "enqueue_all_us": round((t_enq - t0) * 1e6, 1), "total_us": round((t1 - t0) * 1e6, 1)}
+
+    elapsed, region_profile = value_region(nxt)
     dist.barrier()
-    elapsed = dist.max(t1 - t0)
-    if exchange:
-        avg_kernel_s = elapsed / args.steps   # the work runs on the owners' streams
+    elapsed = dist.max(elapsed)
+    nxt += args.steps
+    # diagnostics only (BENCH_DIAG_REGIONS=n): n more regions shaped exactly like
+    # the value region, to show its spread; `value` stays the first region
+    diag = []
+    for _ in range(int(os.environ.get("BENCH_DIAG_REGIONS", "0"))):
+        L.comex_barrier(0)
+        dist.barrier()
+        ga_amd.sync()
+        e, prof = value_region(nxt)
+        nxt += args.steps
+        diag.append(dict(prof, us_per_step=round(e / args.steps * 1e6, 2)))
+    if seg_dst:
+        avg_kernel_s = elapsed / args.steps   # the work runs on the owners' streams / progress thread
     else:
         # roofline: the same K steps again inside per-stream HIP events
-        region_ms, _ = event_region(L, step, args.steps, nxt + args.steps)
+        region_ms, _ = event_region(L, step, args.steps, nxt)
         avg_kernel_s = dist.max(region_ms / 1e3 / args.steps)
 
     res = dict(op=op, desc=desc, payload=payload, alg_bytes=alg_bytes, elems=elems, elapsed=elapsed,
                avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), pipeline=pipeline,
-               xfer=xfer, warmup_steps=nxt)
+               xfer=xfer, warmup_steps=warmup_steps, region_profile=region_profile, diag_regions=diag)
     for b in packed:
         b.free()
     if args.host_rates and dist.rank == 0:
         res["host"] = host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_bytes)
-    for s, d in sets:
-        s.free()
+    routes = ga_amd.route_counts()
+    for s, d, _ in sets:
+        if s is not None:
+            s.free()
         if d is not None:
             d.free()
-    if exchange:
+    if segs or src_segs:
         L.comex_barrier(0)
-        for seg in segs:
+        for seg in segs + src_segs:
             ga_amd.comex_free(seg[dist.rank])
     res["exchange"] = exchange
+    res["self_packed"] = self_packed
+    res["routes"] = routes
     if finalize:
         ga_amd.comex_finalize()
     return res
@@ -438,8 +483,14 @@ def c5_extras(args, dist):
     the owner's unpack-acc reading it over xGMI).  Few steps: these are reported
     beside the headline, not as `value`."""
     out = {}
-    for mode, exchange, steps in (("M1", False, args.c5_steps), ("M2", True, max(1, args.c5_steps // 2))):
-        r = run_ga(args, dist, exchange=exchange, steps=steps, warmup_ms=0.0, terminate=(mode == "M2"))
+    saved = args.src_seg
+    m2 = max(1, args.c5_steps // 2)
+    for mode, exchange, steps, src_seg in (("M1", False, args.c5_steps, False), ("M2", True, m2, False),
+                                           ("M2_src_in_segment", True, m2, True)):
+        args.src_seg = src_seg
+        r = run_ga(args, dist, exchange=exchange, steps=steps, warmup_ms=0.0,
+                   terminate=(mode == "M2_src_in_segment"))
+        args.src_seg = saved
         p = dist.size
         t = r["elapsed"] / steps
         d = {"desc": r["desc"], "steps": steps, "ms_per_step": round(t * 1e3, 3),
@@ -448,7 +499,11 @@ def c5_extras(args, dist):
             # each owner receives (p-1) blocks' worth of packed rows from its peers per step
             xgmi = (p - 1) * r["block_bytes"]
             d["xgmi_GBps_per_gpu"] = round(xgmi / t / 1e9, 1)
-            d["note"] = "whole-array accumulate by every rank; value counts 3 x payload of HBM-side traffic per rank"
+            d["note"] = ("whole-array accumulate by every rank; value counts 3 x payload of HBM-side traffic per rank; "
+                         + ("the local buffer lies in the rank's comex segment: owners accumulate straight from it "
+                            "(direct-source route, no pack)" if src_seg else
+                            "the local buffer is a plain device buffer: pack -> staging -> owner unpack-acc"))
+            d["routes"] = r.get("routes")
         else:
             d["hbm_peak_frac_per_gpu"] = round(r["alg_bytes"] / t / (HBM_PEAK_GBS * 1e9), 4)
         out[mode] = d
@@ -632,6 +687,10 @@ def main():
     ap.add_argument("--host-rates", action="store_true", help="also measure host-inclusive rates")
     ap.add_argument("--exchange", action="store_true",
                     help="N>1: rank r accumulates into rank r+1's partition (remote path, SURVEY 8(d) M2)")
+    ap.add_argument("--self-packed", action="store_true",
+                    help="N=1: force the packed route for accumulates to self (COMEX_ENABLE_ACC_SELF/SMP=0)")
+    ap.add_argument("--src-seg", action="store_true",
+                    help="sources in this rank's comex_malloc segment (the direct-source route for --exchange)")
     ap.add_argument("--pipeline", action="store_true",
                     help="step = pack + unpack-acc (the remote path's two kernels) instead of the fused acc")
     ap.add_argument("--xfer", default="acc", choices=["acc", "put", "get"],
@@ -645,6 +704,9 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
+    if args.self_packed:   # read once at comex_init
+        for k in ("COMEX_ENABLE_ACC_SELF", "COMEX_ENABLE_ACC_SMP"):
+            os.environ[k] = "0"
 
     dist = Dist(args.gpus)
     extras_on = dist.size > 1 and not args.no_extras and args.workload != "C5"
@@ -702,6 +764,10 @@ def main():
         "api": ("comex_nbaccs per step, handles waited 64 back + comex_wait_all" if args.api == "nb"
                 else "comex_accs per step (blocking: returns after its kernel)"),
     }
+    if r.get("region_profile"):
+        line["value_region"] = r["region_profile"]   # host-clock marks inside the timed region
+    if r.get("diag_regions"):
+        line["diag_regions"] = r["diag_regions"]
     if c5:
         line["c5"] = c5
     if r.get("xfer", "acc") != "acc":
@@ -715,6 +781,14 @@ def main():
         line["roofline"]["frac"] = round(moved / r["avg_kernel_s"] / 1e9 / HBM_PEAK_GBS, 4)
         line["roofline"]["traffic"] = None
         line["roofline"]["timing"] = "bytes both kernels move (5 x payload) / (event-pair region / steps)"
+    if r.get("routes") and (r["exchange"] or r.get("self_packed") or args.src_seg):
+        line["routes"] = r["routes"]
+    if r.get("self_packed"):
+        line["metric"] = "GiB/s strided f64 accumulate to self through the packed route (not the headline metric)"
+        line["config"]["step"] = ("comex_nbaccs to self with COMEX_ENABLE_ACC_SELF=0 / COMEX_ENABLE_ACC_SMP=0: pack -> "
+                                  "staging -> progress thread unpack-acc; value credits 3 x payload per step")
+        line["roofline"] = None
+        line["moved_GBps"] = round(5 * r["payload"] * args.steps / r["elapsed"] / 1e9, 1)
     if r["exchange"]:
         # the kernels run on the owners' streams: no single-kernel roofline; the
         # per-step time is the whole exchange (pack, hand-off, unpack-acc)

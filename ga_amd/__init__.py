@@ -158,6 +158,13 @@ def kernel_counts():
     return {"rows": c[1], "flat": c[2], "serial": c[3], "ordered": c[4]}
 
 
+def route_counts():
+    """requests this rank posted to same-node owners, by route"""
+    c = (ctypes.c_ulonglong * 4)()
+    lib().gaamd_route_counts(c)
+    return {"packed": c[0], "direct_src": c[1], "iov": c[2], "rmw": c[3]}
+
+
 def set_tuning(key, value):
     return lib().gaamd_set_tuning(key.encode(), int(value))
 

@@ -267,7 +267,13 @@ static void release_view(View &v) {
 
 // ---- non-blocking handles ------------------------------------------------
 static int g_nb_job[kMaxNb];   // nb handle -> its remote accumulate job (0: none; see progress_jobs)
+// nb handle -> a direct-source request (target, its posted sequence; 0: none):
+// complete once the owner has applied it (the source is read in place)
+static int g_nb_rt[kMaxNb];
+static uint64_t g_nb_rseq[kMaxNb];
+static std::vector<uint64_t> g_direct_last;   // per target: last direct-source request posted
 static void run_job(int id);
+static void wait_done(int t, uint64_t seq);
 
 static int nb_alloc() {
     Runtime &r = rt();
@@ -283,6 +289,8 @@ static int nb_alloc() {
     const int i = r.nb_next;
     if (g_nb_job[i]) run_job(g_nb_job[i]);
     g_nb_job[i] = 0;
+    if (g_nb_rseq[i]) wait_done(g_nb_rt[i], g_nb_rseq[i]);
+    g_nb_rseq[i] = 0;
     (void)sched_complete(r.nb_stream[i], r.nb_seq[i], true);
     r.nb_next = (i + 1) % kMaxNb;
     return i;
@@ -295,6 +303,7 @@ static void nb_complete_now(comex_request_t *h, int stream_idx = 0, bool on_stre
     Runtime &r = rt();
     const int i = nb_alloc();
     g_nb_job[i] = 0;
+    g_nb_rseq[i] = 0;
     r.nb_stream[i] = stream_idx;
     r.nb_seq[i] = on_stream ? sched_track(stream_idx) : 0;
     *h = i;
@@ -357,6 +366,8 @@ static uint64_t stage_alloc(int t, uint64_t len) {
     }
 }
 
+static std::atomic<unsigned long long> g_route[4];   // gaamd_route_counts
+
 static void post_request(int t, int op, const void *scale, uint64_t dst_addr, const int *dst_stride,
                          const int *count, int levels, uint64_t off, uint64_t len, uint64_t rb, uint64_t re) {
     Runtime &r = rt();
@@ -385,6 +396,7 @@ static void post_request(int t, int op, const void *scale, uint64_t dst_addr, co
     memset(q.scale, 0, sizeof(q.scale));
     if (scale) memcpy(q.scale, scale, (size_t)elem_size(op));
     q.kind = 0;
+    g_route[0].fetch_add(1, std::memory_order_relaxed);
     q.iov_serial = 0;
     q.iov_align = 0;
     q.dst_hi = 0;
@@ -422,8 +434,49 @@ static void post_request_iov(int t, int op, const void *scale, int bytes, int n,
     memset(q.scale, 0, sizeof(q.scale));
     if (scale) memcpy(q.scale, scale, (size_t)elem_size(op));
     q.kind = 1;
+    g_route[2].fetch_add(1, std::memory_order_relaxed);
     q.iov_serial = mode;
     q.iov_align = align_or;
+    q.state.store(2, std::memory_order_release);
+}
+
+// kind 3: the owner reads the source patch from this rank's segment directly
+static void post_request_direct(int t, int op, const void *scale, uint64_t dst_addr, const int *dst_stride,
+                                uint64_t src_addr, const int *src_stride, const int *count, int levels) {
+    Runtime &r = rt();
+    Inbox *ib = inbox_of(r.shm, r.li(t));
+    const uint64_t ticket = ib->tail.fetch_add(1, std::memory_order_acq_rel);
+    Request &q = ib->slot[ticket % kInboxSlots];
+    for (unsigned spins = 0; ib->head.load(std::memory_order_acquire) + kInboxSlots <= ticket; ++spins)
+        if (spins > 256) sched_yield();
+    for (unsigned spins = 0;; ++spins) {
+        uint32_t expect = 0;
+        if (q.state.compare_exchange_weak(expect, 1, std::memory_order_acq_rel)) break;
+        if (spins > 256) sched_yield();
+    }
+    q.src_rank = r.rank;
+    q.op = op;
+    q.levels = levels;
+    memset(q.count, 0, sizeof(q.count));
+    memset(q.dst_stride, 0, sizeof(q.dst_stride));
+    memset(q.src_stride, 0, sizeof(q.src_stride));
+    for (int j = 0; j <= levels; ++j) q.count[j] = count[j];
+    for (int j = 0; j < levels; ++j) {
+        q.dst_stride[j] = dst_stride[j];
+        q.src_stride[j] = src_stride[j];
+    }
+    q.dst_addr = dst_addr;
+    q.src_addr = src_addr;
+    q.staging_off = 0;
+    q.bytes = 0;
+    q.seq = 0;
+    memset(q.scale, 0, sizeof(q.scale));
+    if (scale) memcpy(q.scale, scale, (size_t)elem_size(op));
+    q.kind = 3;
+    g_route[1].fetch_add(1, std::memory_order_relaxed);
+    q.iov_serial = 0;
+    q.iov_align = 0;
+    q.dst_hi = 0;
     q.state.store(2, std::memory_order_release);
 }
 
@@ -514,6 +567,29 @@ static void progress_loop() {
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
             }
             inflight.push_back({ev, src, true});
+            q.state.store(0, std::memory_order_release);
+            ib->head.store(h + 1, std::memory_order_release);
+            worked = true;
+        } else if (q.state.load(std::memory_order_acquire) == 2 && q.kind == 3) {
+            // strided accumulate read straight from the requester's segment (one
+            // pass: src read + dst read + dst write, as a local accumulate)
+            const int src = q.src_rank;
+            int64_t slo = 0, shi = 0, dlo = 0, dhi = 0;
+            side_span_host(q.src_stride, q.count, q.levels, q.count[0], &slo, &shi);
+            side_span_host(q.dst_stride, q.count, q.levels, q.count[0], &dlo, &dhi);
+            const char *sp = remote_view(src, (const void *)q.src_addr, slo, shi);
+            hipEvent_t ev;
+            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            else { ev = pool.back(); pool.pop_back(); }
+            {
+                std::lock_guard<std::mutex> g(r.launch_mu);
+                const int si = sched_pick(span_of(sp, slo, shi), span_of((void *)q.dst_addr, dlo, dhi));
+                const int rc = launch_strided(q.op, q.scale, sp, q.src_stride, (void *)q.dst_addr, q.dst_stride,
+                                              q.count, q.levels, r.streams[si], nullptr);
+                if (rc) fatal("direct accumulate launch failed (%d)", rc);
+                GA_HIP(hipEventRecord(ev, r.streams[si]));
+            }
+            inflight.push_back({ev, src, false});
             q.state.store(0, std::memory_order_release);
             ib->head.store(h + 1, std::memory_order_release);
             worked = true;
@@ -744,7 +820,7 @@ static int remote_acc_start(int t, int op, const void *scale, void *src, const i
     j.t = t;
     j.op = op;
     j.levels = levels;
-    memcpy(j.scale, scale, (size_t)esz);
+    if (scale) memcpy(j.scale, scale, (size_t)esz);
     for (int k = 0; k <= levels; ++k) j.count[k] = count[k];
     // only whole elements travel (_acc applies bytes/sizeof(T) of them, acc.h:122):
     // packed rows of row_bytes keep every row element-aligned in staging
@@ -790,15 +866,31 @@ static int remote_acc_start(int t, int op, const void *scale, void *src, const i
 
 static void fence_target(int t) {
     Runtime &r = rt();
-    if (r.size == 1 || t == r.rank) return;
-    if (!r.same_node(t)) { wire_fence(t); return; }
-    if (r.posted.empty()) return;
+    if (r.posted.empty()) return;   // no packed route in this job
+    if (t != r.rank && !r.same_node(t)) { wire_fence(t); return; }
     drain_target(t);
     wait_done(t, r.posted[t]);
 }
 
 // ---- the one transfer routine ---------------------------------------------
 enum Xfer { X_ACC, X_PUT, X_GET };
+
+// smallest payload sent by the direct-source route: below it the packed route's
+// asynchronous pack beats the host drain of our streams the direct route needs
+constexpr uint64_t kDirectSrcMin = 1ull << 20;
+
+// [p+lo, p+hi) inside one of our HBM segments that rank t mapped at comex_malloc
+static bool src_segment_shared(const void *p, int64_t lo, int64_t hi, int t) {
+    Runtime &r = rt();
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> g(r.seg_mu);
+    for (const Segment &s : r.segs) {
+        if (!s.live || !s.device || s.peer.empty()) continue;
+        const PeerMap &m = s.peer[r.rank];
+        if (m.bytes && a + lo >= m.base && a + hi <= m.base + m.bytes) return s.peer[t].member;
+    }
+    return false;
+}
 
 static uint64_t payload_bytes(int64_t row_bytes, const int *count, int levels) {
     uint64_t n = (uint64_t)row_bytes;
@@ -860,8 +952,48 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         return COMEX_SUCCESS;
     }
 
-    if (world != r.rank && kind == X_ACC) {
-        const int id = remote_acc_start(world, op, scale, src, ss, dst, ds, count, levels);
+    if (kind == X_ACC && world != r.rank && r.direct_src && r.same_node(world)) {
+        const int64_t rbd = row_bytes_of(op, count[0]);
+        int64_t slo = 0, shi = 0;
+        side_span_host(ss, count, levels, rbd, &slo, &shi);
+        if (rbd > 0 && payload_bytes(rbd, count, levels) >= kDirectSrcMin &&
+            src_segment_shared(src, slo, shi, world)) {
+            // the owner reads the patch from our segment through its IPC mapping:
+            // one pass instead of pack + unpack-acc (5 -> 3 x payload)
+            int64_t dlo = 0, dhi = 0;
+            side_span_host(ds, count, levels, rbd, &dlo, &dhi);
+            check_remote(world, dst, dlo, dhi);
+            drain_target(world);   // earlier packed chunks to world are posted first (inbox order)
+            {
+                // the owner's kernel must see every write of ours to the source
+                // (and our IPC puts into world's memory): our streams drain first
+                std::lock_guard<std::mutex> g(r.launch_mu);
+                sched_sync_all();
+            }
+            int cnt[8];
+            for (int k = 0; k <= levels; ++k) cnt[k] = count[k];
+            cnt[0] = (int)rbd;   // whole elements only (acc.h:122)
+            post_request_direct(world, op, scale, (uint64_t)(uintptr_t)dst, ds, (uint64_t)(uintptr_t)src, ss, cnt,
+                                levels);
+            const uint64_t seq = ++r.posted[world];
+            if (g_direct_last.size() != (size_t)r.size) g_direct_last.assign(r.size, 0);
+            g_direct_last[world] = seq;
+            if (hdl) {
+                nb_complete_now(hdl);
+                g_nb_rt[*hdl] = world;
+                g_nb_rseq[*hdl] = seq;
+            } else {
+                wait_done(world, seq);   // local completion = the owner has read the source
+            }
+            return COMEX_SUCCESS;
+        }
+    }
+    // the packed route: remote accumulates on this node, and -- under the
+    // COMEX_ENABLE_* toggles -- accumulates / puts to self or same-node puts
+    const bool packed = (kind == X_ACC && (world != r.rank || !r.acc_self_direct)) ||
+                        (kind == X_PUT && (world == r.rank ? !r.put_self_direct : !r.put_smp_direct));
+    if (packed) {
+        const int id = remote_acc_start(world, cop, scale, src, ss, dst, ds, count, levels);
         if (hdl) {
             nb_complete_now(hdl);
             g_nb_job[*hdl] = id;
@@ -1530,6 +1662,7 @@ static void post_request_rmw(int t, int swap, uint64_t addr, int bytes, uint64_t
     memset(q.scale, 0, sizeof(q.scale));
     memcpy(q.scale, &val, 8);
     q.kind = 2;
+    g_route[3].fetch_add(1, std::memory_order_relaxed);
     q.iov_serial = 0;
     q.iov_align = 0;
     q.dst_hi = 0;
@@ -1636,9 +1769,20 @@ int comex_init() {
     }
     const char *bs = getenv("COMEX_AMD_BLOCKING_SYNC");
     r.blocking_sync = !bs || atoi(bs) != 0;
+    {
+        const char *ds = getenv("COMEX_AMD_DIRECT_SRC");
+        r.direct_src = !ds || atoi(ds) != 0;
+        auto flag = [](const char *name) {
+            const char *v = getenv(name);
+            return !v || atoi(v) != 0;
+        };
+        r.acc_self_direct = flag("COMEX_ENABLE_ACC_SELF") || flag("COMEX_ENABLE_ACC_SMP");
+        r.put_smp_direct = flag("COMEX_ENABLE_PUT_SMP");
+        r.put_self_direct = flag("COMEX_ENABLE_PUT_SELF") || r.put_smp_direct;
+    }
     const char *dbg = getenv("COMEX_AMD_DEBUG");
     r.debug = dbg ? atoi(dbg) : 0;
-    if (r.size > 1) {
+    if (r.size > 1 || !r.acc_self_direct || !r.put_self_direct) {
         // staging HBM for remote accumulates, exported to every local rank
         const char *mb = getenv("COMEX_AMD_STAGING_MB");
         r.staging_bytes = (size_t)(mb ? atol(mb) : 256) << 20;
@@ -1675,11 +1819,13 @@ int comex_init() {
         const char *seg = getenv("COMEX_AMD_SEGMENT");
         fprintf(stderr,
                 "%s: ranks %d on %d node(s), device %d (%s, %d CUs), library streams %d, "
-                "staging %zu MiB/rank, remote acc %s, segments in %s, blocking sync %d\n",
+                "staging %zu MiB/rank, remote acc %s, segments in %s, blocking sync %d, "
+                "acc to self %s, put to self %s, same-node put %s\n",
                 gaamd_version(), r.size, r.nnodes, r.device, okp ? prop.gcnArchName : "?",
                 okp ? prop.multiProcessorCount : 0, (int)r.streams.size(), r.staging_bytes >> 20,
                 (async && !atoi(async)) ? "synchronous" : "asynchronous jobs", (seg && !strcmp(seg, "host")) ? "host" : "HBM",
-                r.blocking_sync ? 1 : 0);
+                r.blocking_sync ? 1 : 0, r.acc_self_direct ? "direct" : "packed",
+                r.put_self_direct ? "direct" : "packed", r.put_smp_direct ? "IPC" : "packed");
     }
     return COMEX_SUCCESS;
 }
@@ -1872,6 +2018,8 @@ int comex_wait(comex_request_t *h) {
     if (r.nb_used[*h]) {
         if (g_nb_job[*h]) run_job(g_nb_job[*h]);
         g_nb_job[*h] = 0;
+        if (g_nb_rseq[*h]) wait_done(g_nb_rt[*h], g_nb_rseq[*h]);
+        g_nb_rseq[*h] = 0;
         (void)sched_complete(r.nb_stream[*h], r.nb_seq[*h], true);
         r.nb_used[*h] = false;
     }
@@ -1889,6 +2037,13 @@ int comex_test(comex_request_t *h, int *status) {
         if (find_job(g_nb_job[*h])) { *status = 1; return COMEX_SUCCESS; }
         g_nb_job[*h] = 0;
     }
+    if (g_nb_rseq[*h]) {
+        if (r.shm->done[r.li(r.rank)][r.li(g_nb_rt[*h])].load(std::memory_order_acquire) < g_nb_rseq[*h]) {
+            *status = 1;
+            return COMEX_SUCCESS;
+        }
+        g_nb_rseq[*h] = 0;
+    }
     if (!sched_complete(r.nb_stream[*h], r.nb_seq[*h], false)) { *status = 1; return COMEX_SUCCESS; }
     r.nb_used[*h] = false;
     *h = -1;
@@ -1900,7 +2055,12 @@ int comex_wait_all(comex_group_t group) {
     (void)group;
     Runtime &r = rt();
     drain_all_jobs();
-    for (int i = 0; i < kMaxNb; ++i) g_nb_job[i] = 0;
+    for (int t = 0; t < (int)g_direct_last.size(); ++t)
+        if (g_direct_last[t]) wait_done(t, g_direct_last[t]);
+    for (int i = 0; i < kMaxNb; ++i) {
+        g_nb_job[i] = 0;
+        g_nb_rseq[i] = 0;
+    }
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
         sched_sync_all();
@@ -1951,10 +2111,11 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         ptr_arr[k] = (void *)(uintptr_t)gathered[k].base;
     }
     Segment s;
+    s.peer.resize(r.size);
+    for (int q : members) s.peer[q].member = true;
     s.live = true;
     s.device = device;
     s.local = p;
-    s.peer.resize(r.size);
     for (int q = 0; q < r.size; ++q) {
         s.peer[q].base = all[q].base;
         s.peer[q].bytes = all[q].bytes;
@@ -2152,6 +2313,11 @@ int comex_group_translate_ranks(int n, comex_group_t group_from, int *ranks_from
 int comex_group_comm(comex_group_t group, void *comm) {
     (void)comm;
     fatal("comex_group_comm(%d): libga_amd has no MPI communicator (it bootstraps without MPI)", group);
+}
+
+int gaamd_route_counts(unsigned long long counts[4]) {
+    for (int k = 0; k < 4; ++k) counts[k] = g_route[k].load(std::memory_order_relaxed);
+    return 0;
 }
 
 }  // extern "C"

@@ -56,10 +56,13 @@ struct alignas(64) Request {
     uint64_t bytes;                  // packed bytes
     uint64_t seq;                    // strided: row range (begin << 32 | end)
     uint8_t scale[16];
-    int32_t kind;                    // 0 strided (count/dst_stride), 1 io-vector, 2 rmw
+    int32_t kind;                    // 0 strided (count/dst_stride), 1 io-vector, 2 rmw,
+                                     // 3 strided read straight from src_rank's segment
     int32_t iov_serial;              // io-vector: destinations overlap -> in order
     uint64_t iov_align;              // io-vector: OR of the destination addresses
     uint64_t dst_hi;                 // io-vector: [dst_addr, dst_hi) covers every pair
+    int32_t src_stride[8];           // kind 3: the source patch in src_rank's segment
+    uint64_t src_addr;               // kind 3: src_rank's address space
 };
 
 struct alignas(64) Inbox {
@@ -103,6 +106,7 @@ struct PeerMap {
     uintptr_t base = 0;   // segment address in the owner's address space
     size_t bytes = 0;
     char *mapped = nullptr;   // same bytes as seen from this process
+    bool member = false;      // the rank took part in the segment's comex_malloc
 };
 
 struct Segment {
@@ -129,6 +133,16 @@ struct Runtime {
     // reference's blocking calls promise; 0 is the documented
     // opt-out where blocking calls are only stream-ordered
     bool blocking_sync = true;
+    // COMEX_ENABLE_{ACC,PUT}_{SELF,SMP} (comex.c:438-471, defaults 1): with both
+    // SELF and SMP off, an accumulate / put to this rank takes the packed route
+    // (pack into staging, the progress thread unpacks) as a remote one does;
+    // PUT_SMP off also sends same-node puts that way instead of through the IPC
+    // mapping.  (Same-node accumulates always take the packed route here.)
+    bool acc_self_direct = true, put_self_direct = true, put_smp_direct = true;
+    // COMEX_AMD_DIRECT_SRC (default 1): a same-node accumulate whose source lies
+    // in one of this rank's HBM segments is applied by the owner straight from
+    // that segment (its IPC mapping) -- no pack pass, no staging
+    bool direct_src = true;
     int debug = 0;                  // COMEX_AMD_DEBUG: trace transfers on stderr
     // bootstrap
     gaamd_allgather_fn ag = nullptr;

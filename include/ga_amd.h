@@ -76,6 +76,10 @@ int gaamd_last_launch(int *kind, int *width, int *unroll, int *launches,
 /* kernel launches since start, by kind: counts[0..4] = {unused, rows, flat,
  * serial, ordered}, every caller of this process (user calls, progress thread, wire) */
 int gaamd_kernel_counts(unsigned long long counts[5]);
+/* requests this rank posted to same-node owners, by route: counts[0..3] =
+ * {packed chunks (pack -> staging -> owner unpack), direct-source (owner reads
+ * our segment), io-vector, rmw} */
+int gaamd_route_counts(unsigned long long counts[4]);
 /* keys: "kind" (0 auto, 1 rows, 2 flat, 3 serial, 4 ordered), "unroll16" (1/2/4),
  * "nontemporal", "block" (0 auto/64/128/256), "flat_max_nvec", "align", "direct",
  * "flat_nt", "flat_shape", "flat_line_min", "wide_unaligned", "streams";

@@ -93,6 +93,8 @@ def main():
         ga_ref_test(L, rank, size)
     elif mode == "order":
         order_test(L, rank, size)
+    elif mode == "directsrc":
+        direct_src_test(L, rank, size)
     elif mode in ("armcimisc", "armcimisc-gloo"):
         armci_misc_test(L, rank, size)
     else:
@@ -308,6 +310,65 @@ def order_test(L, rank, size):
     ga_amd.comex_finalize()
 
 
+def direct_src_test(L, rank, size):
+    """Same-node accumulates whose source patch lies in the caller's own HBM
+    segment: the owner applies them straight from that segment (kind-3 request,
+    no pack pass).  Blocking and non-blocking, f64 and double complex, a patch
+    below the direct route's 1 MiB floor (packed route), and the source
+    overwritten right after the blocking call returns (the owner must have read
+    it by then).  Integer-valued data: every order of the ranks' accumulates
+    sums exactly; the result is checked against the oracle's restatement."""
+    import ga_amd
+    from oracle import Oracle
+    ora = Oracle()
+    DBL, DCP = 38, 41
+    assert ga_amd.comex_init() == 0
+    rows, ld = 512, 4096                      # 16 MiB segment: src half, dst half
+    half = rows * ld * 8
+    seg = ga_amd.comex_malloc(2 * half, size)
+    nxt, prv = (rank + 1) % size, (rank - 1) % size
+
+    def srcvals(r, it):
+        return (np.arange(rows * ld, dtype=np.float64) % 61 - 30 + r + it).astype(np.float64)
+
+    base = (np.arange(rows * ld, dtype=np.float64) % 7).astype(np.float64)
+    counts0 = ga_amd.route_counts()
+    for it, (op, alpha, rowb, nb) in enumerate([(DBL, 2.0, 2048 * 8, False), (DBL, -1.0, 3000 * 8, True),
+                                                (DCP, 1 + 2j, 1024 * 16, False), (DBL, 3.0, 64 * 8, False)]):
+        src_h = srcvals(rank, it)
+        assert L.comex_put(src_h.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(seg[rank]), half, rank, 0) == 0
+        b = base.copy()
+        assert L.comex_put(b.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(seg[rank] + half), half, rank, 0) == 0
+        ga_amd.comex_barrier()
+        scale = ga_amd.scale_buffer(op, alpha)
+        cnt = [rowb, rows]
+        args = (op, scale[1], ctypes.c_void_p(seg[rank]), ga_amd.int_array([ld * 8]), ctypes.c_void_p(seg[nxt] + half),
+                ga_amd.int_array([ld * 8]), ga_amd.int_array(cnt), 1, nxt, 0)
+        if nb:
+            h = ctypes.c_int(-1)
+            assert L.comex_nbaccs(*args, ctypes.byref(h)) == 0
+            assert L.comex_wait(ctypes.byref(h)) == 0
+        else:
+            assert L.comex_accs(*args) == 0
+        # the source is reusable once the call (or its wait) returned
+        junk = np.full(rows * ld, 1e300)
+        assert L.comex_put(junk.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(seg[rank]), half, rank, 0) == 0
+        ga_amd.comex_barrier()
+        got = np.zeros(rows * ld, dtype=np.float64)
+        assert L.comex_get(ctypes.c_void_p(seg[rank] + half), got.ctypes.data_as(ctypes.c_void_p), half, rank, 0) == 0
+        want = base.copy().view(np.uint8)
+        ora.accs(op, alpha, srcvals(prv, it).view(np.uint8), 0, [ld * 8], want, 0, [ld * 8], cnt, 1)
+        assert np.array_equal(got.view(np.uint8), want), f"rank {rank}: case {it} differs"
+        say(rank, f"direct-source case {it} checked")
+    counts = ga_amd.route_counts()
+    if size > 1:
+        assert counts["direct_src"] - counts0["direct_src"] == 3, (counts0, counts)   # the 64-column case is packed
+        assert counts["packed"] > counts0["packed"]
+    ga_amd.comex_barrier()
+    assert ga_amd.comex_free(seg[rank]) == 0
+    ga_amd.comex_finalize()
+
+
 class MemInfo(ctypes.Structure):   # armci_meminfo_t (include/armci.h)
     _fields_ = [("armci_addr", ctypes.c_void_p), ("addr", ctypes.c_void_p), ("size", ctypes.c_size_t),
                 ("cpid", ctypes.c_int), ("idlist", ctypes.c_long * 128)]
@@ -382,7 +443,8 @@ def armci_misc_test(L, rank, size):
     L.armci_msg_bintree(333, byref(root), byref(up), byref(left), byref(right))
     want_l = 2 * rank + 1 if 2 * rank + 1 < size else -1
     want_r = 2 * rank + 2 if 2 * rank + 2 < size else -1
-    assert (root.value, up.value, left.value, right.value) == (0, (rank - 1) // 2 if rank else -1, want_l, want_r)
+    # message.c:553 in C: (index-1)/2 truncates toward zero, so the root's Up is 0, not -1
+    assert (root.value, up.value, left.value, right.value) == (0, int((rank - 1) / 2), want_l, want_r)
     addrs = (vp * size)()
     addrs[rank] = 0x1000 * (rank + 1)
     L.armci_exchange_address(addrs, size)

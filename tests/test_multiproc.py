@@ -56,6 +56,7 @@ def launch(mode, n=2, timeout=240, nodes=None, extra_env=None):
                 p.kill()
     for r, (rc, out) in enumerate(outs):
         assert rc == 0 and f"RANK {r} OK" in out, f"rank {r} rc={rc}\n{out[-3000:]}"
+    return [out for _, out in outs]
 
 
 def test_bootstrap_env_shm_two_ranks():
@@ -220,3 +221,26 @@ def test_armci_message_groups_rmw_mutexes(n, nodes):
     armci_read/write_strided over n ranks; with `nodes` the cross-node cases go
     through the wire protocol's FETCH_AND_ADD / SWAP / LOCK / UNLOCK frames."""
     launch("armcimisc-gloo" if nodes else "armcimisc", n=n, timeout=120, nodes=nodes)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2])
+def test_packed_route_forced_by_comex_enable_toggles(n):
+    """COMEX_ENABLE_{ACC,PUT}_{SELF,SMP}=0 (comex.c:438-471): accumulates and
+    puts to this rank, and same-node puts, take the packed route (pack ->
+    staging -> progress thread unpack) as the reference's tests force it; the
+    whole remote suite still matches the oracle.  With n=1 every operation is to
+    self, so the route is exercised on a single rank."""
+    toggles = {"COMEX_ENABLE_ACC_SELF": "0", "COMEX_ENABLE_ACC_SMP": "0", "COMEX_ENABLE_PUT_SELF": "0",
+               "COMEX_ENABLE_PUT_SMP": "0", "COMEX_AMD_VERBOSE": "1"}
+    outs = launch("remote", n=n, timeout=120, extra_env=toggles)
+    assert "acc to self packed, put to self packed, same-node put packed" in outs[0], outs[0][-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 3])
+def test_direct_source_remote_accumulate(n):
+    """Source in the caller's segment: the owner accumulates straight from it
+    (no pack, no staging), bit-exact against the oracle; smaller patches keep
+    the packed route."""
+    launch("directsrc", n=n, timeout=120)
