@@ -10,6 +10,8 @@ package; the product library (ga_amd/libga_amd.so) never links or calls it.
 * ``Ref``: ctypes wrapper of _ref/libref_acc.so, the REFERENCE's own _acc
   compiled from /root/reference/comex/src-common/acc.h (built only where the
   reference tree exists; the .so travels to the GPU box).
+* ``LegacyRef``: _ref/libref_legacy_acc.so, the legacy ARMCI accumulate loops
+  (armci/src/xfer/caccumulate.c) compiled as they lie.
 """
 import ctypes
 import os
@@ -19,6 +21,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libref_acc.so")
+LEGACY_SO = os.path.join(HERE, "_ref", "libref_legacy_acc.so")
 
 _ip = ctypes.POINTER(ctypes.c_int)
 _vp = ctypes.c_void_p
@@ -51,6 +54,10 @@ class Oracle:
             "ora_puts": (ctypes.c_int, [_vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
             "ora_gets": (ctypes.c_int, [_vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
             "ora_check_contiguous": (ctypes.c_int, [_ip, _ip, _ip, ctypes.c_int]),
+            "ora_legacy_acc_2d": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int,
+                                                 _vp, ctypes.c_int]),
+            "ora_legacy_acc_2D": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_int]),
             "ora_fill_f64": (None, [_vp, ctypes.c_long, ctypes.c_uint64]),
             "ora_fill_f32": (None, [_vp, ctypes.c_long, ctypes.c_uint64]),
             "ora_fill_i32": (None, [_vp, ctypes.c_long, ctypes.c_uint64]),
@@ -102,6 +109,17 @@ class Oracle:
         self.L.ora_unpack_acc(op, _ptr(s), _ptr(packed), _vp(dst.ctypes.data + dst_off), _ints(dst_stride),
                               _ints(count), levels)
 
+    def legacy_acc_2d(self, op, alpha, rows, cols, A, ald, B, bld):
+        """caccumulate.c: A (numpy, column-major with leading dim ald elements) += alpha * B"""
+        s = np.array([alpha], dtype=_scale_dtype(op))
+        assert self.L.ora_legacy_acc_2d(op, _ptr(s), rows, cols, _ptr(A), ald, _ptr(B), bld) == 0
+
+    def legacy_acc_2D(self, op, alpha, src, dst, nbytes, cols, src_stride, dst_stride):
+        """strided.c armci_acc_2D on numpy buffers (byte strides, truncated to elements)"""
+        s = np.array([alpha], dtype=_scale_dtype(op))
+        assert self.L.ora_legacy_acc_2D(op, _ptr(s), _ptr(src), _ptr(dst), nbytes, cols, src_stride,
+                                        dst_stride) == 0
+
     def check_contiguous(self, src_stride, dst_stride, count, n_stride):
         return self.L.ora_check_contiguous(_ints(src_stride), _ints(dst_stride), _ints(count), n_stride)
 
@@ -146,6 +164,37 @@ class Ref:
         s = np.array([scale], dtype=_scale_dtype(op))
         assert self.L.ref_accv(op, _ptr(s), _vp(src_addrs.ctypes.data), _vp(dst_addrs.ctypes.data),
                                len(src_addrs), nbytes) == 0
+
+
+LEGACY_NAME = {38: "d", 39: "f", 40: "c", 41: "z", 37: "i", 42: "l"}
+
+
+class LegacyRef:
+    """The reference's legacy c_?_accumulate_2d_ loops, called as GA's legacy
+    ARMCI calls them (pointers to scalars, column-major)."""
+
+    def __init__(self, path=LEGACY_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.L = ctypes.CDLL(path)
+
+    def acc_2d(self, op, alpha, rows, cols, A, ald, B, bld, unrolled=False, name=None):
+        s = np.array([alpha], dtype=_scale_dtype(op))
+        fn = getattr(self.L, f"c_{name or LEGACY_NAME[op]}_accumulate_2d{'_u' if unrolled else ''}_")
+        fn.restype = None
+        r, c, a, b = ctypes.c_int(rows), ctypes.c_int(cols), ctypes.c_int(ald), ctypes.c_int(bld)
+        fn(_ptr(s), ctypes.byref(r), ctypes.byref(c), _ptr(A), ctypes.byref(a), _ptr(B), ctypes.byref(b))
+
+    def acc_1d(self, op, alpha, A, B, rows, name=None):
+        s = np.array([alpha], dtype=_scale_dtype(op))
+        fn = getattr(self.L, f"c_{name or LEGACY_NAME[op]}_accumulate_1d_")
+        fn.restype = None
+        r = ctypes.c_int(rows)
+        fn(_ptr(s), _ptr(A), _ptr(B), ctypes.byref(r))
+
+
+def legacy_ref_available():
+    return os.path.exists(LEGACY_SO)
 
 
 def ref_available():

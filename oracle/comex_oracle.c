@@ -23,6 +23,10 @@
  *                        the progress-rank unpack-accumulate 4238-4268
  *   ora_puts / ora_gets  comex.c:6342-6427 / 6617-6696 per-row memcpy odometer
  *   ora_check_contiguous comex/src-armci/armci.c:114-170
+ *   ora_legacy_acc_2d    armci/src/xfer/caccumulate.c (c_?_accumulate_2d_:
+ *                        97-121, 149-173, 202-217, 256-271, 333-382)
+ *   ora_legacy_acc_2D    armci/src/xfer/strided.c:257-328 (armci_acc_2D: byte
+ *                        counts and strides to elements by integer division)
  *   ora_splitmix64_*     synthetic input generator of SURVEY.md §8(d)
  *
  * Build flags (oracle/Makefile): -O2 -fwrapv -ffp-contract=off, no -march, so
@@ -346,4 +350,53 @@ int ora_accs_mt(int op, const void *scale, const char *src, const int *src_strid
 {
     return mt_accs(ora_accs, ora_elem_size(op), op, scale, src, src_stride, dst, dst_stride, count,
                    stride_levels, nthreads);
+}
+
+/* caccumulate.c: column-major A(ald, *) += alpha * B(bld, *), columns outer,
+ * rows inner; complex real part alpha.r*B.r - alpha.i*B.i, imaginary part
+ * alpha.i*B.r + alpha.r*B.i (183-184).  ld in elements. */
+int ora_legacy_acc_2d(int op, const void *alpha, int rows, int cols, void *A, int ald, const void *B, int bld)
+{
+    int r, c;
+#define ORA_LREG(T)                                                           \
+    {                                                                         \
+        const T a = *(const T *)alpha;                                        \
+        T *x = (T *)A; const T *y = (const T *)B;                             \
+        for (c = 0; c < cols; ++c)                                            \
+            for (r = 0; r < rows; ++r)                                        \
+                x[(long)c * ald + r] += a * y[(long)c * bld + r];             \
+    }
+#define ORA_LCPL(CT)                                                          \
+    {                                                                         \
+        const CT a = *(const CT *)alpha;                                      \
+        CT *x = (CT *)A; const CT *y = (const CT *)B;                         \
+        for (c = 0; c < cols; ++c)                                            \
+            for (r = 0; r < rows; ++r) {                                      \
+                const CT b = y[(long)c * bld + r];                            \
+                x[(long)c * ald + r].real += a.real * b.real - a.imag * b.imag; \
+                x[(long)c * ald + r].imag += a.imag * b.real + a.real * b.imag; \
+            }                                                                 \
+    }
+    switch (op) {
+    case ORA_ACC_DBL: ORA_LREG(double); break;
+    case ORA_ACC_FLT: ORA_LREG(float); break;
+    case ORA_ACC_INT: ORA_LREG(int); break;
+    case ORA_ACC_LNG: ORA_LREG(long); break;
+    case ORA_ACC_DCP: ORA_LCPL(ora_dcpl); break;
+    case ORA_ACC_CPL: ORA_LCPL(ora_scpl); break;
+    default: return -1;
+    }
+#undef ORA_LREG
+#undef ORA_LCPL
+    return 0;
+}
+
+/* strided.c:257-328: bytes / strides in bytes -> rows / leading dimensions in
+ * elements (integer division), then the 2-D loop above */
+int ora_legacy_acc_2D(int op, const void *scale, const void *src, void *dst, int bytes, int cols, int src_stride,
+                      int dst_stride)
+{
+    const int esz = ora_elem_size(op);
+    if (esz <= 0) return -1;
+    return ora_legacy_acc_2d(op, scale, bytes / esz, cols, dst, dst_stride / esz, src, src_stride / esz);
 }

@@ -12,7 +12,7 @@ import ga_amd
 from ga_amd._lib import LIB_PATH, SIGNATURES
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("comex.h", "armci.h", "message.h", "ga_amd.h", "ga.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("comex.h", "armci.h", "message.h", "armci_acc.h", "ga_amd.h", "ga.h")]
 
 
 def declared_functions(path):

@@ -13,7 +13,7 @@ step() {
     echo "$name rc=$rc"
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
-step mp 500 python -u -m pytest tests/test_multiproc.py -v -k "armci_message or packed_route or direct_source" --timeout 150 --timeout-method thread -p no:cacheprovider -rf
+step mp 600 python -u -m pytest tests/test_multiproc.py tests/test_legacy_acc.py -v -k "armci_message or packed_route or direct_source or gpu_legacy" --timeout 150 --timeout-method thread -p no:cacheprovider -rf
 tail -15 "$O/mp.out"
 step diag 180 env BENCH_DIAG_REGIONS=12 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu
 cat "$O/diag.out"
