@@ -280,10 +280,15 @@ def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True
     saved = args.warmup_ms
     if warmup_ms is not None:
         args.warmup_ms = warmup_ms
+    if args.verbose:
+        print(f"rank {dist.rank}: GA created, src {'segment' if src_seg else 'buffer'}, warming", file=sys.stderr,
+              flush=True)
     nxt = warm(step, args)
     args.warmup_ms = saved
     ga_amd.sync()
     L.GA_Sync()
+    if args.verbose:
+        print(f"rank {dist.rank}: warm-up done", file=sys.stderr, flush=True)
     launch = ga_amd.last_launch()
     # value region: wall clock only (no marker packets between the steps)
     dist.barrier()
@@ -487,6 +492,8 @@ def c5_extras(args, dist):
     m2 = max(1, args.c5_steps // 2)
     for mode, exchange, steps, src_seg in (("M1", False, args.c5_steps, False), ("M2", True, m2, False),
                                            ("M2_src_in_segment", True, m2, True)):
+        if args.verbose:
+            print(f"rank {dist.rank}: C5 {mode} starts", file=sys.stderr, flush=True)
         args.src_seg = src_seg
         r = run_ga(args, dist, exchange=exchange, steps=steps, warmup_ms=0.0,
                    terminate=(mode == "M2_src_in_segment"))

@@ -476,17 +476,21 @@ def armci_misc_test(L, rank, size):
 
     # fetch-and-add: every rank adds (rank+1) 50 times to rank 0's int and long
     FETCH_AND_ADD, FETCH_AND_ADD_LONG, SWAP, SWAP_LONG = 12, 13, 10, 11
+    if rank == 0:   # a 64-bit base: the long form must carry past 32 bits (extra itself is an int)
+        assert L.ARMCI_PutValueLong(1 << 40, vp(seg[0] + 72), 0) == 0
+    L.ARMCI_Barrier()
     olds = []
     for _ in range(50):
         old = c_int()
         assert L.ARMCI_Rmw(FETCH_AND_ADD, byref(old), vp(seg[0] + 64), rank + 1, 0) == 0
         olds.append(old.value)
         oldl = ctypes.c_long()
-        assert L.ARMCI_Rmw(FETCH_AND_ADD_LONG, byref(oldl), vp(seg[0] + 72), (rank + 1) << 33, 0) == 0
+        assert L.ARMCI_Rmw(FETCH_AND_ADD_LONG, byref(oldl), vp(seg[0] + 72), rank + 1, 0) == 0
+        assert oldl.value >= 1 << 40
     assert len(set(olds)) == 50 and all(0 <= o < 50 * n1 for o in olds)
     L.ARMCI_Barrier()
     assert L.ARMCI_GetValueInt(vp(seg[0] + 64), 0) == 50 * n1
-    assert L.ARMCI_GetValueLong(vp(seg[0] + 72), 0) == 50 * (n1 << 33)
+    assert L.ARMCI_GetValueLong(vp(seg[0] + 72), 0) == (1 << 40) + 50 * n1
     # swap: a token passes through every rank; the values seen are a permutation
     if rank == 0:
         assert L.ARMCI_PutValueInt(-1, vp(seg[0] + 80), 0) == 0
