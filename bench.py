@@ -708,6 +708,9 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="N>1: skip the C5 M1/M2 measurements")
     ap.add_argument("--verbose", action="store_true", help="progress lines on stderr")
     args = ap.parse_args()
+    if os.environ.get("BENCH_STACK_DUMP_S"):   # diagnostics: where a hung rank is stuck
+        import faulthandler
+        faulthandler.dump_traceback_later(int(os.environ["BENCH_STACK_DUMP_S"]), exit=False)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))

@@ -50,6 +50,9 @@ def torch_hooks(rank, size):
 
 
 def main():
+    import faulthandler
+    # a hung rank prints where it is stuck before the test's timeout kills it
+    faulthandler.dump_traceback_later(int(os.environ.get("TEST_STACK_DUMP_S", "600")), exit=False)
     mode = sys.argv[1]
     rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import ga_amd

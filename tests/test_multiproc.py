@@ -31,7 +31,8 @@ def launch(mode, n=2, timeout=240, nodes=None, extra_env=None):
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=port, COMEX_AMD_JOBID=f"t{port}", COMEX_AMD_STAGING_MB="16")
+                   MASTER_PORT=port, COMEX_AMD_JOBID=f"t{port}", COMEX_AMD_STAGING_MB="16",
+                   TEST_STACK_DUMP_S=str(max(10, timeout - 15)))
         if nodes is not None:
             env["COMEX_AMD_NODE"] = str(nodes[r])
             env["TEST_NODES"] = ",".join(str(x) for x in nodes)
