@@ -2081,6 +2081,8 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     // collective over the group's members (comex.c comex_malloc): ptr_arr is
     // indexed by group rank; non-members keep no view of the segment
     const std::vector<int> members = group_members(group);
+    const bool trace = r.debug >= 2;
+    if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc(%zu, group %d): enter\n", r.rank, bytes, group);
     struct Info { uint64_t base, bytes; hipIpcMemHandle_t h; int32_t device, pad; } mine;
     memset(&mine, 0, sizeof(mine));
     void *p = nullptr;
@@ -2102,8 +2104,10 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     mine.base = (uint64_t)(uintptr_t)p;
     mine.bytes = bytes;
     mine.device = r.device;
+    if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: allocated %p, allgather\n", r.rank, p);
     std::vector<Info> gathered(members.size());
     members_allgather(members, group, &mine, gathered.data(), sizeof(Info));
+    if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: allgather done, opening peers\n", r.rank);
     std::vector<Info> all(r.size);
     memset(all.data(), 0, sizeof(Info) * all.size());
     for (size_t k = 0; k < members.size(); ++k) {
@@ -2130,7 +2134,9 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         std::lock_guard<std::mutex> g(r.seg_mu);
         r.segs.push_back(std::move(s));
     }
+    if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: peers mapped, barrier\n", r.rank);
     members_barrier(members, group);
+    if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: done\n", r.rank);
     return COMEX_SUCCESS;
 }
 
