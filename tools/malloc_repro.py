@@ -26,12 +26,19 @@ def main():
     import ga_amd
     rank = int(os.environ["RANK"])
     assert ga_amd.comex_init() == 0
+    keep = os.environ.get("REPRO_KEEP") == "1"     # keep every segment live (no free between sizes)
+    live = []
     for gib in [float(x) for x in (sys.argv[1:] or ["1", "2", "3"])]:
         n = int(gib * (1 << 30))
         print(f"rank {rank}: malloc {gib} GiB", file=sys.stderr, flush=True)
         seg = ga_amd.comex_malloc(n, 2)
         print(f"rank {rank}: malloc {gib} GiB ok", file=sys.stderr, flush=True)
         ga_amd.comex_barrier()
+        if keep:
+            live.append(seg)
+        else:
+            assert ga_amd.comex_free(seg[rank]) == 0
+    for seg in live:
         assert ga_amd.comex_free(seg[rank]) == 0
     ga_amd.comex_finalize()
     print(f"rank {rank}: OK", file=sys.stderr, flush=True)
