@@ -23,6 +23,9 @@ def main():
                  for r in range(2)]
         sys.exit(max(p.wait() for p in procs))
     faulthandler.dump_traceback_later(50, exit=True)
+    if os.environ.get("REPRO_TORCH") == "1":   # torch's own HIP runtime loaded first, as in bench.py N>1
+        import torch  # noqa: F401
+        import torch.distributed  # noqa: F401
     import ga_amd
     rank = int(os.environ["RANK"])
     assert ga_amd.comex_init() == 0

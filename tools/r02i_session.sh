@@ -1,0 +1,15 @@
+#!/bin/bash
+set -uo pipefail
+O=gpurun_out/r02i
+mkdir -p "$O"
+export TMPDIR=/tmp
+step() {
+    local name=$1 t=$2; shift 2
+    timeout -k 10 "$t" "$@" > "$O/$name.out" 2> "$O/$name.err"
+    local rc=$?
+    echo "$name rc=$rc"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+}
+step t_1_2 70 env REPRO_TORCH=1 REPRO_KEEP=1 python3 -u tools/malloc_repro.py 1 2
+grep "rank\|Timeout\|File" "$O/t_1_2.err" | tail -12
+echo done
