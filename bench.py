@@ -694,6 +694,8 @@ def main():
     ap.add_argument("--host-rates", action="store_true", help="also measure host-inclusive rates")
     ap.add_argument("--exchange", action="store_true",
                     help="N>1: rank r accumulates into rank r+1's partition (remote path, SURVEY 8(d) M2)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="library HIP streams (COMEX_AMD_STREAMS; 0 = the library default, 2)")
     ap.add_argument("--self-packed", action="store_true",
                     help="N=1: force the packed route for accumulates to self (COMEX_ENABLE_ACC_SELF/SMP=0)")
     ap.add_argument("--src-seg", action="store_true",
@@ -714,6 +716,15 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
+    # Load libga_amd (and with it /opt/rocm's HIP runtime) before torch: torch's
+    # wheel bundles its own libamdhip64 with the same SONAME, and whichever loads
+    # first serves the library.  The bundled runtime hangs in hipIpcOpenMemHandle
+    # of a 2 GiB segment while a 1 GiB one is mapped (tools/malloc_repro.py,
+    # profiles/r02/README.md); /opt/rocm's does not.
+    import ga_amd
+    ga_amd.lib()
+    if args.streams:
+        os.environ["COMEX_AMD_STREAMS"] = str(args.streams)
     if args.self_packed:   # read once at comex_init
         for k in ("COMEX_ENABLE_ACC_SELF", "COMEX_ENABLE_ACC_SMP"):
             os.environ[k] = "0"
@@ -774,6 +785,7 @@ def main():
         "api": ("comex_nbaccs per step, handles waited 64 back + comex_wait_all" if args.api == "nb"
                 else "comex_accs per step (blocking: returns after its kernel)"),
     }
+    line["hip_runtime"] = ga_amd.lib().gaamd_hip_runtime().decode()
     if r.get("region_profile"):
         line["value_region"] = r["region_profile"]   # host-clock marks inside the timed region
     if r.get("diag_regions"):

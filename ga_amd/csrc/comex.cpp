@@ -22,6 +22,7 @@
 // place (device-mapped), pageable memory is registered for the call.  All
 // arithmetic runs on the GPU; there is no CPU compute path.
 #include "runtime.hpp"
+#include "../../include/ga_amd.h"
 #include "gaamd_kernels.h"
 #include "../../include/comex.h"
 #include <stdio.h>
@@ -1742,6 +1743,16 @@ int comex_init() {
         hook = true;
     }
     boot_init();
+    {
+        // a torch wheel bundles a libamdhip64 with the same SONAME: imported
+        // before this library it serves our HIP calls, and that build hangs in
+        // hipIpcOpenMemHandle of a 2 GiB segment while another is mapped
+        // (profiles/r02/README.md)
+        const char *rt_path = gaamd_hip_runtime();
+        if (strstr(rt_path, "/torch/lib/") && r.rank == 0)
+            fprintf(stderr, "ga_amd: HIP calls resolve to %s (loaded before libga_amd); load libga_amd first "
+                    "(import ga_amd before torch) to use /opt/rocm's runtime\n", rt_path);
+    }
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev <= 0)

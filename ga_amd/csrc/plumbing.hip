@@ -4,6 +4,7 @@
 #include "runtime.hpp"
 #include <string.h>
 #include <stdlib.h>
+#include <dlfcn.h>
 
 namespace gaamd {
 
@@ -257,5 +258,14 @@ float gaamd_event_elapsed_ms(void *start, void *stop) {
 }
 
 const char *gaamd_version(void) { return "ga_amd 0.1 (gfx950)"; }
+
+// the file of the HIP runtime this library's calls resolve to: /opt/rocm's, or
+// a copy with the same SONAME that another library (a torch wheel) loaded first
+const char *gaamd_hip_runtime(void) {
+    Dl_info info;
+    hipError_t (*fn)(void **, size_t) = &hipMalloc;
+    if (dladdr(reinterpret_cast<void *>(fn), &info) && info.dli_fname) return info.dli_fname;
+    return "unknown";
+}
 
 }  // extern "C"
