@@ -497,6 +497,21 @@ static void progress_loop() {
     char *prog_work = nullptr;          // launch_iov_runs scratch of this thread
     size_t prog_work_bytes = 0;
     hipEvent_t prog_work_ev = nullptr;
+    // idle policy: the reference's progress rank polls without sleeping
+    // (comex.c:3379-3565); here the thread keeps polling (yielding the core)
+    // while kernels it launched are in flight -- their completion releases the
+    // requesters' staging and fences -- and for COMEX_AMD_PROGRESS_SPIN_US after
+    // the last request (default 2000), then backs off to short sleeps
+    static const double spin_s = [] {
+        const char *e = getenv("COMEX_AMD_PROGRESS_SPIN_US");
+        return (e ? atof(e) : 2000.0) * 1e-6;
+    }();
+    auto now_s = [] {
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+    };
+    double last_work = now_s();
     unsigned idle = 0;
     for (;;) {
         bool worked = false;
@@ -637,12 +652,23 @@ static void progress_loop() {
             inflight.pop_front();
             worked = true;
         }
-        if (worked) { idle = 0; continue; }
+        if (worked) {
+            idle = 0;
+            last_work = -1.0;   // refreshed on the next idle pass
+            continue;
+        }
         if (r.stop.load(std::memory_order_acquire) && inflight.empty() &&
             ib->head.load() == ib->tail.load())
             break;
-        if (++idle > 64) usleep(idle > 4096 ? 200 : 20);
-        else sched_yield();
+        ++idle;
+        if (!inflight.empty() || idle <= 64) {
+            sched_yield();
+            continue;
+        }
+        const double t = now_s();
+        if (last_work < 0) last_work = t;
+        if (t - last_work < spin_s) sched_yield();
+        else usleep(idle > 4096 ? 200 : 20);
     }
     for (hipEvent_t e : pool) (void)hipEventDestroy(e);
     if (prog_work_ev) {
