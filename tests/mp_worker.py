@@ -1553,7 +1553,11 @@ def test_vector_ref(L, rank, size, loop=60):
     cc = np.zeros(ELEMS)
     assert L.comex_get(ctypes.c_void_p(b[0]), ctypes.c_void_p(cc.ctypes.data), 8 * ELEMS, 0, 0) == 0
     want = a * (alpha * TIMES * size * size)
-    assert np.allclose(cc, want, rtol=1e-4, atol=0), np.max(np.abs(cc - want))
+    if not np.allclose(cc, want, rtol=1e-4, atol=0):
+        bad = np.nonzero(~np.isclose(cc, want, rtol=1e-4, atol=0))[0]
+        raise AssertionError(f"test_vector_acc: {bad.size} elements off: " + ", ".join(
+            f"[{j}] got {cc[j]!r} want {want[j]!r} (diff/(alpha*a) {(cc[j] - want[j]) / (alpha * a[j]) if a[j] else 0:+.3f})"
+            for j in bad[:8]))
     if size == 1:
         seq = np.zeros(ELEMS)
         for _ in range(TIMES):
