@@ -1537,6 +1537,9 @@ def test_vector_ref(L, rank, size, loop=60):
     say(rank, "test_vector ok")
     # ---- test_vector_acc
     ELEMS, TIMES, alpha = 200, 20, 0.1
+    # diagnostics only (TEST_VEC_RANK_ALPHA=1): rank r uses alpha*(1+r), so a miss names its rank
+    rank_alpha = os.environ.get("TEST_VEC_RANK_ALPHA") == "1"
+    my_alpha = alpha * (1 + rank) if rank_alpha else alpha
     b = ga_amd.comex_malloc(8 * ELEMS, size)
     L.gaamd_memset(ctypes.c_void_p(b[rank]), 0, 8 * ELEMS)
     ga_amd.sync()
@@ -1547,18 +1550,27 @@ def test_vector_ref(L, rank, size, loop=60):
         for par in (0, 1):
             idx = range(par, ELEMS, 2)
             descs = [([A + 8 * j for j in idx], [b[0] + 8 * j for j in idx], 8)]
-            assert ga_amd.comex_accv(38, alpha, descs, 0) == 0
+            assert ga_amd.comex_accv(38, my_alpha, descs, 0) == 0
     ga_amd.comex_fence_all()
     ga_amd.comex_barrier()
     cc = np.zeros(ELEMS)
     assert L.comex_get(ctypes.c_void_p(b[0]), ctypes.c_void_p(cc.ctypes.data), 8 * ELEMS, 0, 0) == 0
-    want = a * (alpha * TIMES * size * size)
+    want = a * (alpha * TIMES * size * (sum(1 + r for r in range(size)) if rank_alpha else size))
     if not np.allclose(cc, want, rtol=1e-4, atol=0):
         bad = np.nonzero(~np.isclose(cc, want, rtol=1e-4, atol=0))[0]
-        raise AssertionError(f"test_vector_acc: {bad.size} elements off: " + ", ".join(
+        msg = f"test_vector_acc: {bad.size} elements off: " + ", ".join(
             f"[{j}] got {cc[j]!r} want {want[j]!r} (diff/(alpha*a) {(cc[j] - want[j]) / (alpha * a[j]) if a[j] else 0:+.3f})"
-            for j in bad[:8]))
-    if size == 1:
+            for j in bad[:4])
+        # diagnosis: read again after a pause -- a late update means completion was
+        # reported early, a permanent miss means an update was lost
+        import time
+        time.sleep(0.5)
+        again = np.zeros(ELEMS)
+        assert L.comex_get(ctypes.c_void_p(b[0]), ctypes.c_void_p(again.ctypes.data), 8 * ELEMS, 0, 0) == 0
+        ga_amd.comex_fence_all()
+        healed = np.allclose(again, want, rtol=1e-4, atol=0)
+        raise AssertionError(msg + f"; after 0.5 s: {'correct (late update)' if healed else 'still off (lost update)'}")
+    if size == 1 and not rank_alpha:
         seq = np.zeros(ELEMS)
         for _ in range(TIMES):
             seq = seq + a * alpha
