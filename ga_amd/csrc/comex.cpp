@@ -1105,6 +1105,16 @@ static char *iov_host_scratch(size_t bytes) {   // pinned upload staging; caller
     return g_iov_host;
 }
 
+static char *g_riov_pin = nullptr;   // remote io-vector request upload (pinned)
+static size_t g_riov_pin_bytes = 0;
+static char *remote_iov_pinned(size_t bytes) {   // caller holds launch_mu; no upload from it in flight
+    if (bytes <= g_riov_pin_bytes) return g_riov_pin;
+    if (g_riov_pin) GA_HIP(hipHostFree(g_riov_pin));
+    g_riov_pin_bytes = std::max<size_t>(bytes, 1 << 20);
+    GA_HIP(hipHostMalloc((void **)&g_riov_pin, g_riov_pin_bytes, hipHostMallocDefault));
+    return g_riov_pin;
+}
+
 static char *iov_scratch(size_t bytes) {   // caller holds launch_mu
     if (bytes <= g_iov_scratch_bytes) return g_iov_scratch;
     sched_sync_all();
@@ -1607,14 +1617,18 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             char *stage = r.staging + (size_t)world * sub + off;
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
+                // the request's bytes (packed host sources, owner addresses) go up from
+                // pinned memory: a copy from pageable memory was seen to leave the payload
+                // invisible to the owner's kernel once in a while (a lost update,
+                // profiles/r02/README.md); the previous request's upload from this buffer
+                // completed before its post
+                char *pin = remote_iov_pinned((size_t)len_b);
+                memcpy(pin + loff, dv + i0, (size_t)m * 8);
                 if (src_host) {
                     // pageable sources (GA's MA buffer): gathered on the host, one upload
-                    static std::vector<char> g_rpacked;
-                    if (g_rpacked.size() < (size_t)m * (size_t)bytes) g_rpacked.resize((size_t)m * (size_t)bytes);
-                    gather_runs(g_rpacked.data(), darr[k].src + i0, m, bytes);
+                    gather_runs(pin, darr[k].src + i0, m, bytes);
                     sched_join();
-                    GA_HIP(hipMemcpyAsync(stage, g_rpacked.data(), (size_t)m * (size_t)bytes, hipMemcpyHostToDevice,
-                                          r.streams[0]));
+                    GA_HIP(hipMemcpyAsync(stage, pin, (size_t)len_b, hipMemcpyHostToDevice, r.streams[0]));
                 } else {
                     char *dev = iov_scratch((size_t)m * 8);
                     sched_sync_all();
@@ -1631,8 +1645,9 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
                     const int rc = launch_iov(kOpCopy, nullptr, d, salign, false, r.streams[0]);
                     if (rc) fatal("io-vector pack failed (%d)", rc);
                 }
-                GA_HIP(hipMemcpyAsync(stage + loff, dv + i0, (size_t)m * 8, hipMemcpyHostToDevice,
-                                      r.streams[0]));
+                if (!src_host)
+                    GA_HIP(hipMemcpyAsync(stage + loff, pin + loff, (size_t)m * 8, hipMemcpyHostToDevice,
+                                          r.streams[0]));
                 GA_HIP(hipStreamSynchronize(r.streams[0]));
             }
             const uint64_t seq = ++r.posted[world];
