@@ -1111,8 +1111,21 @@ static char *remote_iov_pinned(size_t bytes) {   // caller holds launch_mu; no u
     if (bytes <= g_riov_pin_bytes) return g_riov_pin;
     if (g_riov_pin) GA_HIP(hipHostFree(g_riov_pin));
     g_riov_pin_bytes = std::max<size_t>(bytes, 1 << 20);
-    GA_HIP(hipHostMalloc((void **)&g_riov_pin, g_riov_pin_bytes, hipHostMallocDefault));
+    GA_HIP(hipHostMalloc((void **)&g_riov_pin, g_riov_pin_bytes, hipHostMallocMapped));
     return g_riov_pin;
+}
+
+// copy `bytes` of the pinned upload buffer into staging with a kernel on `st`: a
+// host-side copy into HBM (hipMemcpyAsync H2D) was seen, once in a while, not to be
+// visible yet to the owner's kernel in another process when the request was
+// posted after the stream synchronisation -- a whole request applied as zeros
+// (profiles/r02/README.md); a kernel's writes are released at its end
+static void upload_pinned(char *stage, const char *pin, size_t bytes, hipStream_t st) {
+    void *dev = nullptr;
+    GA_HIP(hipHostGetDevicePointer(&dev, (void *)pin, 0));
+    int count[1] = {(int)bytes};
+    const int rc = launch_strided(kOpCopy, nullptr, (const char *)dev, nullptr, stage, nullptr, count, 0, st, nullptr);
+    if (rc) fatal("io-vector upload failed (%d)", rc);
 }
 
 static char *iov_scratch(size_t bytes) {   // caller holds launch_mu
@@ -1628,7 +1641,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
                     // pageable sources (GA's MA buffer): gathered on the host, one upload
                     gather_runs(pin, darr[k].src + i0, m, bytes);
                     sched_join();
-                    GA_HIP(hipMemcpyAsync(stage, pin, (size_t)len_b, hipMemcpyHostToDevice, r.streams[0]));
+                    upload_pinned(stage, pin, (size_t)len_b, r.streams[0]);
                 } else {
                     char *dev = iov_scratch((size_t)m * 8);
                     sched_sync_all();
@@ -1645,9 +1658,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
                     const int rc = launch_iov(kOpCopy, nullptr, d, salign, false, r.streams[0]);
                     if (rc) fatal("io-vector pack failed (%d)", rc);
                 }
-                if (!src_host)
-                    GA_HIP(hipMemcpyAsync(stage + loff, pin + loff, (size_t)m * 8, hipMemcpyHostToDevice,
-                                          r.streams[0]));
+                if (!src_host) upload_pinned(stage + loff, pin + loff, (size_t)m * 8, r.streams[0]);
                 GA_HIP(hipStreamSynchronize(r.streams[0]));
             }
             const uint64_t seq = ++r.posted[world];
