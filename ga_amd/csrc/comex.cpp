@@ -367,6 +367,19 @@ static uint64_t stage_alloc(int t, uint64_t len) {
     }
 }
 
+static uint64_t fnv1a(const char *p, size_t n) {
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; ++i) h = (h ^ (unsigned char)p[i]) * 1099511628211ull;
+    return h | 1;   // never 0 (0 = no check)
+}
+static bool check_iov() {   // COMEX_AMD_CHECK_IOV=1: the owner verifies each io-vector upload
+    static const bool on = [] {
+        const char *e = getenv("COMEX_AMD_CHECK_IOV");
+        return e && atoi(e) != 0;
+    }();
+    return on;
+}
+
 static std::atomic<unsigned long long> g_route[4];   // gaamd_route_counts
 
 static void post_request(int t, int op, const void *scale, uint64_t dst_addr, const int *dst_stride,
@@ -408,7 +421,7 @@ static void post_request(int t, int op, const void *scale, uint64_t dst_addr, co
 // addresses (8-byte aligned)
 // mode: 0 parallel, 1 in order on one lane (destinations overlap), 2 GPU-sorted runs
 static void post_request_iov(int t, int op, const void *scale, int bytes, int n, uint64_t off, uint64_t len,
-                             uint64_t dlo, uint64_t dhi, uint64_t align_or, int mode) {
+                             uint64_t dlo, uint64_t dhi, uint64_t align_or, int mode, uint64_t check = 0) {
     Runtime &r = rt();
     Inbox *ib = inbox_of(r.shm, r.li(t));
     const uint64_t ticket = ib->tail.fetch_add(1, std::memory_order_acq_rel);
@@ -431,7 +444,7 @@ static void post_request_iov(int t, int op, const void *scale, int bytes, int n,
     q.dst_hi = dhi;
     q.staging_off = off;
     q.bytes = len;
-    q.seq = 0;
+    q.seq = check;                   // COMEX_AMD_CHECK_IOV: FNV-1a of the uploaded bytes
     memset(q.scale, 0, sizeof(q.scale));
     if (scale) memcpy(q.scale, scale, (size_t)elem_size(op));
     q.kind = 1;
@@ -527,6 +540,17 @@ static void progress_loop() {
             d.dst_list = (const uint64_t *)(packed + iov_list_off(q.count[1], q.count[0]));
             d.bytes = q.count[0];
             d.n = (uint32_t)q.count[1];
+            if (q.seq) {   // COMEX_AMD_CHECK_IOV: compare the staging bytes with the requester's checksum
+                const size_t pb = (size_t)q.count[1] * (size_t)q.count[0];
+                const size_t lo = iov_list_off(q.count[1], q.count[0]);
+                std::vector<char> host(lo + (size_t)q.count[1] * 8);
+                GA_HIP(hipMemcpy(host.data(), packed, host.size(), hipMemcpyDeviceToHost));
+                const uint64_t got = fnv1a(host.data(), pb) ^ (fnv1a(host.data() + lo, (size_t)q.count[1] * 8) << 1);
+                if (got != q.seq)
+                    fprintf(stderr, "[ga_amd %d] io-vector request from %d (staging +%lu, %d pairs): staging bytes "
+                            "differ from what the requester uploaded\n", r.rank, src, (unsigned long)q.staging_off,
+                            q.count[1]);
+            }
             hipEvent_t ev;
             if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
             else { ev = pool.back(); pool.pop_back(); }
@@ -1664,8 +1688,14 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             const uint64_t seq = ++r.posted[world];
             g_pend[world].push_back({seq, off, ring_len(len_b)});
             r.stage_head[world] = off + ring_len(len_b);
+            uint64_t chk = 0;
+            if (check_iov()) {   // the bytes the owner should see in staging
+                std::vector<char> host((size_t)len_b);
+                GA_HIP(hipMemcpy(host.data(), stage, (size_t)len_b, hipMemcpyDeviceToHost));
+                chk = fnv1a(host.data(), (size_t)m * (size_t)bytes) ^ (fnv1a(host.data() + loff, (size_t)m * 8) << 1);
+            }
             post_request_iov(world, op, scale, bytes, m, (uint64_t)world * sub + off, len_b, dlo, dhi, align_or,
-                             mode);
+                             mode, chk);
         }
     }
     // io-vector kernels may sit on any library stream (sched_pick per descriptor):
