@@ -540,6 +540,11 @@ static void progress_loop() {
             d.dst_list = (const uint64_t *)(packed + iov_list_off(q.count[1], q.count[0]));
             d.bytes = q.count[0];
             d.n = (uint32_t)q.count[1];
+            static const int own_delay = [] {
+                const char *e = getenv("COMEX_AMD_DIAG_OWNER_DELAY_US");   // diagnostics only
+                return e ? atoi(e) : 0;
+            }();
+            if (own_delay) usleep(own_delay);
             if (q.seq) {   // COMEX_AMD_CHECK_IOV: compare the staging bytes with the requester's checksum
                 const size_t pb = (size_t)q.count[1] * (size_t)q.count[0];
                 const size_t lo = iov_list_off(q.count[1], q.count[0]);
@@ -1688,6 +1693,11 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             const uint64_t seq = ++r.posted[world];
             g_pend[world].push_back({seq, off, ring_len(len_b)});
             r.stage_head[world] = off + ring_len(len_b);
+            static const int req_delay = [] {
+                const char *e = getenv("COMEX_AMD_DIAG_REQ_DELAY_US");   // diagnostics only
+                return e ? atoi(e) : 0;
+            }();
+            if (req_delay) usleep(req_delay);
             uint64_t chk = 0;
             if (check_iov()) {   // the bytes the owner should see in staging
                 std::vector<char> host((size_t)len_b);
