@@ -586,6 +586,11 @@ static void progress_loop() {
                 }
                 if (rc) fatal("io-vector accumulate launch failed (%d)", rc);
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
+                static const bool own_sync = [] {
+                    const char *e = getenv("COMEX_AMD_DIAG_OWNER_SYNC");   // diagnostics only
+                    return e && atoi(e) != 0;
+                }();
+                if (own_sync) GA_HIP(hipStreamSynchronize(r.streams[si]));
             }
             inflight.push_back({ev, src, false});
             q.state.store(0, std::memory_order_release);
