@@ -165,6 +165,13 @@ def route_counts():
     return {"packed": c[0], "direct_src": c[1], "iov": c[2], "rmw": c[3]}
 
 
+def owner_counts():
+    """requests this rank's progress thread applied, by kind"""
+    c = (ctypes.c_ulonglong * 4)()
+    lib().gaamd_owner_counts(c)
+    return {"packed": c[0], "iov": c[1], "rmw": c[2], "direct_src": c[3]}
+
+
 def set_tuning(key, value):
     return lib().gaamd_set_tuning(key.encode(), int(value))
 

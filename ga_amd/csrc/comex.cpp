@@ -367,20 +367,8 @@ static uint64_t stage_alloc(int t, uint64_t len) {
     }
 }
 
-static uint64_t fnv1a(const char *p, size_t n) {
-    uint64_t h = 1469598103934665603ull;
-    for (size_t i = 0; i < n; ++i) h = (h ^ (unsigned char)p[i]) * 1099511628211ull;
-    return h | 1;   // never 0 (0 = no check)
-}
-static bool check_iov() {   // COMEX_AMD_CHECK_IOV=1: the owner verifies each io-vector upload
-    static const bool on = [] {
-        const char *e = getenv("COMEX_AMD_CHECK_IOV");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-
 static std::atomic<unsigned long long> g_route[4];   // gaamd_route_counts
+static std::atomic<unsigned long long> g_owned[4];   // gaamd_owner_counts: requests applied, by kind
 
 static void post_request(int t, int op, const void *scale, uint64_t dst_addr, const int *dst_stride,
                          const int *count, int levels, uint64_t off, uint64_t len, uint64_t rb, uint64_t re) {
@@ -421,7 +409,7 @@ static void post_request(int t, int op, const void *scale, uint64_t dst_addr, co
 // addresses (8-byte aligned)
 // mode: 0 parallel, 1 in order on one lane (destinations overlap), 2 GPU-sorted runs
 static void post_request_iov(int t, int op, const void *scale, int bytes, int n, uint64_t off, uint64_t len,
-                             uint64_t dlo, uint64_t dhi, uint64_t align_or, int mode, uint64_t check = 0) {
+                             uint64_t dlo, uint64_t dhi, uint64_t align_or, int mode) {
     Runtime &r = rt();
     Inbox *ib = inbox_of(r.shm, r.li(t));
     const uint64_t ticket = ib->tail.fetch_add(1, std::memory_order_acq_rel);
@@ -444,7 +432,7 @@ static void post_request_iov(int t, int op, const void *scale, int bytes, int n,
     q.dst_hi = dhi;
     q.staging_off = off;
     q.bytes = len;
-    q.seq = check;                   // COMEX_AMD_CHECK_IOV: FNV-1a of the uploaded bytes
+    q.seq = 0;
     memset(q.scale, 0, sizeof(q.scale));
     if (scale) memcpy(q.scale, scale, (size_t)elem_size(op));
     q.kind = 1;
@@ -530,7 +518,14 @@ static void progress_loop() {
         bool worked = false;
         const uint64_t h = ib->head.load(std::memory_order_relaxed);
         Request &q = ib->slot[h % kInboxSlots];
-        if (q.state.load(std::memory_order_acquire) == 2 && q.kind == 1) {
+        // the slot's state is read ONCE per pass and the kind dispatched on that
+        // reading: re-reading it per branch let a request that became ready between
+        // the kind tests fall through to the last branch as a packed one (an
+        // io-vector request applied as an 8-byte unpack-acc: a whole request lost)
+        const bool ready = q.state.load(std::memory_order_acquire) == 2;
+        if (ready && q.kind != 0 && q.kind != 1 && q.kind != 2 && q.kind != 3)
+            fatal("inbox request of unknown kind %d from rank %d", (int)q.kind, (int)q.src_rank);
+        if (ready && q.kind == 1) {
             // io-vector accumulate (the _acc_iov_handler analogue, comex.c:4284-4397)
             const int src = q.src_rank;
             const char *packed = peer_staging_or_die(src) + q.staging_off;
@@ -540,22 +535,6 @@ static void progress_loop() {
             d.dst_list = (const uint64_t *)(packed + iov_list_off(q.count[1], q.count[0]));
             d.bytes = q.count[0];
             d.n = (uint32_t)q.count[1];
-            static const int own_delay = [] {
-                const char *e = getenv("COMEX_AMD_DIAG_OWNER_DELAY_US");   // diagnostics only
-                return e ? atoi(e) : 0;
-            }();
-            if (own_delay) usleep(own_delay);
-            if (q.seq) {   // COMEX_AMD_CHECK_IOV: compare the staging bytes with the requester's checksum
-                const size_t pb = (size_t)q.count[1] * (size_t)q.count[0];
-                const size_t lo = iov_list_off(q.count[1], q.count[0]);
-                std::vector<char> host(lo + (size_t)q.count[1] * 8);
-                GA_HIP(hipMemcpy(host.data(), packed, host.size(), hipMemcpyDeviceToHost));
-                const uint64_t got = fnv1a(host.data(), pb) ^ (fnv1a(host.data() + lo, (size_t)q.count[1] * 8) << 1);
-                if (got != q.seq)
-                    fprintf(stderr, "[ga_amd %d] io-vector request from %d (staging +%lu, %d pairs): staging bytes "
-                            "differ from what the requester uploaded\n", r.rank, src, (unsigned long)q.staging_off,
-                            q.count[1]);
-            }
             hipEvent_t ev;
             if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
             else { ev = pool.back(); pool.pop_back(); }
@@ -586,17 +565,13 @@ static void progress_loop() {
                 }
                 if (rc) fatal("io-vector accumulate launch failed (%d)", rc);
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
-                static const bool own_sync = [] {
-                    const char *e = getenv("COMEX_AMD_DIAG_OWNER_SYNC");   // diagnostics only
-                    return e && atoi(e) != 0;
-                }();
-                if (own_sync) GA_HIP(hipStreamSynchronize(r.streams[si]));
             }
             inflight.push_back({ev, src, false});
+            g_owned[1].fetch_add(1, std::memory_order_relaxed);
             q.state.store(0, std::memory_order_release);
             ib->head.store(h + 1, std::memory_order_release);
             worked = true;
-        } else if (q.state.load(std::memory_order_acquire) == 2 && q.kind == 2) {
+        } else if (ready && q.kind == 2) {
             // comex_rmw from a rank of this node (the progress rank's OP_FETCH_AND_ADD /
             // OP_SWAP): one lane on this GPU, after earlier operations on those bytes
             const int src = q.src_rank;
@@ -617,10 +592,11 @@ static void progress_loop() {
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
             }
             inflight.push_back({ev, src, true});
+            g_owned[2].fetch_add(1, std::memory_order_relaxed);
             q.state.store(0, std::memory_order_release);
             ib->head.store(h + 1, std::memory_order_release);
             worked = true;
-        } else if (q.state.load(std::memory_order_acquire) == 2 && q.kind == 3) {
+        } else if (ready && q.kind == 3) {
             // strided accumulate read straight from the requester's segment (one
             // pass: src read + dst read + dst write, as a local accumulate)
             const int src = q.src_rank;
@@ -640,10 +616,11 @@ static void progress_loop() {
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
             }
             inflight.push_back({ev, src, false});
+            g_owned[3].fetch_add(1, std::memory_order_relaxed);
             q.state.store(0, std::memory_order_release);
             ib->head.store(h + 1, std::memory_order_release);
             worked = true;
-        } else if (q.state.load(std::memory_order_acquire) == 2) {
+        } else if (ready && q.kind == 0) {
             const int src = q.src_rank;
             const char *packed = peer_staging_or_die(src) + q.staging_off;
             const uint64_t rb = q.seq >> 32, re = q.seq & 0xffffffffull;
@@ -668,6 +645,7 @@ static void progress_loop() {
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
             }
             inflight.push_back({ev, src, false});
+            g_owned[0].fetch_add(1, std::memory_order_relaxed);
             q.state.store(0, std::memory_order_release);
             ib->head.store(h + 1, std::memory_order_release);
             worked = true;
@@ -1149,11 +1127,8 @@ static char *remote_iov_pinned(size_t bytes) {   // caller holds launch_mu; no u
     return g_riov_pin;
 }
 
-// copy `bytes` of the pinned upload buffer into staging with a kernel on `st`: a
-// host-side copy into HBM (hipMemcpyAsync H2D) was seen, once in a while, not to be
-// visible yet to the owner's kernel in another process when the request was
-// posted after the stream synchronisation -- a whole request applied as zeros
-// (profiles/r02/README.md); a kernel's writes are released at its end
+// copy `bytes` of the pinned (device-mapped) upload buffer into staging with the
+// copy kernel on `st` (one launch, no runtime staging of the host bytes)
 static void upload_pinned(char *stage, const char *pin, size_t bytes, hipStream_t st) {
     void *dev = nullptr;
     GA_HIP(hipHostGetDevicePointer(&dev, (void *)pin, 0));
@@ -1665,9 +1640,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
                 // the request's bytes (packed host sources, owner addresses) go up from
-                // pinned memory: a copy from pageable memory was seen to leave the payload
-                // invisible to the owner's kernel once in a while (a lost update,
-                // profiles/r02/README.md); the previous request's upload from this buffer
+                // pinned memory; the previous request's upload from this buffer
                 // completed before its post
                 char *pin = remote_iov_pinned((size_t)len_b);
                 memcpy(pin + loff, dv + i0, (size_t)m * 8);
@@ -1698,19 +1671,8 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             const uint64_t seq = ++r.posted[world];
             g_pend[world].push_back({seq, off, ring_len(len_b)});
             r.stage_head[world] = off + ring_len(len_b);
-            static const int req_delay = [] {
-                const char *e = getenv("COMEX_AMD_DIAG_REQ_DELAY_US");   // diagnostics only
-                return e ? atoi(e) : 0;
-            }();
-            if (req_delay) usleep(req_delay);
-            uint64_t chk = 0;
-            if (check_iov()) {   // the bytes the owner should see in staging
-                std::vector<char> host((size_t)len_b);
-                GA_HIP(hipMemcpy(host.data(), stage, (size_t)len_b, hipMemcpyDeviceToHost));
-                chk = fnv1a(host.data(), (size_t)m * (size_t)bytes) ^ (fnv1a(host.data() + loff, (size_t)m * 8) << 1);
-            }
             post_request_iov(world, op, scale, bytes, m, (uint64_t)world * sub + off, len_b, dlo, dhi, align_or,
-                             mode, chk);
+                             mode);
         }
     }
     // io-vector kernels may sit on any library stream (sched_pick per descriptor):
@@ -2427,6 +2389,11 @@ int comex_group_translate_ranks(int n, comex_group_t group_from, int *ranks_from
 int comex_group_comm(comex_group_t group, void *comm) {
     (void)comm;
     fatal("comex_group_comm(%d): libga_amd has no MPI communicator (it bootstraps without MPI)", group);
+}
+
+int gaamd_owner_counts(unsigned long long counts[4]) {
+    for (int k = 0; k < 4; ++k) counts[k] = g_owned[k].load(std::memory_order_relaxed);
+    return 0;
 }
 
 int gaamd_route_counts(unsigned long long counts[4]) {

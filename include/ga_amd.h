@@ -80,6 +80,8 @@ int gaamd_kernel_counts(unsigned long long counts[5]);
  * {packed chunks (pack -> staging -> owner unpack), direct-source (owner reads
  * our segment), io-vector, rmw} */
 int gaamd_route_counts(unsigned long long counts[4]);
+/* requests this rank's progress thread applied, by kind: packed, io-vector, rmw, direct-source */
+int gaamd_owner_counts(unsigned long long counts[4]);
 /* keys: "kind" (0 auto, 1 rows, 2 flat, 3 serial, 4 ordered), "unroll16" (1/2/4),
  * "nontemporal", "block" (0 auto/64/128/256), "flat_max_nvec", "align", "direct",
  * "flat_nt", "flat_shape", "flat_line_min", "wide_unaligned", "streams";

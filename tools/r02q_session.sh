@@ -1,0 +1,20 @@
+#!/bin/bash
+# round-2 GPU session q: the vector-acc test in its default configuration, repeated
+set -uo pipefail
+O=gpurun_out/r02q
+mkdir -p "$O"
+export TMPDIR=/tmp
+step() {
+    local name=$1 t=$2; shift 2
+    timeout -k 10 "$t" "$@" > "$O/$name.out" 2> "$O/$name.err"
+    local rc=$?
+    echo "$name rc=$rc"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+}
+for i in $(seq 1 12); do
+  step vec_$i 150 env TEST_VEC_RANK_ALPHA=1 python -u -m pytest tests/test_multiproc.py -q -x -k "test_comex_test_vector_restated and not 1" --timeout 120 --timeout-method thread -p no:cacheprovider
+  grep -ho "test_vector_acc: .*\|[0-9]* passed.*\|[0-9]* failed.*" "$O/vec_$i.out" "$O/vec_$i.err" | cut -c1-400 | head -6
+done
+step mp 600 python -u -m pytest tests/test_multiproc.py -q --timeout 150 --timeout-method thread -p no:cacheprovider -rf -m gpu
+tail -5 "$O/mp.out"
+echo done
