@@ -427,8 +427,9 @@ def run_gpu(args, dist, finalize=True):
         for i in range(1, args.steps):
             step(first + i)
         t_enq = time.perf_counter()
-        hd.drain()                          # every step's kernel has finished (comex_wait_all)
-        ga_amd.sync()
+        # every step's kernel has finished: comex_wait_all synchronises every library
+        # stream (hipStreamSynchronize each), i.e. all GPU work of this rank
+        hd.drain()
         if seg_dst:
             L.comex_fence_all(0)            # remote completion: the owner has applied every request
         t1 = time.perf_counter()
