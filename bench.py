@@ -48,7 +48,8 @@ torch.distributed (gloo, CPU) only carries the bootstrap allgather/barrier and
 the max-over-ranks reduction.  At N > 1 the line also carries C5 (GA_Acc into a
 block-distributed 32768^2 f64 GA): M1 (every rank its own
 block) and M2 (every rank the whole array: (p-1)/p of it through the remote
-path over xGMI), with per-GPU HBM fraction and per-GPU xGMI bytes/s.
+path over xGMI), with per-GPU HBM fraction and per-GPU xGMI bytes/s, and an
+exactness check of the exchange on both remote routes (c5.exchange_check).
 """
 import argparse
 import ctypes
@@ -496,8 +497,7 @@ def c5_extras(args, dist):
         if args.verbose:
             print(f"rank {dist.rank}: C5 {mode} starts", file=sys.stderr, flush=True)
         args.src_seg = src_seg
-        r = run_ga(args, dist, exchange=exchange, steps=steps, warmup_ms=0.0,
-                   terminate=(mode == "M2_src_in_segment"))
+        r = run_ga(args, dist, exchange=exchange, steps=steps, warmup_ms=0.0, terminate=False)
         args.src_seg = saved
         p = dist.size
         t = r["elapsed"] / steps
@@ -515,7 +515,67 @@ def c5_extras(args, dist):
         else:
             d["hbm_peak_frac_per_gpu"] = round(r["alg_bytes"] / t / (HBM_PEAK_GBS * 1e9), 4)
         out[mode] = d
+    out["exchange_check"] = {route: c5_exchange_check(dist, src_seg) for route, src_seg in
+                             (("packed", False), ("direct_src", True))}
+    ga_amd_lib().GA_Terminate()
     return out
+
+
+def ga_amd_lib():
+    import ga_amd
+    return ga_amd.lib()
+
+
+def c5_exchange_check(dist, src_seg, n=4096):
+    """Cross-GPU exactness of the exchange (the driver's N > 1 run is the first on
+    separate GPUs): every rank NGA_Acc's a whole n x n f64 GA from a source of the
+    constant 2**rank (alpha 1, the array zeroed first), so every element must read
+    exactly 2**p - 1 afterwards -- a lost, doubled or stale contribution shows as a
+    wrong element and its value says whose.  The source is a plain device buffer
+    (packed route) or lies in the rank's segment (direct-source route)."""
+    import ga_amd
+    L = ga_amd.lib()
+    ia = ga_amd.int_array
+    g = L.NGA_Create(C_DBL, 2, ia([n, n]), b"C5chk", None)
+    assert g > 0
+    L.GA_Zero(g)
+    L.GA_Sync()
+    host = np.full(n * n, float(2 ** dist.rank))
+    seg, buf = None, None
+    if src_seg:
+        seg = ga_amd.comex_malloc(host.nbytes, dist.size)
+        ptr = seg[dist.rank]
+        assert L.gaamd_memcpy(ctypes.c_void_p(ptr), host.ctypes.data_as(ctypes.c_void_p), host.nbytes) == 0
+    else:
+        buf = ga_amd.DeviceBuffer(host.nbytes)
+        buf.upload(host)
+        ptr = buf.ptr
+    routes0 = ga_amd.route_counts()
+    alpha = ctypes.c_double(1.0)
+    L.NGA_Acc(g, ia([0, 0]), ia([n - 1, n - 1]), ctypes.c_void_p(ptr), ia([n]), ctypes.byref(alpha))
+    ga_amd.sync()
+    L.GA_Sync()
+    routes = {k: v - routes0[k] for k, v in ga_amd.route_counts().items()}
+    blo, bhi = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
+    L.NGA_Distribution(g, dist.rank, blo, bhi)
+    rows, cols = bhi[0] - blo[0] + 1, bhi[1] - blo[1] + 1
+    out = np.empty(rows * cols)
+    L.NGA_Get(g, blo, bhi, out.ctypes.data_as(ctypes.c_void_p), ia([cols]))
+    want = float(2 ** dist.size - 1)
+    bad = int(np.count_nonzero(out != want))
+    sample = None if not bad else float(out[np.nonzero(out != want)[0][0]])
+    L.GA_Sync()
+    if seg is not None:
+        ga_amd.comex_free(seg[dist.rank])
+    if buf is not None:
+        buf.free()
+    L.GA_Destroy(g)
+    worst = int(dist.max(float(bad)))
+    res = {"array": f"{n}x{n} f64", "expect_every_element": want, "wrong_elements_max_over_ranks": worst,
+           "result": "exact" if worst == 0 else "MISMATCH", "routes_rank": routes}
+    if bad:
+        res["first_wrong_value_this_rank"] = sample
+    return res
 
 
 def host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_bytes, iters=5):

@@ -63,8 +63,9 @@ def main():
     stream = L.gaamd_stream()
     variants = [v for v in args.variants.split(";") if v]
     # every knob is reset to its default before each variant (a variant sets only its own keys)
-    defaults = {k: ga_amd.get_tuning(k) for k in ("kind", "unroll16", "nontemporal", "flat_max_nvec", "max_grid",
-                                                   "block", "align", "cpol", "xcd", "order", "direct", "flat_nt", "lds_pad", "flat_shape", "flat_line_min", "wide_unaligned")}
+    defaults = {k: ga_amd.get_tuning(k) for k in ("kind", "unroll16", "nontemporal", "flat_max_nvec", "block", "align",
+                                                   "direct", "flat_nt", "flat_shape", "flat_line_min",
+                                                   "wide_unaligned")}
     defaults["streams"] = L.gaamd_num_streams()
     res = {v: [] for v in variants}
     wall = {v: [] for v in variants}
