@@ -53,6 +53,7 @@ exactness check of the exchange on both remote routes (c5.exchange_check).
 """
 import argparse
 import ctypes
+import gc
 import json
 import os
 import socket
@@ -417,7 +418,11 @@ def run_gpu(args, dist, finalize=True):
     ga_amd.sync()
     launch = ga_amd.last_launch()
 
-    # value region: barrier + sync on both sides, wall clock, no timing events
+    # value region: barrier + sync on both sides, wall clock, no timing events; no
+    # garbage collection inside it (as timeit): a collection pass there is host time
+    # the GPU work does not need
+    gc.collect()
+    gc.disable()
     L.comex_barrier(0)
     dist.barrier()
     ga_amd.sync()
@@ -438,6 +443,7 @@ def run_gpu(args, dist, finalize=True):
                          "enqueue_all_us": round((t_enq - t0) * 1e6, 1), "total_us": round((t1 - t0) * 1e6, 1)}
 
     elapsed, region_profile = value_region(nxt)
+    gc.enable()
     dist.barrier()
     elapsed = dist.max(elapsed)
     nxt += args.steps

@@ -23,7 +23,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def run_pass(counter, workload, outdir, steps):
     d = os.path.join(outdir, counter)
-    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+    # each counter pass under its own hard time limit (a pass asked for more counters than
+    # the hardware holds hangs after printing error 38)
+    cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
            sys.executable, os.path.join(ROOT, "tools", "sweep.py"), "--workload", workload, "--rounds", "1",
            "--steps", str(steps), "--sets", "8", "--variants", "default"]
     env = dict(os.environ, TMPDIR="/tmp")
