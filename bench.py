@@ -421,12 +421,12 @@ def run_gpu(args, dist, finalize=True):
     # value region: barrier + sync on both sides, wall clock, no timing events; no
     # garbage collection inside it (as timeit): a collection pass there is host time
     # the GPU work does not need
-    gc.collect()
     gc.disable()
     L.comex_barrier(0)
     dist.barrier()
     ga_amd.sync()
     def value_region(first):
+        b0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
         t0 = time.perf_counter()
         step(first)
         t_first = time.perf_counter()
@@ -439,8 +439,12 @@ def run_gpu(args, dist, finalize=True):
         if seg_dst:
             L.comex_fence_all(0)            # remote completion: the owner has applied every request
         t1 = time.perf_counter()
+        b1 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
+        # boottime_ns: the region's ends on the clock rocprofv3 stamps kernels with,
+        # so a profiled run can place the first kernel's start and the last one's end
         return t1 - t0, {"first_call_us": round((t_first - t0) * 1e6, 1),
-                         "enqueue_all_us": round((t_enq - t0) * 1e6, 1), "total_us": round((t1 - t0) * 1e6, 1)}
+                         "enqueue_all_us": round((t_enq - t0) * 1e6, 1), "total_us": round((t1 - t0) * 1e6, 1),
+                         "boottime_ns": [b0, b1]}
 
     elapsed, region_profile = value_region(nxt)
     gc.enable()
