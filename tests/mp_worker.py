@@ -98,6 +98,8 @@ def main():
         order_test(L, rank, size)
     elif mode == "directsrc":
         direct_src_test(L, rank, size)
+    elif mode == "gemm":
+        ga_gemm_test(L, rank, size)
     elif mode in ("armcimisc", "armcimisc-gloo"):
         armci_misc_test(L, rank, size)
     else:
@@ -1804,5 +1806,68 @@ def ngatest_gs(L, rank, size):
     L.GA_Terminate()
 
 
+# ---------------------------------------------------------------------------
+# GA_Dgemm / GA_Sgemm / GA_Zgemm / GA_Cgemm (global/src/capi.c:3279-3548 ->
+# pnga_matmul, matmul.c:1290): C = alpha*op(A)*op(B) + beta*C on the leading
+# m x k / k x n / m x n patches of larger GAs, every transpose pair, against
+# numpy on the host; the part of C outside the patch must be untouched.  The
+# tolerance is the GEMM's (summation order differs from any CPU BLAS): f64
+# 1e-12 and f32 1e-4 relative to k*max|A|*max|B| + |beta|*max|C|.
+def ga_gemm_test(L, rank, size):
+    import ga_amd
+    from ga_amd._lib import DoubleComplex, SingleComplex
+    C_FLOAT, C_DBL, C_SCPL, C_DCPL = 1003, 1004, 1006, 1007
+    assert L.GA_Initialize() == 0
+    ia = ga_amd.int_array
+    rng = np.random.default_rng(77)
+    cases = [(C_DBL, np.float64, L.GA_Dgemm, 1e-12), (C_FLOAT, np.float32, L.GA_Sgemm, 1e-4),
+             (C_DCPL, np.complex128, L.GA_Zgemm, 1e-12), (C_SCPL, np.complex64, L.GA_Cgemm, 1e-4)]
+    m, n, k = 61, 47, 83
+    for ctype, dt, fn, tol in cases:
+        for ta in "NT":
+            for tb in "NT":
+                adims = [m + 3, k + 2] if ta == "N" else [k + 2, m + 3]
+                bdims = [k + 1, n + 4] if tb == "N" else [n + 4, k + 1]
+                cdims = [m + 2, n + 5]
+                def rand(shape):
+                    x = rng.integers(-8, 9, shape).astype(np.float64)
+                    if np.iscomplexobj(np.zeros(1, dt)):
+                        x = x + 1j * rng.integers(-8, 9, shape)
+                    return x.astype(dt)
+                A, B, C0 = rand(adims), rand(bdims), rand(cdims)
+                g = [L.NGA_Create(ctype, 2, ia(d), b"gm", None) for d in (adims, bdims, cdims)]
+                assert all(x > 0 for x in g)
+                if rank == 0:
+                    for h, X in zip(g, (A, B, C0)):
+                        L.NGA_Put(h, ia([0, 0]), ia([X.shape[0] - 1, X.shape[1] - 1]),
+                                  X.ctypes.data_as(ctypes.c_void_p), ia([X.shape[1]]))
+                L.GA_Sync()
+                if ctype in (C_DCPL, C_SCPL):
+                    S = DoubleComplex if ctype == C_DCPL else SingleComplex
+                    alpha, beta = S(0.5, -1.25), S(-2.0, 0.75)
+                    av, bv = complex(0.5, -1.25), complex(-2.0, 0.75)
+                else:
+                    alpha, beta = 0.5, -2.0
+                    av, bv = 0.5, -2.0
+                fn(ta.encode(), tb.encode(), m, n, k, alpha, g[0], g[1], beta, g[2])
+                out = np.zeros(cdims, dt)
+                L.NGA_Get(g[2], ia([0, 0]), ia([cdims[0] - 1, cdims[1] - 1]),
+                          out.ctypes.data_as(ctypes.c_void_p), ia([cdims[1]]))
+                opA = (A[:m, :k] if ta == "N" else A[:k, :m].T).astype(np.complex128)
+                opB = (B[:k, :n] if tb == "N" else B[:n, :k].T).astype(np.complex128)
+                want = C0.astype(np.complex128).copy()
+                want[:m, :n] = av * (opA @ opB) + bv * C0[:m, :n]
+                scale = k * np.abs(A).max() * np.abs(B).max() + abs(bv) * np.abs(C0).max()
+                err = np.abs(out.astype(np.complex128) - want)
+                assert err[:m, :n].max() <= tol * scale, (dt.__name__, ta, tb, err.max(), scale)
+                assert np.array_equal(out[m:, :], C0[m:, :]) and np.array_equal(out[:, n:], C0[:, n:]), \
+                    (dt.__name__, ta, tb, "outside the patch changed")
+                for h in g:
+                    L.GA_Destroy(h)
+    say(rank, "ga gemm ok")
+    L.GA_Terminate()
+
+
 if __name__ == "__main__":
     main()
+

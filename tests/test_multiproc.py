@@ -245,3 +245,12 @@ def test_direct_source_remote_accumulate(n):
     (no pack, no staging), bit-exact against the oracle; smaller patches keep
     the packed route."""
     launch("directsrc", n=n, timeout=120)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,panel", [(1, None), (3, None), (3, "4096")])
+def test_ga_gemm(n, panel):
+    """GA_Dgemm/Sgemm/Zgemm/Cgemm (capi.c:3279-3548 -> pnga_matmul, matmul.c:1290)
+    on the leading patches of larger GAs, all four transpose pairs, vs numpy; with
+    4 KiB panels every k chunk is a separate get + gemm."""
+    launch("gemm", n=n, timeout=150, extra_env={"COMEX_AMD_GEMM_PANEL_BYTES": panel} if panel else None)
