@@ -803,7 +803,16 @@ def main():
     dist = Dist(args.gpus)
     extras_on = dist.size > 1 and not args.no_extras and args.workload != "C5"
     r = run_gpu(args, dist, finalize=not extras_on)
-    c5 = c5_extras(args, dist) if extras_on else None
+    c5 = None
+    if extras_on:
+        # the C5 exchange needs every same-node peer mapped by IPC; a rank that could not
+        # map one would abort there, so the extras are skipped (by every rank) instead
+        unmapped = int(dist.max(float(ga_amd.lib().gaamd_peers_unmapped())))
+        if unmapped:
+            ga_amd.lib().comex_finalize()
+            c5 = {"skipped": f"a rank could not map {unmapped} same-node peer(s) by IPC at comex_init"}
+        else:
+            c5 = c5_extras(args, dist)
     if dist.rank != 0:
         return
     n = dist.size

@@ -2396,6 +2396,15 @@ int gaamd_owner_counts(unsigned long long counts[4]) {
     return 0;
 }
 
+int gaamd_peers_unmapped(void) {
+    Runtime &r = rt();
+    if (!r.initialized) return -1;
+    int n = 0;
+    for (int q = 0; q < r.size && q < (int)r.peer_staging.size(); ++q)
+        if (q != r.rank && r.same_node(q) && !r.peer_staging[q]) ++n;
+    return n;
+}
+
 int gaamd_route_counts(unsigned long long counts[4]) {
     for (int k = 0; k < 4; ++k) counts[k] = g_route[k].load(std::memory_order_relaxed);
     return 0;

@@ -80,6 +80,9 @@ int gaamd_kernel_counts(unsigned long long counts[5]);
  * {packed chunks (pack -> staging -> owner unpack), direct-source (owner reads
  * our segment), io-vector, rmw} */
 int gaamd_route_counts(unsigned long long counts[4]);
+/* same-node peers whose staging buffer this rank could not map by IPC at
+ * comex_init (remote accumulates to or from them would abort); -1 before init */
+int gaamd_peers_unmapped(void);
 /* requests this rank's progress thread applied, by kind: packed, io-vector, rmw, direct-source */
 int gaamd_owner_counts(unsigned long long counts[4]);
 /* keys: "kind" (0 auto, 1 rows, 2 flat, 3 serial, 4 ordered), "unroll16" (1/2/4),
