@@ -592,11 +592,8 @@ Rocblas &rocblas() {
     return rb;
 }
 
-bool trans_flag(char t) {
-    if (t == 'n' || t == 'N') return false;
-    if (t == 't' || t == 'T') return true;
-    fatal("GA gemm: transpose flag '%c' (expected N or T)", t);
-}
+// matmul.c:1358-1368: 'n'/'N' is the matrix itself, any other flag its transpose
+bool trans_flag(char t) { return !(t == 'n' || t == 'N'); }
 
 // kind: 0 s, 1 d, 2 c, 3 z (rocBLAS order)
 void ga_gemm(int kind, int ctype, char ta, char tb, int m, int n, int k, const void *alpha, int g_a, int g_b,
@@ -635,9 +632,7 @@ void ga_gemm(int kind, int ctype, char ta, char tb, int m, int n, int k, const v
         GA_HIP(hipMalloc((void **)&pa, (size_t)R * kc_max * esz + 1));
         GA_HIP(hipMalloc((void **)&pb, (size_t)Cc * kc_max * esz + 1));
         GA_HIP(rb.set_stream(rb.handle, r.stream) == 0 ? hipSuccess : hipErrorUnknown);
-        const unsigned char one_s[16] = {0};
-        unsigned char one[16];
-        memcpy(one, one_s, sizeof(one));
+        unsigned char one[16] = {0};   // the type's 1 (beta of the chunks after the first)
         if (kind == 0) { const float v = 1.0f; memcpy(one, &v, 4); }
         else if (kind == 1) { const double v = 1.0; memcpy(one, &v, 8); }
         else if (kind == 2) { const float v[2] = {1.0f, 0.0f}; memcpy(one, v, 8); }
