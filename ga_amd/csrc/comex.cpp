@@ -2166,7 +2166,27 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
                 fprintf(stderr, "[ga_amd %d] segment %p (%zu B): allocation base %p size %zu\n", r.rank, p,
                         bytes, base, sz);
             }
-            if (r.size > 1) GA_HIP(hipIpcGetMemHandle(&mine.h, p));
+            if (r.size > 1) {
+                // an allocation the runtime could not export (seen once, on a block handed
+                // out again after a free of the same size): allocate another while holding
+                // it, then release it, a few times, before giving up
+                std::vector<void *> held;
+                hipError_t e = hipIpcGetMemHandle(&mine.h, p);
+                for (int tries = 0; e != hipSuccess && tries < 4; ++tries) {
+                    (void)hipGetLastError();
+                    void *base = nullptr;
+                    size_t sz = 0;
+                    (void)hipMemGetAddressRange((hipDeviceptr_t *)&base, &sz, (hipDeviceptr_t)p);
+                    fprintf(stderr, "[ga_amd %d] hipIpcGetMemHandle of a %zu-byte segment at %p (allocation %p, %zu B) "
+                            "failed (%s); allocating another\n", r.rank, bytes, p, base, sz, hipGetErrorString(e));
+                    held.push_back(p);
+                    GA_HIP(hipMalloc(&p, bytes));
+                    e = hipIpcGetMemHandle(&mine.h, p);
+                }
+                for (void *h : held) GA_HIP(hipFree(h));
+                if (e != hipSuccess) fatal("hipIpcGetMemHandle of a %zu-byte segment failed: %s", bytes,
+                                           hipGetErrorString(e));
+            }
         } else {
             GA_HIP(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
         }
