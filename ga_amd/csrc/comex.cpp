@@ -2251,20 +2251,33 @@ int comex_free(void *ptr, comex_group_t group) {
     members_allgather(members, group, &mine, gathered.data(), sizeof(mine));
     for (size_t k = 0; k < members.size(); ++k) all[members[k]] = gathered[k];
     members_barrier(members, group);   // nobody still reads the segment
-    std::lock_guard<std::mutex> g(r.seg_mu);
-    for (Segment &s : r.segs) {
-        if (!s.live) continue;
-        bool match = true;
-        for (int q = 0; q < r.size; ++q) if (s.peer[q].base != all[q]) { match = false; break; }
-        if (!match) continue;
-        for (int q = 0; q < r.size; ++q)
-            if (q != r.rank && s.peer[q].mapped) GA_HIP(hipIpcCloseMemHandle(s.peer[q].mapped));
-        if (s.local) GA_HIP(s.device ? hipFree(s.local) : hipHostFree(s.local));
-        s.live = false;
-        s.local = nullptr;
-        return COMEX_SUCCESS;
+    void *local = nullptr;
+    bool device = true, found = false;
+    {
+        std::lock_guard<std::mutex> g(r.seg_mu);
+        for (Segment &s : r.segs) {
+            if (!s.live) continue;
+            bool match = true;
+            for (int q = 0; q < r.size; ++q) if (s.peer[q].base != all[q]) { match = false; break; }
+            if (!match) continue;
+            for (int q = 0; q < r.size; ++q)
+                if (q != r.rank && s.peer[q].mapped) GA_HIP(hipIpcCloseMemHandle(s.peer[q].mapped));
+            local = s.local;
+            device = s.device;
+            s.live = false;
+            s.local = nullptr;
+            found = true;
+            break;
+        }
     }
-    fatal("comex_free(%p): not a comex_malloc segment", ptr);
+    if (!found) fatal("comex_free(%p): not a comex_malloc segment", ptr);
+    // every member has closed its mapping of every block before any block is freed:
+    // freeing a block a peer still maps leaves its export alive, and the runtime then
+    // refuses to export a new allocation it hands out at the same address
+    // (hipIpcGetMemHandle: invalid argument in the next comex_malloc)
+    members_barrier(members, group);
+    if (local) GA_HIP(device ? hipFree(local) : hipHostFree(local));
+    return COMEX_SUCCESS;
 }
 
 int comex_free_dev(void *ptr, comex_group_t group) { return comex_free(ptr, group); }
