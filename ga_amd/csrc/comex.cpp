@@ -1793,6 +1793,8 @@ static void exit_without_finalize() {
     wire_detach();
 }
 
+static void export_alloc(void **p, size_t bytes, hipIpcMemHandle_t *h, const char *what);
+
 int comex_init() {
     Runtime &r = rt();
     if (r.initialized) return COMEX_SUCCESS;
@@ -1859,7 +1861,7 @@ int comex_init() {
         GA_HIP(hipMalloc((void **)&r.staging, r.staging_bytes));
         struct { hipIpcMemHandle_t h; uint64_t bytes; } mine, *all;
         memset(&mine, 0, sizeof(mine));
-        GA_HIP(hipIpcGetMemHandle(&mine.h, r.staging));
+        export_alloc((void **)&r.staging, r.staging_bytes, &mine.h, "staging buffer");
         mine.bytes = r.staging_bytes;
         std::vector<char> buf(sizeof(mine) * (size_t)r.size);
         boot_allgather(&mine, buf.data(), sizeof(mine));
@@ -2145,6 +2147,27 @@ int comex_wait_proc(int proc, comex_group_t group) {
 }
 
 // ---- memory ----
+// IPC handle of a fresh hipMalloc block `*p`.  The runtime now and then refuses to
+// export a block (invalid argument) at an address an earlier, freed and exported
+// block had (seen in about 1 of 6 C5 runs, 64 MiB-1 GiB segments, base and size
+// exactly the allocation's): then allocate another while holding the refused one,
+// a few times, and release the refused ones.
+static void export_alloc(void **p, size_t bytes, hipIpcMemHandle_t *h, const char *what) {
+    Runtime &r = rt();
+    std::vector<void *> held;
+    hipError_t e = hipIpcGetMemHandle(h, *p);
+    for (int tries = 0; e != hipSuccess && tries < 4; ++tries) {
+        (void)hipGetLastError();
+        fprintf(stderr, "[ga_amd %d] hipIpcGetMemHandle of a %zu-byte %s at %p failed (%s); allocating another\n",
+                r.rank, bytes, what, *p, hipGetErrorString(e));
+        held.push_back(*p);
+        GA_HIP(hipMalloc(p, bytes));
+        e = hipIpcGetMemHandle(h, *p);
+    }
+    for (void *q : held) GA_HIP(hipFree(q));
+    if (e != hipSuccess) fatal("hipIpcGetMemHandle of a %zu-byte %s failed: %s", bytes, what, hipGetErrorString(e));
+}
+
 static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool device) {
     ensure_init();
     Runtime &r = rt();
@@ -2166,27 +2189,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
                 fprintf(stderr, "[ga_amd %d] segment %p (%zu B): allocation base %p size %zu\n", r.rank, p,
                         bytes, base, sz);
             }
-            if (r.size > 1) {
-                // an allocation the runtime could not export (seen once, on a block handed
-                // out again after a free of the same size): allocate another while holding
-                // it, then release it, a few times, before giving up
-                std::vector<void *> held;
-                hipError_t e = hipIpcGetMemHandle(&mine.h, p);
-                for (int tries = 0; e != hipSuccess && tries < 4; ++tries) {
-                    (void)hipGetLastError();
-                    void *base = nullptr;
-                    size_t sz = 0;
-                    (void)hipMemGetAddressRange((hipDeviceptr_t *)&base, &sz, (hipDeviceptr_t)p);
-                    fprintf(stderr, "[ga_amd %d] hipIpcGetMemHandle of a %zu-byte segment at %p (allocation %p, %zu B) "
-                            "failed (%s); allocating another\n", r.rank, bytes, p, base, sz, hipGetErrorString(e));
-                    held.push_back(p);
-                    GA_HIP(hipMalloc(&p, bytes));
-                    e = hipIpcGetMemHandle(&mine.h, p);
-                }
-                for (void *h : held) GA_HIP(hipFree(h));
-                if (e != hipSuccess) fatal("hipIpcGetMemHandle of a %zu-byte segment failed: %s", bytes,
-                                           hipGetErrorString(e));
-            }
+            if (r.size > 1) export_alloc(&p, bytes, &mine.h, "segment");
         } else {
             GA_HIP(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
         }
