@@ -254,3 +254,24 @@ def test_ga_gemm(n, panel):
     on the leading patches of larger GAs, all four transpose pairs, vs numpy; with
     4 KiB panels every k chunk is a separate get + gemm."""
     launch("gemm", n=n, timeout=150, extra_env={"COMEX_AMD_GEMM_PANEL_BYTES": panel} if panel else None)
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_exchange_exact():
+    """The driver's N > 1 invocation shape (bench.py --gpus 2 spawning its own ranks)
+    ends with the C5 exchange check: every element of a 4096^2 GA accumulated by
+    both ranks from constant sources must be exact on the packed and the
+    direct-source route, and rank 0 prints one JSON line."""
+    import json
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+                        "--warmup-ms", "0", "--no-cpu", "--ga-dims", "8192", "--c5-steps", "2"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2
+    chk = line["c5"]["exchange_check"]
+    assert chk["packed"]["result"] == "exact" and chk["direct_src"]["result"] == "exact", chk
