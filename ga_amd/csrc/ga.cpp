@@ -654,11 +654,15 @@ void ga_gemm(int kind, int ctype, char ta, char tb, int m, int n, int k, const v
             const int opx = bt ? kRbTrans : kRbNone, ldx = bt ? std::max(kc, 1) : Cc;
             const int opy = at ? kRbTrans : kRbNone, ldy = at ? R : std::max(kc, 1);
             const void *bk = (k0 == 0) ? beta : one;
-            std::lock_guard<std::mutex> g(r.launch_mu);
-            sched_join();   // after the gets' kernels on every library stream
-            if (rb.gemm[kind](rb.handle, opx, opy, Cc, R, kc, alpha, pb, ldx, pa, ldy, bk, cblk, ldc) != 0)
-                fatal("GA gemm: rocBLAS gemm failed");
-            GA_HIP(hipStreamSynchronize(r.stream));   // the panels are reused by the next chunk
+            {
+                std::lock_guard<std::mutex> g(r.launch_mu);
+                sched_join();   // after the gets' kernels on every library stream
+                if (rb.gemm[kind](rb.handle, opx, opy, Cc, R, kc, alpha, pb, ldx, pa, ldy, bk, cblk, ldc) != 0)
+                    fatal("GA gemm: rocBLAS gemm failed");
+            }
+            // the panels are reused by the next chunk (the launch lock is not held here:
+            // the progress thread keeps serving other ranks' requests meanwhile)
+            GA_HIP(hipStreamSynchronize(r.stream));
             if (!k) break;
         }
         GA_HIP(hipFree(pa));
