@@ -596,31 +596,50 @@ Rocblas &rocblas() {
 bool trans_flag(char t) { return !(t == 'n' || t == 'N'); }
 
 // kind: 0 s, 1 d, 2 c, 3 z (rocBLAS order)
-void ga_gemm(int kind, int ctype, char ta, char tb, int m, int n, int k, const void *alpha, int g_a, int g_b,
-             const void *beta, int g_c) {
+// C[clo..chi] = alpha*op(A[alo..ahi])*op(B[blo..bhi]) + beta*C[clo..chi], C-order
+// 0-based inclusive patches (NGA_Matmul_patch; GA_?gemm = the leading patches)
+void ga_matmul(char ta, char tb, const void *alpha, const void *beta, int g_a, const int alo[2], const int ahi[2],
+               int g_b, const int blo[2], const int bhi[2], int g_c, const int clo[2], const int chi[2]) {
     const bool at = trans_flag(ta), bt = trans_flag(tb);
     GArray &A = arr(g_a), &B = arr(g_b), &C = arr(g_c);
-    if (A.type != ctype || B.type != ctype || C.type != ctype) fatal("GA gemm: types mismatch");   // matmul.c:1354
-    if (A.ndim != 2 || B.ndim != 2 || C.ndim != 2) fatal("GA gemm: arrays must be 2-D");
-    if (g_c == g_a || g_c == g_b) fatal("GA gemm: C must differ from A and B");
-    if (m < 0 || n < 0 || k < 0) fatal("GA gemm: negative dimension");
-    // C-order extents (Fortran dims reversed) and the patch checks of matmul.c:1358-1377
-    auto rows = [](const GArray &x) { return x.dims[1]; };
-    auto cols = [](const GArray &x) { return x.dims[0]; };
-    if ((at ? cols(A) : rows(A)) < m || (at ? rows(A) : cols(A)) < k) fatal("GA gemm: g_a indices out of range");
-    if ((bt ? cols(B) : rows(B)) < k || (bt ? rows(B) : cols(B)) < n) fatal("GA gemm: g_b indices out of range");
-    if (rows(C) < m || cols(C) < n) fatal("GA gemm: g_c indices out of range");
+    if (A.type != C.type || B.type != C.type) fatal("GA matmul: types mismatch");   // matmul.c:1354
+    int kind;
+    switch (C.type) {   // matmul.c:1355: float, double, single and double complex only
+    case C_FLOAT: kind = 0; break;
+    case C_DBL: kind = 1; break;
+    case C_SCPL: kind = 2; break;
+    case C_DCPL: kind = 3; break;
+    default: fatal("GA matmul: type error %d", C.type);
+    }
+    if (A.ndim != 2 || B.ndim != 2 || C.ndim != 2) fatal("GA matmul: arrays must be 2-D");
+    if (g_c == g_a || g_c == g_b) fatal("GA matmul: C must differ from A and B");
+    // C-order extents (Fortran dims reversed); the patch checks of matmul.c:1358-1384
+    auto inside = [](const GArray &x, const int lo[2], const int hi[2]) {
+        return lo[0] >= 0 && lo[1] >= 0 && hi[0] < x.dims[1] && hi[1] < x.dims[0] && lo[0] <= hi[0] + 1 &&
+               lo[1] <= hi[1] + 1;
+    };
+    if (!inside(A, alo, ahi)) fatal("GA matmul: g_a indices out of range");
+    if (!inside(B, blo, bhi)) fatal("GA matmul: g_b indices out of range");
+    if (!inside(C, clo, chi)) fatal("GA matmul: g_c indices out of range");
+    const int m = chi[0] - clo[0] + 1, n = chi[1] - clo[1] + 1;
+    const int ar = ahi[0] - alo[0] + 1, ac = ahi[1] - alo[1] + 1, br = bhi[0] - blo[0] + 1, bc = bhi[1] - blo[1] + 1;
+    const int k = at ? ar : ac;
+    if ((at ? ac : ar) != m) fatal("GA matmul: a & c dims error");
+    if ((bt ? br : bc) != n) fatal("GA matmul: b & c dims error");
+    if ((bt ? bc : br) != k) fatal("GA matmul: a & b dims error");
     Runtime &r = rt();
     const int esz = C.elemsize;
     comex_barrier(COMEX_GROUP_WORLD);   // pnga_matmul starts with a sync: A and B are complete
-    int blo[2], bhi[2];
-    NGA_Distribution(g_c, r.rank, blo, bhi);
-    const int r0 = blo[0], r1 = std::min(bhi[0], m - 1), c0 = blo[1], c1 = std::min(bhi[1], n - 1);
-    if (r0 <= r1 && c0 <= c1 && bhi[0] >= blo[0]) {
+    int blk_lo[2], blk_hi[2];
+    NGA_Distribution(g_c, r.rank, blk_lo, blk_hi);
+    // the part of the C patch this rank owns, in C indices and patch-relative (i, j)
+    const int r0 = std::max(blk_lo[0], clo[0]), r1 = std::min(blk_hi[0], chi[0]);
+    const int c0 = std::max(blk_lo[1], clo[1]), c1 = std::min(blk_hi[1], chi[1]);
+    if (m > 0 && n > 0 && r0 <= r1 && c0 <= c1) {
         Rocblas &rb = rocblas();
-        const int R = r1 - r0 + 1, Cc = c1 - c0 + 1;
-        const int ldc = bhi[1] - blo[1] + 1;
-        char *cblk = (char *)C.ptr[r.rank] + ((size_t)(r0 - blo[0]) * ldc + (size_t)(c0 - blo[1])) * esz;
+        const int R = r1 - r0 + 1, Cc = c1 - c0 + 1, i0 = r0 - clo[0], j0 = c0 - clo[1];
+        const int ldc = blk_hi[1] - blk_lo[1] + 1;
+        char *cblk = (char *)C.ptr[r.rank] + ((size_t)(r0 - blk_lo[0]) * ldc + (size_t)(c0 - blk_lo[1])) * esz;
         // k chunks: each panel at most 256 MiB (an owner's op(A) row panel is R x kc)
         static const size_t panel = [] {   // COMEX_AMD_GEMM_PANEL_BYTES: smaller panels (tests: many chunks)
             const char *e = getenv("COMEX_AMD_GEMM_PANEL_BYTES");
@@ -641,13 +660,19 @@ void ga_gemm(int kind, int ctype, char ta, char tb, int m, int n, int k, const v
             const int kc = k ? std::min(kc_max, k - k0) : 0;
             if (kc) {
                 int lo[2], hi[2], ld[1];
-                // op(A)[r0..r1][k0..k0+kc): A rows r0..r1, cols k0.. ('N') or A rows k0.., cols r0..r1 ('T')
-                if (!at) { lo[0] = r0; hi[0] = r1; lo[1] = k0; hi[1] = k0 + kc - 1; ld[0] = kc; }
-                else { lo[0] = k0; hi[0] = k0 + kc - 1; lo[1] = r0; hi[1] = r1; ld[0] = R; }
+                // op(A)[i0..][k0..k0+kc): A rows i.., cols k.. ('N') or A rows k.., cols i.. ('T')
+                if (!at) {
+                    lo[0] = alo[0] + i0; hi[0] = lo[0] + R - 1; lo[1] = alo[1] + k0; hi[1] = lo[1] + kc - 1; ld[0] = kc;
+                } else {
+                    lo[0] = alo[0] + k0; hi[0] = lo[0] + kc - 1; lo[1] = alo[1] + i0; hi[1] = lo[1] + R - 1; ld[0] = R;
+                }
                 NGA_Get(g_a, lo, hi, pa, ld);
-                // op(B)[k0..][c0..c1]: B rows k0.., cols c0..c1 ('N') or B rows c0..c1, cols k0.. ('T')
-                if (!bt) { lo[0] = k0; hi[0] = k0 + kc - 1; lo[1] = c0; hi[1] = c1; ld[0] = Cc; }
-                else { lo[0] = c0; hi[0] = c1; lo[1] = k0; hi[1] = k0 + kc - 1; ld[0] = kc; }
+                // op(B)[k0..][j0..]: B rows k.., cols j.. ('N') or B rows j.., cols k.. ('T')
+                if (!bt) {
+                    lo[0] = blo[0] + k0; hi[0] = lo[0] + kc - 1; lo[1] = blo[1] + j0; hi[1] = lo[1] + Cc - 1; ld[0] = Cc;
+                } else {
+                    lo[0] = blo[0] + j0; hi[0] = lo[0] + Cc - 1; lo[1] = blo[1] + k0; hi[1] = lo[1] + kc - 1; ld[0] = kc;
+                }
                 NGA_Get(g_b, lo, hi, pb, ld);
             }
             // column-major: C^T (Cc x R, ldc) = X (Cc x kc) * Y (kc x R)
@@ -658,7 +683,7 @@ void ga_gemm(int kind, int ctype, char ta, char tb, int m, int n, int k, const v
                 std::lock_guard<std::mutex> g(r.launch_mu);
                 sched_join();   // after the gets' kernels on every library stream
                 if (rb.gemm[kind](rb.handle, opx, opy, Cc, R, kc, alpha, pb, ldx, pa, ldy, bk, cblk, ldc) != 0)
-                    fatal("GA gemm: rocBLAS gemm failed");
+                    fatal("GA matmul: rocBLAS gemm failed");
             }
             // the panels are reused by the next chunk (the launch lock is not held here:
             // the progress thread keeps serving other ranks' requests meanwhile)
@@ -669,6 +694,18 @@ void ga_gemm(int kind, int ctype, char ta, char tb, int m, int n, int k, const v
         GA_HIP(hipFree(pb));
     }
     comex_barrier(COMEX_GROUP_WORLD);   // ... and ends with one: C is complete everywhere
+}
+
+// GA_?gemm: the leading m x n / m x k (k x m) / k x n (n x k) patches
+void ga_gemm(int ctype, char ta, char tb, int m, int n, int k, const void *alpha, int g_a, int g_b,
+             const void *beta, int g_c) {
+    if (m < 0 || n < 0 || k < 0) fatal("GA gemm: negative dimension");
+    if (arr(g_c).type != ctype) fatal("GA gemm: types mismatch");
+    const bool at = trans_flag(ta), bt = trans_flag(tb);
+    const int alo[2] = {0, 0}, ahi[2] = {(at ? k : m) - 1, (at ? m : k) - 1};
+    const int blo[2] = {0, 0}, bhi[2] = {(bt ? n : k) - 1, (bt ? k : n) - 1};
+    const int clo[2] = {0, 0}, chi[2] = {m - 1, n - 1};
+    ga_matmul(ta, tb, alpha, beta, g_a, alo, ahi, g_b, blo, bhi, g_c, clo, chi);
 }
 }  // namespace
 
@@ -929,18 +966,24 @@ void NGA_Gather_flat(int g_a, void *v, int subsArray[], int n) {
 // column-major BLAS sees as C^T = op(B)^T op(A)^T.
 
 void GA_Sgemm(char ta, char tb, int m, int n, int k, float alpha, int g_a, int g_b, float beta, int g_c) {
-    ga_gemm(0, C_FLOAT, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
+    ga_gemm(C_FLOAT, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
 }
 void GA_Dgemm(char ta, char tb, int m, int n, int k, double alpha, int g_a, int g_b, double beta, int g_c) {
-    ga_gemm(1, C_DBL, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
+    ga_gemm(C_DBL, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
 }
 void GA_Cgemm(char ta, char tb, int m, int n, int k, SingleComplex alpha, int g_a, int g_b, SingleComplex beta,
               int g_c) {
-    ga_gemm(2, C_SCPL, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
+    ga_gemm(C_SCPL, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
 }
 void GA_Zgemm(char ta, char tb, int m, int n, int k, DoubleComplex alpha, int g_a, int g_b, DoubleComplex beta,
               int g_c) {
-    ga_gemm(3, C_DCPL, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
+    ga_gemm(C_DCPL, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
+}
+
+// capi.c:3690-3722: C-order patches (the reference swaps to (b, a) for its Fortran core)
+void NGA_Matmul_patch(char transa, char transb, void *alpha, void *beta, int g_a, int alo[], int ahi[], int g_b,
+                      int blo[], int bhi[], int g_c, int clo[], int chi[]) {
+    ga_matmul(transa, transb, alpha, beta, g_a, alo, ahi, g_b, blo, bhi, g_c, clo, chi);
 }
 
 void GA_Get_proc_grid(int g_a, int dims[]) {

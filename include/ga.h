@@ -96,6 +96,10 @@ void GA_Zgemm(char ta, char tb, int m, int n, int k, DoubleComplex alpha, int g_
               int g_c);
 void GA_Cgemm(char ta, char tb, int m, int n, int k, SingleComplex alpha, int g_a, int g_b, SingleComplex beta,
               int g_c);
+/* the same on arbitrary C-order patches, alpha/beta of the arrays' type
+ * (capi.c:3690 NGA_Matmul_patch -> pnga_matmul_patch) */
+void NGA_Matmul_patch(char transa, char transb, void *alpha, void *beta, int g_a, int alo[], int ahi[], int g_b,
+                      int blo[], int bhi[], int g_c, int clo[], int chi[]);
 
 #if defined(__cplusplus)
 }

@@ -1864,6 +1864,56 @@ def ga_gemm_test(L, rank, size):
                     (dt.__name__, ta, tb, "outside the patch changed")
                 for h in g:
                     L.GA_Destroy(h)
+    # NGA_Matmul_patch (capi.c:3690): patches at offsets inside larger arrays
+    m, n, k = 45, 38, 57
+    for ctype, dt, tol in ((C_DBL, np.float64, 1e-12), (C_DCPL, np.complex128, 1e-12), (C_FLOAT, np.float32, 1e-4)):
+        for ta in "NT":
+            for tb in "NT":
+                ao = (int(rng.integers(0, 7)), int(rng.integers(0, 7)))
+                bo = (int(rng.integers(0, 7)), int(rng.integers(0, 7)))
+                co = (int(rng.integers(0, 9)), int(rng.integers(0, 9)))
+                ash = (m, k) if ta == "N" else (k, m)
+                bsh = (k, n) if tb == "N" else (n, k)
+                adims = [ao[0] + ash[0] + 3, ao[1] + ash[1] + 2]
+                bdims = [bo[0] + bsh[0] + 1, bo[1] + bsh[1] + 4]
+                cdims = [co[0] + m + 5, co[1] + n + 2]
+                def rand(shape):
+                    x = rng.integers(-8, 9, shape).astype(np.float64)
+                    if np.iscomplexobj(np.zeros(1, dt)):
+                        x = x + 1j * rng.integers(-8, 9, shape)
+                    return x.astype(dt)
+                A, B, C0 = rand(adims), rand(bdims), rand(cdims)
+                g = [L.NGA_Create(ctype, 2, ia(d), b"mp", None) for d in (adims, bdims, cdims)]
+                if rank == 0:
+                    for h, X in zip(g, (A, B, C0)):
+                        L.NGA_Put(h, ia([0, 0]), ia([X.shape[0] - 1, X.shape[1] - 1]),
+                                  X.ctypes.data_as(ctypes.c_void_p), ia([X.shape[1]]))
+                L.GA_Sync()
+                av, bv = (0.75 - 0.5j, 1.5 + 0.25j) if np.iscomplexobj(np.zeros(1, dt)) else (0.75, 1.5)
+                sa, sb = np.array([av], dtype=dt), np.array([bv], dtype=dt)
+                L.NGA_Matmul_patch(ta.encode(), tb.encode(), sa.ctypes.data_as(ctypes.c_void_p),
+                                   sb.ctypes.data_as(ctypes.c_void_p),
+                                   g[0], ia([ao[0], ao[1]]), ia([ao[0] + ash[0] - 1, ao[1] + ash[1] - 1]),
+                                   g[1], ia([bo[0], bo[1]]), ia([bo[0] + bsh[0] - 1, bo[1] + bsh[1] - 1]),
+                                   g[2], ia([co[0], co[1]]), ia([co[0] + m - 1, co[1] + n - 1]))
+                out = np.zeros(cdims, dt)
+                L.NGA_Get(g[2], ia([0, 0]), ia([cdims[0] - 1, cdims[1] - 1]),
+                          out.ctypes.data_as(ctypes.c_void_p), ia([cdims[1]]))
+                Ap = A[ao[0]:ao[0] + ash[0], ao[1]:ao[1] + ash[1]].astype(np.complex128)
+                Bp = B[bo[0]:bo[0] + bsh[0], bo[1]:bo[1] + bsh[1]].astype(np.complex128)
+                opA = Ap if ta == "N" else Ap.T
+                opB = Bp if tb == "N" else Bp.T
+                want = C0.astype(np.complex128).copy()
+                sl = (slice(co[0], co[0] + m), slice(co[1], co[1] + n))
+                want[sl] = complex(sa[0]) * (opA @ opB) + complex(sb[0]) * C0[sl]
+                scale = k * np.abs(A).max() * np.abs(B).max() + abs(bv) * np.abs(C0).max()
+                err = np.abs(out.astype(np.complex128) - want)
+                assert err[sl].max() <= tol * scale, ("patch", dt.__name__, ta, tb, err.max(), scale)
+                mask = np.ones(cdims, bool)
+                mask[sl] = False
+                assert np.array_equal(out[mask], C0[mask]), ("patch", dt.__name__, ta, tb, "outside changed")
+                for h in g:
+                    L.GA_Destroy(h)
     say(rank, "ga gemm ok")
     L.GA_Terminate()
 
