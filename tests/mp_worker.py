@@ -1914,6 +1914,48 @@ def ga_gemm_test(L, rank, size):
                 assert np.array_equal(out[mask], C0[mask]), ("patch", dt.__name__, ta, tb, "outside changed")
                 for h in g:
                     L.GA_Destroy(h)
+    # global/testing/gemmtest.c restated (REGULAR distribution, N = 8): A[i][j] = i*N+j and
+    # B[i][j] = j*N+i (imaginary part 1), NGA_Matmul_patch('N','N', 1, 0) over the whole
+    # arrays and then over the central N/2 x N/2 patch of zeroed arrays.  The reference's
+    # own element check is compiled out (#if 0); integer-valued data makes it exact here.
+    NN = 8
+    for ctype, dt in ((C_FLOAT, np.float32), (C_DBL, np.float64), (C_DCPL, np.complex128), (C_SCPL, np.complex64)):
+        cplx = np.iscomplexobj(np.zeros(1, dt))
+        ii, jj = np.meshgrid(np.arange(NN), np.arange(NN), indexing="ij")
+        A = (ii * NN + jj).astype(dt) + (1j if cplx else 0)
+        B = (jj * NN + ii).astype(dt) + (1j if cplx else 0)
+        A, B = A.astype(dt), B.astype(dt)
+        g = [L.NGA_Create(ctype, 2, ia([NN, NN]), b"gt", None) for _ in range(3)]
+        one, zero = np.array([1], dtype=dt), np.array([0], dtype=dt)
+        full_lo, full_hi = ia([0, 0]), ia([NN - 1, NN - 1])
+        if rank == 0:
+            L.NGA_Put(g[0], full_lo, full_hi, A.ctypes.data_as(ctypes.c_void_p), ia([NN]))
+            L.NGA_Put(g[1], full_lo, full_hi, B.ctypes.data_as(ctypes.c_void_p), ia([NN]))
+        L.GA_Sync()
+        L.NGA_Matmul_patch(b"N", b"N", one.ctypes.data_as(ctypes.c_void_p), zero.ctypes.data_as(ctypes.c_void_p),
+                           g[0], full_lo, full_hi, g[1], full_lo, full_hi, g[2], full_lo, full_hi)
+        out = np.zeros((NN, NN), dt)
+        L.NGA_Get(g[2], full_lo, full_hi, out.ctypes.data_as(ctypes.c_void_p), ia([NN]))
+        want = (A.astype(np.complex128) @ B.astype(np.complex128))
+        assert np.array_equal(out.astype(np.complex128), want), ("gemmtest full", dt.__name__)
+        for h in g:
+            L.GA_Zero(h)
+        lo, hi, h2 = [NN // 4, NN // 4], [3 * NN // 4 - 1, 3 * NN // 4 - 1], NN // 2
+        Ap = np.ascontiguousarray(A[NN // 4:3 * NN // 4, NN // 4:3 * NN // 4])
+        Bp = np.ascontiguousarray(B[NN // 4:3 * NN // 4, NN // 4:3 * NN // 4])
+        if rank == 0:
+            L.NGA_Put(g[0], ia(lo), ia(hi), Ap.ctypes.data_as(ctypes.c_void_p), ia([h2]))
+            L.NGA_Put(g[1], ia(lo), ia(hi), Bp.ctypes.data_as(ctypes.c_void_p), ia([h2]))
+        L.GA_Sync()
+        L.NGA_Matmul_patch(b"N", b"N", one.ctypes.data_as(ctypes.c_void_p), zero.ctypes.data_as(ctypes.c_void_p),
+                           g[0], ia(lo), ia(hi), g[1], ia(lo), ia(hi), g[2], ia(lo), ia(hi))
+        out = np.zeros((NN, NN), dt)
+        L.NGA_Get(g[2], full_lo, full_hi, out.ctypes.data_as(ctypes.c_void_p), ia([NN]))
+        want = np.zeros((NN, NN), np.complex128)
+        want[NN // 4:3 * NN // 4, NN // 4:3 * NN // 4] = Ap.astype(np.complex128) @ Bp.astype(np.complex128)
+        assert np.array_equal(out.astype(np.complex128), want), ("gemmtest patch", dt.__name__)
+        for h in g:
+            L.GA_Destroy(h)
     say(rank, "ga gemm ok")
     L.GA_Terminate()
 
