@@ -993,7 +993,8 @@ ST_ZONE = 4 * 1024          # f64 elements of one rank's put zone in every segme
 
 
 def stress_program(s, size, n_ops):
-    rng = np.random.default_rng(1000 + s)
+    # STRESS_SEED (campaigns): another family of programs
+    rng = np.random.default_rng(1000 + s + 7919 * int(os.environ.get("STRESS_SEED", "0")))
     ops = []
     for _ in range(n_ops):
         u = rng.random()
