@@ -711,7 +711,8 @@ struct RJob {
     int ss[8] = {}, ds[8] = {}, count[8] = {}, pstride[8] = {};
     char *dst = nullptr;
     int64_t slo = 0, shi = 0;
-    uint64_t rows = 0, per_req = 0, next_rb = 0;
+    uint64_t rows = 0, per_req = 0;
+    uint64_t nchunks = 0, next_i = 0, first = 0;   // chunk c = (first + i) % nchunks, i = 0, 1, ...
     int outstanding = 0;
 };
 static std::deque<RJob> g_jobs;                 // unfinished jobs, creation order
@@ -768,8 +769,9 @@ static bool progress_jobs() {
     }
     // pack new chunks where the target's ring has room
     for (RJob &j : g_jobs) {
-        while (j.next_rb < j.rows) {
-            const uint64_t rb = j.next_rb, re = std::min(j.rows, rb + j.per_req);
+        while (j.next_i < j.nchunks) {
+            const uint64_t c = (j.first + j.next_i) % j.nchunks;
+            const uint64_t rb = c * j.per_req, re = std::min(j.rows, rb + j.per_req);
             const uint64_t len = (re - rb) * (uint64_t)j.count[0];
             uint64_t off = 0;
             if (!try_stage_alloc(j.t, ring_len(len), off)) break;
@@ -793,13 +795,13 @@ static bool progress_jobs() {
             }
             g_out[j.t].push_back({j.id, off, len, rb, re, ev});
             ++j.outstanding;
-            j.next_rb = re;
+            ++j.next_i;
             any = true;
         }
     }
     // retire jobs whose every chunk is posted (the source is reusable)
     for (auto it = g_jobs.begin(); it != g_jobs.end();) {
-        if (it->next_rb >= it->rows && it->outstanding == 0) {
+        if (it->next_i >= it->nchunks && it->outstanding == 0) {
             release_view(it->sv);
             it = g_jobs.erase(it);
             any = true;
@@ -835,6 +837,24 @@ static void drain_all_jobs() {
 }
 
 // start a remote accumulate; returns its job id (0: nothing to do)
+// Are the rows of one side pairwise byte-disjoint?  Sufficient test: with the
+// levels sorted by |stride|, each stride covers the whole extent below it.
+static bool dst_rows_disjoint(const int *str, const int *count, int levels, int64_t row_bytes) {
+    int64_t s[8];
+    int64_t c[8];
+    int n = 0;
+    for (int j = 0; j < levels; ++j)
+        if (count[j + 1] > 1) { s[n] = str[j] < 0 ? -(int64_t)str[j] : (int64_t)str[j]; c[n] = count[j + 1]; ++n; }
+    for (int i = 1; i < n; ++i)
+        for (int k = i; k > 0 && s[k] < s[k - 1]; --k) { std::swap(s[k], s[k - 1]); std::swap(c[k], c[k - 1]); }
+    int64_t extent = row_bytes;
+    for (int i = 0; i < n; ++i) {
+        if (s[i] < extent) return false;
+        extent = s[i] * (c[i] - 1) + extent;
+    }
+    return true;
+}
+
 static int remote_acc_start(int t, int op, const void *scale, void *src, const int *ss, void *dst, const int *ds,
                             const int *count, int levels) {
     Runtime &r = rt();
@@ -883,6 +903,14 @@ static int remote_acc_start(int t, int op, const void *scale, void *src, const i
     j.rows = rows;
     int64_t acc = row_bytes;
     for (int k = 0; k < levels; ++k) { j.pstride[k] = (int)acc; acc *= count[k + 1]; }
+    j.nchunks = (rows + j.per_req - 1) / j.per_req;
+    // Chunks of one accumulate go out in row order, except that a requester starts at
+    // chunk rank * nchunks / size when the patch's destination rows are pairwise
+    // disjoint (then their order is free): when every rank accumulates the same rows of
+    // an owner (a GA reduction, C5 M2), their chunks in flight then cover different
+    // rows, which the owner can apply side by side instead of one after another.
+    if (j.nchunks > 1 && t != r.rank && dst_rows_disjoint(ds, count, levels, row_bytes))
+        j.first = (uint64_t)r.rank * j.nchunks / (uint64_t)r.size;
     if (g_out.size() != (size_t)r.size) g_out.resize(r.size);
     static const bool async_ok = [] {
         const char *e = getenv("COMEX_AMD_ASYNC_ACC");   // 0: every remote accumulate completes in its call
