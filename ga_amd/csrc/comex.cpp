@@ -1227,6 +1227,14 @@ struct ViewCache {
         }
         return true;
     }
+    // the allocation holding address a: its range [lo, hi) and device-view offset
+    bool range_of(uint64_t a, uint64_t *lo, uint64_t *hi, int64_t *delta) {
+        uint64_t d = 0;
+        if (!view((void *)(uintptr_t)a, 1, &d)) return false;
+        for (const Range &x : r)
+            if (a >= x.lo && a < x.hi) { *lo = x.lo; *hi = x.hi; *delta = x.delta; return true; }
+        return false;
+    }
     // one allocation holding every byte of [lo, hi): its (uniform) device-view offset
     bool span(uint64_t lo, uint64_t hi, int64_t *delta) {
         uint64_t d = 0;
@@ -1330,9 +1338,13 @@ constexpr int kIovMapsMin = 65536;
 // results go packed to `host_dst` (getv into pageable memory: the caller
 // scatters them).  Reference: nb_accv / nb_putv / nb_getv to a self/SMP target,
 // comex.c:7327-7400 (one _acc / memcpy per pair, in order).
-static void iov_local(int cop, const void *scale, const uint64_t *src, const uint64_t *dst, int bytes, int n,
+// `bounds` (the fast path of xfer_vec): {src lo, src hi, dst lo, dst hi} of the
+// allocations the first pair's addresses lie in, with sdelta / ddelta their device-view
+// offsets; when some listed address falls outside them the call returns false before
+// anything is uploaded or launched (the caller classifies per address instead).
+static bool iov_local(int cop, const void *scale, const uint64_t *src, const uint64_t *dst, int bytes, int n,
                       const char *host_src = nullptr, char *host_dst = nullptr, int64_t sdelta = 0,
-                      int64_t ddelta = 0, void *const *gather_src = nullptr) {
+                      int64_t ddelta = 0, void *const *gather_src = nullptr, const uint64_t *bounds = nullptr) {
     Runtime &r = rt();
     const bool src_listed = src != nullptr, dst_listed = dst != nullptr;
     // device scratch: [dst list | src list or packed sources | packed results | run-sort work],
@@ -1344,33 +1356,40 @@ static void iov_local(int cop, const void *scale, const uint64_t *src, const uin
     std::unique_lock<std::mutex> g(r.launch_mu);
     sched_sync_all();   // the previous io-vector kernel and its upload are done with both scratches
     char *up = iov_host_scratch(o_res);
-    uint64_t align_or = 0, slo = ~0ull, shi = 0, dlo = ~0ull, dhi = 0;
-    // translate a list into the staging, taking its OR / min / max (per range, then combined)
-    auto translate = [&](const uint64_t *in, int64_t delta, uint64_t *u, uint64_t *lo_out, uint64_t *hi_out) {
+    uint64_t align_or = 0, slo = ~0ull, shi = 0, dlo = ~0ull, dhi = 0, dxor = 0;
+    // translate a list into the staging, taking its OR / min / max and the OR of every
+    // address XOR the first one (per range, then combined)
+    auto translate = [&](const uint64_t *in, int64_t delta, uint64_t *u, uint64_t *lo_out, uint64_t *hi_out,
+                         uint64_t *xor_out) {
         const int T = par_threads(n);
-        uint64_t o[8] = {0}, lo[8], hi[8] = {0};
+        uint64_t o[8] = {0}, lo[8], hi[8] = {0}, xo[8] = {0};
         for (int t = 0; t < 8; ++t) lo[t] = ~0ull;
+        const uint64_t a0 = in[0] + (uint64_t)delta;
         par_for(n, T, [&](int t, long i0, long i1) {
-            uint64_t ot = 0, lt = ~0ull, ht = 0;
+            uint64_t ot = 0, lt = ~0ull, ht = 0, xt = 0;
             for (long i = i0; i < i1; ++i) {
                 const uint64_t a = in[i] + (uint64_t)delta;
                 u[i] = a;
                 ot |= a;
+                xt |= a ^ a0;
                 lt = a < lt ? a : lt;
                 ht = a > ht ? a : ht;
             }
             o[t] = ot;
+            xo[t] = xt;
             lo[t] = lt;
             hi[t] = ht;
         });
         for (int t = 0; t < T; ++t) {
             align_or |= o[t];
+            *xor_out |= xo[t];
             *lo_out = std::min(*lo_out, lo[t]);
             *hi_out = std::max(*hi_out, hi[t]);
         }
     };
+    uint64_t sxor = 0;
     if (src_listed) {
-        translate(src, sdelta, (uint64_t *)(up + o_src), &slo, &shi);
+        translate(src, sdelta, (uint64_t *)(up + o_src), &slo, &shi, &sxor);
         shi += (uint64_t)bytes;
     } else if (gather_src) {
         // pageable sources gathered straight into the pinned staging, in pair order, on
@@ -1381,9 +1400,13 @@ static void iov_local(int cop, const void *scale, const uint64_t *src, const uin
         memcpy(up + o_src, host_src, (size_t)n * (size_t)bytes);
     }
     if (dst_listed) {
-        translate(dst, ddelta, (uint64_t *)(up + o_dst), &dlo, &dhi);
+        translate(dst, ddelta, (uint64_t *)(up + o_dst), &dlo, &dhi, &dxor);
         dhi += (uint64_t)bytes;
     }
+    if (bounds && src_listed && dst_listed &&
+        (slo - (uint64_t)sdelta < bounds[0] || shi - (uint64_t)sdelta > bounds[1] ||
+         dlo - (uint64_t)ddelta < bounds[2] || dhi - (uint64_t)ddelta > bounds[3]))
+        return false;   // an address outside the first pair's allocations: nothing enqueued yet
     // from here on the lists are the translated (device-view) copies in the staging
     if (src_listed) src = (const uint64_t *)(up + o_src);
     if (dst_listed) dst = (const uint64_t *)(up + o_dst);
@@ -1402,9 +1425,8 @@ static void iov_local(int cop, const void *scale, const uint64_t *src, const uin
         // every destination a whole number of pairs from dlo (no partial overlaps)
         bool congruent = true;
         if ((bytes & (bytes - 1)) == 0) {
-            uint64_t x = 0;
-            for (int i = 0; i < n; ++i) x |= dst[i] - dlo;
-            congruent = (x & (uint64_t)(bytes - 1)) == 0;
+            // all dst[i] == dst[0] (mod bytes), dlo being one of them: from the translate pass
+            congruent = (dxor & (uint64_t)(bytes - 1)) == 0;
         } else {
             const FastDiv fd = make_fastdiv((uint32_t)bytes);   // no 64-bit divide per pair
             for (int i = 0; i < n && congruent; ++i) {
@@ -1451,6 +1473,7 @@ static void iov_local(int cop, const void *scale, const uint64_t *src, const uin
         GA_HIP(hipMemcpy(host_dst, dev + o_res, (size_t)n * (size_t)bytes, hipMemcpyDeviceToHost));
     }
     // completion (blocking call) or the handle (non-blocking) is taken by xfer_vec
+    return true;
 }
 
 static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int proc, int group,
@@ -1509,6 +1532,15 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             // (GA's `v` buffer and array block): one range lookup per side, the lists go to
             // the staging translated in the same pass that takes their spans
             const uint64_t *rs = (const uint64_t *)darr[k].src, *rd = (const uint64_t *)darr[k].dst;
+            {
+                // the allocations of the first pair, checked against every address in the
+                // translate pass (no separate min/max pass over both lists)
+                uint64_t b[4];
+                int64_t sd0 = 0, dd0 = 0;
+                if (vc.range_of(rs[0], &b[0], &b[1], &sd0) && vc.range_of(rd[0], &b[2], &b[3], &dd0) &&
+                    iov_local(cop, scale, rs, rd, bytes, n, nullptr, nullptr, sd0, dd0, nullptr, b))
+                    continue;
+            }
             uint64_t smin = ~0ull, smax = 0, dmin = ~0ull, dmax = 0;
             {
                 const int T = par_threads(n);

@@ -470,6 +470,43 @@ def test_accv_local(gpu_lib, oracle, op, nbytes, dups):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("split", ["src", "dst", "both"])
+def test_accv_sides_in_two_allocations(gpu_lib, oracle, split):
+    """A descriptor of >= 1024 pairs whose sources (or destinations) lie in two
+    separate HBM allocations: the one-allocation fast path (bounds of the first
+    pair's allocations checked in the translate pass) must step aside for the
+    per-address classification; same bits as the reference's loop."""
+    op, nbytes, n, nslots = C.DBL, 8, 5000, 6000
+    rng = np.random.default_rng(5 + len(split))
+    src = [C.fill_bytes(op, nslots * nbytes, 11 + i) for i in range(2)]
+    dst = [C.fill_bytes(op, nslots * nbytes, 21 + i) for i in range(2)]
+    sb = [ga_amd.DeviceBuffer(x.size) for x in src]
+    db = [ga_amd.DeviceBuffer(x.size) for x in dst]
+    for b, x in zip(sb + db, src + dst):
+        b.upload(x)
+    # pair i: source slot in buffer sbuf[i], destination slot (distinct) in buffer dbuf[i]
+    sbuf = (rng.random(n) < 0.5).astype(int) if split in ("src", "both") else np.zeros(n, int)
+    dbuf = (rng.random(n) < 0.5).astype(int) if split in ("dst", "both") else np.zeros(n, int)
+    sbuf[0] = dbuf[0] = 0                           # the first pair in buffer 0: the fast path tries first
+    sbuf[-1] = 1 if split in ("src", "both") else 0
+    dbuf[-1] = 1 if split in ("dst", "both") else 0
+    so = rng.integers(0, nslots, n)
+    do = np.concatenate([rng.permutation(nslots)[:n]])
+    descs = [([sb[int(b)].ptr + int(a) * nbytes for a, b in zip(so, sbuf)],
+              [db[int(b)].ptr + int(a) * nbytes for a, b in zip(do, dbuf)], nbytes)]
+    assert ga_amd.comex_accv(op, C.SCALE[op], descs, 0) == 0
+    ga_amd.comex_fence_all()
+    want = [x.copy() for x in dst]
+    for i in range(n):   # the reference's per-pair _acc, in order
+        one_s = src[int(sbuf[i])][int(so[i]) * nbytes:(int(so[i]) + 1) * nbytes].copy()
+        w = want[int(dbuf[i])]
+        seg = w[int(do[i]) * nbytes:(int(do[i]) + 1) * nbytes].copy()
+        _oracle_acc_pairs(oracle, op, C.SCALE[op], one_s, seg, [(0, 0)], nbytes)
+        w[int(do[i]) * nbytes:(int(do[i]) + 1) * nbytes] = seg
+    for b, w in zip(db, want):
+        assert np.array_equal(b.download(np.uint8, w.size), w)
+
+
 def test_putv_getv_local(gpu_lib):
     rng = np.random.default_rng(9)
     nbytes, n = 24, 900
