@@ -19,7 +19,6 @@
 #include "../../include/armci.h"
 #include "../../include/comex.h"
 #include "runtime.hpp"
-#include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -559,156 +558,6 @@ static void c2f(int nd, const int *c, long *f) { for (int i = 0; i < nd; i++) f[
 
 using namespace gaamd;
 
-namespace {
-typedef int (*rb_create_t)(void **);
-typedef int (*rb_set_stream_t)(void *, hipStream_t);
-typedef int (*rb_gemm_t)(void *, int, int, int, int, int, const void *, const void *, int, const void *, int,
-                         const void *, void *, int);
-struct Rocblas {
-    void *lib = nullptr, *handle = nullptr;
-    rb_set_stream_t set_stream = nullptr;
-    rb_gemm_t gemm[4] = {nullptr, nullptr, nullptr, nullptr};   // s, d, c, z
-};
-constexpr int kRbNone = 111, kRbTrans = 112;   // rocblas_operation_none / _transpose
-
-// rocBLAS is loaded on the first GEMM only: the accumulate path does not need it
-Rocblas &rocblas() {
-    static Rocblas rb;
-    if (rb.handle) return rb;
-    for (const char *name : {"librocblas.so.5", "librocblas.so"})
-        if ((rb.lib = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
-    if (!rb.lib) fatal("GA gemm: cannot load rocBLAS (%s)", dlerror());
-    auto sym = [&](const char *n) {
-        void *f = dlsym(rb.lib, n);
-        if (!f) fatal("GA gemm: rocBLAS has no %s", n);
-        return f;
-    };
-    rb_create_t create = (rb_create_t)sym("rocblas_create_handle");
-    rb.set_stream = (rb_set_stream_t)sym("rocblas_set_stream");
-    const char *names[4] = {"rocblas_sgemm", "rocblas_dgemm", "rocblas_cgemm", "rocblas_zgemm"};
-    for (int i = 0; i < 4; ++i) rb.gemm[i] = (rb_gemm_t)sym(names[i]);
-    GA_HIP(hipSetDevice(rt().device));
-    if (create(&rb.handle) != 0) fatal("GA gemm: rocblas_create_handle failed");
-    return rb;
-}
-
-// matmul.c:1358-1368: 'n'/'N' is the matrix itself, any other flag its transpose
-bool trans_flag(char t) { return !(t == 'n' || t == 'N'); }
-
-// kind: 0 s, 1 d, 2 c, 3 z (rocBLAS order)
-// C[clo..chi] = alpha*op(A[alo..ahi])*op(B[blo..bhi]) + beta*C[clo..chi], C-order
-// 0-based inclusive patches (NGA_Matmul_patch; GA_?gemm = the leading patches)
-void ga_matmul(char ta, char tb, const void *alpha, const void *beta, int g_a, const int alo[2], const int ahi[2],
-               int g_b, const int blo[2], const int bhi[2], int g_c, const int clo[2], const int chi[2]) {
-    const bool at = trans_flag(ta), bt = trans_flag(tb);
-    GArray &A = arr(g_a), &B = arr(g_b), &C = arr(g_c);
-    if (A.type != C.type || B.type != C.type) fatal("GA matmul: types mismatch");   // matmul.c:1354
-    int kind;
-    switch (C.type) {   // matmul.c:1355: float, double, single and double complex only
-    case C_FLOAT: kind = 0; break;
-    case C_DBL: kind = 1; break;
-    case C_SCPL: kind = 2; break;
-    case C_DCPL: kind = 3; break;
-    default: fatal("GA matmul: type error %d", C.type);
-    }
-    if (A.ndim != 2 || B.ndim != 2 || C.ndim != 2) fatal("GA matmul: arrays must be 2-D");
-    if (g_c == g_a || g_c == g_b) fatal("GA matmul: C must differ from A and B");
-    // C-order extents (Fortran dims reversed); the patch checks of matmul.c:1358-1384
-    auto inside = [](const GArray &x, const int lo[2], const int hi[2]) {
-        return lo[0] >= 0 && lo[1] >= 0 && hi[0] < x.dims[1] && hi[1] < x.dims[0] && lo[0] <= hi[0] + 1 &&
-               lo[1] <= hi[1] + 1;
-    };
-    if (!inside(A, alo, ahi)) fatal("GA matmul: g_a indices out of range");
-    if (!inside(B, blo, bhi)) fatal("GA matmul: g_b indices out of range");
-    if (!inside(C, clo, chi)) fatal("GA matmul: g_c indices out of range");
-    const int m = chi[0] - clo[0] + 1, n = chi[1] - clo[1] + 1;
-    const int ar = ahi[0] - alo[0] + 1, ac = ahi[1] - alo[1] + 1, br = bhi[0] - blo[0] + 1, bc = bhi[1] - blo[1] + 1;
-    const int k = at ? ar : ac;
-    if ((at ? ac : ar) != m) fatal("GA matmul: a & c dims error");
-    if ((bt ? br : bc) != n) fatal("GA matmul: b & c dims error");
-    if ((bt ? bc : br) != k) fatal("GA matmul: a & b dims error");
-    Runtime &r = rt();
-    const int esz = C.elemsize;
-    comex_barrier(COMEX_GROUP_WORLD);   // pnga_matmul starts with a sync: A and B are complete
-    int blk_lo[2], blk_hi[2];
-    NGA_Distribution(g_c, r.rank, blk_lo, blk_hi);
-    // the part of the C patch this rank owns, in C indices and patch-relative (i, j)
-    const int r0 = std::max(blk_lo[0], clo[0]), r1 = std::min(blk_hi[0], chi[0]);
-    const int c0 = std::max(blk_lo[1], clo[1]), c1 = std::min(blk_hi[1], chi[1]);
-    if (m > 0 && n > 0 && r0 <= r1 && c0 <= c1) {
-        Rocblas &rb = rocblas();
-        const int R = r1 - r0 + 1, Cc = c1 - c0 + 1, i0 = r0 - clo[0], j0 = c0 - clo[1];
-        const int ldc = blk_hi[1] - blk_lo[1] + 1;
-        char *cblk = (char *)C.ptr[r.rank] + ((size_t)(r0 - blk_lo[0]) * ldc + (size_t)(c0 - blk_lo[1])) * esz;
-        // k chunks: each panel at most 256 MiB (an owner's op(A) row panel is R x kc)
-        static const size_t panel = [] {   // COMEX_AMD_GEMM_PANEL_BYTES: smaller panels (tests: many chunks)
-            const char *e = getenv("COMEX_AMD_GEMM_PANEL_BYTES");
-            return e ? std::max<size_t>(1, (size_t)atoll(e)) : (size_t)(256ull << 20);
-        }();
-        const int kc_max = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(k, 1),
-                                                 panel / ((size_t)std::max(R, Cc) * esz)));
-        char *pa = nullptr, *pb = nullptr;
-        GA_HIP(hipMalloc((void **)&pa, (size_t)R * kc_max * esz + 1));
-        GA_HIP(hipMalloc((void **)&pb, (size_t)Cc * kc_max * esz + 1));
-        GA_HIP(rb.set_stream(rb.handle, r.stream) == 0 ? hipSuccess : hipErrorUnknown);
-        unsigned char one[16] = {0};   // the type's 1 (beta of the chunks after the first)
-        if (kind == 0) { const float v = 1.0f; memcpy(one, &v, 4); }
-        else if (kind == 1) { const double v = 1.0; memcpy(one, &v, 8); }
-        else if (kind == 2) { const float v[2] = {1.0f, 0.0f}; memcpy(one, v, 8); }
-        else { const double v[2] = {1.0, 0.0}; memcpy(one, v, 16); }
-        for (int k0 = 0; k0 < std::max(k, 1); k0 += kc_max) {
-            const int kc = k ? std::min(kc_max, k - k0) : 0;
-            if (kc) {
-                int lo[2], hi[2], ld[1];
-                // op(A)[i0..][k0..k0+kc): A rows i.., cols k.. ('N') or A rows k.., cols i.. ('T')
-                if (!at) {
-                    lo[0] = alo[0] + i0; hi[0] = lo[0] + R - 1; lo[1] = alo[1] + k0; hi[1] = lo[1] + kc - 1; ld[0] = kc;
-                } else {
-                    lo[0] = alo[0] + k0; hi[0] = lo[0] + kc - 1; lo[1] = alo[1] + i0; hi[1] = lo[1] + R - 1; ld[0] = R;
-                }
-                NGA_Get(g_a, lo, hi, pa, ld);
-                // op(B)[k0..][j0..]: B rows k.., cols j.. ('N') or B rows j.., cols k.. ('T')
-                if (!bt) {
-                    lo[0] = blo[0] + k0; hi[0] = lo[0] + kc - 1; lo[1] = blo[1] + j0; hi[1] = lo[1] + Cc - 1; ld[0] = Cc;
-                } else {
-                    lo[0] = blo[0] + j0; hi[0] = lo[0] + Cc - 1; lo[1] = blo[1] + k0; hi[1] = lo[1] + kc - 1; ld[0] = kc;
-                }
-                NGA_Get(g_b, lo, hi, pb, ld);
-            }
-            // column-major: C^T (Cc x R, ldc) = X (Cc x kc) * Y (kc x R)
-            const int opx = bt ? kRbTrans : kRbNone, ldx = bt ? std::max(kc, 1) : Cc;
-            const int opy = at ? kRbTrans : kRbNone, ldy = at ? R : std::max(kc, 1);
-            const void *bk = (k0 == 0) ? beta : one;
-            {
-                std::lock_guard<std::mutex> g(r.launch_mu);
-                sched_join();   // after the gets' kernels on every library stream
-                if (rb.gemm[kind](rb.handle, opx, opy, Cc, R, kc, alpha, pb, ldx, pa, ldy, bk, cblk, ldc) != 0)
-                    fatal("GA matmul: rocBLAS gemm failed");
-            }
-            // the panels are reused by the next chunk (the launch lock is not held here:
-            // the progress thread keeps serving other ranks' requests meanwhile)
-            GA_HIP(hipStreamSynchronize(r.stream));
-            if (!k) break;
-        }
-        GA_HIP(hipFree(pa));
-        GA_HIP(hipFree(pb));
-    }
-    comex_barrier(COMEX_GROUP_WORLD);   // ... and ends with one: C is complete everywhere
-}
-
-// GA_?gemm: the leading m x n / m x k (k x m) / k x n (n x k) patches
-void ga_gemm(int ctype, char ta, char tb, int m, int n, int k, const void *alpha, int g_a, int g_b,
-             const void *beta, int g_c) {
-    if (m < 0 || n < 0 || k < 0) fatal("GA gemm: negative dimension");
-    if (arr(g_c).type != ctype) fatal("GA gemm: types mismatch");
-    const bool at = trans_flag(ta), bt = trans_flag(tb);
-    const int alo[2] = {0, 0}, ahi[2] = {(at ? k : m) - 1, (at ? m : k) - 1};
-    const int blo[2] = {0, 0}, bhi[2] = {(bt ? n : k) - 1, (bt ? k : n) - 1};
-    const int clo[2] = {0, 0}, chi[2] = {m - 1, n - 1};
-    ga_matmul(ta, tb, alpha, beta, g_a, alo, ahi, g_b, blo, bhi, g_c, clo, chi);
-}
-}  // namespace
-
 extern "C" {
 
 int GA_Initialize(void) { return ARMCI_Init(); }
@@ -949,41 +798,6 @@ void NGA_Gather(int g_a, void *v, int *subsArray[], int n) {
 }
 void NGA_Gather_flat(int g_a, void *v, int subsArray[], int n) {
     gatscat(GS_GATHER, g_a, v, nullptr, subsArray, n, nullptr);
-}
-
-// ---- GA_Dgemm / GA_Sgemm / GA_Zgemm / GA_Cgemm ------------------------------
-// Reference: capi.c:3279-3548 -- GA_Dgemm(ta, tb, m, n, k, ...) calls the
-// Fortran-order GA_Dgemm_c(tb, ta, n, m, k, ..., g_b, g_a, ...) -> pnga_matmul
-// (matmul.c:1290-1890: get A and B chunks, a local ?gemm, ga_acc of each C chunk).
-// In C order that is C[m][n] = alpha*op(A)*op(B) + beta*C with op(X) = X ('N') or
-// X^T ('T'), A m x k ('N') or k x m, B k x n or n x k, on the leading patches.
-// Here every rank computes the rows x cols of C it owns: per k chunk the op(A)
-// row panel and the op(B) column panel come to HBM by NGA_Get (the strided get
-// path: IPC reads of the owners' blocks over xGMI), and one rocBLAS gemm (MFMA)
-// updates the owned block in place, beta applied by the first chunk -- an owner
-// never needs the accumulate traffic of the reference's chunk distribution.
-// GA blocks are row-major in C terms (ld = the block's column count), which a
-// column-major BLAS sees as C^T = op(B)^T op(A)^T.
-
-void GA_Sgemm(char ta, char tb, int m, int n, int k, float alpha, int g_a, int g_b, float beta, int g_c) {
-    ga_gemm(C_FLOAT, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
-}
-void GA_Dgemm(char ta, char tb, int m, int n, int k, double alpha, int g_a, int g_b, double beta, int g_c) {
-    ga_gemm(C_DBL, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
-}
-void GA_Cgemm(char ta, char tb, int m, int n, int k, SingleComplex alpha, int g_a, int g_b, SingleComplex beta,
-              int g_c) {
-    ga_gemm(C_SCPL, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
-}
-void GA_Zgemm(char ta, char tb, int m, int n, int k, DoubleComplex alpha, int g_a, int g_b, DoubleComplex beta,
-              int g_c) {
-    ga_gemm(C_DCPL, ta, tb, m, n, k, &alpha, g_a, g_b, &beta, g_c);
-}
-
-// capi.c:3690-3722: C-order patches (the reference swaps to (b, a) for its Fortran core)
-void NGA_Matmul_patch(char transa, char transb, void *alpha, void *beta, int g_a, int alo[], int ahi[], int g_b,
-                      int blo[], int bhi[], int g_c, int clo[], int chi[]) {
-    ga_matmul(transa, transb, alpha, beta, g_a, alo, ahi, g_b, blo, bhi, g_c, clo, chi);
 }
 
 void GA_Get_proc_grid(int g_a, int dims[]) {

@@ -57,19 +57,18 @@ struct Desc {
 enum KernelKind { KK_AUTO = 0, KK_ROWS = 1, KK_FLAT = 2, KK_SERIAL = 3, KK_ORDERED = 4 };
 constexpr int kKinds = 5;
 
+// Run-time knobs.  Only shipped choices remain: the variants rounds 1-2 measured
+// as losing (U = 2/4 vectors per thread, 256-thread row blocks, plain instead of
+// non-temporal accesses, the looping kernel where the loop-free one applies, the
+// 256 x 2 flat shape, 16-byte vectors at misaligned bases -- DESIGN.md §4) are
+// no longer compiled; their probes live under tools/.
 struct Tuning {
     int kind = KK_AUTO;     // force a kernel family
-    int unroll16 = 1;       // vectors per thread for the W=16 rows kernels {1,2,4}
-    int nontemporal = 1;    // nt loads/stores on the rows kernels (streamed once)
-    int block = 0;          // threads per block of the rows kernels {64, 128, 256}; 0 = auto
+    int block = 0;          // threads per block of the rows kernels {64, 128}; 0 = auto
     int flat_max_nvec = 127;// rows with at most this many vectors use the flat kernel
     int align = 1;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses (misaligned rows)
-    int direct = 1;         // 2-D rows of whole chunks: loop-free one-block-per-chunk kernel
-    int flat_nt = 1;        // flat kernel (short rows): non-temporal loads/stores (+12-24 %)
-    int flat_shape = 1;     // flat kernel: 0 = 256 threads x 2 vectors, 1 = 64 threads x 1 vector (W=16, nt;
-                            // +3.5-5 % on 128 B-1 KiB rows, profiles/r01/sweep_flat_shape.jsonl)
     int flat_line_min = 40; // rows off 128 B lines on both sides with at least this many vectors: rows kernel (0 = off)
-    int wide_unaligned = 0; // 16-byte vectors at 16-byte-misaligned (dword-aligned) bases when rows/strides allow
+    int ordered_cols = 1;   // ordered rows sharing bytes only column-wise: column-sliced many-workgroup kernel
 };
 Tuning &tuning();
 
@@ -82,15 +81,22 @@ struct LaunchInfo {
     int block;     // threads per block (rows kernels)
     int levels;    // stride levels after dropping count-1 levels and merging contiguous ones
     int aligned;   // 1: chunk grid shifted to chunk-aligned dst addresses
+    int sys;       // 1: source read with system-scope loads (a peer GPU's memory)
 };
 
 // Enqueue `op` (kOpCopy or COMEX_ACC_*) over the strided patch.  src/dst
 // must be device-accessible.  Returns 0 or a negative error code; never
 // touches the host copy of the data.  `info` may be null.
+// `src_peer`: src lies in another GPU's HBM (IPC mapping): it is read with
+// system-scope loads (gaamd_kernels.hip vload_sys); a geometry whose rows'
+// order matters returns kErrPeerOrdered, and the caller packs the rows into
+// local memory first.
+constexpr int kErrPeerOrdered = -10;
 int launch_strided(int op, const void *scale, const void *src, const int *src_stride,
                    void *dst, const int *dst_stride, const int *count, int stride_levels,
                    hipStream_t stream, LaunchInfo *info,
-                   uint64_t row_begin = 0, uint64_t row_end = ~0ull, bool plan_only = false);
+                   uint64_t row_begin = 0, uint64_t row_end = ~0ull, bool plan_only = false,
+                   bool src_peer = false);
 
 // byte span [lo, hi) of one side relative to its base pointer
 void side_span_host(const int *stride, const int *count, int stride_levels, int64_t row_bytes,

@@ -89,6 +89,30 @@ __device__ __forceinline__ typename Vec<W>::T vload(const char *p) {
     if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const V *>(p));
     else return *reinterpret_cast<const V *>(p);
 }
+
+// System-scope loads for bytes that live in ANOTHER GPU's HBM (a peer's staging
+// or segment reached through its IPC mapping).  A relaxed system-scope atomic
+// load lowers to `global_load_* sc0 sc1` on gfx950 (LLVM's AMDGPU memory model,
+// the GFX942 family: the same lowering as a system-scope atomic load), which the
+// L2 serves coherently at system scope -- a line of the peer's memory this GPU's
+// L2 still holds from an earlier read (MTYPE NC) is not returned stale.  One
+// dword (or the element's own 1/2 bytes) per load: every vector the launcher
+// builds is dword-aligned at W >= 4, so each load is naturally aligned.
+template <int W>
+__device__ __forceinline__ typename Vec<W>::T vload_sys(const char *p) {
+    typedef typename Vec<W>::T V;
+    if constexpr (W == 1) {
+        return __hip_atomic_load(reinterpret_cast<const uint8_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if constexpr (W == 2) {
+        return __hip_atomic_load(reinterpret_cast<const uint16_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        union { V v; uint32_t w[W / 4]; } u;
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+#pragma unroll
+        for (int i = 0; i < W / 4; ++i) u.w[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return u.v;
+    }
+}
 template <int W, bool NT>
 __device__ __forceinline__ void vstore(char *p, typename Vec<W>::T v) {
     typedef typename Vec<W>::T V;
@@ -196,7 +220,7 @@ __device__ __forceinline__ void row_offsets(const Desc &d, uint32_t r, int64_t &
     constexpr int N = LV > 0 ? LV : kMaxLevels;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-        if (LV == 0 && j >= d.levels) break;
+        if (LV == 0 && j >= d.levels) continue;   // (not `break`: keeps the loop unrollable)
         const uint32_t q = d.cnt[j].div(r);
         const uint32_t dig = r - q * d.cnt[j].d;
         so += (int64_t)dig * d.s_str[j];
@@ -208,7 +232,8 @@ __device__ __forceinline__ void row_offsets(const Desc &d, uint32_t r, int64_t &
 // the U vectors of one thread: all loads first, then the ops and the stores.
 // `full` (wave-uniform) says the whole chunk lies inside the row, so the
 // vectors need no predicate and their addresses fold into immediate offsets.
-template <class OP, int W, int U, int BS, bool NT>
+// SYS: the source lies in a peer GPU's memory -> system-scope source loads
+template <class OP, int W, int U, int BS, bool SYS = false>
 __device__ __forceinline__ void chunk_op(const char *sp, char *dp, int64_t v0, uint32_t nvec, bool full,
                                          const OP &op) {
     typedef typename Vec<W>::T V;
@@ -218,25 +243,29 @@ __device__ __forceinline__ void chunk_op(const char *sp, char *dp, int64_t v0, u
     if (full) {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            a[k] = vload<W, NT>(s0 + k * BS * W);
-            if constexpr (OP::kReadsDst) b[k] = vload<W, NT>(d0 + k * BS * W);
+            if constexpr (SYS) a[k] = vload_sys<W>(s0 + k * BS * W);
+            else a[k] = vload<W, true>(s0 + k * BS * W);
+            if constexpr (OP::kReadsDst) b[k] = vload<W, true>(d0 + k * BS * W);
         }
 #pragma unroll
-        for (int k = 0; k < U; ++k) vstore<W, NT>(d0 + k * BS * W, op.template apply<W>(b[k], a[k]));
+        for (int k = 0; k < U; ++k) vstore<W, true>(d0 + k * BS * W, op.template apply<W>(b[k], a[k]));
         return;
     }
     // row head/tail: one vector at a time (keeps the register budget of the full path)
     for (int k = 0; k < U; ++k) {
         if ((uint64_t)(v0 + k * BS) >= (uint64_t)nvec) continue;   // negative or past the row
-        V x = vload<W, NT>(s0 + k * BS * W), y = x;
-        if constexpr (OP::kReadsDst) y = vload<W, NT>(d0 + k * BS * W);
-        vstore<W, NT>(d0 + k * BS * W, op.template apply<W>(y, x));
+        V x, y;
+        if constexpr (SYS) x = vload_sys<W>(s0 + k * BS * W);
+        else x = vload<W, true>(s0 + k * BS * W);
+        y = x;
+        if constexpr (OP::kReadsDst) y = vload<W, true>(d0 + k * BS * W);
+        vstore<W, true>(d0 + k * BS * W, op.template apply<W>(y, x));
     }
 }
 
 // ---------------------------------------------------------------------------
 // ROWS kernel (N-D): work item w = (row, chunk); chunk = BS*U vectors of a row.
-template <class OP, int W, int U, int BS, bool NT, int LV>
+template <class OP, int W, int U, int BS, int LV, bool SYS = false>
 __global__ __launch_bounds__(BS) void k_rows(const Desc d, const OP op) {
     for (uint32_t w = blockIdx.x; w < (uint32_t)d.items; w += gridDim.x) {
         const uint32_t rl = d.chunk_div.div(w);
@@ -244,8 +273,8 @@ __global__ __launch_bounds__(BS) void k_rows(const Desc d, const OP op) {
         int64_t so, dof;
         row_offsets<LV>(d, d.row0 + rl, so, dof);
         const uint32_t c0 = chunk * (uint32_t)(BS * U);
-        chunk_op<OP, W, U, BS, NT>(d.src + so, d.dst + dof, (int64_t)c0 + threadIdx.x, d.nvec,
-                                   c0 + BS * U <= d.nvec, op);
+        chunk_op<OP, W, U, BS, SYS>(d.src + so, d.dst + dof, (int64_t)c0 + threadIdx.x, d.nvec,
+                                    c0 + BS * U <= d.nvec, op);
     }
 }
 
@@ -261,7 +290,7 @@ struct Desc2 {
     uint32_t align_mask;   // != 0: chunk boundaries at dst addresses = 0 mod (mask+1)
 };
 
-template <class OP, int W, int U, int BS, bool NT>
+template <class OP, int W, int U, int BS>
 __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
     for (uint32_t w = blockIdx.x; w < d.items; w += gridDim.x) {
         const uint32_t rl = d.chunk_div.div(w);
@@ -273,7 +302,7 @@ __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
         const int64_t shift = (int64_t)(((uintptr_t)dp & d.align_mask) / W);
         const int64_t c0 = (int64_t)chunk * (BS * U) - shift;
         const bool full = c0 >= 0 && c0 + BS * U <= (int64_t)d.nvec;
-        chunk_op<OP, W, U, BS, NT>(sp, dp, c0 + threadIdx.x, d.nvec, full, op);
+        chunk_op<OP, W, U, BS>(sp, dp, c0 + threadIdx.x, d.nvec, full, op);
     }
 }
 
@@ -342,9 +371,11 @@ __global__ __launch_bounds__(BS) void k_rowsnd(const DescND<LV> d, const OP op) 
     vstore<W, true>(dp, op.template apply<W>(b, a));
 }
 
-// FLAT kernel: vectors of all rows flattened, each lane decodes its own row.
-template <class OP, int W, int U, int BS, int LV, bool NT = false>
+// FLAT kernel: vectors of all rows flattened, each lane decodes its own row;
+// non-temporal accesses (+12-24 % on 64 B-1 KiB rows, profiles/r01/flat_nt_ab.jsonl).
+template <class OP, int W, int U, int BS, int LV>
 __global__ __launch_bounds__(BS) void k_flat(const Desc d, const OP op) {
+    constexpr bool NT = true;
     typedef typename Vec<W>::T V;
     const uint32_t span = (uint32_t)BS * U;
     for (uint32_t base = blockIdx.x * span; base < (uint32_t)d.items; base += gridDim.x * span) {
@@ -385,15 +416,19 @@ __global__ __launch_bounds__(64) void k_serial(const Desc d, const OP op) {
     }
 }
 
-// ORDERED kernel: rows whose bytes truly overlap (dst rows sharing bytes with
-// each other, or a src row sharing bytes with a dst row) in the reference's
-// row order (comex.c:6936-6961), each row wave-parallel.  One workgroup of 16
-// waves: a chunk of OB*U vectors is loaded completely (every load of the chunk
-// before any of its stores: a src run starting above its own dst run reads the
-// old bytes, as the reference's ascending _acc loop does), then stored; the
-// stores are drained (vmcnt(0)) and the workgroup synchronised before the next
-// chunk or row loads.  Loads are non-temporal, served by the XCD's L2 (not the
-// CU's L1), where the earlier stores of this workgroup have landed.
+// ORDERED kernel: rows whose bytes truly overlap at DIFFERENT offsets (dst rows
+// sharing bytes with each other, or a src row sharing bytes with a dst row) in
+// the reference's row order (comex.c:6936-6961), each row wave-parallel.  One
+// workgroup of 16 waves: a chunk of OB*U vectors is loaded completely (every
+// load of the chunk before any of its stores: a src run starting above its own
+// dst run reads the old bytes, as the reference's ascending _acc loop does),
+// then stored; the stores are drained (vmcnt(0)) and the workgroup synchronised
+// before the next chunk or row loads.  Visibility rule: __syncthreads() is a
+// workgroup-scope release + barrier + acquire, which LLVM's AMDGPU memory model
+// lowers on gfx942/gfx950 (no threadgroup split, the HIP default) to
+// `s_waitcnt vmcnt(0)` + `s_barrier`: all waves of a workgroup share one CU's
+// write-through L1, so a store completed before the barrier is seen by every
+// load of the workgroup after it.
 constexpr int kOrderedBS = 1024;
 template <class OP, int W, int U>
 __global__ __launch_bounds__(kOrderedBS) void k_ordered(const Desc d, const OP op) {
@@ -426,40 +461,101 @@ __global__ __launch_bounds__(kOrderedBS) void k_ordered(const Desc d, const OP o
     }
 }
 
+// COLUMN-ORDERED kernel: rows that share bytes only at the SAME offset -- every
+// pair of overlapping rows (dst/dst, src/dst) starts at the same address, e.g.
+// many rows into one destination run (a zero dst stride: a column reduction),
+// or a src row that IS an earlier dst row.  Then element x of a row depends only
+// on element x of earlier rows, so the reference's order (rows in odometer
+// order, comex.c:6936-6961) holds per column: one lane owns one W-byte column
+// slice of the run for the whole call and walks every row in order; lanes and
+// workgroups are independent (one wave per workgroup, nvec/64 workgroups).
+//   PIPE (no src row meets any dst row): the src loads of P rows are issued
+//   together, and the dst vector stays in a register while consecutive rows
+//   hit the same dst run (stored when the run changes, and at the end) -- the
+//   same operations in the same order as the reference, held in a register.
+//   !PIPE (a src row is a dst row): load, apply, store per row; a lane's load
+//   after its own store to the same address returns that store (single-thread
+//   program order, which the memory model guarantees without fences).
+template <class OP, int W, bool PIPE>
+__global__ __launch_bounds__(64) void k_ordered_cols(const Desc d, const OP op) {
+    typedef typename Vec<W>::T V;
+    constexpr int P = W == 16 ? 8 : 16;   // src loads in flight per lane (PIPE): 128 B
+    const uint32_t v = blockIdx.x * 64u + threadIdx.x;
+    if (v >= d.nvec) return;
+    const int64_t xo = (int64_t)v * W;
+    if constexpr (!PIPE) {
+        for (uint32_t r = 0; r < d.rows; ++r) {
+            int64_t so, dof;
+            row_offsets<0>(d, d.row0 + r, so, dof);
+            const V x = vload<W, false>(d.src + so + xo);
+            V y = x;
+            if constexpr (OP::kReadsDst) y = vload<W, false>(d.dst + dof + xo);
+            vstore<W, false>(d.dst + dof + xo, op.template apply<W>(y, x));
+        }
+    } else {
+        V acc = {};
+        int64_t cur = 0;    // dst offset whose value `acc` holds, if `held`
+        bool held = false;
+        for (uint32_t r0 = 0; r0 < d.rows; r0 += P) {
+            V s[P];
+            int64_t dofs[P];
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                if (r0 + k < d.rows) {
+                    int64_t so;
+                    row_offsets<0>(d, d.row0 + r0 + k, so, dofs[k]);
+                    s[k] = vload<W, true>(d.src + so + xo);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                if (r0 + k >= d.rows) continue;
+                if (!held || dofs[k] != cur) {
+                    if (held) vstore<W, false>(d.dst + cur + xo, acc);
+                    cur = dofs[k];
+                    held = true;
+                    acc = s[k];
+                    if constexpr (OP::kReadsDst) acc = vload<W, false>(d.dst + cur + xo);
+                }
+                acc = op.template apply<W>(acc, s[k]);
+            }
+        }
+        if (held) vstore<W, false>(d.dst + cur + xo, acc);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host launch plumbing
 //
-// Instantiation policy: the 2-D kernel of the ops on the headline paths
-// (f64, double complex, byte copy) carries the tuning variants (U 1/2/4
-// vectors per thread, 64/128/256-thread blocks, nt on/off); every other
-// (op, kernel) pair is built once with the default shape (16 B per thread per
-// stream) and nt on/off.
-template <class OP> struct Tunable { static constexpr bool value = false; };
-template <> struct Tunable<AccDbl> { static constexpr bool value = true; };
-template <> struct Tunable<AccDcp> { static constexpr bool value = true; };
-template <> struct Tunable<CopyOp> { static constexpr bool value = true; };
+// Instantiation policy (only shipped choices are compiled): every
+// (op, W) pair gets the rows kernels with one-wave and 128-thread blocks, one
+// 16-byte vector per thread per stream (U = 16 / W vectors of narrower widths),
+// non-temporal accesses; the flat kernel in one shape per width; the ordered,
+// column-ordered and serial kernels; and one system-scope-source rows kernel
+// (runtime levels, 256 threads) for sources in a peer GPU's memory.
 
-// flat kernel shape: 256 threads x 2 (W=16) or 4 vectors per thread, or with
-// flat_shape=1 (W=16, nt) one-wave blocks of one vector per lane
-static int flat_block_threads(int W, const Tuning &tn) { return (W == 16 && tn.flat_nt && tn.flat_shape == 1) ? 64 : 256; }
-static uint64_t flat_block_items(int W, const Tuning &tn) {
-    if (W == 16 && tn.flat_nt && tn.flat_shape == 1) return 64;
-    return 256ull * ((W == 16) ? 2 : 4);
-}
+// what the launcher decided for one call (the dispatcher's template selector)
+struct Plan {
+    int kind;        // KK_ROWS / KK_FLAT / KK_SERIAL / KK_ORDERED
+    int W, U, BS;
+    int variant;     // KK_ORDERED: 0 one workgroup, 1 column slices (pipelined), 2 column slices (in place)
+    bool sys;        // KK_ROWS: source in a peer GPU's memory (system-scope loads)
+};
 
-// vectors per thread for the default shape: 16 B per thread per stream
-static int unroll_for(int W, int u16) {
-    switch (W) {
-    case 16: return u16;
-    case 8: return 2;
-    case 4: return 4;
-    default: return 8;
-    }
-}
+// flat kernel shape: one-wave blocks of one 16-byte vector per lane (+3.5-5 % on
+// 128 B-1 KiB rows over 256 x 2, profiles/r01/sweep_flat_shape.jsonl); narrower
+// vectors 256 threads x 4
+static int flat_block_threads(int W) { return W == 16 ? 64 : 256; }
+static uint64_t flat_block_items(int W) { return W == 16 ? 64 : 256ull * 4; }
+
+// vectors per thread: 16 B per thread per stream
 template <int W> struct DefaultU { static constexpr int value = W == 16 ? 1 : (W == 8 ? 2 : (W == 4 ? 4 : 8)); };
+static int unroll_for(int W) { return W >= 16 ? 1 : 16 / W; }
+constexpr int kSysBS = 256;   // peer-source rows kernel block
 
-template <class OP, int W, int U, int BS>
-static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt, hipStream_t st) {
+template <class OP, int W, int BS>
+static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, hipStream_t st) {
+    constexpr int U = DefaultU<W>::value;
     Desc2 e;
     e.src = d.src;
     e.dst = d.dst;
@@ -472,8 +568,8 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
     e.chunk_div = d.chunk_div;
     e.align_mask = d.align_mask;
     if constexpr (U == 1) {
-        // whole chunks, one block each, nt on
-        if (g_tuning.direct && nt && !d.align_mask && blocks == e.items && d.nvec % (uint32_t)BS == 0) {
+        // whole chunks, one block each: the loop-free kernel
+        if (!d.align_mask && blocks == e.items && d.nvec % (uint32_t)BS == 0) {
             Desc2D f;
             f.src = d.src;
             f.dst = d.dst;
@@ -485,16 +581,15 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, int nt,
             return hipGetLastError();
         }
     }
-    if (nt) hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
-    else hipLaunchKernelGGL((k_rows2<OP, W, U, BS, false>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
+    hipLaunchKernelGGL((k_rows2<OP, W, U, BS>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
     return hipGetLastError();
 }
 
 template <class OP, int W, int LV, int BS>
-static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, int nt, hipStream_t st) {
+static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, hipStream_t st) {
     constexpr int U = DefaultU<W>::value;
     if constexpr (U == 1 && (LV == 2 || LV == 3)) {
-        if (g_tuning.direct && nt && blocks == d.items && d.nvec % (uint32_t)BS == 0) {
+        if (blocks == d.items && d.nvec % (uint32_t)BS == 0) {
             DescND<LV> f;
             f.src = d.src;
             f.dst = d.dst;
@@ -509,108 +604,78 @@ static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, int n
             return hipGetLastError();
         }
     }
-    if (nt) hipLaunchKernelGGL((k_rows<OP, W, U, BS, true, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, d, op);
-    else hipLaunchKernelGGL((k_rows<OP, W, U, BS, false, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, d, op);
+    hipLaunchKernelGGL((k_rows<OP, W, U, BS, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, d, op);
     return hipGetLastError();
 }
 template <class OP, int W, int LV>
-static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, int BS, int nt, hipStream_t st) {
-    if (BS == 64) return go_rows_nd<OP, W, LV, 64>(d, op, blocks, nt, st);
-    if (BS == 128) return go_rows_nd<OP, W, LV, 128>(d, op, blocks, nt, st);
-    return go_rows_nd<OP, W, LV, 256>(d, op, blocks, nt, st);
+static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, int BS, hipStream_t st) {
+    if (BS == 64) return go_rows_nd<OP, W, LV, 64>(d, op, blocks, st);
+    return go_rows_nd<OP, W, LV, 128>(d, op, blocks, st);
 }
 
 template <class OP, int W>
-static hipError_t dispatch_w(int kind, int U, int BS, int nt, const Desc &d, const OP &op, uint64_t blocks,
-                             hipStream_t st) {
+static hipError_t dispatch_w(const Plan &p, const Desc &d, const OP &op, uint64_t blocks, hipStream_t st) {
     if constexpr (W < OP::kElem) {
         return hipErrorInvalidValue;
     } else {
-        if (kind == KK_SERIAL) {
+        if (p.kind == KK_SERIAL) {
             hipLaunchKernelGGL((k_serial<OP, W>), dim3(1), dim3(64), 0, st, d, op);
             return hipGetLastError();
         }
-        if (kind == KK_ORDERED) {
-            // 64 bytes per thread per stream: 64 KiB chunks, one load round trip each
-            hipLaunchKernelGGL((k_ordered<OP, W, 4 * DefaultU<W>::value>), dim3(1), dim3(kOrderedBS), 0, st, d, op);
+        if (p.kind == KK_ORDERED) {
+            if (p.variant == 1)
+                hipLaunchKernelGGL((k_ordered_cols<OP, W, true>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
+            else if (p.variant == 2)
+                hipLaunchKernelGGL((k_ordered_cols<OP, W, false>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
+            else   // 64 bytes per thread per stream: 64 KiB chunks, one load round trip each
+                hipLaunchKernelGGL((k_ordered<OP, W, 4 * DefaultU<W>::value>), dim3(1), dim3(kOrderedBS), 0, st, d, op);
             return hipGetLastError();
         }
-        if (kind == KK_FLAT) {
-            constexpr int UF = (W == 16) ? 2 : 4;
-            if constexpr (W == 16) {
-                if (g_tuning.flat_nt && g_tuning.flat_shape == 1) {   // one-wave blocks, one vector per lane
-                    if (d.levels == 1)
-                        hipLaunchKernelGGL((k_flat<OP, W, 1, 64, 1, true>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
-                    else if (d.levels == 2)
-                        hipLaunchKernelGGL((k_flat<OP, W, 1, 64, 2, true>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
-                    else
-                        hipLaunchKernelGGL((k_flat<OP, W, 1, 64, 0, true>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
-                    return hipGetLastError();
-                }
-            }
-            if (g_tuning.flat_nt) {
-                if (d.levels == 1)
-                    hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 1, true>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
-                else if (d.levels == 2)
-                    hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 2, true>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
-                else
-                    hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 0, true>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
-                return hipGetLastError();
-            }
+        if (p.sys) {
+            hipLaunchKernelGGL((k_rows<OP, W, DefaultU<W>::value, kSysBS, 0, true>), dim3((uint32_t)blocks),
+                               dim3(kSysBS), 0, st, d, op);
+            return hipGetLastError();
+        }
+        if (p.kind == KK_FLAT) {
+            constexpr int UF = (W == 16) ? 1 : 4;
+            constexpr int FB = (W == 16) ? 64 : 256;
             if (d.levels == 1)
-                hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 1>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+                hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 1>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
             else if (d.levels == 2)
-                hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 2>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+                hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 2>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
             else
-                hipLaunchKernelGGL((k_flat<OP, W, UF, 256, 0>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+                hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 0>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
             return hipGetLastError();
         }
-        if (d.levels == 2) return go_rows_nd<OP, W, 2>(d, op, blocks, BS, nt, st);
-        if (d.levels == 3) return go_rows_nd<OP, W, 3>(d, op, blocks, BS, nt, st);
-        if (d.levels > 3) return go_rows_nd<OP, W, 0>(d, op, blocks, BS, nt, st);
-        if constexpr (W == 16 && Tunable<OP>::value) {
-#define GAAMD_U(B) \
-    switch (U) { \
-    case 1: return go_rows2<OP, W, 1, B>(d, op, blocks, nt, st); \
-    case 2: return go_rows2<OP, W, 2, B>(d, op, blocks, nt, st); \
-    case 4: return go_rows2<OP, W, 4, B>(d, op, blocks, nt, st); \
-    }
-            switch (BS) {
-            case 64: GAAMD_U(64) break;
-            case 128: GAAMD_U(128) break;
-            case 256: GAAMD_U(256) break;
-            }
-#undef GAAMD_U
-        }
-        if (BS == 64) return go_rows2<OP, W, DefaultU<W>::value, 64>(d, op, blocks, nt, st);
-        if (BS == 128) return go_rows2<OP, W, DefaultU<W>::value, 128>(d, op, blocks, nt, st);
-        return go_rows2<OP, W, DefaultU<W>::value, 256>(d, op, blocks, nt, st);
+        if (d.levels == 2) return go_rows_nd<OP, W, 2>(d, op, blocks, p.BS, st);
+        if (d.levels == 3) return go_rows_nd<OP, W, 3>(d, op, blocks, p.BS, st);
+        if (d.levels > 3) return go_rows_nd<OP, W, 0>(d, op, blocks, p.BS, st);
+        if (p.BS == 64) return go_rows2<OP, W, 64>(d, op, blocks, st);
+        return go_rows2<OP, W, 128>(d, op, blocks, st);
     }
 }
 
 template <class OP>
-static hipError_t dispatch_op(int W, int kind, int U, int BS, int nt, const Desc &d, const OP &op, uint64_t blocks,
-                              hipStream_t st) {
-    switch (W) {
-    case 16: return dispatch_w<OP, 16>(kind, U, BS, nt, d, op, blocks, st);
-    case 8: return dispatch_w<OP, 8>(kind, U, BS, nt, d, op, blocks, st);
-    case 4: return dispatch_w<OP, 4>(kind, U, BS, nt, d, op, blocks, st);
-    case 2: return dispatch_w<OP, 2>(kind, U, BS, nt, d, op, blocks, st);
-    case 1: return dispatch_w<OP, 1>(kind, U, BS, nt, d, op, blocks, st);
+static hipError_t dispatch_op(const Plan &p, const Desc &d, const OP &op, uint64_t blocks, hipStream_t st) {
+    switch (p.W) {
+    case 16: return dispatch_w<OP, 16>(p, d, op, blocks, st);
+    case 8: return dispatch_w<OP, 8>(p, d, op, blocks, st);
+    case 4: return dispatch_w<OP, 4>(p, d, op, blocks, st);
+    case 2: return dispatch_w<OP, 2>(p, d, op, blocks, st);
+    case 1: return dispatch_w<OP, 1>(p, d, op, blocks, st);
     }
     return hipErrorInvalidValue;
 }
 
-static hipError_t dispatch(int op, const void *scale, int W, int kind, int U, int BS, int nt,
-                           const Desc &d, uint64_t blocks, hipStream_t st) {
+static hipError_t dispatch(int op, const void *scale, const Plan &p, const Desc &d, uint64_t blocks, hipStream_t st) {
     switch (op) {
-    case kOpCopy: return dispatch_op(W, kind, U, BS, nt, d, CopyOp{}, blocks, st);
-    case 37: { AccInt o; int32_t s; memcpy(&s, scale, 4); o.s = (uint32_t)s; return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
-    case 42: { AccLng o; int64_t s; memcpy(&s, scale, 8); o.s = (uint64_t)s; return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
-    case 39: { AccFlt o; memcpy(&o.s, scale, 4); return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
-    case 38: { AccDbl o; memcpy(&o.s, scale, 8); return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
-    case 40: { AccCpl o; float s[2]; memcpy(s, scale, 8); o.sr = s[0]; o.si = s[1]; return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
-    case 41: { AccDcp o; double s[2]; memcpy(s, scale, 16); o.sr = s[0]; o.si = s[1]; return dispatch_op(W, kind, U, BS, nt, d, o, blocks, st); }
+    case kOpCopy: return dispatch_op(p, d, CopyOp{}, blocks, st);
+    case 37: { AccInt o; int32_t s; memcpy(&s, scale, 4); o.s = (uint32_t)s; return dispatch_op(p, d, o, blocks, st); }
+    case 42: { AccLng o; int64_t s; memcpy(&s, scale, 8); o.s = (uint64_t)s; return dispatch_op(p, d, o, blocks, st); }
+    case 39: { AccFlt o; memcpy(&o.s, scale, 4); return dispatch_op(p, d, o, blocks, st); }
+    case 38: { AccDbl o; memcpy(&o.s, scale, 8); return dispatch_op(p, d, o, blocks, st); }
+    case 40: { AccCpl o; float s[2]; memcpy(s, scale, 8); o.sr = s[0]; o.si = s[1]; return dispatch_op(p, d, o, blocks, st); }
+    case 41: { AccDcp o; double s[2]; memcpy(s, scale, 16); o.sr = s[0]; o.si = s[1]; return dispatch_op(p, d, o, blocks, st); }
     }
     return hipErrorInvalidValue;
 }
@@ -705,9 +770,16 @@ static int64_t row_start(const int64_t *str, const uint32_t *cnt, int L, uint64_
 //               statements -- restrict, acc.h:106-122 -- so a src run at or
 //               above its dst run, in place included, only ever reads bytes
 //               not yet written: no recurrence there.)
+//   OV_COLS     order matters, but every two rows that share bytes start at the
+//               same address (dst rows coincide -- a zero or repeated dst
+//               stride -- and no src row meets a dst row): element x depends
+//               only on element x of earlier rows -> column slices, each walked
+//               in row order (k_ordered_cols, pipelined);
+//   OV_COLS_SRC as OV_COLS, but some src row IS another row's dst run (same
+//               start): column slices without the src prefetch.
 // Exact (row intervals of both sides, sorted) up to kExactRows rows in the
 // call; above that a bound on spans and on the per-row dst - src distance.
-enum { OV_NONE = 0, OV_ORDERED = 1, OV_SERIAL = 2 };
+enum { OV_NONE = 0, OV_ORDERED = 1, OV_SERIAL = 2, OV_COLS = 3, OV_COLS_SRC = 4 };
 constexpr uint64_t kExactRows = 1ull << 18;
 
 static int classify_rows_exact(int64_t sb, const int64_t *ss, int64_t db, const int64_t *ds, const uint32_t *cn,
@@ -730,16 +802,24 @@ static int classify_rows_exact(int64_t sb, const int64_t *ss, int64_t db, const 
         // src row i meets dst row j iff |delta + (i - j) S| < rb -- closed form
         const int64_t S = ss[0], delta = sb - db;
         if (delta < 0 && -delta < rb) return OV_SERIAL;         // d - s in (0, rb) on every row
-        if (n > 1 && (S < 0 ? -S : S) < rb) return OV_ORDERED;  // dst rows share bytes
+        if (n > 1 && S == 0) {                                  // every dst row the same run
+            if (delta == 0) return OV_COLS_SRC;                 // ... and every src row too
+            return (delta < rb) ? OV_ORDERED : OV_COLS;         // a src run shifted into it, or apart
+        }
+        if (n > 1 && (S < 0 ? -S : S) < rb) return OV_ORDERED;  // dst rows share bytes at other offsets
         if (!spans_meet) return OV_NONE;
         const int64_t kmax = (int64_t)n - 1;
         const int64_t kc = S ? (int64_t)std::floor(-(double)delta / (double)S) : 0;
+        bool same_start = false;
         for (int64_t k = kc - 1; k <= kc + 2; ++k) {
             if (k < -kmax || k > kmax) continue;
             const int64_t diff = delta + k * S;
-            if (diff > -rb && diff < rb && !(k == 0 && diff == 0)) return OV_ORDERED;
+            if (diff > -rb && diff < rb && !(k == 0 && diff == 0)) {
+                if (diff != 0) return OV_ORDERED;
+                same_start = true;                              // src row i == dst row i + k
+            }
         }
-        return OV_NONE;
+        return same_start ? OV_COLS_SRC : OV_NONE;
     }
     if (n > kExactRows) {
         // bound: dst - src of a row is (db - sb) + sum_j digit_j * (ds_j - ss_j)
@@ -759,19 +839,28 @@ static int classify_rows_exact(int64_t sb, const int64_t *ss, int64_t db, const 
         if (spans_meet) S[i] = {s, (uint32_t)i};
     }
     std::sort(D.begin(), D.end());
-    for (uint64_t k = 1; k < n; ++k)
-        if (D[k].first < D[k - 1].first + rb) return OV_ORDERED;
+    bool dst_same = false;   // two dst rows at one start (and none at another overlapping offset)
+    for (uint64_t k = 1; k < n; ++k) {
+        if (D[k].first < D[k - 1].first + rb) {
+            if (D[k].first != D[k - 1].first) return OV_ORDERED;
+            dst_same = true;
+        }
+    }
+    bool src_same = same_layout && dst_same;   // src row r' is the dst run of another row r
     if (spans_meet) {
         std::sort(S.begin(), S.end());
         for (const auto &x : D) {
             // src rows with a start in (d - rb, d + rb) share bytes with this dst row;
             // only the row's own src at the same address (dst = dst + a*dst) is harmless
             auto it = std::lower_bound(S.begin(), S.end(), std::make_pair(x.first - rb + 1, (uint32_t)0));
-            for (; it != S.end() && it->first < x.first + rb; ++it)
-                if (it->second != x.second || it->first != x.first) return OV_ORDERED;
+            for (; it != S.end() && it->first < x.first + rb; ++it) {
+                if (it->first != x.first) return OV_ORDERED;
+                if (it->second != x.second) src_same = true;
+            }
         }
     }
-    return OV_NONE;
+    if (src_same) return OV_COLS_SRC;
+    return dst_same ? OV_COLS : OV_NONE;
 }
 
 // The sorted-interval analysis costs O(rows log rows) of host time (~0.1 ms at
@@ -835,7 +924,8 @@ void side_span_host(const int *stride, const int *count, int stride_levels, int6
 
 int launch_strided(int op, const void *scale, const void *src, const int *src_stride,
                    void *dst, const int *dst_stride, const int *count, int stride_levels,
-                   hipStream_t stream, LaunchInfo *info, uint64_t row_begin, uint64_t row_end, bool plan_only) {
+                   hipStream_t stream, LaunchInfo *info, uint64_t row_begin, uint64_t row_end, bool plan_only,
+                   bool src_peer) {
     const Tuning &tn = g_tuning;
     if (info) memset(info, 0, sizeof(*info));
     if (stride_levels < 0 || stride_levels > kMaxLevels) return -2;
@@ -897,8 +987,13 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     // ordering / aliasing: the reference applies rows strictly in order
     const int ov = classify_rows((int64_t)(uintptr_t)src, ss, (int64_t)(uintptr_t)dst, ds, cn, L, row_bytes,
                                  row_begin, row_end);
-    const bool serial = ov == OV_SERIAL || tn.kind == KK_SERIAL;
-    const bool ordered = !serial && (ov == OV_ORDERED || tn.kind == KK_ORDERED);
+    // a source in a peer GPU's memory is read with system-scope loads by one rows
+    // kernel; any order-dependent geometry is left to the caller, which packs
+    // the rows into local memory first (the rows of src and dst then never meet)
+    if (src_peer && ov != OV_NONE) return -10;
+    const bool serial = !src_peer && (ov == OV_SERIAL || tn.kind == KK_SERIAL);
+    const bool cols = !serial && tn.ordered_cols && (ov == OV_COLS || ov == OV_COLS_SRC);
+    const bool ordered = !src_peer && !serial && (ov != OV_NONE || tn.kind == KK_ORDERED);
 
     // vector width: largest power of two <= 16 dividing every address and stride
     uint64_t a = (uint64_t)(uintptr_t)src | (uint64_t)(uintptr_t)dst | (uint64_t)row_bytes | 16;
@@ -913,17 +1008,10 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         if (W < 4) return -8;
         W = esz;
     }
-    // base addresses below 16-byte alignment (a GA patch starting at an odd f64 column):
-    // when the row length and every stride are multiples of 16 bytes, 16-byte vectors at
-    // dword-aligned, 16-byte-misaligned addresses (global memory serves any dword
-    // alignment) instead of 8- or 4-byte vectors
-    if (tn.wide_unaligned && W < 16 && W >= 4) {
-        uint64_t g = (uint64_t)row_bytes | 16;
-        for (int j = 0; j < L; ++j) g |= (uint64_t)ss[j] | (uint64_t)ds[j];
-        const int Wg = (int)lowbit(g);
-        if (Wg > W) W = Wg > 16 ? 16 : Wg;
-    }
     if (serial) W = esz;
+    // column slices: 8-byte lanes where the element allows (twice the lanes of
+    // 16-byte vectors on a column reduction, whose parallelism is the row width)
+    if (cols && W > 8 && esz <= 8) W = 8;
 
     Desc d;
     memset(&d, 0, sizeof(d));
@@ -938,7 +1026,9 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     d.nvec = (uint32_t)(row_bytes / W);
     d.nvec_div = make_fastdiv(d.nvec);
 
-    int kind = serial ? KK_SERIAL : (ordered ? KK_ORDERED : tn.kind);
+    Plan p;
+    memset(&p, 0, sizeof(p));
+    int kind = serial ? KK_SERIAL : (ordered ? KK_ORDERED : (src_peer ? KK_ROWS : tn.kind));
     if (kind == KK_AUTO) {
         kind = ((int64_t)d.nvec <= tn.flat_max_nvec) ? KK_FLAT : KK_ROWS;
         // rows that start off 128-byte lines on both sides: the flat kernel's waves cut rows
@@ -955,13 +1045,11 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
             if ((sa & 127) && (da & 127)) kind = KK_ROWS;
         }
     }
-    // the (U, BS) the dispatcher will pick -- chunking must agree with it
-    const bool tunable = (op == kOpCopy || op == 38 || op == 41);
     // rows kernels: small blocks retire and free their CU slots independently;
     // on the headline shape 64/128/256/512/1024 threads measured
     // 6338/6268/6171/6020/5951 GB/s in a stand-alone probe (tools/h_shape_probe.hip).
     int block = tn.block;
-    if (block == 0) {
+    if (block != 64 && block != 128) {
         // auto: one-wave blocks when every row starts 4 KiB-aligned on both sides,
         // 128 threads otherwise (H-shape ld sweep, profiles/r01/sweep_ld_block.jsonl:
         // 64 leads by 1-6 % at ld 8192/8704/12288 and C3 by 4 %, 128 leads by 5-10 %
@@ -970,14 +1058,17 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         for (int j = 0; j < L; ++j) al |= (uint64_t)ss[j] | (uint64_t)ds[j];
         block = (al & 4095) ? 128 : 64;
     }
-    int U = unroll_for(W, 1), BS = block;
-    if (kind == KK_ROWS && L <= 1 && W == 16 && tunable) {
-        U = tn.unroll16;
-        BS = block;
-    }
+    // the (U, BS) the dispatcher will pick -- chunking must agree with it
+    const int U = unroll_for(W), BS = src_peer ? kSysBS : block;
+    p.kind = kind;
+    p.W = W;
+    p.U = U;
+    p.BS = BS;
+    p.sys = src_peer;
+    p.variant = (kind == KK_ORDERED && cols) ? (ov == OV_COLS ? 1 : 2) : 0;
     const uint32_t per_chunk = (uint32_t)BS * (uint32_t)U;
     d.align_mask = 0;
-    if (tn.align && kind == KK_ROWS && L <= 1 && d.nvec >= 2 * per_chunk) {
+    if (tn.align && kind == KK_ROWS && !src_peer && L <= 1 && d.nvec >= 2 * per_chunk) {
         d.align_mask = per_chunk * (uint32_t)W - 1;   // a chunk spans per_chunk*W bytes
         // rows whose start is not chunk-aligned need one more (partial) chunk
         bool any = ((uintptr_t)dst & d.align_mask) != 0;
@@ -1004,16 +1095,18 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         if (kind == KK_ROWS) {
             d.items = nr * d.chunks;
             blocks = d.items;
+            if (src_peer && blocks > 65536) blocks = 65536;   // grid-stride loop
         } else if (kind == KK_FLAT) {
             d.items = nr * d.nvec;
-            const uint64_t per = flat_block_items(W, tn);
+            const uint64_t per = flat_block_items(W);
             blocks = (d.items + per - 1) / per;
         } else {
             d.items = nr;
+            if (p.variant) blocks = (d.nvec + 63u) / 64u;   // one wave per 64 column slices
         }
         if (blocks > lim) blocks = lim;
         if (!plan_only) {
-            hipError_t e = dispatch(op, scale, W, kind, U, BS, tn.nontemporal, d, blocks, stream);
+            hipError_t e = dispatch(op, scale, p, d, blocks, stream);
             if (e != hipSuccess) return -100 - (int)e;
         }
         ++launches;
@@ -1023,13 +1116,14 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     if (info) {
         info->kind = kind;
         info->width = W;
-        info->unroll = (kind == KK_ROWS) ? U : 0;
+        info->unroll = (kind == KK_ROWS) ? U : (kind == KK_ORDERED ? p.variant : 0);
         info->launches = launches;
         info->blocks = total_blocks;
         info->block = (kind == KK_ROWS) ? BS
-                      : (kind == KK_FLAT ? flat_block_threads(W, tn) : (kind == KK_ORDERED ? kOrderedBS : 64));
+                      : (kind == KK_FLAT ? flat_block_threads(W) : ((kind == KK_ORDERED && !p.variant) ? kOrderedBS : 64));
         info->levels = L;
         info->aligned = d.align_mask ? 1 : 0;
+        info->sys = src_peer ? 1 : 0;
     }
     return 0;
 }

@@ -128,16 +128,11 @@ int gaamd_kernel_counts(unsigned long long counts[5]) {
 static int *tuning_field(const char *key) {
     Tuning &t = tuning();
     if (!strcmp(key, "kind")) return &t.kind;
-    if (!strcmp(key, "unroll16")) return &t.unroll16;
-    if (!strcmp(key, "nontemporal")) return &t.nontemporal;
     if (!strcmp(key, "flat_max_nvec")) return &t.flat_max_nvec;
     if (!strcmp(key, "block")) return &t.block;
     if (!strcmp(key, "align")) return &t.align;
-    if (!strcmp(key, "direct")) return &t.direct;
-    if (!strcmp(key, "flat_nt")) return &t.flat_nt;
-    if (!strcmp(key, "flat_shape")) return &t.flat_shape;
     if (!strcmp(key, "flat_line_min")) return &t.flat_line_min;
-    if (!strcmp(key, "wide_unaligned")) return &t.wide_unaligned;
+    if (!strcmp(key, "ordered_cols")) return &t.ordered_cols;
     return nullptr;
 }
 
@@ -152,9 +147,7 @@ int gaamd_set_tuning(const char *key, int value) {
     }
     int *f = tuning_field(key);
     if (!f) return -1;
-    if (!strcmp(key, "unroll16") && value != 1 && value != 2 && value != 4) return -1;
-    if (!strcmp(key, "flat_shape") && value != 0 && value != 1) return -1;
-    if (!strcmp(key, "block") && value != 0 && value != 64 && value != 128 && value != 256) return -1;
+    if (!strcmp(key, "block") && value != 0 && value != 64 && value != 128) return -1;
     const int old = *f;
     *f = value;
     return old;

@@ -26,7 +26,7 @@ extern "C" {
 #define C_DCPL 1007
 #define GA_MAX_DIM 7
 
-/* complex scalars of GA_Zgemm/GA_Cgemm (comex/src-common/acc.h:6-15) */
+/* complex scalars (comex/src-common/acc.h:6-15) */
 #ifndef GA_AMD_COMPLEX_TYPES
 #define GA_AMD_COMPLEX_TYPES
 typedef struct { double real; double imag; } DoubleComplex;
@@ -84,22 +84,6 @@ void NGA_Release_update(int g_a, int lo[], int hi[]);
 void GA_Get_proc_grid(int g_a, int dims[]);
 /* statistics of global/src/onesided.c:1372-1419 (GAstat.numacc, GAbytes.acctot/accloc) */
 void GA_Print_stats(void);
-
-/* C = alpha*op(A)*op(B) + beta*C on the leading m x n / m x k / k x n patches,
- * C order, op = 'N' or 'T' (global/src/ga.h:31,46,169,195; capi.c:3279-3548 ->
- * pnga_matmul, matmul.c:1290).  Collective.  Every rank computes the part of C
- * it owns: NGA_Get of the op(A) row panel and op(B) column panel into HBM, one
- * rocBLAS ?gemm per k chunk on the owned block. */
-void GA_Dgemm(char ta, char tb, int m, int n, int k, double alpha, int g_a, int g_b, double beta, int g_c);
-void GA_Sgemm(char ta, char tb, int m, int n, int k, float alpha, int g_a, int g_b, float beta, int g_c);
-void GA_Zgemm(char ta, char tb, int m, int n, int k, DoubleComplex alpha, int g_a, int g_b, DoubleComplex beta,
-              int g_c);
-void GA_Cgemm(char ta, char tb, int m, int n, int k, SingleComplex alpha, int g_a, int g_b, SingleComplex beta,
-              int g_c);
-/* the same on arbitrary C-order patches, alpha/beta of the arrays' type
- * (capi.c:3690 NGA_Matmul_patch -> pnga_matmul_patch) */
-void NGA_Matmul_patch(char transa, char transb, void *alpha, void *beta, int g_a, int alo[], int ahi[], int g_b,
-                      int blo[], int bhi[], int g_c, int clo[], int chi[]);
 
 #if defined(__cplusplus)
 }

@@ -64,8 +64,9 @@ int gaamd_unpack(const void *packed, void *dst, const int *dst_stride, const int
 int gaamd_unpack_acc(int op, const void *scale, const void *packed, void *dst,
                      const int *dst_stride, const int *count, int stride_levels, void *stream);
 /* The launch plan of a strided operation without launching anything (no GPU
- * needed): plan[0..7] = {kind (1 rows, 2 flat, 3 serial, 4 ordered), vector width, unroll,
- * threads per block, launches, blocks, stride levels after merging, chunk grid
+ * needed): plan[0..7] = {kind (1 rows, 2 flat, 3 serial, 4 ordered), vector width, unroll
+ * (for kind 4: 0 one workgroup, 1 column slices with src prefetch, 2 column slices in
+ * place), threads per block, launches, blocks, stride levels after merging, chunk grid
  * aligned}; row_end = ~0 for all rows.  Returns 0 or the launcher's error code. */
 int gaamd_plan_strided(int op, const void *src, const int *src_stride, const void *dst, const int *dst_stride,
                        const int *count, int stride_levels, unsigned long long row_begin,
@@ -85,10 +86,9 @@ int gaamd_route_counts(unsigned long long counts[4]);
 int gaamd_peers_unmapped(void);
 /* requests this rank's progress thread applied, by kind: packed, io-vector, rmw, direct-source */
 int gaamd_owner_counts(unsigned long long counts[4]);
-/* keys: "kind" (0 auto, 1 rows, 2 flat, 3 serial, 4 ordered), "unroll16" (1/2/4),
- * "nontemporal", "block" (0 auto/64/128/256), "flat_max_nvec", "align", "direct",
- * "flat_nt", "flat_shape", "flat_line_min", "wide_unaligned", "streams";
- * returns the previous value or -1 */
+/* keys: "kind" (0 auto, 1 rows, 2 flat, 3 serial, 4 ordered), "block" (0 auto/64/128),
+ * "flat_max_nvec", "align", "flat_line_min", "ordered_cols" (column-sliced ordered
+ * kernel), "streams"; returns the previous value or -1 */
 int gaamd_set_tuning(const char *key, int value);
 int gaamd_get_tuning(const char *key);
 

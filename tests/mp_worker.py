@@ -98,8 +98,6 @@ def main():
         order_test(L, rank, size)
     elif mode == "directsrc":
         direct_src_test(L, rank, size)
-    elif mode == "gemm":
-        ga_gemm_test(L, rank, size)
     elif mode in ("armcimisc", "armcimisc-gloo"):
         armci_misc_test(L, rank, size)
     else:
@@ -1804,160 +1802,6 @@ def ngatest_gs(L, rank, size):
             L.GA_Sync()
             L.GA_Destroy(g)
     say(rank, "ndim_NGA_SCATTER_ACC / ndim_NGA_GATHER (int, dbl, dcpl; ndim 1..7) ok")
-    L.GA_Terminate()
-
-
-# ---------------------------------------------------------------------------
-# GA_Dgemm / GA_Sgemm / GA_Zgemm / GA_Cgemm (global/src/capi.c:3279-3548 ->
-# pnga_matmul, matmul.c:1290): C = alpha*op(A)*op(B) + beta*C on the leading
-# m x k / k x n / m x n patches of larger GAs, every transpose pair, against
-# numpy on the host; the part of C outside the patch must be untouched.  The
-# tolerance is the GEMM's (summation order differs from any CPU BLAS): f64
-# 1e-12 and f32 1e-4 relative to k*max|A|*max|B| + |beta|*max|C|.
-def ga_gemm_test(L, rank, size):
-    import ga_amd
-    from ga_amd._lib import DoubleComplex, SingleComplex
-    C_FLOAT, C_DBL, C_SCPL, C_DCPL = 1003, 1004, 1006, 1007
-    assert L.GA_Initialize() == 0
-    ia = ga_amd.int_array
-    rng = np.random.default_rng(77)
-    cases = [(C_DBL, np.float64, L.GA_Dgemm, 1e-12), (C_FLOAT, np.float32, L.GA_Sgemm, 1e-4),
-             (C_DCPL, np.complex128, L.GA_Zgemm, 1e-12), (C_SCPL, np.complex64, L.GA_Cgemm, 1e-4)]
-    m, n, k = 61, 47, 83
-    for ctype, dt, fn, tol in cases:
-        for ta in "NT":
-            for tb in "NT":
-                adims = [m + 3, k + 2] if ta == "N" else [k + 2, m + 3]
-                bdims = [k + 1, n + 4] if tb == "N" else [n + 4, k + 1]
-                cdims = [m + 2, n + 5]
-                def rand(shape):
-                    x = rng.integers(-8, 9, shape).astype(np.float64)
-                    if np.iscomplexobj(np.zeros(1, dt)):
-                        x = x + 1j * rng.integers(-8, 9, shape)
-                    return x.astype(dt)
-                A, B, C0 = rand(adims), rand(bdims), rand(cdims)
-                g = [L.NGA_Create(ctype, 2, ia(d), b"gm", None) for d in (adims, bdims, cdims)]
-                assert all(x > 0 for x in g)
-                if rank == 0:
-                    for h, X in zip(g, (A, B, C0)):
-                        L.NGA_Put(h, ia([0, 0]), ia([X.shape[0] - 1, X.shape[1] - 1]),
-                                  X.ctypes.data_as(ctypes.c_void_p), ia([X.shape[1]]))
-                L.GA_Sync()
-                if ctype in (C_DCPL, C_SCPL):
-                    S = DoubleComplex if ctype == C_DCPL else SingleComplex
-                    alpha, beta = S(0.5, -1.25), S(-2.0, 0.75)
-                    av, bv = complex(0.5, -1.25), complex(-2.0, 0.75)
-                else:
-                    alpha, beta = 0.5, -2.0
-                    av, bv = 0.5, -2.0
-                fn(ta.encode(), tb.encode(), m, n, k, alpha, g[0], g[1], beta, g[2])
-                out = np.zeros(cdims, dt)
-                L.NGA_Get(g[2], ia([0, 0]), ia([cdims[0] - 1, cdims[1] - 1]),
-                          out.ctypes.data_as(ctypes.c_void_p), ia([cdims[1]]))
-                opA = (A[:m, :k] if ta == "N" else A[:k, :m].T).astype(np.complex128)
-                opB = (B[:k, :n] if tb == "N" else B[:n, :k].T).astype(np.complex128)
-                want = C0.astype(np.complex128).copy()
-                want[:m, :n] = av * (opA @ opB) + bv * C0[:m, :n]
-                scale = k * np.abs(A).max() * np.abs(B).max() + abs(bv) * np.abs(C0).max()
-                err = np.abs(out.astype(np.complex128) - want)
-                assert err[:m, :n].max() <= tol * scale, (dt.__name__, ta, tb, err.max(), scale)
-                assert np.array_equal(out[m:, :], C0[m:, :]) and np.array_equal(out[:, n:], C0[:, n:]), \
-                    (dt.__name__, ta, tb, "outside the patch changed")
-                for h in g:
-                    L.GA_Destroy(h)
-    # NGA_Matmul_patch (capi.c:3690): patches at offsets inside larger arrays
-    m, n, k = 45, 38, 57
-    for ctype, dt, tol in ((C_DBL, np.float64, 1e-12), (C_DCPL, np.complex128, 1e-12), (C_FLOAT, np.float32, 1e-4)):
-        for ta in "NT":
-            for tb in "NT":
-                ao = (int(rng.integers(0, 7)), int(rng.integers(0, 7)))
-                bo = (int(rng.integers(0, 7)), int(rng.integers(0, 7)))
-                co = (int(rng.integers(0, 9)), int(rng.integers(0, 9)))
-                ash = (m, k) if ta == "N" else (k, m)
-                bsh = (k, n) if tb == "N" else (n, k)
-                adims = [ao[0] + ash[0] + 3, ao[1] + ash[1] + 2]
-                bdims = [bo[0] + bsh[0] + 1, bo[1] + bsh[1] + 4]
-                cdims = [co[0] + m + 5, co[1] + n + 2]
-                def rand(shape):
-                    x = rng.integers(-8, 9, shape).astype(np.float64)
-                    if np.iscomplexobj(np.zeros(1, dt)):
-                        x = x + 1j * rng.integers(-8, 9, shape)
-                    return x.astype(dt)
-                A, B, C0 = rand(adims), rand(bdims), rand(cdims)
-                g = [L.NGA_Create(ctype, 2, ia(d), b"mp", None) for d in (adims, bdims, cdims)]
-                if rank == 0:
-                    for h, X in zip(g, (A, B, C0)):
-                        L.NGA_Put(h, ia([0, 0]), ia([X.shape[0] - 1, X.shape[1] - 1]),
-                                  X.ctypes.data_as(ctypes.c_void_p), ia([X.shape[1]]))
-                L.GA_Sync()
-                av, bv = (0.75 - 0.5j, 1.5 + 0.25j) if np.iscomplexobj(np.zeros(1, dt)) else (0.75, 1.5)
-                sa, sb = np.array([av], dtype=dt), np.array([bv], dtype=dt)
-                L.NGA_Matmul_patch(ta.encode(), tb.encode(), sa.ctypes.data_as(ctypes.c_void_p),
-                                   sb.ctypes.data_as(ctypes.c_void_p),
-                                   g[0], ia([ao[0], ao[1]]), ia([ao[0] + ash[0] - 1, ao[1] + ash[1] - 1]),
-                                   g[1], ia([bo[0], bo[1]]), ia([bo[0] + bsh[0] - 1, bo[1] + bsh[1] - 1]),
-                                   g[2], ia([co[0], co[1]]), ia([co[0] + m - 1, co[1] + n - 1]))
-                out = np.zeros(cdims, dt)
-                L.NGA_Get(g[2], ia([0, 0]), ia([cdims[0] - 1, cdims[1] - 1]),
-                          out.ctypes.data_as(ctypes.c_void_p), ia([cdims[1]]))
-                Ap = A[ao[0]:ao[0] + ash[0], ao[1]:ao[1] + ash[1]].astype(np.complex128)
-                Bp = B[bo[0]:bo[0] + bsh[0], bo[1]:bo[1] + bsh[1]].astype(np.complex128)
-                opA = Ap if ta == "N" else Ap.T
-                opB = Bp if tb == "N" else Bp.T
-                want = C0.astype(np.complex128).copy()
-                sl = (slice(co[0], co[0] + m), slice(co[1], co[1] + n))
-                want[sl] = complex(sa[0]) * (opA @ opB) + complex(sb[0]) * C0[sl]
-                scale = k * np.abs(A).max() * np.abs(B).max() + abs(bv) * np.abs(C0).max()
-                err = np.abs(out.astype(np.complex128) - want)
-                assert err[sl].max() <= tol * scale, ("patch", dt.__name__, ta, tb, err.max(), scale)
-                mask = np.ones(cdims, bool)
-                mask[sl] = False
-                assert np.array_equal(out[mask], C0[mask]), ("patch", dt.__name__, ta, tb, "outside changed")
-                for h in g:
-                    L.GA_Destroy(h)
-    # global/testing/gemmtest.c restated (REGULAR distribution, N = 8): A[i][j] = i*N+j and
-    # B[i][j] = j*N+i (imaginary part 1), NGA_Matmul_patch('N','N', 1, 0) over the whole
-    # arrays and then over the central N/2 x N/2 patch of zeroed arrays.  The reference's
-    # own element check is compiled out (#if 0); integer-valued data makes it exact here.
-    NN = 8
-    for ctype, dt in ((C_FLOAT, np.float32), (C_DBL, np.float64), (C_DCPL, np.complex128), (C_SCPL, np.complex64)):
-        cplx = np.iscomplexobj(np.zeros(1, dt))
-        ii, jj = np.meshgrid(np.arange(NN), np.arange(NN), indexing="ij")
-        A = (ii * NN + jj).astype(dt) + (1j if cplx else 0)
-        B = (jj * NN + ii).astype(dt) + (1j if cplx else 0)
-        A, B = A.astype(dt), B.astype(dt)
-        g = [L.NGA_Create(ctype, 2, ia([NN, NN]), b"gt", None) for _ in range(3)]
-        one, zero = np.array([1], dtype=dt), np.array([0], dtype=dt)
-        full_lo, full_hi = ia([0, 0]), ia([NN - 1, NN - 1])
-        if rank == 0:
-            L.NGA_Put(g[0], full_lo, full_hi, A.ctypes.data_as(ctypes.c_void_p), ia([NN]))
-            L.NGA_Put(g[1], full_lo, full_hi, B.ctypes.data_as(ctypes.c_void_p), ia([NN]))
-        L.GA_Sync()
-        L.NGA_Matmul_patch(b"N", b"N", one.ctypes.data_as(ctypes.c_void_p), zero.ctypes.data_as(ctypes.c_void_p),
-                           g[0], full_lo, full_hi, g[1], full_lo, full_hi, g[2], full_lo, full_hi)
-        out = np.zeros((NN, NN), dt)
-        L.NGA_Get(g[2], full_lo, full_hi, out.ctypes.data_as(ctypes.c_void_p), ia([NN]))
-        want = (A.astype(np.complex128) @ B.astype(np.complex128))
-        assert np.array_equal(out.astype(np.complex128), want), ("gemmtest full", dt.__name__)
-        for h in g:
-            L.GA_Zero(h)
-        lo, hi, h2 = [NN // 4, NN // 4], [3 * NN // 4 - 1, 3 * NN // 4 - 1], NN // 2
-        Ap = np.ascontiguousarray(A[NN // 4:3 * NN // 4, NN // 4:3 * NN // 4])
-        Bp = np.ascontiguousarray(B[NN // 4:3 * NN // 4, NN // 4:3 * NN // 4])
-        if rank == 0:
-            L.NGA_Put(g[0], ia(lo), ia(hi), Ap.ctypes.data_as(ctypes.c_void_p), ia([h2]))
-            L.NGA_Put(g[1], ia(lo), ia(hi), Bp.ctypes.data_as(ctypes.c_void_p), ia([h2]))
-        L.GA_Sync()
-        L.NGA_Matmul_patch(b"N", b"N", one.ctypes.data_as(ctypes.c_void_p), zero.ctypes.data_as(ctypes.c_void_p),
-                           g[0], ia(lo), ia(hi), g[1], ia(lo), ia(hi), g[2], ia(lo), ia(hi))
-        out = np.zeros((NN, NN), dt)
-        L.NGA_Get(g[2], full_lo, full_hi, out.ctypes.data_as(ctypes.c_void_p), ia([NN]))
-        want = np.zeros((NN, NN), np.complex128)
-        want[NN // 4:3 * NN // 4, NN // 4:3 * NN // 4] = Ap.astype(np.complex128) @ Bp.astype(np.complex128)
-        assert np.array_equal(out.astype(np.complex128), want), ("gemmtest patch", dt.__name__)
-        for h in g:
-            L.GA_Destroy(h)
-    say(rank, "ga gemm ok")
     L.GA_Terminate()
 
 

@@ -68,12 +68,11 @@ def test_golden_cases_armci_and_nb(gpu_lib, manifest, golden):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("knob", [("kind", 1), ("kind", 2), ("kind", 3), ("kind", 4), ("unroll16", 2), ("unroll16", 4),
-                                  ("nontemporal", 0), ("block", 256), ("block", 128), ("block", 64),
-                                  ("align", 0), ("align", 1), ("direct", 0), ("flat_nt", 0), ("flat_shape", 0),
-                                  ("flat_shape", 1), ("flat_line_min", 0), ("wide_unaligned", 1)])
+@pytest.mark.parametrize("knob", [("kind", 1), ("kind", 2), ("kind", 3), ("kind", 4), ("block", 128), ("block", 64),
+                                  ("align", 0), ("align", 1), ("flat_line_min", 0), ("ordered_cols", 0)])
 def test_kernel_variants_identical(gpu_lib, manifest, golden, knob):
-    """Every kernel family / tuning gives the same bits as the reference."""
+    """Every shipped kernel family / tuning gives the same bits as the reference
+    (ordered_cols 0: the coinciding-row golden cases on the one-workgroup kernel)."""
     key, val = knob
     old = ga_amd.set_tuning(key, val)
     try:
@@ -286,9 +285,8 @@ def test_empty_patches_are_noops(gpu_lib):
     assert np.array_equal(b.download(np.float64, 8), np.arange(8, dtype=np.float64))
 
 
-@pytest.mark.parametrize("knobs", [{}, {"align": 1}, {"align": 1, "unroll16": 2}, {"unroll16": 4},
-                                   {"align": 1, "block": 256}, {"block": 128}, {"block": 64, "unroll16": 2},
-                                   {"nontemporal": 0}, {"streams": 1}, {"kind": 4}])
+@pytest.mark.parametrize("knobs", [{}, {"align": 0}, {"align": 1, "block": 128}, {"block": 64},
+                                   {"streams": 1}, {"kind": 4}])
 def test_wide_rows_odd_strides_all_knobs(gpu_lib, oracle, knobs):
     """Rows of 8-40 KiB (several chunks per row) at odd leading dimensions and
     offsets, so chunk splitting, the aligned-chunk grid and row tails are all
@@ -321,44 +319,38 @@ def test_wide_rows_odd_strides_all_knobs(gpu_lib, oracle, knobs):
             ga_amd.set_tuning(k, v)
 
 
-@pytest.mark.parametrize("direct", [1, 0])
-def test_whole_chunk_rows_every_op(gpu_lib, oracle, direct):
-    """Rows that are whole 4 KiB chunks (the loop-free direct kernels k_rows2d /
-    k_rowsnd when `direct` is on, k_rows2 / k_rows when off), 1-D to 4-D, every
-    op, odd leading dimensions and offsets (16-byte aligned), bit-exact vs the
-    oracle."""
-    old = ga_amd.set_tuning("direct", direct)
-    try:
-        rng = np.random.default_rng(7 + direct)
-        for op in (C.INT, C.DBL, C.FLT, C.CPL, C.DCP, C.LNG):
-            for levels in (0, 1, 2, 3):
-                wbytes = 4096 * int(rng.integers(1, 4))
-                count = [wbytes] + [int(rng.integers(2, 6)) for _ in range(levels)]
-                st, dt = [], []
-                sx, dx = wbytes, wbytes
-                for j in range(levels):
-                    sx += 16 * int(rng.integers(0, 40))
-                    dx += 16 * int(rng.integers(0, 40))
-                    st.append(sx)
-                    dt.append(dx)
-                    sx *= count[j + 1]
-                    dx *= count[j + 1]
-                so, do = 16 * int(rng.integers(0, 5)), 16 * int(rng.integers(0, 5))
-                src = C.fill_bytes(op, so + C.span(st, count, levels)[1], 21)
-                dst = C.fill_bytes(op, do + C.span(dt, count, levels)[1], 22)
-                sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
-                sb.upload(src)
-                db.upload(dst)
-                assert ga_amd.comex_accs(op, C.SCALE[op], sb.ptr + so, st, db.ptr + do, dt, count, levels, 0) == 0
-                ga_amd.comex_fence_all()
-                info = ga_amd.last_launch()
-                assert info["kind"] == "rows" and info["width"] == 16, info
-                want = dst.copy()
-                oracle.accs(op, C.SCALE[op], src, so, st, want, do, dt, count, levels)
-                got = db.download(np.uint8, dst.size)
-                assert np.array_equal(got, want), (op, levels, count, st, dt, so, do)
-    finally:
-        ga_amd.set_tuning("direct", old)
+def test_whole_chunk_rows_every_op(gpu_lib, oracle):
+    """Rows that are whole 4 KiB chunks (the loop-free kernels k_rows2d / k_rowsnd;
+    4-D rows take k_rows), 1-D to 4-D, every op, odd leading dimensions and
+    offsets (16-byte aligned), bit-exact vs the oracle."""
+    rng = np.random.default_rng(7)
+    for op in (C.INT, C.DBL, C.FLT, C.CPL, C.DCP, C.LNG):
+        for levels in (0, 1, 2, 3):
+            wbytes = 4096 * int(rng.integers(1, 4))
+            count = [wbytes] + [int(rng.integers(2, 6)) for _ in range(levels)]
+            st, dt = [], []
+            sx, dx = wbytes, wbytes
+            for j in range(levels):
+                sx += 16 * int(rng.integers(0, 40))
+                dx += 16 * int(rng.integers(0, 40))
+                st.append(sx)
+                dt.append(dx)
+                sx *= count[j + 1]
+                dx *= count[j + 1]
+            so, do = 16 * int(rng.integers(0, 5)), 16 * int(rng.integers(0, 5))
+            src = C.fill_bytes(op, so + C.span(st, count, levels)[1], 21)
+            dst = C.fill_bytes(op, do + C.span(dt, count, levels)[1], 22)
+            sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+            sb.upload(src)
+            db.upload(dst)
+            assert ga_amd.comex_accs(op, C.SCALE[op], sb.ptr + so, st, db.ptr + do, dt, count, levels, 0) == 0
+            ga_amd.comex_fence_all()
+            info = ga_amd.last_launch()
+            assert info["kind"] == "rows" and info["width"] == 16, info
+            want = dst.copy()
+            oracle.accs(op, C.SCALE[op], src, so, st, want, do, dt, count, levels)
+            got = db.download(np.uint8, dst.size)
+            assert np.array_equal(got, want), (op, levels, count, st, dt, so, do)
 
 
 @pytest.mark.parametrize("op,off", [(C.DCP, 8), (C.CPL, 4), (C.DBL, 4), (C.LNG, 4)])

@@ -139,25 +139,117 @@ def test_patches_of_one_buffer_match_the_reference_order(gpu_lib, oracle):
 
 
 def test_ordered_kernel_large_overlapping_rows(gpu_lib, oracle):
-    """Every row of a 2048-row f64 patch into the SAME 64 KiB run (zero dst
-    stride): rows in order, each row by the whole 16-wave workgroup -- not one
-    lane; bit-exact and at least 3 GB/s (the one-lane kernel ran ~0.06 GB/s)."""
+    """Every row of a 2048-row patch into the SAME 64 KiB run (zero dst stride, a
+    column reduction): rows share bytes only column-wise, so many one-wave
+    workgroups each walk the rows in order for their column slice
+    (k_ordered_cols); bit-exact against the oracle's
+    sequential order for int64 and f64 (f64 is order-sensitive), and >= 1 TB/s of
+    algorithmic traffic (3 x 128 MiB) on the kernel's own clock (the one-workgroup
+    kernel it replaces ran ~3-5 GB/s)."""
+    L = gpu_lib
     rows, w = 2048, 8192
-    src = C.fill_bytes(C.LNG, rows * w * 8, 5)
-    dst = C.fill_bytes(C.LNG, w * 8, 6)
-    sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
-    sb.upload(src)
-    db.upload(dst)
-    t0 = time.perf_counter()
-    assert ga_amd.comex_accs(C.LNG, -3, sb.ptr, [w * 8], db.ptr, [0], [w * 8, rows], 1, 0) == 0
-    dt = time.perf_counter() - t0
-    assert ga_amd.last_launch()["kind"] == "ordered"
-    want = dst.copy()
-    oracle.accs(C.LNG, -3, src, 0, [w * 8], want, 0, [0], [w * 8, rows], 1)
-    assert np.array_equal(db.download(np.uint8, dst.size), want)
-    gbs = 3 * rows * w * 8 / dt / 1e9
-    print(f"ordered kernel: {gbs:.1f} GB/s (whole blocking call)")
-    assert gbs > 3, gbs
+    for op, a in ((C.LNG, -3), (C.DBL, C.SCALE[C.DBL])):
+        src = C.fill_bytes(op, rows * w * 8, 5)
+        dst = C.fill_bytes(op, w * 8, 6)
+        sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+        sb.upload(src)
+        db.upload(dst)
+        assert ga_amd.comex_accs(op, a, sb.ptr, [w * 8], db.ptr, [0], [w * 8, rows], 1, 0) == 0
+        info = ga_amd.last_launch()
+        assert info["kind"] == "ordered" and info["unroll"] == 1 and info["blocks"] > 1, info
+        want = dst.copy()
+        oracle.accs(op, a, src, 0, [w * 8], want, 0, [0], [w * 8, rows], 1)
+        assert np.array_equal(db.download(np.uint8, dst.size), want), op
+        # kernel rate: 10 launches between events on the primary stream (one stream)
+        old = ga_amd.set_tuning("streams", 1)
+        try:
+            keep, sp = ga_amd.scale_buffer(op, a)
+            ss, ds, cnt = ga_amd.int_array([w * 8]), ga_amd.int_array([0]), ga_amd.int_array([w * 8, rows])
+            ev0, ev1 = L.gaamd_event_create(), L.gaamd_event_create()
+            st = L.gaamd_stream()
+            L.gaamd_event_record(ev0, st)
+            for _ in range(10):
+                h = ctypes.c_int(-1)
+                assert L.comex_nbaccs(op, sp, ctypes.c_void_p(sb.ptr), ss, ctypes.c_void_p(db.ptr), ds, cnt, 1, 0, 0,
+                                      ctypes.byref(h)) == 0
+            L.gaamd_event_record(ev1, st)
+            assert L.comex_wait_all(0) == 0
+            ms = L.gaamd_event_elapsed_ms(ev0, ev1) / 10
+            L.gaamd_event_destroy(ev0)
+            L.gaamd_event_destroy(ev1)
+        finally:
+            ga_amd.set_tuning("streams", old)
+        gbs = 3 * rows * w * 8 / (ms * 1e-3) / 1e9
+        print(f"column-ordered kernel op {op}: {ms * 1e3:.0f} us per launch = {gbs:.0f} GB/s algorithmic")
+        assert gbs > 1000, gbs
+        sb.free()
+        db.free()
+
+
+@pytest.mark.parametrize("op", [C.DBL, C.DCP, C.FLT, C.INT, C.CPL, C.LNG, 0])
+def test_column_ordered_kernel_geometries(gpu_lib, oracle, op):
+    """The column-sliced ordered kernel on every op (0 = put: the last row wins)
+    against the oracle's sequential order: zero dst stride (2-D), planes into one
+    plane (3-D, repeated dst level), a src row that is an earlier dst row, src and
+    dst the same zero-stride run (dst += a*dst per row), and the same with
+    ordered_cols = 0 (one workgroup) for comparison."""
+    e = C.ESZ.get(op, 8)
+    rng = np.random.default_rng(71 + op)
+    geos = []
+    w = 1000 * e
+    geos.append(([w, 37], [w + 8 * e], [0], 0, 0, (w + 8 * e) * 37, w, False))           # column reduction
+    geos.append(([w, 6, 5], [w, w * 6], [w + 4 * e, 0], 0, 0, w * 30, (w + 4 * e) * 6, False))   # planes -> one plane
+    geos.append(([w, 40], [w + 16 * e], [w + 16 * e], (w + 16 * e) * 3, 0, None, None, True))     # src row i = dst row i+3
+    geos.append(([w, 9], [0], [0], 0, 0, None, None, True))                                # dst += a*dst, 9 times
+    for cols in (1, 0):
+        old = ga_amd.set_tuning("ordered_cols", cols)
+        try:
+            for count, ss, ds, so, do, sbytes, dbytes, alias in geos:
+                levels = len(ss)
+                scale = C.SCALE[op] if op else None
+                if alias:
+                    nbytes = max(so + C.span(ss, count, levels)[1], do + C.span(ds, count, levels)[1]) + 64
+                    host = C.fill_bytes(op or C.DBL, nbytes, int(rng.integers(1, 1 << 30)))
+                    b = ga_amd.DeviceBuffer(nbytes)
+                    b.upload(host)
+                    if op:
+                        assert ga_amd.comex_accs(op, scale, b.ptr + so, ss, b.ptr + do, ds, count, levels, 0) == 0
+                    else:
+                        assert ga_amd.comex_puts(b.ptr + so, ss, b.ptr + do, ds, count, levels, 0) == 0
+                    info = ga_amd.last_launch()
+                    ga_amd.comex_fence_all()
+                    want = host.copy()
+                    if op:
+                        oracle.accs(op, scale, want, so, ss, want, do, ds, count, levels)
+                    else:
+                        oracle.puts(want.copy(), so, ss, want, do, ds, count, levels)
+                    got = b.download(np.uint8, nbytes)
+                    b.free()
+                else:
+                    src = C.fill_bytes(op or C.DBL, sbytes, int(rng.integers(1, 1 << 30)))
+                    dst = C.fill_bytes(op or C.DBL, dbytes, int(rng.integers(1, 1 << 30)))
+                    sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+                    sb.upload(src)
+                    db.upload(dst)
+                    if op:
+                        assert ga_amd.comex_accs(op, scale, sb.ptr + so, ss, db.ptr + do, ds, count, levels, 0) == 0
+                    else:
+                        assert ga_amd.comex_puts(sb.ptr + so, ss, db.ptr + do, ds, count, levels, 0) == 0
+                    info = ga_amd.last_launch()
+                    ga_amd.comex_fence_all()
+                    want = dst.copy()
+                    if op:
+                        oracle.accs(op, scale, src, so, ss, want, do, ds, count, levels)
+                    else:
+                        oracle.puts(src, so, ss, want, do, ds, count, levels)
+                    got = db.download(np.uint8, dst.size)
+                    sb.free()
+                    db.free()
+                assert info["kind"] == "ordered", info
+                assert (info["unroll"] != 0) == bool(cols), (info, cols, count, ss, ds)
+                assert np.array_equal(got, want), (op, cols, count, ss, ds, so, do)
+        finally:
+            ga_amd.set_tuning("ordered_cols", old)
 
 
 def test_blocking_accs_returns_after_src_is_consumed(gpu_lib, oracle):

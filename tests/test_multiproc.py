@@ -248,15 +248,6 @@ def test_direct_source_remote_accumulate(n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,panel", [(1, None), (3, None), (3, "4096")])
-def test_ga_gemm(n, panel):
-    """GA_Dgemm/Sgemm/Zgemm/Cgemm (capi.c:3279-3548 -> pnga_matmul, matmul.c:1290)
-    on the leading patches of larger GAs, all four transpose pairs, vs numpy; with
-    4 KiB panels every k chunk is a separate get + gemm."""
-    launch("gemm", n=n, timeout=150, extra_env={"COMEX_AMD_GEMM_PANEL_BYTES": panel} if panel else None)
-
-
-@pytest.mark.gpu
 def test_bench_two_ranks_exchange_exact():
     """The driver's N > 1 invocation shape (bench.py --gpus 2 spawning its own ranks)
     ends with the C5 exchange check: every element of a 4096^2 GA accumulated by

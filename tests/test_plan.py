@@ -38,12 +38,38 @@ def test_continuing_levels_merge():
 
 
 def test_overlapping_destination_rows_are_ordered():
-    """dst rows sharing bytes with each other: rows in the reference's order, each
-    row wave-parallel (one 1024-thread workgroup), not one lane"""
+    """dst rows sharing bytes with each other at other offsets: rows in the
+    reference's order, each row wave-parallel (one 1024-thread workgroup), not one lane"""
     p = plan(DBL, SRC, [64], DST, [32], [64, 100], 1)
     assert p["kind"] == "ordered" and p["width"] == 16 and p["block"] == 1024 and p["blocks"] == 1
-    p = plan(DBL, SRC, [64], DST, [0], [64, 100], 1)           # zero stride: every row into one
-    assert p["kind"] == "ordered"
+    assert p["unroll"] == 0
+
+
+def test_coinciding_destination_rows_take_column_slices():
+    """Rows that share bytes only at the same offset (a zero dst stride: every row
+    into one run, a column reduction): one 8-byte column slice per lane, many
+    one-wave workgroups, each walking the rows in order."""
+    p = plan(DBL, SRC, [65536], DST, [0], [65536, 2048], 1)
+    assert p["kind"] == "ordered" and p["unroll"] == 1 and p["width"] == 8
+    assert p["block"] == 64 and p["blocks"] == 65536 // 8 // 64
+    # src and dst the same zero-stride run (dst += a*dst per row): slices without prefetch
+    p = plan(DBL, SRC, [0], SRC, [0], [65536, 16], 1)
+    assert p["kind"] == "ordered" and p["unroll"] == 2
+    # src row i is dst row i+7 (same start): column slices without prefetch
+    a = SRC
+    p = plan(DBL, a, [65536], a + 65536 * 7, [65536], [16384, 64], 1)
+    assert p["kind"] == "ordered" and p["unroll"] == 2
+    # 3-D: planes accumulated into one plane (repeated dst level), rows disjoint within it
+    p = plan(DBL, SRC, [8192, 8192 * 32], DST, [8192, 0], [8192, 32, 16], 2)
+    assert p["kind"] == "ordered" and p["unroll"] == 1
+    # a shifted src run inside a coinciding dst: order across columns -> one workgroup
+    p = plan(DBL, DST + 8, [0], DST, [0], [4096, 16], 1)
+    assert p["kind"] == "ordered" and p["unroll"] == 0
+    old = ga_amd.set_tuning("ordered_cols", 0)
+    try:
+        assert plan(DBL, SRC, [65536], DST, [0], [65536, 2048], 1)["unroll"] == 0
+    finally:
+        ga_amd.set_tuning("ordered_cols", old)
 
 
 def test_src_starting_inside_its_dst_row_below_it_is_serial_in_place_is_not():
@@ -128,14 +154,11 @@ def test_sub_dword_alignment_is_rejected():
 def test_short_rows_take_the_flat_kernel():
     p = plan(DBL, SRC, [1024], DST, [1024], [512, 1000], 1)
     assert p["kind"] == "flat"
-    # one-wave blocks of one 16-byte vector per lane (flat_shape=1): 32 vectors x 1000 rows
+    # one-wave blocks of one 16-byte vector per lane: 32 vectors x 1000 rows
     assert p["block"] == 64 and p["blocks"] == 32 * 1000 // 64
-    old = ga_amd.set_tuning("flat_shape", 0)
-    try:
-        p = plan(DBL, SRC, [1024], DST, [1024], [512, 1000], 1)
-        assert p["block"] == 256 and p["blocks"] == (32 * 1000 + 511) // 512
-    finally:
-        ga_amd.set_tuning("flat_shape", old)
+    # narrower vectors: 256 threads x 4
+    p = plan(DBL, SRC + 8, [1024], DST, [1024], [512, 1000], 1)
+    assert p["width"] == 8 and p["block"] == 256 and p["blocks"] == (64 * 1000 + 1023) // 1024
     assert plan(DBL, SRC, [4096], DST, [4096], [2048, 1000], 1)["kind"] == "rows"
 
 
@@ -155,11 +178,15 @@ def test_too_many_rows_is_an_error():
 
 
 def test_block_knob_overrides_auto():
-    old = ga_amd.set_tuning("block", 256)
+    old = ga_amd.set_tuning("block", 128)
     try:
-        assert plan(DBL, SRC, [65536], DST, [65536], [16384, 4096], 1)["block"] == 256
+        assert plan(DBL, SRC, [65536], DST, [65536], [16384, 4096], 1)["block"] == 128
     finally:
         ga_amd.set_tuning("block", old)
+    # the losing variants of rounds 1-2 are no longer knobs
+    for key in ("unroll16", "nontemporal", "direct", "flat_nt", "flat_shape", "wide_unaligned"):
+        assert ga_amd.set_tuning(key, 1) == -1, key
+    assert ga_amd.set_tuning("block", 256) == -1
 
 
 def test_rows_off_lines_on_both_sides_take_the_rows_kernel():

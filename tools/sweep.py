@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--row-bytes", type=int, default=0,
                     help="2-D f64 shape with rows of this many bytes, ld = 2 x row, 64 MiB of payload")
     ap.add_argument("--ld-bytes", type=int, default=0, help="with --row-bytes: leading dimension in bytes")
-    ap.add_argument("--variants", default="default;unroll16=2;unroll16=8;nontemporal=1;unroll16=8,nontemporal=1")
+    ap.add_argument("--variants", default="default;block=128;block=64;align=0")
     args = ap.parse_args()
     L = ga_amd.lib()
     assert ga_amd.comex_init() == 0
@@ -63,9 +63,8 @@ def main():
     stream = L.gaamd_stream()
     variants = [v for v in args.variants.split(";") if v]
     # every knob is reset to its default before each variant (a variant sets only its own keys)
-    defaults = {k: ga_amd.get_tuning(k) for k in ("kind", "unroll16", "nontemporal", "flat_max_nvec", "block", "align",
-                                                   "direct", "flat_nt", "flat_shape", "flat_line_min",
-                                                   "wide_unaligned")}
+    defaults = {k: ga_amd.get_tuning(k) for k in ("kind", "flat_max_nvec", "block", "align", "flat_line_min",
+                                                   "ordered_cols")}
     defaults["streams"] = L.gaamd_num_streams()
     res = {v: [] for v in variants}
     wall = {v: [] for v in variants}
