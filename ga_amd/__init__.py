@@ -193,6 +193,25 @@ def fill(ptr, n, type_code, seed, stream=None):
 
 
 # ---- io-vector descriptors (comex.h:13-18, armci.h:17-22) ------------------
+def fill_const(ptr, nbytes, value, dtype="float64"):
+    """Fill nbytes of device memory at ptr with a constant: one <= 64 MiB upload,
+    then device-to-device doubling copies (no host array of the full size)."""
+    import numpy as np
+    item = np.dtype(dtype).itemsize
+    assert nbytes % item == 0
+    chunk = min(nbytes, 64 << 20)
+    host = np.full(chunk // item, value, dtype=dtype)
+    L = lib()
+    if L.gaamd_memcpy(ctypes.c_void_p(ptr), host.ctypes.data_as(ctypes.c_void_p), chunk) != 0:
+        raise RuntimeError("fill_const upload failed")
+    done = chunk
+    while done < nbytes:
+        n = min(done, nbytes - done)
+        if L.gaamd_memcpy(ctypes.c_void_p(ptr + done), ctypes.c_void_p(ptr), n) != 0:
+            raise RuntimeError("fill_const copy failed")
+        done += n
+
+
 class GIOV(ctypes.Structure):
     _fields_ = [("src", ctypes.POINTER(ctypes.c_void_p)), ("dst", ctypes.POINTER(ctypes.c_void_p)),
                 ("count", ctypes.c_int), ("bytes", ctypes.c_int)]

@@ -69,13 +69,7 @@ int PARMCI_Init_args(int *argc, char ***argv) {
     ARMCI_Default_Proc_Group = 0;
     return comex_init_args(argc, argv);
 }
-// armci.c:428-441 initialises over the caller's communicator and returns 1 on
-// success; without MPI underneath the communicator is only a token
-int PARMCI_Init_mpi_comm(long comm) {
-    (void)comm;
-    ARMCI_Default_Proc_Group = 0;
-    return comex_init() == COMEX_SUCCESS ? 1 : 0;
-}
+// PARMCI_Init_mpi_comm / armci_group_comm: mpi_bridge.cpp (MPI_Comm in the signature)
 int PARMCI_Initialized() { return comex_initialized(); }
 void PARMCI_Finalize() { comex_finalize(); }
 void PARMCI_Barrier() { comex_barrier(ARMCI_Default_Proc_Group); }
@@ -443,7 +437,6 @@ int ARMCI_Free(void *) GA_WEAK(ARMCI_Free, PARMCI_Free);
 int ARMCI_Free_memdev(void *) GA_WEAK(ARMCI_Free_memdev, PARMCI_Free_memdev);
 void *ARMCI_Malloc_local(armci_size_t) GA_WEAK(ARMCI_Malloc_local, PARMCI_Malloc_local);
 int ARMCI_Free_local(void *) GA_WEAK(ARMCI_Free_local, PARMCI_Free_local);
-int ARMCI_Init_mpi_comm(long) GA_WEAK(ARMCI_Init_mpi_comm, PARMCI_Init_mpi_comm);
 void ARMCI_GroupFence(ARMCI_Group *) GA_WEAK(ARMCI_GroupFence, PARMCI_GroupFence);
 int ARMCI_Create_mutexes(int) GA_WEAK(ARMCI_Create_mutexes, PARMCI_Create_mutexes);
 int ARMCI_Destroy_mutexes() GA_WEAK(ARMCI_Destroy_mutexes, PARMCI_Destroy_mutexes);

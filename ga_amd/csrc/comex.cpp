@@ -514,6 +514,44 @@ static void progress_loop() {
     };
     double last_work = now_s();
     unsigned idle = 0;
+    // Requests from a rank on ANOTHER GPU (r.peer_src): their bytes are read with
+    // system-scope loads, on a pull stream of that source rank when nothing orders
+    // them (one stream per source: different peers' chunks come over different
+    // xGMI links and are applied side by side).  Where the rows' order matters the
+    // bytes are first pulled into local scratch (per source rank, reused once the
+    // kernel that read it has finished) and applied from there.
+    std::vector<int> pull_slot(r.size, -1);
+    {
+        int k = 0;
+        for (int q = 0; q < r.size; ++q)
+            if (r.same_node(q) && r.peer_src(q)) pull_slot[q] = k++;
+    }
+    auto pull_stream = [&](int src) {
+        const int np = (int)r.streams.size() - r.user_streams;
+        return (np > 0 && pull_slot[src] >= 0) ? r.user_streams + pull_slot[src] % np : -1;
+    };
+    struct Scratch { char *p = nullptr; size_t bytes = 0; hipEvent_t ev = nullptr; };
+    std::vector<Scratch> scratch(r.size);
+    auto scratch_for = [&](int src, size_t need) -> char * {
+        Scratch &x = scratch[src];
+        if (x.ev) GA_HIP(hipEventSynchronize(x.ev));   // the previous reader has finished
+        if (need > x.bytes) {
+            if (x.p) GA_HIP(hipFree(x.p));
+            x.bytes = std::max<size_t>(need, 1 << 20);
+            GA_HIP(hipMalloc((void **)&x.p, x.bytes));
+        }
+        if (!x.ev) GA_HIP(hipEventCreateWithFlags(&x.ev, hipEventDisableTiming));
+        return x.p;
+    };
+    // contiguous bytes of a peer GPU into local memory (system-scope loads)
+    auto pull = [&](char *loc, const char *peer, uint64_t bytes, hipStream_t st) {
+        for (uint64_t off = 0; off < bytes; off += (1ull << 30)) {
+            int c1[1] = {(int)std::min<uint64_t>(bytes - off, 1ull << 30)};
+            const int rc = launch_strided(kOpCopy, nullptr, peer + off, nullptr, loc + off, nullptr, c1, 0, st,
+                                          nullptr, 0, ~0ull, false, true);
+            if (rc) fatal("pull from rank's staging failed (%d)", rc);
+        }
+    };
     for (;;) {
         bool worked = false;
         const uint64_t h = ib->head.load(std::memory_order_relaxed);
@@ -528,13 +566,8 @@ static void progress_loop() {
         if (ready && q.kind == 1) {
             // io-vector accumulate (the _acc_iov_handler analogue, comex.c:4284-4397)
             const int src = q.src_rank;
+            const bool peer = r.peer_src(src);
             const char *packed = peer_staging_or_die(src) + q.staging_off;
-            IovDesc d;
-            memset(&d, 0, sizeof(d));
-            d.src_base = packed;
-            d.dst_list = (const uint64_t *)(packed + iov_list_off(q.count[1], q.count[0]));
-            d.bytes = q.count[0];
-            d.n = (uint32_t)q.count[1];
             hipEvent_t ev;
             if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
             else { ev = pool.back(); pool.pop_back(); }
@@ -543,7 +576,20 @@ static void progress_loop() {
                 Span dsp;
                 dsp.lo = (int64_t)q.dst_addr;
                 dsp.hi = (int64_t)q.dst_hi;
-                const int si = sched_pick(span_of(packed, 0, (int64_t)q.bytes), dsp);
+                const int si = sched_pick(span_of(packed, 0, (int64_t)q.bytes), dsp, 0, peer ? pull_stream(src) : -1);
+                if (peer) {
+                    // sources and owner addresses come from another GPU's staging: pull the
+                    // request into local scratch first, then apply it from there
+                    char *loc = scratch_for(src, q.bytes);
+                    pull(loc, packed, q.bytes, r.streams[si]);
+                    packed = loc;
+                }
+                IovDesc d;
+                memset(&d, 0, sizeof(d));
+                d.src_base = packed;
+                d.dst_list = (const uint64_t *)(packed + iov_list_off(q.count[1], q.count[0]));
+                d.bytes = q.count[0];
+                d.n = (uint32_t)q.count[1];
                 int rc;
                 if (q.iov_serial == 2) {
                     // repeated destinations ordered on the GPU; the progress thread's own sort
@@ -564,6 +610,7 @@ static void progress_loop() {
                     rc = launch_iov(q.op, q.scale, d, q.iov_align, q.iov_serial != 0, r.streams[si]);
                 }
                 if (rc) fatal("io-vector accumulate launch failed (%d)", rc);
+                if (peer) GA_HIP(hipEventRecord(scratch[src].ev, r.streams[si]));
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
             }
             inflight.push_back({ev, src, false});
@@ -609,9 +656,34 @@ static void progress_loop() {
             else { ev = pool.back(); pool.pop_back(); }
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
-                const int si = sched_pick(span_of(sp, slo, shi), span_of((void *)q.dst_addr, dlo, dhi));
-                const int rc = launch_strided(q.op, q.scale, sp, q.src_stride, (void *)q.dst_addr, q.dst_stride,
-                                              q.count, q.levels, r.streams[si], nullptr);
+                const bool peer = r.peer_src(src);
+                const int si = sched_pick(span_of(sp, slo, shi), span_of((void *)q.dst_addr, dlo, dhi), 0,
+                                          peer ? pull_stream(src) : -1);
+                int rc = launch_strided(q.op, q.scale, sp, q.src_stride, (void *)q.dst_addr, q.dst_stride, q.count,
+                                        q.levels, r.streams[si], nullptr, 0, ~0ull, false, peer);
+                if (rc == kErrPeerOrdered) {
+                    // rows whose order matters, source on another GPU: pack row ranges of
+                    // <= 64 MiB into local scratch (system-scope loads), apply each from
+                    // there; one stream keeps the ranges (and the reuse of the scratch) in order
+                    uint64_t rows = 1;
+                    for (int j = 1; j <= q.levels; ++j) rows *= (uint64_t)q.count[j];
+                    const uint64_t per = std::max<uint64_t>(1, (64ull << 20) / (uint64_t)q.count[0]);
+                    char *loc = scratch_for(src, std::min(rows, per) * (uint64_t)q.count[0]);
+                    int ps[8];
+                    int64_t acc = q.count[0];
+                    for (int j = 0; j < q.levels; ++j) { ps[j] = (int)acc; acc *= q.count[j + 1]; }
+                    rc = 0;
+                    for (uint64_t rb = 0; rb < rows && !rc; rb += per) {
+                        const uint64_t re = std::min(rows, rb + per);
+                        char *base = loc - (int64_t)rb * q.count[0];   // row rb lands at the scratch start
+                        rc = launch_strided(kOpCopy, nullptr, sp, q.src_stride, base, ps, q.count, q.levels,
+                                            r.streams[si], nullptr, rb, re, false, true);
+                        if (!rc)
+                            rc = launch_strided(q.op, q.scale, base, ps, (void *)q.dst_addr, q.dst_stride, q.count,
+                                                q.levels, r.streams[si], nullptr, rb, re);
+                    }
+                    GA_HIP(hipEventRecord(scratch[src].ev, r.streams[si]));
+                }
                 if (rc) fatal("direct accumulate launch failed (%d)", rc);
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
             }
@@ -636,11 +708,22 @@ static void progress_loop() {
             else { ev = pool.back(); pool.pop_back(); }
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
+                const bool peer = r.peer_src(src);
                 int64_t dlo = 0, dhi = 0;
                 side_span_host(q.dst_stride, q.count, q.levels, q.count[0], &dlo, &dhi);
-                const int si = sched_pick(span_of(packed, 0, (int64_t)q.bytes), span_of((void *)q.dst_addr, dlo, dhi));
-                const int rc = launch_strided(q.op, q.scale, packed0, pstride, (void *)q.dst_addr, q.dst_stride,
-                                              q.count, q.levels, r.streams[si], nullptr, rb, re);
+                const int si = sched_pick(span_of(packed, 0, (int64_t)q.bytes), span_of((void *)q.dst_addr, dlo, dhi),
+                                          0, peer ? pull_stream(src) : -1);
+                int rc = launch_strided(q.op, q.scale, packed0, pstride, (void *)q.dst_addr, q.dst_stride, q.count,
+                                        q.levels, r.streams[si], nullptr, rb, re, false, peer);
+                if (rc == kErrPeerOrdered) {
+                    // the chunk's rows must apply in order: pull the packed chunk into local
+                    // scratch first, then the ordinary unpack-acc from there
+                    char *loc = scratch_for(src, q.bytes);
+                    pull(loc, packed, q.bytes, r.streams[si]);
+                    rc = launch_strided(q.op, q.scale, loc - (int64_t)rb * q.count[0], pstride, (void *)q.dst_addr,
+                                        q.dst_stride, q.count, q.levels, r.streams[si], nullptr, rb, re);
+                    GA_HIP(hipEventRecord(scratch[src].ev, r.streams[si]));
+                }
                 if (rc) fatal("unpack-acc launch failed (%d)", rc);
                 GA_HIP(hipEventRecord(ev, r.streams[si]));
             }
@@ -683,6 +766,13 @@ static void progress_loop() {
         else usleep(idle > 4096 ? 200 : 20);
     }
     for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+    for (Scratch &x : scratch) {
+        if (x.ev) {
+            (void)hipEventSynchronize(x.ev);
+            (void)hipEventDestroy(x.ev);
+        }
+        if (x.p) (void)hipFree(x.p);
+    }
     if (prog_work_ev) {
         (void)hipEventSynchronize(prog_work_ev);
         (void)hipEventDestroy(prog_work_ev);
@@ -939,6 +1029,20 @@ static void fence_target(int t) {
     wait_done(t, r.posted[t]);
 }
 
+// With COMEX_ENABLE_{ACC,PUT}_{SELF,SMP} = 0 operations on this rank's own memory
+// take the packed route: a blocking call returns once its chunks are posted,
+// before the progress thread has applied them.  A later direct operation on this
+// rank's memory (put, get, accumulate, io-vector, rmw) is ordered after them
+// first, as the reference flushes before a self/SMP operation when fence_array
+// is set (_fence_master, comex.c:6073-6080, 6228-6235).
+static void fence_self_if_pending() {
+    Runtime &r = rt();
+    if (r.posted.empty()) return;
+    if (target_busy(r.rank) ||
+        r.shm->done[r.li(r.rank)][r.li(r.rank)].load(std::memory_order_acquire) < r.posted[r.rank])
+        fence_target(r.rank);
+}
+
 // ---- the one transfer routine ---------------------------------------------
 enum Xfer { X_ACC, X_PUT, X_GET };
 
@@ -968,6 +1072,42 @@ static uint64_t payload_bytes(int64_t row_bytes, const int *count, int levels) {
 static int64_t row_bytes_of(int op, int count0) {
     const int esz = elem_size(op);
     return (op == kOpCopy) ? count0 : (int64_t)(count0 / esz) * esz;
+}
+
+// A get from another GPU whose destination rows must be written in order (they
+// overlap): the rows are packed into local scratch with system-scope loads, then
+// copied to the destination by the ordered local kernel, in row ranges of
+// <= 64 MiB on one stream.  Caller holds launch_mu; the scratch is reused only
+// after the previous such get has finished.
+static char *g_get_scratch = nullptr;
+static size_t g_get_scratch_bytes = 0;
+static hipEvent_t g_get_scratch_ev = nullptr;
+
+static int get_via_scratch(const char *src, const int *ss, char *dst, const int *ds, const int *count, int levels,
+                           hipStream_t st) {
+    uint64_t rows = 1;
+    for (int j = 1; j <= levels; ++j) rows *= (uint64_t)count[j];
+    const uint64_t per = std::max<uint64_t>(1, (64ull << 20) / (uint64_t)count[0]);
+    const size_t need = (size_t)(std::min(rows, per) * (uint64_t)count[0]);
+    if (g_get_scratch_ev) GA_HIP(hipEventSynchronize(g_get_scratch_ev));
+    else GA_HIP(hipEventCreateWithFlags(&g_get_scratch_ev, hipEventDisableTiming));
+    if (need > g_get_scratch_bytes) {
+        if (g_get_scratch) GA_HIP(hipFree(g_get_scratch));
+        g_get_scratch_bytes = std::max<size_t>(need, 1 << 20);
+        GA_HIP(hipMalloc((void **)&g_get_scratch, g_get_scratch_bytes));
+    }
+    int ps[8];
+    int64_t acc = count[0];
+    for (int j = 0; j < levels; ++j) { ps[j] = (int)acc; acc *= count[j + 1]; }
+    int rc = 0;
+    for (uint64_t rb = 0; rb < rows && !rc; rb += per) {
+        const uint64_t re = std::min(rows, rb + per);
+        char *base = g_get_scratch - (int64_t)rb * count[0];
+        rc = launch_strided(kOpCopy, nullptr, src, ss, base, ps, count, levels, st, nullptr, rb, re, false, true);
+        if (!rc) rc = launch_strided(kOpCopy, nullptr, base, ps, dst, ds, count, levels, st, nullptr, rb, re);
+    }
+    GA_HIP(hipEventRecord(g_get_scratch_ev, st));
+    return rc;
 }
 
 static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, int *ds, int *count,
@@ -1019,7 +1159,9 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         return COMEX_SUCCESS;
     }
 
-    if (kind == X_ACC && world != r.rank && r.direct_src && r.same_node(world)) {
+    // the direct-source route is a direct (SMP) route: COMEX_ENABLE_ACC_SMP=0 sends
+    // same-node accumulates down the packed route, as the reference (comex.c:6911-6915)
+    if (kind == X_ACC && world != r.rank && r.direct_src && r.acc_smp_direct && r.same_node(world)) {
         const int64_t rbd = row_bytes_of(op, count[0]);
         int64_t slo = 0, shi = 0;
         side_span_host(ss, count, levels, rbd, &slo, &shi);
@@ -1057,8 +1199,11 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     }
     // the packed route: remote accumulates on this node, and -- under the
     // COMEX_ENABLE_* toggles -- accumulates / puts to self or same-node puts
+    // a put into another GPU's memory is applied by its owner too (no rank writes
+    // another GPU's HBM: runtime.hpp same_dev / DESIGN.md §6)
     const bool packed = (kind == X_ACC && (world != r.rank || !r.acc_self_direct)) ||
-                        (kind == X_PUT && (world == r.rank ? !r.put_self_direct : !r.put_smp_direct));
+                        (kind == X_PUT && (world == r.rank ? !r.put_self_direct
+                                                           : (!r.put_smp_direct || r.peer_src(world))));
     if (packed) {
         const int id = remote_acc_start(world, cop, scale, src, ss, dst, ds, count, levels);
         if (hdl) {
@@ -1075,6 +1220,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     side_span_host(ss, count, levels, rb, &slo, &shi);
     side_span_host(ds, count, levels, rb, &dlo, &dhi);
     View sv, dv;
+    if (world == r.rank) fence_self_if_pending();
     if (world != r.rank) {
         // put: remote dst / get: remote src, through the owner's IPC mapping
         fence_target(world);   // order after our own pending accumulates to it
@@ -1089,6 +1235,8 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         local_views(src, slo, shi, dst, dlo, dhi, sv, dv);
     }
     const bool host_side = needs_sync(sv) || needs_sync(dv);
+    // a get from another GPU's memory reads it with system-scope loads
+    const bool peer = kind == X_GET && world != r.rank && r.peer_src(world);
     int si = 0;
     hipStream_t st;
     {
@@ -1096,7 +1244,9 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         if (host_side) sched_join();   // staged copies sit on stream 0: run there, after everything
         else si = sched_pick(span_of(sv.dev, slo, shi), span_of(dv.dev, dlo, dhi), payload_bytes(rb, count, levels));
         st = r.streams[si];
-        const int rc = launch_strided(cop, scale, sv.dev, ss, dv.dev, ds, count, levels, st, last_launch_info());
+        int rc = launch_strided(cop, scale, sv.dev, ss, dv.dev, ds, count, levels, st, last_launch_info(), 0, ~0ull,
+                                false, peer);
+        if (rc == kErrPeerOrdered) rc = get_via_scratch(sv.dev, ss, dv.dev, ds, count, levels, st);
         if (rc) fatal("strided %s launch failed (code %d): misaligned elements or bad descriptor",
                       kind == X_ACC ? "acc" : (kind == X_PUT ? "put" : "get"), rc);
         if (host_side) sched_sync_all();
@@ -1342,9 +1492,11 @@ constexpr int kIovMapsMin = 65536;
 // allocations the first pair's addresses lie in, with sdelta / ddelta their device-view
 // offsets; when some listed address falls outside them the call returns false before
 // anything is uploaded or launched (the caller classifies per address instead).
+// `src_peer`: the listed sources lie in another GPU's memory (getv): system-scope loads.
 static bool iov_local(int cop, const void *scale, const uint64_t *src, const uint64_t *dst, int bytes, int n,
                       const char *host_src = nullptr, char *host_dst = nullptr, int64_t sdelta = 0,
-                      int64_t ddelta = 0, void *const *gather_src = nullptr, const uint64_t *bounds = nullptr) {
+                      int64_t ddelta = 0, void *const *gather_src = nullptr, const uint64_t *bounds = nullptr,
+                      bool src_peer = false) {
     Runtime &r = rt();
     const bool src_listed = src != nullptr, dst_listed = dst != nullptr;
     // device scratch: [dst list | src list or packed sources | packed results | run-sort work],
@@ -1465,8 +1617,8 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     const int si = sched_pick(ss, ds);
     GA_HIP(hipMemcpyAsync(dev, up, o_res, hipMemcpyHostToDevice, r.streams[si]));
     const int rc = runs ? launch_iov_runs(cop, scale, d, align_or, dlo, (dhi - dlo) / (uint64_t)bytes + 1,
-                                          dev + o_work, work, r.streams[si])
-                        : launch_iov(cop, scale, d, align_or, serial, r.streams[si]);
+                                          dev + o_work, work, r.streams[si], src_peer)
+                        : launch_iov(cop, scale, d, align_or, serial, r.streams[si], src_peer);
     if (rc) fatal("io-vector launch failed (%d): misaligned elements?", rc);
     if (!dst_listed) {
         GA_HIP(hipStreamSynchronize(r.streams[si]));
@@ -1488,6 +1640,11 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         if (n <= 0) continue;
         if (bytes <= 0) fatal("io-vector of %d bytes", bytes);
         const bool remote_side_is_dst = (kind != X_GET);
+        // the owner applies it (staging + inbox request): every remote accumulate, and
+        // a put into another GPU's memory (no rank writes another GPU's HBM)
+        const bool remote_apply = world != r.rank && (kind == X_ACC || (kind == X_PUT && r.peer_src(world)));
+        // a getv from another GPU's memory reads it with system-scope loads
+        const bool getv_peer = kind == X_GET && world != r.rank && r.peer_src(world);
         // address lists in buffers kept across calls: fresh ones cost a page fault per
         // 512 entries, more than the classification itself at scatter-acc sizes
         static std::vector<uint64_t> g_sv, g_dv;
@@ -1497,6 +1654,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         }
         uint64_t *sv = g_sv.data(), *dv = g_dv.data();
         bool host_bounce = false;
+        if (world == r.rank) fence_self_if_pending();
         if (world != r.rank && !r.same_node(world)) {
             // another node: one io-vector message per descriptor chunk (wire.cpp)
             for (int i = 0; i < n && !host_bounce; ++i) {
@@ -1586,7 +1744,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         }
         bool src_host = false, dst_host = false;   // a whole side in pageable host memory
         bool classified = false;
-        if (world != r.rank && kind == X_ACC && n >= kIovMapsMin) {
+        if (remote_apply && n >= kIovMapsMin) {
             // remote accumulate from GA's `v`: a source side in one ordinary host mapping is
             // recognised with one lookup (host_cpu_range) instead of a query per page
             const uint64_t *rs = (const uint64_t *)darr[k].src;
@@ -1614,7 +1772,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
                 host_bounce = true;
             }
             if (world != r.rank && remote_side_is_dst) {
-                if (kind == X_ACC) dv[i] = (uint64_t)(uintptr_t)dp;   // owner's address, checked below
+                if (remote_apply) dv[i] = (uint64_t)(uintptr_t)dp;   // owner's address, checked below
                 else dv[i] = (uint64_t)(uintptr_t)remote_view(world, dp, 0, bytes);
             } else if (vc.view(dp, bytes, &v)) {
                 if (dst_host) host_bounce = true;
@@ -1630,7 +1788,7 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         // needs the old values and stays per pair
         if (src_host && dst_host) host_bounce = true;
         if (dst_host && cop != kOpCopy) host_bounce = true;
-        if (!host_bounce && (src_host || dst_host) && (world == r.rank || kind != X_ACC)) {
+        if (!host_bounce && (src_host || dst_host) && !remote_apply) {
             // pageable host runs on one side (GA's MA buffer `v` of a scatter/gather): the
             // sources are gathered on the host and uploaded packed, or the results come
             // back packed and are scattered on the host, in pair order
@@ -1640,7 +1798,8 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
             } else {
                 static std::vector<char> g_packed;   // kept across calls (no page faults per call)
                 if (g_packed.size() < (size_t)n * (size_t)bytes) g_packed.resize((size_t)n * (size_t)bytes);
-                iov_local(cop, scale, sv, nullptr, bytes, n, nullptr, g_packed.data());
+                iov_local(cop, scale, sv, nullptr, bytes, n, nullptr, g_packed.data(), 0, 0, nullptr, nullptr,
+                          getv_peer);
                 scatter_runs(darr[k].dst, g_packed.data(), n, bytes);
             }
             continue;
@@ -1652,13 +1811,13 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
                 xfer_contig(kind, op, scale, darr[k].src[i], darr[k].dst[i], bytes, proc, group, nullptr);
             continue;
         }
-        if (world == r.rank || kind != X_ACC) {
+        if (!remote_apply) {
             if (world != r.rank) fence_target(world);
-            iov_local(cop, scale, sv, dv, bytes, n);
+            iov_local(cop, scale, sv, dv, bytes, n, nullptr, nullptr, 0, 0, nullptr, nullptr, getv_peer);
             continue;
         }
-        // remote io-vector accumulate: pack the sources + the owner addresses into
-        // staging, the owner's progress thread applies them (k_iov)
+        // remote io-vector accumulate (or put into another GPU): pack the sources + the
+        // owner addresses into staging, the owner's progress thread applies them (k_iov)
         drain_target(world);   // its staging ring is allocated and posted in order
         const uint64_t sub = sub_ring_bytes();
         const uint64_t per_pair = (uint64_t)bytes + 8;
@@ -1896,8 +2055,32 @@ int comex_init() {
     }
     GA_HIP(hipStreamCreateWithFlags(&r.stream, hipStreamDefault));
     {
+        // which ranks share this physical GPU (PCI bus id): another GPU's memory is
+        // read with system-scope loads and never written by this rank (runtime.hpp)
+        struct Dev { char bus[32]; int32_t node; } mine_dev;
+        memset(&mine_dev, 0, sizeof(mine_dev));
+        if (hipDeviceGetPCIBusId(mine_dev.bus, (int)sizeof(mine_dev.bus) - 1, r.device) != hipSuccess) {
+            (void)hipGetLastError();
+            snprintf(mine_dev.bus, sizeof(mine_dev.bus), "device-%d", r.device);
+        }
+        mine_dev.node = r.node;
+        std::vector<Dev> devs(r.size);
+        if (r.size > 1) boot_allgather(&mine_dev, devs.data(), sizeof(Dev));
+        else devs[0] = mine_dev;
+        r.same_dev.assign(r.size, 0);
+        for (int q = 0; q < r.size; ++q)
+            r.same_dev[q] = devs[q].node == r.node && !strcmp(devs[q].bus, mine_dev.bus);
+        const char *pl = getenv("COMEX_AMD_PEER_LOADS");
+        r.peer_loads = (pl && !strcmp(pl, "all")) ? 1 : ((pl && !strcmp(pl, "off")) ? 2 : 0);
+        int peers = 0;   // same-node ranks whose memory is read as another GPU's
+        for (int q = 0; q < r.size; ++q)
+            if (r.same_node(q) && r.peer_src(q)) ++peers;
+        // owner pulls from peer GPUs: one stream per source rank, so the chunks of
+        // different peers (different xGMI links) are applied side by side
+        const char *ps = getenv("COMEX_AMD_PULL_STREAMS");
+        const int pull = std::min(peers, ps ? atoi(ps) : 6);
         const char *ns = getenv("COMEX_AMD_STREAMS");
-        sched_init(ns ? atoi(ns) : 2);   // 2: independent ops overlap kernel edges
+        sched_init(ns ? atoi(ns) : 2, pull);   // 2: independent ops overlap kernel edges
     }
     const char *bs = getenv("COMEX_AMD_BLOCKING_SYNC");
     r.blocking_sync = !bs || atoi(bs) != 0;
@@ -1908,7 +2091,8 @@ int comex_init() {
             const char *v = getenv(name);
             return !v || atoi(v) != 0;
         };
-        r.acc_self_direct = flag("COMEX_ENABLE_ACC_SELF") || flag("COMEX_ENABLE_ACC_SMP");
+        r.acc_smp_direct = flag("COMEX_ENABLE_ACC_SMP");
+        r.acc_self_direct = flag("COMEX_ENABLE_ACC_SELF") || r.acc_smp_direct;
         r.put_smp_direct = flag("COMEX_ENABLE_PUT_SMP");
         r.put_self_direct = flag("COMEX_ENABLE_PUT_SELF") || r.put_smp_direct;
     }
@@ -1999,6 +2183,11 @@ int comex_finalize() {
     r.staging = nullptr;
     sched_sync_all();
     sched_fini();
+    if (g_get_scratch) (void)hipFree(g_get_scratch);
+    g_get_scratch = nullptr;
+    g_get_scratch_bytes = 0;
+    if (g_get_scratch_ev) (void)hipEventDestroy(g_get_scratch_ev);
+    g_get_scratch_ev = nullptr;
     if (g_iov_scratch) (void)hipFree(g_iov_scratch);
     g_iov_scratch = nullptr;
     if (g_iov_host) (void)hipHostFree(g_iov_host);
@@ -2376,6 +2565,7 @@ int comex_rmw(int op, void *ploc, void *prem, int extra, int proc, comex_group_t
     if (!ploc || !prem) fatal("comex_rmw: NULL ploc or prem");
     uint64_t old = 0;
     if (world == r.rank) {
+        fence_self_if_pending();
         old = rmw_local(swap, prem, bytes, val);
     } else if (!r.same_node(world)) {
         check_remote(world, prem, 0, bytes);
@@ -2479,13 +2669,7 @@ int comex_group_translate_ranks(int n, comex_group_t group_from, int *ranks_from
     return COMEX_SUCCESS;
 }
 
-// comex.h:147 returns the group's MPI_Comm.  This runtime bootstraps without MPI
-// (launcher hooks or the node-shm rendezvous), so there is no communicator to hand
-// out: the call fails loudly instead of returning an unusable handle.
-int comex_group_comm(comex_group_t group, void *comm) {
-    (void)comm;
-    fatal("comex_group_comm(%d): libga_amd has no MPI communicator (it bootstraps without MPI)", group);
-}
+// comex_group_comm / comex_init_comm: mpi_bridge.cpp
 
 int gaamd_owner_counts(unsigned long long counts[4]) {
     for (int k = 0; k < 4; ++k) counts[k] = g_owned[k].load(std::memory_order_relaxed);

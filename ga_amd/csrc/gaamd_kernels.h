@@ -126,7 +126,9 @@ struct IovDesc {
 };
 // `align_or` = OR of every listed address (the launcher cannot read device lists);
 // `serial` applies the pairs one by one in order (overlapping destinations)
-int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool serial, hipStream_t stream);
+// `src_peer`: the sources lie in a peer GPU's memory (byte copy only: getv)
+int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool serial, hipStream_t stream,
+               bool src_peer = false);
 // Pairs whose destinations may repeat (GA scatter-accumulate with repeated
 // subscripts), without a host-side overlap check: the destinations are sorted on
 // the GPU (stable radix sort of (dst - dlo) / bytes, so equal destinations keep
@@ -137,6 +139,6 @@ int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool ser
 constexpr int kIovRunsMaxBytes = 256;
 size_t iov_runs_work_bytes(uint32_t n);
 int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
-                    void *work, size_t work_bytes, hipStream_t stream);
+                    void *work, size_t work_bytes, hipStream_t stream, bool src_peer = false);
 
 }  // namespace gaamd

@@ -1164,7 +1164,15 @@ int launch_rmw(int swap, void *addr, int bytes, uint64_t val, uint64_t *out_dev,
 // addresses or one packed buffer (address = base + i*bytes).  Vectors of all
 // pairs are flattened so short pairs (GA scatter-acc: one element each) still
 // fill every lane.
-template <class OP, int W, int U>
+// SYS: the sources lie in a peer GPU's memory (getv from another device):
+// system-scope source loads, as the strided kernels' vload_sys
+template <int W, bool SYS>
+__device__ __forceinline__ typename Vec<W>::T src_load(const char *p) {
+    if constexpr (SYS) return vload_sys<W>(p);
+    else return vload<W, false>(p);
+}
+
+template <class OP, int W, int U, bool SYS = false>
 __global__ __launch_bounds__(256) void k_iov(const IovDesc d, const OP op) {
     typedef typename Vec<W>::T V;
     const uint32_t span = 256u * U;
@@ -1181,7 +1189,7 @@ __global__ __launch_bounds__(256) void k_iov(const IovDesc d, const OP op) {
                 const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
                 char *dp = d.dst_list ? (char *)d.dst_list[i] : d.dst_base + (size_t)i * d.bytes;
                 dps[k] = dp + (size_t)v * W;
-                a[k] = vload<W, false>(sp + (size_t)v * W);
+                a[k] = src_load<W, SYS>(sp + (size_t)v * W);
                 if constexpr (OP::kReadsDst) b[k] = vload<W, false>(dps[k]);
             }
         }
@@ -1192,14 +1200,14 @@ __global__ __launch_bounds__(256) void k_iov(const IovDesc d, const OP op) {
 }
 
 // pairs in reference order when destinations overlap (duplicates in a scatter-acc)
-template <class OP, int W>
+template <class OP, int W, bool SYS = false>
 __global__ __launch_bounds__(64) void k_iov_serial(const IovDesc d, const OP op) {
     if (threadIdx.x != 0) return;
     for (uint32_t i = 0; i < d.n; ++i) {
         const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
         char *dp = d.dst_list ? (char *)d.dst_list[i] : d.dst_base + (size_t)i * d.bytes;
         for (uint32_t v = 0; v < d.nvec; ++v) {
-            typename Vec<W>::T x = vload<W, false>(sp + (size_t)v * W), y = x;
+            typename Vec<W>::T x = src_load<W, SYS>(sp + (size_t)v * W), y = x;
             if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
             vstore<W, false>(dp + (size_t)v * W, op.template apply<W>(y, x));
         }
@@ -1217,7 +1225,7 @@ __global__ __launch_bounds__(256) void k_iov_keys(const uint64_t *dst_list, uint
 
 // one lane per distinct destination (the first sorted position of its run)
 // applies the run's pairs in input order
-template <class OP, int W>
+template <class OP, int W, bool SYS = false>
 __global__ __launch_bounds__(256) void k_iov_runs(const IovDesc d, const OP op) {
     const uint32_t j0 = blockIdx.x * 256u + threadIdx.x;
     if (j0 >= d.n) return;
@@ -1228,47 +1236,60 @@ __global__ __launch_bounds__(256) void k_iov_runs(const IovDesc d, const OP op) 
         const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
         char *dp = (char *)d.dst_list[i];
         for (uint32_t v = 0; v < d.nvec; ++v) {
-            typename Vec<W>::T x = vload<W, false>(sp + (size_t)v * W), y = x;
+            typename Vec<W>::T x = src_load<W, SYS>(sp + (size_t)v * W), y = x;
             if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
             vstore<W, false>(dp + (size_t)v * W, op.template apply<W>(y, x));
         }
     }
 }
 
+template <class OP, int W, bool SYS>
+static hipError_t iov_ws(const IovDesc &d, const OP &op, bool serial, hipStream_t st) {
+    if (d.run_key) {
+        hipLaunchKernelGGL((k_iov_runs<OP, W, SYS>), dim3((d.n + 255u) / 256u), dim3(256), 0, st, d, op);
+    } else if (serial) {
+        hipLaunchKernelGGL((k_iov_serial<OP, W, SYS>), dim3(1), dim3(64), 0, st, d, op);
+    } else {
+        constexpr int U = 2;
+        uint64_t blocks = ((uint64_t)d.items + 256u * U - 1) / (256u * U);
+        if (blocks > 65536) blocks = 65536;
+        hipLaunchKernelGGL((k_iov<OP, W, U, SYS>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+    }
+    return hipGetLastError();
+}
+
+// sys: sources in a peer GPU's memory -- built for the byte copy only (getv from
+// another device; every other cross-device io-vector is applied by the owner)
 template <class OP, int W>
-static hipError_t iov_w(const IovDesc &d, const OP &op, bool serial, hipStream_t st) {
+static hipError_t iov_w(const IovDesc &d, const OP &op, bool serial, bool sys, hipStream_t st) {
     if constexpr (W < OP::kElem) {
         return hipErrorInvalidValue;
     } else {
-        if (d.run_key) {
-            hipLaunchKernelGGL((k_iov_runs<OP, W>), dim3((d.n + 255u) / 256u), dim3(256), 0, st, d, op);
-        } else if (serial) {
-            hipLaunchKernelGGL((k_iov_serial<OP, W>), dim3(1), dim3(64), 0, st, d, op);
-        } else {
-            constexpr int U = 2;
-            uint64_t blocks = ((uint64_t)d.items + 256u * U - 1) / (256u * U);
-            if (blocks > 65536) blocks = 65536;
-            hipLaunchKernelGGL((k_iov<OP, W, U>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+        if (sys) {
+            if constexpr (std::is_same<OP, CopyOp>::value) return iov_ws<OP, W, true>(d, op, serial, st);
+            else return hipErrorInvalidValue;
         }
-        return hipGetLastError();
+        return iov_ws<OP, W, false>(d, op, serial, st);
     }
 }
 
 template <class OP>
-static hipError_t iov_op(int W, const IovDesc &d, const OP &op, bool serial, hipStream_t st) {
+static hipError_t iov_op(int W, const IovDesc &d, const OP &op, bool serial, bool sys, hipStream_t st) {
     switch (W) {
-    case 16: return iov_w<OP, 16>(d, op, serial, st);
-    case 8: return iov_w<OP, 8>(d, op, serial, st);
-    case 4: return iov_w<OP, 4>(d, op, serial, st);
-    case 2: return iov_w<OP, 2>(d, op, serial, st);
-    case 1: return iov_w<OP, 1>(d, op, serial, st);
+    case 16: return iov_w<OP, 16>(d, op, serial, sys, st);
+    case 8: return iov_w<OP, 8>(d, op, serial, sys, st);
+    case 4: return iov_w<OP, 4>(d, op, serial, sys, st);
+    case 2: return iov_w<OP, 2>(d, op, serial, sys, st);
+    case 1: return iov_w<OP, 1>(d, op, serial, sys, st);
     }
     return hipErrorInvalidValue;
 }
 
-static int iov_dispatch(int op, const void *scale, int W, const IovDesc &d, bool serial, hipStream_t stream);
+static int iov_dispatch(int op, const void *scale, int W, const IovDesc &d, bool serial, bool sys,
+                        hipStream_t stream);
 
-int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool serial, hipStream_t stream) {
+int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool serial, hipStream_t stream,
+               bool src_peer) {
     const int esz = elem_size(op);
     if (!esz || d.bytes <= 0) return -4;
     if (op != kOpCopy && !scale) return -5;
@@ -1288,7 +1309,7 @@ int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool ser
     d.nvec_div = make_fastdiv(d.nvec);
     if ((uint64_t)d.n * d.nvec >= (1ull << 31)) return -7;
     d.items = d.n * d.nvec;
-    return iov_dispatch(op, scale, W, d, serial, stream);
+    return iov_dispatch(op, scale, W, d, serial, src_peer, stream);
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1303,7 +1324,7 @@ static size_t iov_sort_temp_bytes(uint32_t n) {
 size_t iov_runs_work_bytes(uint32_t n) { return 4 * align256((size_t)n * 4) + align256(iov_sort_temp_bytes(n)); }
 
 int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
-                    void *work, size_t work_bytes, hipStream_t stream) {
+                    void *work, size_t work_bytes, hipStream_t stream, bool src_peer) {
     const int esz = elem_size(op);
     if (!esz || d.bytes <= 0 || d.bytes > kIovRunsMaxBytes || !d.dst_list) return -4;
     if (op != kOpCopy && !scale) return -5;
@@ -1338,19 +1359,20 @@ int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uin
     if (e != hipSuccess) return -100 - (int)e;
     d.run_key = kout;
     d.run_perm = vout;
-    return iov_dispatch(op, scale, W, d, false, stream);
+    return iov_dispatch(op, scale, W, d, false, src_peer, stream);
 }
 
-static int iov_dispatch(int op, const void *scale, int W, const IovDesc &d, bool serial, hipStream_t stream) {
+static int iov_dispatch(int op, const void *scale, int W, const IovDesc &d, bool serial, bool sys,
+                        hipStream_t stream) {
     hipError_t e;
     switch (op) {
-    case kOpCopy: e = iov_op(W, d, CopyOp{}, serial, stream); break;
-    case 37: { AccInt o; int32_t s; memcpy(&s, scale, 4); o.s = (uint32_t)s; e = iov_op(W, d, o, serial, stream); break; }
-    case 42: { AccLng o; int64_t s; memcpy(&s, scale, 8); o.s = (uint64_t)s; e = iov_op(W, d, o, serial, stream); break; }
-    case 39: { AccFlt o; memcpy(&o.s, scale, 4); e = iov_op(W, d, o, serial, stream); break; }
-    case 38: { AccDbl o; memcpy(&o.s, scale, 8); e = iov_op(W, d, o, serial, stream); break; }
-    case 40: { AccCpl o; float s[2]; memcpy(s, scale, 8); o.sr = s[0]; o.si = s[1]; e = iov_op(W, d, o, serial, stream); break; }
-    case 41: { AccDcp o; double s[2]; memcpy(s, scale, 16); o.sr = s[0]; o.si = s[1]; e = iov_op(W, d, o, serial, stream); break; }
+    case kOpCopy: e = iov_op(W, d, CopyOp{}, serial, sys, stream); break;
+    case 37: { AccInt o; int32_t s; memcpy(&s, scale, 4); o.s = (uint32_t)s; e = iov_op(W, d, o, serial, sys, stream); break; }
+    case 42: { AccLng o; int64_t s; memcpy(&s, scale, 8); o.s = (uint64_t)s; e = iov_op(W, d, o, serial, sys, stream); break; }
+    case 39: { AccFlt o; memcpy(&o.s, scale, 4); e = iov_op(W, d, o, serial, sys, stream); break; }
+    case 38: { AccDbl o; memcpy(&o.s, scale, 8); e = iov_op(W, d, o, serial, sys, stream); break; }
+    case 40: { AccCpl o; float s[2]; memcpy(s, scale, 8); o.sr = s[0]; o.si = s[1]; e = iov_op(W, d, o, serial, sys, stream); break; }
+    case 41: { AccDcp o; double s[2]; memcpy(s, scale, 16); o.sr = s[0]; o.si = s[1]; e = iov_op(W, d, o, serial, sys, stream); break; }
     default: return -4;
     }
     return e == hipSuccess ? 0 : -100 - (int)e;

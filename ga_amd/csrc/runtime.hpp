@@ -138,7 +138,9 @@ struct Runtime {
     // (pack into staging, the progress thread unpacks) as a remote one does;
     // PUT_SMP off also sends same-node puts that way instead of through the IPC
     // mapping.  (Same-node accumulates always take the packed route here.)
-    bool acc_self_direct = true, put_self_direct = true, put_smp_direct = true;
+    // ACC_SMP off also turns the direct-source route off (a same-node accumulate
+    // then always packs, comex.c:6911-6915)
+    bool acc_self_direct = true, acc_smp_direct = true, put_self_direct = true, put_smp_direct = true;
     // COMEX_AMD_DIRECT_SRC (default 1): a same-node accumulate whose source lies
     // in one of this rank's HBM segments is applied by the owner straight from
     // that segment (its IPC mapping) -- no pack pass, no staging
@@ -173,6 +175,19 @@ struct Runtime {
     std::thread progress;
     std::atomic<bool> stop{false};
     std::mutex launch_mu;
+    // devices: same_dev[q] = rank q's HIP device is this rank's physical GPU (PCI
+    // bus id), so its HBM is local memory here.  Another GPU's memory is only ever
+    // READ by this rank's kernels, with system-scope loads (peer_src), and every
+    // write into it is made by its owner: puts to it take the packed route.
+    // COMEX_AMD_PEER_LOADS: auto (default: per device), all (every other rank's
+    // memory as if on another GPU -- exercises that path on one GPU), off.
+    std::vector<uint8_t> same_dev;
+    int peer_loads = 0;                 // 0 auto, 1 all, 2 off
+    bool peer_src(int q) const {
+        if (q == rank || peer_loads == 2) return false;
+        return peer_loads == 1 || q >= (int)same_dev.size() || !same_dev[q];
+    }
+    int user_streams = 2;               // streams[0, user_streams): every operation; the rest: owner pulls
 };
 
 Runtime &rt();
@@ -184,10 +199,12 @@ void boot_barrier();
 void boot_finalize();
 
 // sched.cpp (callers hold launch_mu)
-void sched_init(int nstreams);
+void sched_init(int nstreams, int pull_streams = 0);
 void sched_fini();
 void sched_resize(int nstreams);
-int sched_pick(const Span &src, const Span &dst, uint64_t payload = 0);   // payload bytes of the op (0: unknown)   // stream index for an op
+// stream index for an op; payload = its bytes (0: unknown); prefer = stream for an
+// op with no dependency (owner pulls from a peer GPU: one stream per source rank)
+int sched_pick(const Span &src, const Span &dst, uint64_t payload = 0, int prefer = -1);
 void sched_join();
 void sched_sync_all();
 // completion marks (user thread): sequence number of an op just enqueued on

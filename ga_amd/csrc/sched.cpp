@@ -22,12 +22,14 @@
 //     little longer than its op, never shorter.  (An event per op put a marker
 //     packet between every two kernels: +1.7 us per 33 us launch measured on
 //     MI355X, profiles/r02/.)
-// Callers hold Runtime::launch_mu around pick + launch.  The marks are used by
-// the calling (user) thread only.
+// Callers hold Runtime::launch_mu around pick + launch.  The completion marks
+// have their own lock (g_marks_mu): sched_track / sched_complete run outside
+// launch_mu, and a wait on an event is done with the lock released.
 #include "runtime.hpp"
 #include <string.h>
 #include <stdlib.h>
 #include <deque>
+#include <algorithm>
 
 namespace gaamd {
 
@@ -59,8 +61,9 @@ struct Marks {
 };
 std::vector<Marks> g_marks;
 std::vector<hipEvent_t> g_mark_pool;
+std::mutex g_marks_mu;   // g_marks, g_mark_pool
 
-void marks_reset_done() {
+void marks_reset_done() {   // caller holds g_marks_mu
     for (Marks &m : g_marks) {
         m.done = m.marked = m.issued;
         for (const Mark &k : m.q) g_mark_pool.push_back(k.ev);
@@ -68,7 +71,7 @@ void marks_reset_done() {
     }
 }
 
-void mark_now(int s) {
+void mark_now(int s) {   // caller holds g_marks_mu
     Marks &m = g_marks[s];
     if (m.marked == m.issued) return;
     hipEvent_t e;
@@ -81,6 +84,7 @@ void mark_now(int s) {
 }  // namespace
 
 uint64_t sched_track(int s) {
+    std::lock_guard<std::mutex> g(g_marks_mu);
     if (s < 0 || s >= (int)g_marks.size()) return 0;
     Marks &m = g_marks[s];
     const uint64_t seq = ++m.issued;
@@ -89,13 +93,25 @@ uint64_t sched_track(int s) {
 }
 
 bool sched_complete(int s, uint64_t seq, bool wait) {
+    std::unique_lock<std::mutex> g(g_marks_mu);
     if (seq == 0 || s < 0 || s >= (int)g_marks.size()) return true;
     Marks &m = g_marks[s];
     if (seq <= m.done) return true;
     if (m.marked < seq) mark_now(s);   // no event covers it yet
     while (!m.q.empty()) {
         const Mark k = m.q.front();
-        const hipError_t e = wait ? hipEventSynchronize(k.ev) : hipEventQuery(k.ev);
+        hipError_t e = hipEventQuery(k.ev);
+        if (e == hipErrorNotReady && wait) {
+            // wait without the lock; the event is not recycled meanwhile (it stays
+            // in the queue until someone sees it complete, under the lock)
+            g.unlock();
+            e = hipEventSynchronize(k.ev);
+            g.lock();
+            if (m.q.empty() || m.q.front().ev != k.ev) {   // another thread retired it
+                if (m.done >= seq) return true;
+                continue;
+            }
+        }
         if (e == hipErrorNotReady) return false;
         if (e != hipSuccess) fatal("operation failed: %s", hipGetErrorString(e));
         m.done = k.seq;
@@ -106,10 +122,14 @@ bool sched_complete(int s, uint64_t seq, bool wait) {
     return m.done >= seq;
 }
 
-void sched_init(int n) {
+void sched_init(int n, int pull) {
     Runtime &r = rt();
     if (n < 1) n = 1;
     if (n > 8) n = 8;
+    if (pull < 0) pull = 0;
+    if (pull > 8) pull = 8;
+    r.user_streams = n;
+    n += pull;
     r.streams.assign(1, r.stream);
     for (int i = 1; i < n; ++i) {
         hipStream_t s;
@@ -118,6 +138,7 @@ void sched_init(int n) {
     }
     g_ev.assign(n, nullptr);
     for (int i = 0; i < n; ++i) GA_HIP(hipEventCreateWithFlags(&g_ev[i], hipEventDisableTiming));
+    std::lock_guard<std::mutex> g(g_marks_mu);
     g_marks.assign(n, Marks());
     g_hist.clear();
     g_rr = 0;
@@ -126,11 +147,12 @@ void sched_init(int n) {
 
 // change the number of library streams at run time (all work drained first)
 void sched_resize(int n) {
+    Runtime &r = rt();
+    const int pull = (int)r.streams.size() - r.user_streams;
     sched_sync_all();
     sched_fini();
-    Runtime &r = rt();
     r.streams.clear();
-    sched_init(n);
+    sched_init(n, pull);
 }
 
 void sched_fini() {
@@ -138,6 +160,7 @@ void sched_fini() {
     for (size_t i = 1; i < r.streams.size(); ++i) (void)hipStreamDestroy(r.streams[i]);
     for (hipEvent_t e : g_ev) (void)hipEventDestroy(e);
     g_ev.clear();
+    std::lock_guard<std::mutex> g(g_marks_mu);
     marks_reset_done();
     for (hipEvent_t e : g_mark_pool) (void)hipEventDestroy(e);
     g_mark_pool.clear();
@@ -169,7 +192,10 @@ void sched_sync_all() {
     // latency: the floor is the GPU's launch-to-completion, not the host wake-up)
     for (hipStream_t s : r.streams) GA_HIP(hipStreamSynchronize(s));
     for (uint8_t &p : r.direct_pending) p = 0;   // every put/get kernel has finished
-    marks_reset_done();                           // every tracked op is complete
+    {
+        std::lock_guard<std::mutex> g(g_marks_mu);
+        marks_reset_done();                       // every tracked op is complete
+    }
     g_hist.clear();
     g_base = -1;
 }
@@ -185,10 +211,11 @@ constexpr uint64_t kBigPayload = 192ull << 20;
 // gained from 16 MiB on (tools/perf_strided.cpp, profiles/r01/perf_strided.jsonl).
 constexpr uint64_t kSmallPayload = 8ull << 20;
 
-int sched_pick(const Span &src, const Span &dst, uint64_t payload) {
+int sched_pick(const Span &src, const Span &dst, uint64_t payload, int prefer) {
     Runtime &r = rt();
     const int n = (int)r.streams.size();
     if (n <= 1) return 0;
+    const int nu = std::max(1, std::min(r.user_streams, n));   // round robin over the user streams
     if ((int)g_hist.size() >= kHist) {
         const int s0 = g_hist.front().stream;
         bool one = g_base < 0 || g_base == s0;
@@ -211,8 +238,12 @@ int sched_pick(const Span &src, const Span &dst, uint64_t payload) {
     }
     int s;
     if (!mask) {
-        if (payload == 0 || (payload >= kSmallPayload && payload < kBigPayload)) g_rr = (g_rr + 1) % n;
-        s = g_rr;
+        if (prefer >= 0 && prefer < n) {
+            s = prefer;
+        } else {
+            if (payload == 0 || (payload >= kSmallPayload && payload < kBigPayload)) g_rr = (g_rr + 1) % nu;
+            s = g_rr % nu;
+        }
     } else {
         s = last;   // the most recent dependency's stream; wait for the others
         for (int x = 0; x < n; ++x)

@@ -7,10 +7,10 @@
  * comex/src-armci/capi.c wraps is a weak alias of PARMCI_X here too, so
  * PMPI-style interposers (comex/tools/armci_prof.c, GA's WAPI layer) keep
  * working.  Differences, all where the reference has no MPI-free meaning:
- *   - ARMCI_Init_mpi_comm takes the communicator as an opaque word and
- *     initialises over the launcher's bootstrap (no MPI underneath);
- *   - armci_group_comm (MPI_Comm of a group) is declared only when <mpi.h>
- *     was included first, and aborts: there is no communicator to return;
+ *   - ARMCI_Init_mpi_comm / armci_group_comm take / return an MPI_Comm and are
+ *     declared only when <mpi.h> was included first (no <mpi.h> dependency
+ *     otherwise); the library itself has no MPI link dependency and uses the
+ *     caller's MPI (MPICH ABI) only through these calls (ga_amd/csrc/mpi_bridge.cpp);
  *   - ARMCI_PutS_flag / _flag_dir / ARMCI_Put_flag are implemented (put, then
  *     the flag after remote completion) where the reference asserts;
  *   - ARMCI_Same_node returns 0 exactly as the reference (no direct load/store
@@ -126,9 +126,11 @@ extern int ARMCI_Free_local(void *ptr);
 /* contiguity collapse used by the strided wrappers (comex/src-armci/armci.c:114) */
 extern int armci_check_contiguous(int *src_stride, int *dst_stride, int *count, int n_stride);
 
-/* init over an external communicator (armci.h:33): an opaque word here */
-extern int ARMCI_Init_mpi_comm(long comm);
 #ifdef MPI_VERSION
+/* init over an external communicator (armci.h:28; armci.c:427-440): the
+ * communicator's ranks are ARMCI's world; 1 on success */
+extern int ARMCI_Init_mpi_comm(MPI_Comm comm);
+/* the group's communicator (groups.c); world: a dup of the init communicator */
 extern MPI_Comm armci_group_comm(ARMCI_Group *group);
 #endif
 
@@ -247,7 +249,9 @@ extern int PARMCI_Free(void *ptr);
 extern int PARMCI_Free_memdev(void *ptr);
 extern void *PARMCI_Malloc_local(armci_size_t bytes);
 extern int PARMCI_Free_local(void *ptr);
-extern int PARMCI_Init_mpi_comm(long comm);
+#ifdef MPI_VERSION
+extern int PARMCI_Init_mpi_comm(MPI_Comm comm);
+#endif
 extern void PARMCI_GroupFence(ARMCI_Group *group);
 extern int PARMCI_Create_mutexes(int num);
 extern int PARMCI_Destroy_mutexes();

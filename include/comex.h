@@ -9,7 +9,8 @@
  *   - `extern "C"` (the reference writes `extern "c"`, comex.h:10, which does
  *     not compile as C++);
  *   - no <mpi.h> dependency: comex_init_comm / comex_group_comm are declared
- *     only when the includer has already included <mpi.h>;
+ *     only when the includer has already included <mpi.h> (MPICH ABI; the
+ *     library looks the caller's MPI functions up at the call);
  *   - segments from comex_malloc live in the owner GPU's HBM (hipMalloc),
  *     exported to the other ranks of the node by IPC handle.
  */
@@ -58,6 +59,7 @@ typedef int comex_group_t;     /* comex.h:22 */
 extern int comex_init();
 extern int comex_init_args(int *argc, char ***argv);
 #ifdef MPI_VERSION
+/* comex.h:58 (comex.c:726-730): the communicator's ranks are ComEx's world */
 extern int comex_init_comm(MPI_Comm comm);
 #endif
 extern int comex_initialized();
@@ -74,7 +76,8 @@ extern int comex_group_translate_world(comex_group_t group, int group_rank, int 
 extern int comex_group_translate_ranks(int n, comex_group_t group_from, int *ranks_from,
                                        comex_group_t group_to, int *ranks_to);
 #ifdef MPI_VERSION
-/* comex.h:147: aborts -- libga_amd bootstraps without MPI, there is no communicator */
+/* comex.h:147: the group's communicator; only after comex_init_comm (a runtime
+ * bootstrapped without MPI has none, and the call aborts) */
 extern int comex_group_comm(comex_group_t group, MPI_Comm *comm);
 #endif
 extern int comex_barrier(comex_group_t group);

@@ -39,6 +39,10 @@ typedef int (*gaamd_allgather_fn)(const void *send, void *recv, size_t bytes, vo
 typedef int (*gaamd_barrier_fn)(void *ctx);
 int gaamd_set_bootstrap(int rank, int size, int local_rank,
                         gaamd_allgather_fn allgather, gaamd_barrier_fn barrier, void *ctx);
+#ifdef MPI_VERSION
+/* hooks over an MPI communicator (the bootstrap half of comex_init_comm, no GPU) */
+int gaamd_set_bootstrap_comm(MPI_Comm comm);
+#endif
 /* exercise the bootstrap alone (no GPU): allgather of ranks + barriers */
 int gaamd_bootstrap_selftest(int rounds);
 int gaamd_rank(void);

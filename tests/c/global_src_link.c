@@ -10,10 +10,19 @@
  * macro of armci.h; ARMCI_PutS_flag__ (ghosts.c:2442) is GA's own function.
  *
  * Nothing is called: the table only takes each function's address, so the
- * program links and runs without a GPU.
+ * program links and runs without a GPU.  Built twice by tests/test_abi.py: as
+ * is, and with WITH_MPI (MPICH's <mpi.h> first), where the communicator entry
+ * points (ARMCI_Init_mpi_comm, armci_group_comm, comex_init_comm,
+ * comex_group_comm) are declared too and must resolve without an MPI library.
  */
+#ifdef WITH_MPI
+#include <mpi.h>
+#endif
 #include <stdio.h>
 #include "armci.h"
+#ifdef WITH_MPI
+#include "comex.h"
+#endif
 #include "message.h"
 
 typedef void (*fn_t)(void);
@@ -89,7 +98,12 @@ static const struct { const char *name; fn_t fn; } table[] = {
     {"ARMCI_Malloc_group_memdev", (fn_t)ARMCI_Malloc_group_memdev},
     {"ARMCI_Lock", (fn_t)ARMCI_Lock},
     {"ARMCI_Initialized", (fn_t)ARMCI_Initialized},
+#ifdef WITH_MPI
     {"ARMCI_Init_mpi_comm", (fn_t)ARMCI_Init_mpi_comm},
+    {"armci_group_comm", (fn_t)armci_group_comm},
+    {"comex_init_comm", (fn_t)comex_init_comm},
+    {"comex_group_comm", (fn_t)comex_group_comm},
+#endif
     {"ARMCI_Init", (fn_t)ARMCI_Init},
     {"ARMCI_Group_set_default", (fn_t)ARMCI_Group_set_default},
     {"ARMCI_Group_free", (fn_t)ARMCI_Group_free},

@@ -96,6 +96,12 @@ def main():
         ga_ref_test(L, rank, size)
     elif mode == "order":
         order_test(L, rank, size)
+    elif mode == "selforder":
+        self_order_test(L, rank, size)
+    elif mode == "c1":
+        c1_test(L, rank, size)
+    elif mode == "c5full":
+        c5_full_test(L, rank, size)
     elif mode == "directsrc":
         direct_src_test(L, rank, size)
     elif mode in ("armcimisc", "armcimisc-gloo"):
@@ -310,6 +316,207 @@ def order_test(L, rank, size):
         say(rank, f"order round {it} checked")
     ga_amd.comex_barrier()
     assert ga_amd.comex_free(seg[rank]) == 0
+    ga_amd.comex_finalize()
+
+
+def c1_test(L, rank, size):
+    """BASELINE config C1: 1-D contiguous f64 accumulate of 1 MiB
+    (131 072 elements) between ranks, rank r -> rank (r+1) % size, the survey's
+    synthetic data (splitmix64, seed 0x5EED0000 + rank, dst seed + 1; alpha =
+    0.7071067811865476), bit-exact against the oracle's _acc (acc.h:137-143) on
+    the same bytes.  One source per target, so the order is fixed and the f64
+    result exact.  Three source kinds, each into a fresh dst: pageable host memory
+    (MA-style, the packed route), a plain device buffer (packed route) and the
+    rank's own segment (1 MiB: the direct-source route's threshold)."""
+    import ga_amd
+    import cases as C
+    from oracle import Oracle
+    ora = Oracle()
+    DBL, n = 38, 131072
+    nbytes = n * 8
+    alpha = 0.7071067811865476
+    assert ga_amd.comex_init() == 0
+    seg = ga_amd.comex_malloc(nbytes, size)
+    srcseg = ga_amd.comex_malloc(nbytes, size)
+    nxt, prv = (rank + 1) % size, (rank - 1) % size
+    src = C.fill_real(np.float64, n, C.SEED + rank)
+    dst0 = C.fill_real(np.float64, n, C.SEED + rank + 1)       # this rank's own dst (seed + 1)
+    want = dst0.copy()
+    ora_src = C.fill_real(np.float64, n, C.SEED + prv)         # what the previous rank sends us
+    sc = np.array([alpha])
+    dbuf = ga_amd.DeviceBuffer(nbytes)
+    dbuf.upload(src)
+    assert L.gaamd_memcpy(ctypes.c_void_p(srcseg[rank]), src.ctypes.data_as(ctypes.c_void_p), nbytes) == 0
+    routes = []
+    for kind in ("host", "device", "segment"):
+        assert L.gaamd_memcpy(ctypes.c_void_p(seg[rank]), dst0.ctypes.data_as(ctypes.c_void_p), nbytes) == 0
+        ga_amd.comex_barrier()
+        r0 = ga_amd.route_counts()
+        sp = {"host": src.ctypes.data, "device": dbuf.ptr, "segment": srcseg[rank]}[kind]
+        assert ga_amd.comex_acc(DBL, alpha, sp, seg[nxt], nbytes, nxt) == 0
+        ga_amd.comex_barrier()
+        r1 = ga_amd.route_counts()
+        routes.append((kind, {k: r1[k] - r0[k] for k in r1}))
+        got = np.zeros(n)
+        assert L.comex_get(ctypes.c_void_p(seg[rank]), got.ctypes.data_as(ctypes.c_void_p), nbytes, rank, 0) == 0
+        w = dst0.copy()
+        assert ora.L.ora_acc(DBL, nbytes, w.ctypes.data_as(ctypes.c_void_p), ora_src.ctypes.data_as(ctypes.c_void_p),
+                             sc.ctypes.data_as(ctypes.c_void_p)) == 0
+        assert np.array_equal(got.view(np.uint64), w.view(np.uint64)), f"rank {rank}: C1 {kind} source not bit-exact"
+        ga_amd.comex_barrier()
+    if size > 1:
+        d = dict(routes)
+        assert d["host"]["packed"] > 0 and d["device"]["packed"] > 0 and d["segment"]["direct_src"] > 0, routes
+    say(rank, f"C1 1 MiB f64 remote acc bit-exact; routes {routes}")
+    dbuf.free()
+    ga_amd.comex_barrier()
+    assert ga_amd.comex_free(srcseg[rank]) == 0
+    assert ga_amd.comex_free(seg[rank]) == 0
+    ga_amd.comex_finalize()
+
+
+def c5_full_test(L, rank, size):
+    """BASELINE config C5 at its stated size: NGA_Acc into a 32768 x 32768 f64 GA
+    (8 GiB, REGULAR distribution over `size` ranks, ddb_h2 grid: 4 x 2 blocks of
+    8192 x 16384 = 1 GiB at 8 ranks), every rank on this one GPU.
+      M1: every rank NGA_Acc's its own block from a device buffer of the constant
+          2**rank (alpha 1): the block must read 2**rank exactly.
+      M2: every rank NGA_Acc's the WHOLE array from an 8 GiB source of 2**rank --
+          even ranks from a plain device buffer (packed route: pack -> staging ->
+          owner unpack-acc), odd ranks from their own comex segment (direct-source
+          route: the owner reads it in place) -- so every element must read exactly
+          2**size - 1; a lost, doubled or stale contribution shows as a wrong value
+          that says whose (onesided.c:1387-1440; comex.c:6965-7109, 4133-4281)."""
+    import time
+    import ga_amd
+    ia = ga_amd.int_array
+    C_DBL = 1004
+    n = int(os.environ.get("TEST_C5_N", "32768"))
+    assert L.GA_Initialize() == 0
+    if os.environ.get("TEST_DISTINCT_DEVICES"):
+        assert L.gaamd_device() == rank, (L.gaamd_device(), rank)
+    t0 = time.perf_counter()
+    g = L.NGA_Create(C_DBL, 2, ia([n, n]), b"C5", None)
+    assert g > 0
+    blo, bhi = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
+    L.NGA_Distribution(g, rank, blo, bhi)
+    rows, cols = bhi[0] - blo[0] + 1, bhi[1] - blo[1] + 1
+    if size == 8 and n == 32768:
+        assert (rows, cols) == (8192, 16384), (rows, cols)   # the 4 x 2 grid of ddb_h2 (SURVEY 8(a) a15)
+    L.GA_Zero(g)
+    L.GA_Sync()
+
+    def check_block(want, what):
+        out = np.empty(rows * cols)
+        L.NGA_Get(g, blo, bhi, out.ctypes.data_as(ctypes.c_void_p), ia([cols]))
+        bad = np.count_nonzero(out != want)
+        assert bad == 0, f"rank {rank} {what}: {bad} wrong elements, e.g. {out[np.nonzero(out != want)[0][0]]} != {want}"
+
+    # M1: own block, device-resident source
+    one = ctypes.c_double(1.0)
+    b1 = ga_amd.DeviceBuffer(rows * cols * 8)
+    ga_amd.fill_const(b1.ptr, rows * cols * 8, float(2 ** rank))
+    ga_amd.sync()
+    L.GA_Sync()
+    t1 = time.perf_counter()
+    L.NGA_Acc(g, blo, bhi, ctypes.c_void_p(b1.ptr), ia([cols]), ctypes.byref(one))
+    L.GA_Sync()
+    t_m1 = time.perf_counter() - t1
+    check_block(float(2 ** rank), "M1")
+    b1.free()
+    L.GA_Zero(g)
+    L.GA_Sync()
+    say(rank, f"C5 M1 exact ({rows}x{cols} block, {t_m1 * 1e3:.0f} ms)")
+
+    # M2: the whole array from every rank; even ranks packed, odd ranks direct-source
+    whole = n * n * 8
+    use_seg = rank % 2 == 1
+    seg = ga_amd.comex_malloc(whole if use_seg else 0, size)
+    if use_seg:
+        ptr, buf = seg[rank], None
+    else:
+        buf = ga_amd.DeviceBuffer(whole)
+        ptr = buf.ptr
+    ga_amd.fill_const(ptr, whole, float(2 ** rank))
+    ga_amd.sync()
+    L.GA_Sync()
+    r0 = ga_amd.route_counts()
+    t1 = time.perf_counter()
+    L.NGA_Acc(g, ia([0, 0]), ia([n - 1, n - 1]), ctypes.c_void_p(ptr), ia([n]), ctypes.byref(one))
+    L.GA_Sync()
+    t_m2 = time.perf_counter() - t1
+    r1 = ga_amd.route_counts()
+    routes = {k: r1[k] - r0[k] for k in r1}
+    check_block(float(2 ** size - 1), "M2")
+    if size > 1:
+        if use_seg:
+            assert routes["direct_src"] > 0 and routes["packed"] == 0, routes
+        else:
+            assert routes["packed"] > 0 and routes["direct_src"] == 0, routes
+    L.GA_Sync()
+    if buf is not None:
+        buf.free()
+    assert ga_amd.comex_free(seg[rank]) == 0
+    L.GA_Destroy(g)
+    say(rank, f"C5 M2 exact ({'direct-source' if use_seg else 'packed'} route {routes}, {t_m2:.1f} s; "
+              f"total {time.perf_counter() - t0:.1f} s)")
+    L.GA_Terminate()
+
+
+def self_order_test(L, rank, size):
+    """Run with COMEX_ENABLE_{ACC,PUT}_{SELF,SMP}=0: puts and accumulates to this
+    rank's own segment take the packed route (the progress thread applies them
+    after the call returns).  With NO barrier or fence in between, a put to self,
+    then an accumulate to self, then a get / an io-vector get / an rmw on the same
+    bytes must see them applied (the reference flushes before a
+    self/SMP operation, comex.c:6073-6080, 6228-6235).  32 MiB patches, so the
+    packed chunks are still in flight when the direct operation is issued.  Also,
+    a same-node accumulate of >= 1 MiB from a segment source must take the packed
+    route with COMEX_ENABLE_ACC_SMP=0 (comex.c:6911-6915), not the direct-source one."""
+    import ga_amd
+    DBL = 38
+    assert ga_amd.comex_init() == 0
+    n = 4 << 20                                   # 4 Mi f64 = 32 MiB
+    seg = ga_amd.comex_malloc(n * 8, size)
+    me = seg[rank]
+    for it in range(3):
+        a = (np.arange(n, dtype=np.float64) % 4093) + it
+        b = (np.arange(n, dtype=np.float64) % 511) - 255
+        assert L.comex_put(a.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(me), n * 8, rank, 0) == 0
+        assert L.comex_acc(DBL, ctypes.byref(ctypes.c_double(3.0)), b.ctypes.data_as(ctypes.c_void_p),
+                           ctypes.c_void_p(me), n * 8, rank, 0) == 0
+        got = np.zeros(n, dtype=np.float64)
+        assert L.comex_get(ctypes.c_void_p(me), got.ctypes.data_as(ctypes.c_void_p), n * 8, rank, 0) == 0
+        want = a + 3.0 * b
+        assert np.array_equal(got, want), f"rank {rank} round {it}: get overtook the packed put/acc to self"
+        # the same through an io-vector get of the last 1000 elements
+        a2 = a + 7
+        assert L.comex_put(a2.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(me), n * 8, rank, 0) == 0
+        tail = np.zeros(1000, dtype=np.float64)
+        descs = [([me + (n - 1000 + i) * 8 for i in range(1000)], [tail.ctypes.data + i * 8 for i in range(1000)], 8)]
+        assert ga_amd.comex_getv(descs, rank) == 0
+        assert np.array_equal(tail, a2[-1000:]), f"rank {rank} round {it}: getv overtook the packed put to self"
+        # and an rmw on the first word right after a packed put of it
+        one = np.zeros(2, dtype=np.int64)
+        one[0] = 40 + it
+        assert L.comex_put(one.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(me), 16, rank, 0) == 0
+        old = ctypes.c_long(0)
+        assert L.comex_rmw(13, ctypes.byref(old), ctypes.c_void_p(me), 5, rank, 0) == 0   # COMEX_FETCH_AND_ADD_LONG
+        assert old.value == 40 + it, (old.value, it)
+    before = ga_amd.route_counts()
+    ga_amd.comex_barrier()
+    if size > 1:
+        # >= 1 MiB same-node accumulate whose source is in our segment: with ACC_SMP=0 packed
+        nxt = (rank + 1) % size
+        src2 = ga_amd.comex_malloc(n * 8, size)
+        assert L.comex_acc(DBL, ctypes.byref(ctypes.c_double(1.0)), ctypes.c_void_p(src2[rank]), ctypes.c_void_p(seg[nxt]),
+                           n * 8, nxt, 0) == 0
+        after = ga_amd.route_counts()
+        assert after["direct_src"] == before["direct_src"] and after["packed"] > before["packed"], (before, after)
+        ga_amd.comex_barrier()
+        assert ga_amd.comex_free(src2[rank]) == 0
+    ga_amd.comex_barrier()
+    assert ga_amd.comex_free(me) == 0
     ga_amd.comex_finalize()
 
 

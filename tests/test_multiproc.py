@@ -91,15 +91,43 @@ def test_remote_put_then_acc_same_patch_no_fence():
 
 
 @pytest.mark.gpu
-def test_remote_across_two_devices():
-    """Two ranks on two distinct MI355X: each opens the other's segment and
-    staging by IPC on another device and runs remote acc/put/get/accv/getv/putv
-    over xGMI.  Needs a box with at least two GPUs (skipped on one)."""
+def test_remote_across_devices():
+    """One rank per MI355X of the box (2..8): each opens the others' segments and
+    staging by IPC on other devices; remote acc/put/get/accv/getv/putv over xGMI
+    (peer memory read with system-scope loads, puts applied by the owner), the
+    put/acc ordering case, and the full-size C5 exchange check (32768^2 f64 GA,
+    M1 + M2 on both routes, exact).  Needs a multi-GPU box (skipped on one)."""
     import ga_amd
-    if ga_amd.lib().gaamd_device_count() < 2:
-        pytest.skip("one GPU visible: the two-device case needs a multi-GPU node")
-    launch("remote", n=2, timeout=120, extra_env={"TEST_DISTINCT_DEVICES": "1"})
-    launch("order", n=2, timeout=120)
+    ndev = ga_amd.lib().gaamd_device_count()
+    if ndev < 2:
+        pytest.skip("one GPU visible: the cross-device case needs a multi-GPU node")
+    n = min(ndev, 8)
+    launch("remote", n=n, timeout=180, extra_env={"TEST_DISTINCT_DEVICES": "1"})
+    launch("order", n=n, timeout=180)
+    launch("c5full", n=n, timeout=420, extra_env={"COMEX_AMD_STAGING_MB": "256", "TEST_DISTINCT_DEVICES": "1"})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,n", [("remote", 2), ("remote", 3), ("order", 2), ("directsrc", 3), ("c1", 2),
+                                    ("stress", 3), ("scatremote", 3)])
+def test_cross_device_path_forced_on_one_gpu(mode, n):
+    """COMEX_AMD_PEER_LOADS=all treats every other rank's memory as another GPU's
+    (the path test_remote_across_devices takes on a multi-GPU node): the owner
+    reads peer staging / segments with system-scope loads, on its pull streams,
+    pulling ordered chunks and io-vector requests into local scratch first; puts
+    and putv into peer memory go through the owner; gets/getv read with
+    system-scope loads.  Same exact checks as the ordinary runs."""
+    env = {"COMEX_AMD_PEER_LOADS": "all"}
+    if mode == "stress":
+        env["COMEX_AMD_STAGING_MB"] = "1"
+    launch(mode, n=n, timeout=180, extra_env=env)
+
+
+@pytest.mark.gpu
+def test_cross_device_c5_exchange_forced_on_one_gpu():
+    """The C5 exchange (M1 + M2, both routes, exact) on 4 ranks with every other
+    rank's memory treated as another GPU's (COMEX_AMD_PEER_LOADS=all), 8192^2 GA."""
+    launch("c5full", n=4, timeout=240, extra_env={"COMEX_AMD_PEER_LOADS": "all", "TEST_C5_N": "8192"})
 
 
 @pytest.mark.gpu
@@ -236,6 +264,37 @@ def test_packed_route_forced_by_comex_enable_toggles(n):
                "COMEX_ENABLE_PUT_SMP": "0", "COMEX_AMD_VERBOSE": "1"}
     outs = launch("remote", n=n, timeout=120, extra_env=toggles)
     assert "acc to self packed, put to self packed, same-node put packed" in outs[0], outs[0][-2000:]
+
+
+@pytest.mark.gpu
+def test_config_c1_one_mib_remote_acc_two_ranks():
+    """BASELINE config C1: a 1-D contiguous f64 accumulate of 1 MiB from rank 0 to
+    rank 1 and back (2 ranks, one GPU), the survey's synthetic data, bit-exact
+    against the oracle; host, device and segment sources (packed and
+    direct-source routes)."""
+    launch("c1", n=2, timeout=120)
+
+
+@pytest.mark.gpu
+def test_config_c5_full_size_eight_ranks_one_gpu():
+    """BASELINE config C5 at its stated size: NGA_Acc into a 32768^2 f64 GA on 8 ranks
+    sharing this GPU -- M1 (own 1 GiB block) and M2 (every rank the whole 8 GiB
+    array; half the ranks on the packed route, half on the direct-source route),
+    checked exactly with the 2**rank scheme."""
+    launch("c5full", n=8, timeout=420, extra_env={"COMEX_AMD_STAGING_MB": "256"})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2])
+def test_direct_ops_on_self_after_packed_self_traffic(n):
+    """COMEX_ENABLE_{ACC,PUT}_{SELF,SMP}=0: a put and an accumulate to this rank take
+    the packed route; a get, an io-vector get and an rmw on the same bytes issued
+    right after (no barrier, no fence) see them applied (the
+    reference flushes first, comex.c:6073-6080, 6228-6235).  With ACC_SMP=0 a
+    >= 1 MiB same-node accumulate from a segment takes the packed route too."""
+    toggles = {"COMEX_ENABLE_ACC_SELF": "0", "COMEX_ENABLE_ACC_SMP": "0", "COMEX_ENABLE_PUT_SELF": "0",
+               "COMEX_ENABLE_PUT_SMP": "0", "COMEX_AMD_STAGING_MB": "64"}
+    launch("selforder", n=n, timeout=150, extra_env=toggles)
 
 
 @pytest.mark.gpu
