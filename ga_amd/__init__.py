@@ -162,7 +162,7 @@ def route_counts():
     """requests this rank posted to same-node owners, by route"""
     c = (ctypes.c_ulonglong * 4)()
     lib().gaamd_route_counts(c)
-    return {"packed": c[0], "direct_src": c[1], "iov": c[2], "rmw": c[3]}
+    return {"packed": c[0], "direct_src": c[1], "iov": c[2], "rmw": c[3], "one_pass": lib().gaamd_one_pass_count()}
 
 
 def owner_counts():

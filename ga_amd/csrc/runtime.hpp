@@ -88,6 +88,12 @@ struct alignas(64) NodeShm {
     // done[s][t]: requests from s applied by t (monotonic); s, t = positions on the node
     std::atomic<uint64_t> done[kMaxRanks][kMaxRanks];
     RmwReply rmw[kMaxRanks];         // indexed by the requester's position on the node
+    // one-pass accumulates between ranks sharing a GPU (comex.cpp one_pass_acc):
+    // mem_lock[t] = 0 free, 1 + p held by node position p (the owner t itself while
+    // its own writes into its segments may be in flight, or a requester while its
+    // kernel writing t's segment runs); mem_want[t] = requesters waiting for it
+    std::atomic<uint32_t> mem_lock[kMaxRanks];
+    std::atomic<uint32_t> mem_want[kMaxRanks];
     Inbox inbox[1];                  // [size] follows; then boot data area
 };
 
@@ -188,6 +194,11 @@ struct Runtime {
         return peer_loads == 1 || q >= (int)same_dev.size() || !same_dev[q];
     }
     int user_streams = 2;               // streams[0, user_streams): every operation; the rest: owner pulls
+    // one-pass accumulate into a segment of a rank on THIS GPU (COMEX_AMD_ONE_PASS,
+    // default on when such a rank exists): the requester's fused kernel writes the
+    // owner's segment, under the owner's node-shm memory lock (NodeShm::mem_lock)
+    bool one_pass = false;
+    bool own_holds = false;             // this process holds its own mem_lock (launch_mu)
 };
 
 Runtime &rt();
@@ -202,6 +213,10 @@ void boot_finalize();
 void sched_init(int nstreams, int pull_streams = 0);
 void sched_fini();
 void sched_resize(int nstreams);
+// comex.cpp: before a launch that writes `dst` (caller holds launch_mu): a write
+// into one of this rank's segments takes this rank's memory lock when a rank on the
+// same GPU may write them too (one-pass accumulates); a no-op otherwise
+void own_write_guard(const Span &dst);
 // stream index for an op; payload = its bytes (0: unknown); prefer = stream for an
 // op with no dependency (owner pulls from a peer GPU: one stream per source rank)
 int sched_pick(const Span &src, const Span &dst, uint64_t payload = 0, int prefer = -1);

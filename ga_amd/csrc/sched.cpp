@@ -213,6 +213,7 @@ constexpr uint64_t kSmallPayload = 8ull << 20;
 
 int sched_pick(const Span &src, const Span &dst, uint64_t payload, int prefer) {
     Runtime &r = rt();
+    own_write_guard(dst);
     const int n = (int)r.streams.size();
     if (n <= 1) return 0;
     const int nu = std::max(1, std::min(r.user_streams, n));   // round robin over the user streams

@@ -85,6 +85,8 @@ int gaamd_kernel_counts(unsigned long long counts[5]);
  * {packed chunks (pack -> staging -> owner unpack), direct-source (owner reads
  * our segment), io-vector, rmw} */
 int gaamd_route_counts(unsigned long long counts[4]);
+/* one-pass accumulates this rank applied into the segment of a rank on the same GPU */
+unsigned long long gaamd_one_pass_count(void);
 /* same-node peers whose staging buffer this rank could not map by IPC at
  * comex_init (remote accumulates to or from them would abort); -1 before init */
 int gaamd_peers_unmapped(void);

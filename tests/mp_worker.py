@@ -100,6 +100,8 @@ def main():
         self_order_test(L, rank, size)
     elif mode == "c1":
         c1_test(L, rank, size)
+    elif mode == "onepass":
+        one_pass_test(L, rank, size)
     elif mode == "c5full":
         c5_full_test(L, rank, size)
     elif mode == "directsrc":
@@ -319,6 +321,67 @@ def order_test(L, rank, size):
     ga_amd.comex_finalize()
 
 
+def one_pass_expected():
+    """ranks on one GPU with the one-pass route enabled (see comex.cpp one_pass_acc)"""
+    return (not os.environ.get("TEST_DISTINCT_DEVICES") and os.environ.get("COMEX_AMD_PEER_LOADS") != "all"
+            and os.environ.get("COMEX_AMD_ONE_PASS", "1") != "0")
+
+
+def one_pass_test(L, rank, size):
+    """Ranks sharing one GPU: accumulates from plain device
+    buffers into other ranks' segments take the one-pass route (the requester's
+    fused kernel writes the owner's block under the owner's memory lock), while
+    every owner keeps accumulating into its own block too.  Every rank adds the
+    constant 2**rank into EVERY rank's 8 MiB block (itself included), ROUNDS
+    times, blocking and non-blocking alternately, no barrier in between: a lost
+    update (two unexcluded read-modify-writes of one element) shows as a wrong
+    sum; each element must read exactly ROUNDS * (2**size - 1)."""
+    import ga_amd
+    DBL = 38
+    assert ga_amd.comex_init() == 0
+    n = 1 << 20                               # 8 MiB of f64 per block
+    rounds = 12
+    seg = ga_amd.comex_malloc(n * 8, size)
+    zero = np.zeros(n)
+    assert L.comex_put(zero.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(seg[rank]), n * 8, rank, 0) == 0
+    ga_amd.comex_barrier()
+    src = ga_amd.DeviceBuffer(n * 8)
+    ga_amd.fill_const(src.ptr, n * 8, float(2 ** rank))
+    ga_amd.sync()
+    r0 = ga_amd.route_counts()
+    one = ctypes.c_double(1.0)
+    handles = []
+    for it in range(rounds):
+        for k in range(size):
+            t = (rank + k + it) % size           # every rank visits the targets in a different order
+            if it % 2:
+                h = ctypes.c_int(-1)
+                assert L.comex_nbacc(38, ctypes.byref(one), ctypes.c_void_p(src.ptr), ctypes.c_void_p(seg[t]), n * 8,
+                                     t, 0, ctypes.byref(h)) == 0
+                handles.append(h)
+            else:
+                assert L.comex_acc(DBL, ctypes.byref(one), ctypes.c_void_p(src.ptr), ctypes.c_void_p(seg[t]), n * 8,
+                                   t, 0) == 0
+        while len(handles) > 8:
+            assert L.comex_wait(ctypes.byref(handles.pop(0))) == 0
+    for h in handles:
+        assert L.comex_wait(ctypes.byref(h)) == 0
+    ga_amd.comex_barrier()
+    r1 = ga_amd.route_counts()
+    got = np.zeros(n)
+    assert L.comex_get(ctypes.c_void_p(seg[rank]), got.ctypes.data_as(ctypes.c_void_p), n * 8, rank, 0) == 0
+    want = float(rounds * (2 ** size - 1))
+    bad = int(np.count_nonzero(got != want))
+    assert bad == 0, f"rank {rank}: {bad} wrong, e.g. {got[np.nonzero(got != want)[0][0]]} != {want}"
+    if size > 1 and one_pass_expected():
+        assert r1["one_pass"] - r0["one_pass"] == rounds * (size - 1), (r0, r1)
+    say(rank, f"one-pass exchange exact; routes {dict((k, r1[k] - r0[k]) for k in r1)}")
+    src.free()
+    ga_amd.comex_barrier()
+    assert ga_amd.comex_free(seg[rank]) == 0
+    ga_amd.comex_finalize()
+
+
 def c1_test(L, rank, size):
     """BASELINE config C1: 1-D contiguous f64 accumulate of 1 MiB
     (131 072 elements) between ranks, rank r -> rank (r+1) % size, the survey's
@@ -327,7 +390,8 @@ def c1_test(L, rank, size):
     the same bytes.  One source per target, so the order is fixed and the f64
     result exact.  Three source kinds, each into a fresh dst: pageable host memory
     (MA-style, the packed route), a plain device buffer (packed route) and the
-    rank's own segment (1 MiB: the direct-source route's threshold)."""
+    rank's own segment (1 MiB: the direct-source route's threshold); the device
+    buffer takes the one-pass route when both ranks share the GPU."""
     import ga_amd
     import cases as C
     from oracle import Oracle
@@ -366,7 +430,11 @@ def c1_test(L, rank, size):
         ga_amd.comex_barrier()
     if size > 1:
         d = dict(routes)
-        assert d["host"]["packed"] > 0 and d["device"]["packed"] > 0 and d["segment"]["direct_src"] > 0, routes
+        assert d["host"]["packed"] > 0 and d["segment"]["direct_src"] > 0, routes
+        if one_pass_expected():
+            assert d["device"]["one_pass"] > 0 and d["device"]["packed"] == 0, routes
+        else:
+            assert d["device"]["packed"] > 0 and d["device"]["one_pass"] == 0, routes
     say(rank, f"C1 1 MiB f64 remote acc bit-exact; routes {routes}")
     dbuf.free()
     ga_amd.comex_barrier()
@@ -451,8 +519,10 @@ def c5_full_test(L, rank, size):
     if size > 1:
         if use_seg:
             assert routes["direct_src"] > 0 and routes["packed"] == 0, routes
+        elif one_pass_expected():
+            assert routes["one_pass"] > 0 and routes["packed"] == 0 and routes["direct_src"] == 0, routes
         else:
-            assert routes["packed"] > 0 and routes["direct_src"] == 0, routes
+            assert routes["packed"] > 0 and routes["direct_src"] == 0 and routes["one_pass"] == 0, routes
     L.GA_Sync()
     if buf is not None:
         buf.free()

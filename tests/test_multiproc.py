@@ -267,12 +267,23 @@ def test_packed_route_forced_by_comex_enable_toggles(n):
 
 
 @pytest.mark.gpu
-def test_config_c1_one_mib_remote_acc_two_ranks():
+@pytest.mark.parametrize("n,one_pass", [(2, "1"), (4, "1"), (3, "0")])
+def test_one_pass_same_gpu_exchange(n, one_pass):
+    """Ranks sharing this GPU accumulate from plain device buffers into every
+    rank's block (their own included), blocking and non-blocking, concurrently:
+    the one-pass route under the owners' memory locks must lose no update (exact
+    integer sums); with COMEX_AMD_ONE_PASS=0 the same program on the packed route."""
+    launch("onepass", n=n, timeout=180, extra_env={"COMEX_AMD_ONE_PASS": one_pass})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("one_pass", ["1", "0"])
+def test_config_c1_one_mib_remote_acc_two_ranks(one_pass):
     """BASELINE config C1: a 1-D contiguous f64 accumulate of 1 MiB from rank 0 to
     rank 1 and back (2 ranks, one GPU), the survey's synthetic data, bit-exact
-    against the oracle; host, device and segment sources (packed and
-    direct-source routes)."""
-    launch("c1", n=2, timeout=120)
+    against the oracle; host, device and segment sources (packed, one-pass and
+    direct-source routes; COMEX_AMD_ONE_PASS=0 sends the device source packed)."""
+    launch("c1", n=2, timeout=120, extra_env={"COMEX_AMD_ONE_PASS": one_pass})
 
 
 @pytest.mark.gpu
