@@ -479,7 +479,11 @@ __global__ __launch_bounds__(kOrderedBS) void k_ordered(const Desc d, const OP o
 template <class OP, int W, bool PIPE>
 __global__ __launch_bounds__(64) void k_ordered_cols(const Desc d, const OP op) {
     typedef typename Vec<W>::T V;
-    constexpr int P = W == 16 ? 8 : 16;   // src loads in flight per lane (PIPE): 128 B
+    // src loads in flight per lane (PIPE): 256 B, 64 VGPRs -- a column reduction has
+    // only row-width / W lanes (one wave per SIMD at most), so each lane keeps many
+    // independent loads in flight (P = 16 at W = 8 read 0.66 TB/s algorithmic on a
+    // 64 KiB x 2048 reduction: latency-bound)
+    constexpr int P = W >= 16 ? 16 : 32;
     const uint32_t v = blockIdx.x * 64u + threadIdx.x;
     if (v >= d.nvec) return;
     const int64_t xo = (int64_t)v * W;
