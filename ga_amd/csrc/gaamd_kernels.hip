@@ -476,14 +476,14 @@ __global__ __launch_bounds__(kOrderedBS) void k_ordered(const Desc d, const OP o
 //   !PIPE (a src row is a dst row): load, apply, store per row; a lane's load
 //   after its own store to the same address returns that store (single-thread
 //   program order, which the memory model guarantees without fences).
-template <class OP, int W, bool PIPE>
+template <class OP, int W, bool PIPE, int LV = 0>
 __global__ __launch_bounds__(64) void k_ordered_cols(const Desc d, const OP op) {
     typedef typename Vec<W>::T V;
     // src loads in flight per lane (PIPE): 256 B, 64 VGPRs -- a column reduction has
     // only row-width / W lanes (one wave per SIMD at most), so each lane keeps many
     // independent loads in flight (P = 16 at W = 8 read 0.66 TB/s algorithmic on a
     // 64 KiB x 2048 reduction: latency-bound)
-    constexpr int P = W >= 16 ? 16 : 32;
+    constexpr int P = (LV == 1 && W == 8) ? 64 : (W >= 16 ? 16 : 32);
     const uint32_t v = blockIdx.x * 64u + threadIdx.x;
     if (v >= d.nvec) return;
     const int64_t xo = (int64_t)v * W;
@@ -507,7 +507,7 @@ __global__ __launch_bounds__(64) void k_ordered_cols(const Desc d, const OP op) 
             for (int k = 0; k < P; ++k) {
                 if (r0 + k < d.rows) {
                     int64_t so;
-                    row_offsets<0>(d, d.row0 + r0 + k, so, dofs[k]);
+                    row_offsets<LV>(d, d.row0 + r0 + k, so, dofs[k]);
                     s[k] = vload<W, true>(d.src + so + xo);
                 }
             }
@@ -627,7 +627,9 @@ static hipError_t dispatch_w(const Plan &p, const Desc &d, const OP &op, uint64_
             return hipGetLastError();
         }
         if (p.kind == KK_ORDERED) {
-            if (p.variant == 1)
+            if (p.variant == 1 && d.levels == 1)   // 2-D: the row offset is one multiply
+                hipLaunchKernelGGL((k_ordered_cols<OP, W, true, 1>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
+            else if (p.variant == 1)
                 hipLaunchKernelGGL((k_ordered_cols<OP, W, true>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
             else if (p.variant == 2)
                 hipLaunchKernelGGL((k_ordered_cols<OP, W, false>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
