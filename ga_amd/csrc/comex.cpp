@@ -154,43 +154,17 @@ static char *remote_view(int owner, const void *p, int64_t lo, int64_t hi) {
     fatal("address %p [%ld,%ld) of rank %d is not inside a comex_malloc segment", p, (long)lo, (long)hi, owner);
 }
 
-// HIP device allocations seen by direct_view (their whole [base, base + size)):
-// the device view of an address there is the address itself.  A later allocation
-// at a freed range is again device memory of the runtime's GPU address aperture
-// (host memory is never mapped there), so an entry stays correct after free and
-// reuse.  Saves two hipPointerGetAttributes (~1 us each) per call on the
-// headline path's repeated buffers (value_region.first_call_us).
-struct DevRanges {
-    uintptr_t lo[16] = {}, hi[16] = {};
-    int next = 0;
-    bool has(uintptr_t a) const {
-        for (int i = 0; i < 16; ++i)
-            if (a >= lo[i] && a < hi[i]) return true;
-        return false;
-    }
-    void add(void *p) {
-        hipDeviceptr_t base = nullptr;
-        size_t size = 0;
-        if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess || !size) {
-            (void)hipGetLastError();
-            return;
-        }
-        lo[next] = (uintptr_t)base;
-        hi[next] = (uintptr_t)base + size;
-        next = (next + 1) % 16;
-    }
-};
-static thread_local DevRanges t_dev_ranges;
-
 // device-visible without help: our segments, HBM, managed, pinned/registered host
+// (No cache of device ranges across calls: hipFree returns the range's virtual
+// addresses, and a later pageable host allocation can land there -- a cached
+// "device" answer then hands the GPU an unmapped host address: a memory-access
+// fault, round 3, test_pageable_sources_sharing_pages_back_to_back.)
 static bool direct_view(void *p, char **dev) {
-    if (t_dev_ranges.has((uintptr_t)p)) { *dev = (char *)p; return true; }
     if (find_segment_local(p, 0, 1)) { *dev = (char *)p; return true; }
     hipPointerAttribute_t at;
     memset(&at, 0, sizeof(at));
     hipError_t e = hipPointerGetAttributes(&at, p);
     if (e == hipSuccess && (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged)) {
-        if (at.type == hipMemoryTypeDevice) t_dev_ranges.add(p);
         *dev = (char *)p;
         return true;
     }
