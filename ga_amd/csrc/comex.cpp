@@ -1316,7 +1316,44 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
                         (kind == X_PUT && (world == r.rank ? !r.put_self_direct
                                                            : (!r.put_smp_direct || r.peer_src(world))));
     if (packed) {
-        const int id = remote_acc_start(world, cop, scale, src, ss, dst, ds, count, levels);
+        int id = 0;
+        const int64_t rbp = row_bytes_of(cop, count[0]);
+        if (rbp > 0 && (uint64_t)rbp > sub_ring_bytes() && levels < kMaxLevels &&
+            (levels == 0 || dst_rows_disjoint(ds, count, levels, rbp))) {
+            // a row longer than the staging sub-ring (a 1-D accumulate of tens of MiB;
+            // the reference sends such a message in chunks, comex.c:6263-6338): the
+            // row is cut into pieces that become one more stride level (a row's
+            // pieces lie back to back on both sides), plus the rows' tails as a
+            // second patch.  Rows share no dst byte, so the order of the two parts
+            // changes no result.  The first part completes locally here.
+            // pieces of whole 16-byte units: whole elements of every type (1..16 B)
+            const uint64_t unit = 16;
+            uint64_t piece = (sub_ring_bytes() / 2) / unit * unit;
+            if (piece == 0) piece = unit;
+            const uint64_t k = (uint64_t)rbp / piece, tail = (uint64_t)rbp - k * piece;
+            int cb[8], ssb[8], dsb[8];
+            cb[0] = (int)piece;
+            cb[1] = (int)k;
+            ssb[0] = dsb[0] = (int)piece;
+            for (int j = 0; j < levels; ++j) {
+                cb[j + 2] = count[j + 1];
+                ssb[j + 1] = ss[j];
+                dsb[j + 1] = ds[j];
+            }
+            const int body = remote_acc_start(world, cop, scale, src, ssb, dst, dsb, cb, levels + 1);
+            if (tail) {
+                if (body) run_job(body);
+                int ct[8];
+                for (int j = 0; j <= levels; ++j) ct[j] = count[j];
+                ct[0] = (int)tail;
+                id = remote_acc_start(world, cop, scale, (char *)src + k * piece, ss, (char *)dst + k * piece, ds, ct,
+                                      levels);
+            } else {
+                id = body;
+            }
+        } else {
+            id = remote_acc_start(world, cop, scale, src, ss, dst, ds, count, levels);
+        }
         if (hdl) {
             nb_complete_now(hdl);
             g_nb_job[*hdl] = id;

@@ -470,7 +470,9 @@ def c5_full_test(L, rank, size):
     L.NGA_Distribution(g, rank, blo, bhi)
     rows, cols = bhi[0] - blo[0] + 1, bhi[1] - blo[1] + 1
     if size == 8 and n == 32768:
-        assert (rows, cols) == (8192, 16384), (rows, cols)   # the 4 x 2 grid of ddb_h2
+        # ddb_h2's 4 x 2 grid in GA's Fortran order: C-order blocks of
+        # 16384 rows x 8192 columns, ld 8192 (64 KiB), 1 GiB each
+        assert (rows, cols) == (16384, 8192), (rows, cols)
     L.GA_Zero(g)
     L.GA_Sync()
 

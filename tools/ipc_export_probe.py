@@ -27,12 +27,16 @@ import sys
 HIP = "/opt/rocm/lib/libamdhip64.so"
 
 
+class Handle(ctypes.Structure):   # hipIpcMemHandle_t: 64 bytes, passed BY VALUE to hipIpcOpenMemHandle
+    _fields_ = [("reserved", ctypes.c_char * 64)]
+
+
 def hip():
     L = ctypes.CDLL(HIP)
     L.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
     L.hipFree.argtypes = [ctypes.c_void_p]
     L.hipIpcGetMemHandle.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
-    L.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_uint]
+    L.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(ctypes.c_void_p), Handle, ctypes.c_uint]
     L.hipIpcCloseMemHandle.argtypes = [ctypes.c_void_p]
     L.hipSetDevice.argtypes = [ctypes.c_int]
     L.hipGetErrorString.restype = ctypes.c_char_p
@@ -56,7 +60,9 @@ def export(L, p):
 
 def open_h(L, raw):
     p = ctypes.c_void_p()
-    rc = L.hipIpcOpenMemHandle(ctypes.byref(p), ctypes.c_char_p(raw), 1)
+    h = Handle()
+    ctypes.memmove(ctypes.addressof(h), raw, 64)
+    rc = L.hipIpcOpenMemHandle(ctypes.byref(p), h, 1)
     return rc, p.value
 
 
