@@ -520,13 +520,16 @@ def c5_extras(args, dist):
             d["note"] = ("whole-array accumulate by every rank; value counts 3 x payload of HBM-side traffic per rank; "
                          + ("the local buffer lies in the rank's comex segment: owners accumulate straight from it "
                             "(direct-source route, no pack)" if src_seg else
-                            "the local buffer is a plain device buffer: pack -> staging -> owner unpack-acc"))
+                            "the local buffer is a plain device buffer: owners on other GPUs pack -> staging -> owner "
+                            "unpack-acc; ranks sharing a GPU the one-pass route"))
             d["routes"] = r.get("routes")
         else:
             d["hbm_peak_frac_per_gpu"] = round(r["alg_bytes"] / t / (HBM_PEAK_GBS * 1e9), 4)
         out[mode] = d
-    out["exchange_check"] = {route: c5_exchange_check(dist, src_seg) for route, src_seg in
-                             (("packed", False), ("direct_src", True))}
+    # the exactness check runs at the configured GA size, not a reduced one
+    n_chk = args.ga_dims if args.ga_dims else GA_DIMS[0]
+    out["exchange_check"] = {route: c5_exchange_check(dist, src_seg, n=n_chk) for route, src_seg in
+                             (("buffer_src", False), ("segment_src", True))}
     ga_amd_lib().GA_Terminate()
     return out
 
@@ -542,7 +545,8 @@ def c5_exchange_check(dist, src_seg, n=4096):
     constant 2**rank (alpha 1, the array zeroed first), so every element must read
     exactly 2**p - 1 afterwards -- a lost, doubled or stale contribution shows as a
     wrong element and its value says whose.  The source is a plain device buffer
-    (packed route) or lies in the rank's segment (direct-source route)."""
+    (packed route to other GPUs, one-pass to ranks on the same GPU) or lies in the
+    rank's segment (direct-source route)."""
     import ga_amd
     L = ga_amd.lib()
     ia = ga_amd.int_array
@@ -550,16 +554,16 @@ def c5_exchange_check(dist, src_seg, n=4096):
     assert g > 0
     L.GA_Zero(g)
     L.GA_Sync()
-    host = np.full(n * n, float(2 ** dist.rank))
+    nbytes = n * n * 8
     seg, buf = None, None
     if src_seg:
-        seg = ga_amd.comex_malloc(host.nbytes, dist.size)
+        seg = ga_amd.comex_malloc(nbytes, dist.size)
         ptr = seg[dist.rank]
-        assert L.gaamd_memcpy(ctypes.c_void_p(ptr), host.ctypes.data_as(ctypes.c_void_p), host.nbytes) == 0
     else:
-        buf = ga_amd.DeviceBuffer(host.nbytes)
-        buf.upload(host)
+        buf = ga_amd.DeviceBuffer(nbytes)
         ptr = buf.ptr
+    ga_amd.fill_const(ptr, nbytes, float(2 ** dist.rank))   # on the GPU: no n^2 host array at 32768^2
+    ga_amd.sync()
     routes0 = ga_amd.route_counts()
     alpha = ctypes.c_double(1.0)
     L.NGA_Acc(g, ia([0, 0]), ia([n - 1, n - 1]), ctypes.c_void_p(ptr), ia([n]), ctypes.byref(alpha))

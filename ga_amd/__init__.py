@@ -194,22 +194,13 @@ def fill(ptr, n, type_code, seed, stream=None):
 
 # ---- io-vector descriptors (comex.h:13-18, armci.h:17-22) ------------------
 def fill_const(ptr, nbytes, value, dtype="float64"):
-    """Fill nbytes of device memory at ptr with a constant: one <= 64 MiB upload,
-    then device-to-device doubling copies (no host array of the full size)."""
+    """Fill nbytes of device memory at ptr with a constant of an 8-byte dtype (one
+    kernel; enqueued on the library's primary stream -- sync() before use)."""
     import numpy as np
-    item = np.dtype(dtype).itemsize
-    assert nbytes % item == 0
-    chunk = min(nbytes, 64 << 20)
-    host = np.full(chunk // item, value, dtype=dtype)
-    L = lib()
-    if L.gaamd_memcpy(ctypes.c_void_p(ptr), host.ctypes.data_as(ctypes.c_void_p), chunk) != 0:
-        raise RuntimeError("fill_const upload failed")
-    done = chunk
-    while done < nbytes:
-        n = min(done, nbytes - done)
-        if L.gaamd_memcpy(ctypes.c_void_p(ptr + done), ctypes.c_void_p(ptr), n) != 0:
-            raise RuntimeError("fill_const copy failed")
-        done += n
+    word = int(np.array([value], dtype=dtype).view(np.uint64)[0])
+    assert np.dtype(dtype).itemsize == 8 and nbytes % 8 == 0
+    if lib().gaamd_fill_word(ctypes.c_void_p(ptr), nbytes // 8, word, None) != 0:
+        raise RuntimeError("gaamd_fill_word failed")
 
 
 class GIOV(ctypes.Structure):

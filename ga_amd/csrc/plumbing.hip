@@ -39,6 +39,11 @@ __global__ __launch_bounds__(256) void k_fill(void *dst, long n, int type, uint6
     }
 }
 
+// n 8-byte words of the same bit pattern (test and bench data: 2^rank constants)
+__global__ __launch_bounds__(256) void k_fill_word(uint64_t *dst, long n, uint64_t word) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) dst[i] = word;
+}
+
 }  // namespace gaamd
 
 using namespace gaamd;
@@ -216,6 +221,16 @@ int gaamd_join(void) {
 }
 
 int gaamd_num_streams(void) { return (int)rt().streams.size(); }
+
+int gaamd_fill_word(void *dst, long n, unsigned long long word, void *stream) {
+    if (n <= 0) return 0;
+    if ((uintptr_t)dst & 7) return -2;
+    long blocks = (n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_fill_word, dim3((unsigned)blocks), dim3(256), 0, stream_of(stream), (uint64_t *)dst, n,
+                       (uint64_t)word);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int gaamd_fill(void *dst, long n, int type, unsigned long long seed, void *stream) {
     if (n <= 0) return 0;

@@ -118,6 +118,8 @@ int gaamd_num_streams(void);
 /* synthetic inputs of SURVEY.md 8(d) generated on the device; type:
  * 0 f64, 1 f32, 2 i32, 3 i64 ; n elements from splitmix64(seed) */
 int gaamd_fill(void *dst, long n, int type, unsigned long long seed, void *stream);
+/* n 8-byte words of one bit pattern (8-byte aligned dst) */
+int gaamd_fill_word(void *dst, long n, unsigned long long word, void *stream);
 void *gaamd_stream_create(void);       /* an extra blocking HIP stream */
 int gaamd_stream_destroy(void *stream);
 /* HIP events on the library stream (or `stream`) */

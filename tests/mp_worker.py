@@ -510,6 +510,7 @@ def c5_full_test(L, rank, size):
     ga_amd.fill_const(ptr, whole, float(2 ** rank))
     ga_amd.sync()
     L.GA_Sync()
+    say(rank, f"C5 M2 sources ready ({time.perf_counter() - t0:.1f} s)")
     r0 = ga_amd.route_counts()
     t1 = time.perf_counter()
     L.NGA_Acc(g, ia([0, 0]), ia([n - 1, n - 1]), ctypes.c_void_p(ptr), ia([n]), ctypes.byref(one))

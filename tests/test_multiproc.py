@@ -25,8 +25,22 @@ def free_port():
     return p
 
 
+def _progress_file(mode):
+    """On a gpurun box (GRAFT_REPO_ROOT set) the ranks' output is also appended, line
+    by line, to gpurun_out/progress/<mode>.log as it comes: a long multi-rank test
+    then shows activity (the box takes 3 silent minutes for a hang)."""
+    root = os.environ.get("GRAFT_REPO_ROOT")
+    if not root:
+        return None
+    d = os.path.join(root, "gpurun_out", "progress")
+    os.makedirs(d, exist_ok=True)
+    return open(os.path.join(d, f"{mode}.log"), "a", buffering=1)
+
+
 def launch(mode, n=2, timeout=240, nodes=None, extra_env=None):
     """nodes: node id of every rank (COMEX_AMD_NODE), None = all on this host."""
+    import threading
+    import time
     port = str(free_port())
     procs = []
     for r in range(n):
@@ -40,24 +54,42 @@ def launch(mode, n=2, timeout=240, nodes=None, extra_env=None):
         env.update(extra_env or {})
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "mp_worker.py"), mode], cwd=ROOT, env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
-    outs = []
+    prog = _progress_file(mode)
+    outs = [[] for _ in procs]
+
+    def drain(r, p):
+        for line in p.stdout:
+            outs[r].append(line)
+            if prog:
+                prog.write(f"[{time.strftime('%H:%M:%S')} rank {r}] {line}")
+
+    readers = [threading.Thread(target=drain, args=(r, p), daemon=True) for r, p in enumerate(procs)]
+    for t in readers:
+        t.start()
+    deadline = time.monotonic() + timeout
     try:
         for p in procs:
-            out, _ = p.communicate(timeout=timeout)
-            outs.append((p.returncode, out))
+            p.wait(timeout=max(1.0, deadline - time.monotonic()))
     except subprocess.TimeoutExpired:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-        tails = [f"--- rank {r} ---\n" + (p.communicate()[0] or "")[-2000:] for r, p in enumerate(procs)]
+        for t in readers:
+            t.join(5)
+        tails = [f"--- rank {r} ---\n" + "".join(o)[-2000:] for r, o in enumerate(outs)]
         raise AssertionError(f"{mode}: ranks did not finish in {timeout} s\n" + "\n".join(tails))
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    for r, (rc, out) in enumerate(outs):
+    for t in readers:
+        t.join(10)
+    if prog:
+        prog.close()
+    res = [(p.returncode, "".join(o)) for p, o in zip(procs, outs)]
+    for r, (rc, out) in enumerate(res):
         assert rc == 0 and f"RANK {r} OK" in out, f"rank {r} rc={rc}\n{out[-3000:]}"
-    return [out for _, out in outs]
+    return [out for _, out in res]
 
 
 def test_bootstrap_env_shm_two_ranks():
@@ -335,4 +367,5 @@ def test_bench_two_ranks_exchange_exact():
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2
     chk = line["c5"]["exchange_check"]
-    assert chk["packed"]["result"] == "exact" and chk["direct_src"]["result"] == "exact", chk
+    assert chk["buffer_src"]["result"] == "exact" and chk["segment_src"]["result"] == "exact", chk
+    assert chk["buffer_src"]["array"] == "8192x8192 f64", chk   # at --ga-dims, not a fixed 4096
