@@ -114,6 +114,51 @@ static void check_remote(int owner, const void *p, int64_t lo, int64_t hi) {
         fatal("address %p [%ld,%ld) of rank %d is not inside a comex_malloc segment", p, (long)lo, (long)hi, owner);
 }
 
+// ---- IPC address history ---------------------------------
+// Every export, IPC mapping, unmapping and free of device memory this process
+// does (or is told of: gaamd_dev_free) is recorded with its address range, so a
+// refused hipIpcGetMemHandle can print which earlier event touched that range.
+struct AddrEvent { char kind; uintptr_t lo, hi; int peer; };
+static std::mutex g_addr_mu;
+static std::deque<AddrEvent> g_addr_log;   // newest last, at most 4096
+void addr_event(char kind, const void *p, size_t bytes, int peer) {
+    std::lock_guard<std::mutex> g(g_addr_mu);
+    g_addr_log.push_back({kind, (uintptr_t)p, (uintptr_t)p + bytes, peer});
+    if (g_addr_log.size() > 4096) g_addr_log.pop_front();
+}
+static void addr_history(const void *p, size_t bytes) {
+    std::lock_guard<std::mutex> g(g_addr_mu);
+    const uintptr_t lo = (uintptr_t)p, hi = lo + bytes;
+    int n = 0;
+    for (const AddrEvent &e : g_addr_log) {
+        if (e.lo < hi && lo < e.hi) {
+            fprintf(stderr, "[ga_amd %d]   earlier %s [%p, %p) %s%d\n", rt().rank,
+                    e.kind == 'x' ? "export" : e.kind == 'o' ? "IPC map" : e.kind == 'c' ? "IPC unmap" :
+                    e.kind == 'f' ? "free" : e.kind == 'a' ? "alloc" : "?",
+                    (void *)e.lo, (void *)e.hi, e.peer >= 0 ? "of rank " : "", e.peer);
+            ++n;
+        }
+    }
+    fprintf(stderr, "[ga_amd %d]   %d earlier events touched this range (of %zu logged)\n", rt().rank, n,
+            g_addr_log.size());
+}
+
+static size_t mapped_size(const void *p) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return size;
+}
+
+static void ipc_close(void *mapped, int peer) {
+    if (!mapped) return;
+    addr_event('c', mapped, mapped_size(mapped), peer);
+    GA_HIP(hipIpcCloseMemHandle(mapped));
+}
+
 // Map a same-node peer's HBM (IPC handle).  A failure is not fatal here: a job
 // that never touches that peer's memory (owner-aligned accumulates, the weak-
 // scaling bench) runs on; the first operation that needs the mapping aborts with
@@ -128,6 +173,7 @@ static void *ipc_open(hipIpcMemHandle_t h, int q, const char *what) {
                 hipGetErrorString(e));
         return nullptr;
     }
+    addr_event('o', p, mapped_size(p), q);
     return p;
 }
 
@@ -1112,7 +1158,15 @@ static bool in_own_segment(const Span &d) {
     return false;
 }
 
-void own_write_guard(const Span &dst) {   // caller holds launch_mu
+// Caller holds launch_mu (sched_pick).  While a requester holds the lock this
+// waits WITHOUT launch_mu: a thread holding launch_mu never waits for a memory
+// lock, so lock holders (which need their own launch_mu to launch) always get it
+// -- a requester holds one lock and waits only for its launch_mu and its kernel,
+// the owner's release needs only its launch_mu: no cycle (with launch_mu held
+// across the wait, eight ranks accumulating into each other could close one:
+// rank A's progress thread holding A's launch_mu waiting for A's lock held by C,
+// C waiting for its launch_mu held by its progress thread waiting for C's lock...).
+void own_write_guard(const Span &dst) {
     Runtime &r = rt();
     if (!r.one_pass || r.own_holds || dst.lo >= dst.hi || !in_own_segment(dst)) return;
     std::atomic<uint32_t> &w = r.shm->mem_lock[r.li(r.rank)];
@@ -1120,7 +1174,10 @@ void own_write_guard(const Span &dst) {   // caller holds launch_mu
     for (unsigned spins = 0;; ++spins) {
         uint32_t e = 0;
         if (w.compare_exchange_weak(e, me, std::memory_order_acq_rel)) break;
+        r.launch_mu.unlock();
         if (spins > 64) sched_yield();
+        r.launch_mu.lock();
+        if (r.own_holds) return;   // another thread of this process took it meanwhile
     }
     r.own_holds = true;
 }
@@ -2268,6 +2325,7 @@ int comex_init() {
         const char *mb = getenv("COMEX_AMD_STAGING_MB");
         r.staging_bytes = (size_t)(mb ? atol(mb) : 256) << 20;
         GA_HIP(hipMalloc((void **)&r.staging, r.staging_bytes));
+        addr_event('a', r.staging, r.staging_bytes, -1);
         struct { hipIpcMemHandle_t h; uint64_t bytes; } mine, *all;
         memset(&mine, 0, sizeof(mine));
         export_alloc((void **)&r.staging, r.staging_bytes, &mine.h, "staging buffer");
@@ -2335,15 +2393,17 @@ int comex_finalize() {
     for (Segment &s : r.segs) {
         if (!s.live) continue;
         for (int q = 0; q < (int)s.peer.size(); ++q)
-            if (q != r.rank && s.peer[q].mapped) (void)hipIpcCloseMemHandle(s.peer[q].mapped);
+            if (q != r.rank && s.peer[q].mapped) ipc_close(s.peer[q].mapped, q);
+        if (s.local && s.device) addr_event('f', s.local, s.peer[r.rank].bytes, -1);
         if (s.local) (void)(s.device ? hipFree(s.local) : hipHostFree(s.local));
         s.live = false;
     }
     r.segs.clear();
     for (int q = 0; q < (int)r.peer_staging.size(); ++q)
-        if (q != r.rank && r.peer_staging[q]) (void)hipIpcCloseMemHandle(r.peer_staging[q]);
+        if (q != r.rank && r.peer_staging[q]) ipc_close(r.peer_staging[q], q);
     r.peer_staging.clear();
     boot_barrier();
+    if (r.staging) addr_event('f', r.staging, r.staging_bytes, -1);
     if (r.staging) (void)hipFree(r.staging);
     r.staging = nullptr;
     sched_sync_all();
@@ -2561,25 +2621,42 @@ int comex_wait_proc(int proc, comex_group_t group) {
 }
 
 // ---- memory ----
-// IPC handle of a fresh hipMalloc block `*p`.  The runtime now and then refuses to
-// export a block (invalid argument) at an address an earlier, freed and exported
-// block had (seen in about 1 of 6 C5 runs, 64 MiB-1 GiB segments, base and size
-// exactly the allocation's): then allocate another while holding the refused one,
-// a few times, and release the refused ones.
+// IPC handle of a fresh hipMalloc block `*p`.  Round 2 saw the runtime refuse,
+// once in 6 two-rank C5 runs, to export a fresh 64 MiB segment whose base and size
+// were exactly the allocation's (invalid argument).  tools/ipc_export_probe.py
+// drove the candidate sequences -- re-export after the peer closed, after a free
+// while the peer still maps, an importer's VA reused for its own export, double
+// export, the bench's mixed 64 MiB / 1 GiB pattern -- 96 rounds, 0 refusals
+// (profiles/r03/): the cause is not identified.  A refusal now prints every
+// export, IPC map/unmap, alloc and free this process made over that address range
+// (addr_history), then allocates another block while holding the refused one, up
+// to 4 times; COMEX_AMD_IPC_RETRY=0 makes the first refusal fatal instead.
 static void export_alloc(void **p, size_t bytes, hipIpcMemHandle_t *h, const char *what) {
     Runtime &r = rt();
+    static const bool retry = [] {
+        const char *e = getenv("COMEX_AMD_IPC_RETRY");
+        return !e || atoi(e) != 0;
+    }();
     std::vector<void *> held;
     hipError_t e = hipIpcGetMemHandle(h, *p);
     for (int tries = 0; e != hipSuccess && tries < 4; ++tries) {
         (void)hipGetLastError();
-        fprintf(stderr, "[ga_amd %d] hipIpcGetMemHandle of a %zu-byte %s at %p failed (%s); allocating another\n",
-                r.rank, bytes, what, *p, hipGetErrorString(e));
+        fprintf(stderr, "[ga_amd %d] hipIpcGetMemHandle of a %zu-byte %s at %p failed (%s)\n", r.rank, bytes, what, *p,
+                hipGetErrorString(e));
+        addr_history(*p, bytes);
+        if (!retry) break;
+        fprintf(stderr, "[ga_amd %d]   allocating another block (COMEX_AMD_IPC_RETRY=0: abort instead)\n", r.rank);
         held.push_back(*p);
         GA_HIP(hipMalloc(p, bytes));
+        addr_event('a', *p, bytes, -1);
         e = hipIpcGetMemHandle(h, *p);
     }
-    for (void *q : held) GA_HIP(hipFree(q));
+    for (void *q : held) {
+        addr_event('f', q, bytes, -1);
+        GA_HIP(hipFree(q));
+    }
     if (e != hipSuccess) fatal("hipIpcGetMemHandle of a %zu-byte %s failed: %s", bytes, what, hipGetErrorString(e));
+    addr_event('x', *p, bytes, -1);
 }
 
 static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool device) {
@@ -2596,6 +2673,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     if (bytes) {
         if (device) {
             GA_HIP(hipMalloc(&p, bytes));
+            addr_event('a', p, bytes, -1);
             if (r.debug) {
                 void *base = nullptr;
                 size_t sz = 0;
@@ -2678,7 +2756,7 @@ int comex_free(void *ptr, comex_group_t group) {
             for (int q = 0; q < r.size; ++q) if (s.peer[q].base != all[q]) { match = false; break; }
             if (!match) continue;
             for (int q = 0; q < r.size; ++q)
-                if (q != r.rank && s.peer[q].mapped) GA_HIP(hipIpcCloseMemHandle(s.peer[q].mapped));
+                if (q != r.rank && s.peer[q].mapped) ipc_close(s.peer[q].mapped, q);
             local = s.local;
             device = s.device;
             s.live = false;
@@ -2693,6 +2771,7 @@ int comex_free(void *ptr, comex_group_t group) {
     // refuses to export a new allocation it hands out at the same address
     // (hipIpcGetMemHandle: invalid argument in the next comex_malloc)
     members_barrier(members, group);
+    if (local && device) addr_event('f', local, mapped_size(local), -1);
     if (local) GA_HIP(device ? hipFree(local) : hipHostFree(local));
     return COMEX_SUCCESS;
 }

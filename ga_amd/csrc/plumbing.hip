@@ -183,9 +183,16 @@ void *gaamd_stream_at(int i) {
 void *gaamd_dev_malloc(size_t bytes) {
     void *p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    addr_event('a', p, bytes, -1);
     return p;
 }
-int gaamd_dev_free(void *p) { return hipFree(p) == hipSuccess ? 0 : -1; }
+int gaamd_dev_free(void *p) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) == hipSuccess) addr_event('f', p, size, -1);
+    else (void)hipGetLastError();
+    return hipFree(p) == hipSuccess ? 0 : -1;
+}
 
 void *gaamd_host_malloc(size_t bytes) {
     void *p = nullptr;

@@ -256,6 +256,9 @@ bool mutex_try_local(int owner, int mutex);
 void mutex_release_local(int owner, int mutex);
 bool segment_of_rank(int owner, uint64_t p, int64_t lo, int64_t hi);   // comex.cpp (reg_cache_find)
 bool segment_local(const void *p, int64_t lo, int64_t hi);              // comex.cpp
+// comex.cpp: the device-address history a refused IPC export prints (kind: a alloc,
+// f free, x export, o IPC map, c IPC unmap; peer = the other rank, -1 none)
+void addr_event(char kind, const void *p, size_t bytes, int peer);
 
 // comex.cpp helpers shared with armci.cpp / armci_msg.cpp
 int translate_world(int group, int proc);
