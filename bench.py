@@ -465,12 +465,31 @@ def run_gpu(args, dist, finalize=True):
         avg_kernel_s = elapsed / args.steps   # the work runs on the owners' streams / progress thread
     else:
         # roofline: the same K steps again inside per-stream HIP events
-        region_ms, _ = event_region(L, step, args.steps, nxt)
+        region_ms, nxt = event_region(L, step, args.steps, nxt)
         avg_kernel_s = dist.max(region_ms / 1e3 / args.steps)
+    blocking = None
+    if nb and xfer == "acc" and not pipeline and not exchange and not seg_dst:
+        # the blocking API beside the headline: the same K steps through
+        # comex_accs, each returning after its kernel -- a host round trip per step,
+        # the call GA's NGA_Acc makes for its last owner (onesided.c:1421-1438)
+        L.comex_barrier(0)
+        dist.barrier()
+        ga_amd.sync()
+        tb = time.perf_counter()
+        for i in range(args.steps):
+            sp_, dp_ = ptrs[(nxt + i) % len(ptrs)]
+            if L.comex_accs(op, sp, sp_, ss, dp_, ds, cnt, levels, target, 0):
+                raise RuntimeError("blocking step failed")
+        tb = dist.max(time.perf_counter() - tb)
+        blocking = {"api": "comex_accs per step (blocking: returns after its kernel)",
+                    "value": round(dist.size * alg_bytes * args.steps / tb / 2 ** 30, 2),
+                    "hbm_peak_frac": round(alg_bytes * args.steps / tb / (HBM_PEAK_GBS * 1e9), 4),
+                    "ms_per_step": round(tb / args.steps * 1e3, 4)}
 
     res = dict(op=op, desc=desc, payload=payload, alg_bytes=alg_bytes, elems=elems, elapsed=elapsed,
                avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), pipeline=pipeline,
-               xfer=xfer, warmup_steps=warmup_steps, region_profile=region_profile, diag_regions=diag)
+               xfer=xfer, warmup_steps=warmup_steps, region_profile=region_profile, diag_regions=diag,
+               blocking=blocking)
     for b in packed:
         b.free()
     if args.host_rates and dist.rank == 0:
@@ -886,6 +905,8 @@ def main():
         line["value_region"] = r["region_profile"]   # host-clock marks inside the timed region
     if r.get("diag_regions"):
         line["diag_regions"] = r["diag_regions"]
+    if r.get("blocking"):
+        line["blocking_api"] = r["blocking"]   # same K steps through the blocking call, after the value region
     if c5:
         line["c5"] = c5
     if r.get("xfer", "acc") != "acc":
