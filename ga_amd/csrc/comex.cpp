@@ -535,6 +535,7 @@ static void post_request_direct(int t, int op, const void *scale, uint64_t dst_a
 static uint64_t iov_list_off(int n, int bytes) { return (((uint64_t)n * (uint64_t)bytes) + 15) & ~15ull; }
 
 static bool own_release_if_wanted();   // one-pass memory lock (below)
+static bool one_pass_reap(bool wait);
 
 // owner side: drain the inbox in ticket order
 static void progress_loop() {
@@ -786,6 +787,7 @@ static void progress_loop() {
             worked = true;
         }
         if (own_release_if_wanted()) worked = true;
+        if (one_pass_reap(false)) worked = true;   // our one-pass kernels into peers' segments
         while (!inflight.empty()) {
             hipError_t e = hipEventQuery(inflight.front().ev);
             if (e == hipErrorNotReady) break;
@@ -1170,15 +1172,25 @@ void own_write_guard(const Span &dst) {
     Runtime &r = rt();
     if (!r.one_pass || r.own_holds || dst.lo >= dst.hi || !in_own_segment(dst)) return;
     std::atomic<uint32_t> &w = r.shm->mem_lock[r.li(r.rank)];
+    std::atomic<uint32_t> &want = r.shm->mem_want[r.li(r.rank)];
     const uint32_t me = 1 + (uint32_t)r.li(r.rank);
+    bool waiting = false;   // counted in mem_want: a requester holding our lock then hands it back
     for (unsigned spins = 0;; ++spins) {
         uint32_t e = 0;
         if (w.compare_exchange_weak(e, me, std::memory_order_acq_rel)) break;
+        if (!waiting) {
+            want.fetch_add(1, std::memory_order_acq_rel);
+            waiting = true;
+        }
         r.launch_mu.unlock();
         if (spins > 64) sched_yield();
         r.launch_mu.lock();
-        if (r.own_holds) return;   // another thread of this process took it meanwhile
+        if (r.own_holds) {   // another thread of this process took it meanwhile
+            want.fetch_sub(1, std::memory_order_acq_rel);
+            return;
+        }
     }
+    if (waiting) want.fetch_sub(1, std::memory_order_acq_rel);
     r.own_holds = true;
 }
 
@@ -1196,9 +1208,53 @@ static bool own_release_if_wanted() {
 
 static std::atomic<unsigned long long> g_one_pass{0};   // gaamd_route_counts: one-pass accumulates issued
 
-// true: applied (complete on return); false: not eligible (caller takes another route)
+// The requester's side of the lock: per target, whether we hold its memory lock
+// and the events of our one-pass kernels still writing its segment.  A
+// non-blocking one-pass returns after the launch; the lock is released once every
+// such kernel has completed -- by our progress thread (one_pass_reap each pass),
+// or by a blocking call / wait / fence that waited for them.  Further one-pass
+// accumulates into the same target while we hold its lock go straight on (stream
+// order and sched_pick's range dependencies order them among themselves), unless
+// someone else waits for the lock (mem_want): then ours finish and it goes first.
+struct OnePassHold { bool held = false; std::vector<hipEvent_t> evs; };
+static std::mutex g_op_mu;   // g_op_hold, g_op_pool; never held while waiting for a memory lock
+static std::vector<OnePassHold> g_op_hold;
+static std::vector<hipEvent_t> g_op_pool;
+
+static void one_pass_release(int t, OnePassHold &h) {   // caller holds g_op_mu; every event completed
+    Runtime &r = rt();
+    for (hipEvent_t e : h.evs) g_op_pool.push_back(e);
+    h.evs.clear();
+    h.held = false;
+    r.shm->mem_lock[r.li(t)].store(0, std::memory_order_release);
+}
+
+// release the locks whose kernels have all completed (wait: wait for them first);
+// true if one was released
+static bool one_pass_reap(bool wait) {
+    bool any = false;
+    std::lock_guard<std::mutex> g(g_op_mu);
+    for (size_t t = 0; t < g_op_hold.size(); ++t) {
+        OnePassHold &h = g_op_hold[t];
+        if (!h.held) continue;
+        bool done = true;
+        for (hipEvent_t e : h.evs) {
+            const hipError_t x = wait ? hipEventSynchronize(e) : hipEventQuery(e);
+            if (x == hipErrorNotReady) { done = false; break; }
+            if (x != hipSuccess) fatal("one-pass accumulate failed: %s", hipGetErrorString(x));
+        }
+        if (done) {
+            one_pass_release((int)t, h);
+            any = true;
+        }
+    }
+    return any;
+}
+
+// true: launched (blocking: complete on return; else `hdl` tracks it);
+// false: not eligible (the caller takes another route)
 static bool one_pass_acc(int t, int op, void *scale, void *src, const int *ss, void *dst, const int *ds,
-                         const int *count, int levels, int64_t rbd) {
+                         const int *count, int levels, int64_t rbd, comex_request_t *hdl) {
     Runtime &r = rt();
     if (!r.one_pass || t == r.rank || !r.same_node(t) || !r.acc_smp_direct || r.peer_src(t)) return false;
     if (rbd <= 0 || payload_bytes(rbd, count, levels) < kOnePassMin) return false;
@@ -1216,24 +1272,45 @@ static bool one_pass_acc(int t, int op, void *scale, void *src, const int *ss, v
     std::atomic<uint32_t> &lk = r.shm->mem_lock[r.li(t)];
     std::atomic<uint32_t> &want = r.shm->mem_want[r.li(t)];
     const uint32_t me = 1 + (uint32_t)r.li(r.rank);
-    want.fetch_add(1, std::memory_order_acq_rel);
-    for (unsigned spins = 0;; ++spins) {
-        uint32_t e = 0;
-        if (lk.compare_exchange_weak(e, me, std::memory_order_acq_rel)) break;
-        if (spins > 64) sched_yield();
+    std::unique_lock<std::mutex> og(g_op_mu);
+    if (g_op_hold.size() != (size_t)r.size) g_op_hold.resize(r.size);
+    if (g_op_hold[t].held && want.load(std::memory_order_acquire) > 0) {
+        // someone waits for t's memory: let ours finish and hand it over first
+        for (hipEvent_t e : g_op_hold[t].evs) GA_HIP(hipEventSynchronize(e));
+        one_pass_release(t, g_op_hold[t]);
     }
-    want.fetch_sub(1, std::memory_order_acq_rel);
-    hipStream_t st;
+    if (!g_op_hold[t].held) {
+        og.unlock();   // our progress thread may need it to release another target's lock meanwhile
+        want.fetch_add(1, std::memory_order_acq_rel);
+        for (unsigned spins = 0;; ++spins) {
+            uint32_t e = 0;
+            if (lk.compare_exchange_weak(e, me, std::memory_order_acq_rel)) break;
+            if (spins > 64) sched_yield();
+        }
+        want.fetch_sub(1, std::memory_order_acq_rel);
+        og.lock();
+        g_op_hold[t].held = true;
+    }
+    hipEvent_t ev;
+    if (g_op_pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    else { ev = g_op_pool.back(); g_op_pool.pop_back(); }
+    int si;
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
-        const int si = sched_pick(span_of(sdev, slo, shi), span_of(dview, dlo, dhi), payload_bytes(rbd, count, levels));
-        st = r.streams[si];
-        const int rc = launch_strided(op, scale, sdev, ss, dview, ds, count, levels, st, last_launch_info());
+        si = sched_pick(span_of(sdev, slo, shi), span_of(dview, dlo, dhi), payload_bytes(rbd, count, levels));
+        const int rc = launch_strided(op, scale, sdev, ss, dview, ds, count, levels, r.streams[si], last_launch_info());
         if (rc) fatal("one-pass accumulate launch failed (%d)", rc);
+        GA_HIP(hipEventRecord(ev, r.streams[si]));
     }
-    GA_HIP(hipStreamSynchronize(st));
-    lk.store(0, std::memory_order_release);
+    g_op_hold[t].evs.push_back(ev);
+    og.unlock();
     g_one_pass.fetch_add(1, std::memory_order_relaxed);
+    if (hdl) {
+        nb_complete_now(hdl, si, true);
+    } else {
+        GA_HIP(hipEventSynchronize(ev));   // blocking: the source is reusable on return
+        one_pass_reap(false);
+    }
     return true;
 }
 
@@ -1361,10 +1438,8 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         }
     }
     if (kind == X_ACC && world != r.rank &&
-        one_pass_acc(world, op, scale, src, ss, dst, ds, count, levels, row_bytes_of(op, count[0]))) {
-        if (hdl) nb_complete_now(hdl);
+        one_pass_acc(world, op, scale, src, ss, dst, ds, count, levels, row_bytes_of(op, count[0]), hdl))
         return COMEX_SUCCESS;
-    }
     // the packed route: remote accumulates on this node, and -- under the
     // COMEX_ENABLE_* toggles -- accumulates / puts to self or same-node puts
     // a put into another GPU's memory is applied by its owner too (no rank writes
@@ -2381,6 +2456,14 @@ int comex_finalize() {
     Runtime &r = rt();
     if (!r.initialized) return COMEX_SUCCESS;
     comex_barrier(COMEX_GROUP_WORLD);   // drains every remote accumulate job
+    {
+        std::lock_guard<std::mutex> g(g_op_mu);   // one-pass locks were handed back by the barrier's fence
+        for (OnePassHold &h : g_op_hold)
+            for (hipEvent_t e : h.evs) (void)hipEventDestroy(e);
+        g_op_hold.clear();
+        for (hipEvent_t e : g_op_pool) (void)hipEventDestroy(e);
+        g_op_pool.clear();
+    }
     for (hipEvent_t e : g_chunk_ev) (void)hipEventDestroy(e);
     g_chunk_ev.clear();
     g_out.clear();
@@ -2464,8 +2547,11 @@ int comex_group_translate_world(comex_group_t group, int group_rank, int *world_
 int comex_fence_proc(int proc, comex_group_t group) {
     ensure_init();
     fence_target(translate_world(group, proc));
-    std::lock_guard<std::mutex> g(rt().launch_mu);
-    sched_sync_all();
+    {
+        std::lock_guard<std::mutex> g(rt().launch_mu);
+        sched_sync_all();
+    }
+    one_pass_reap(true);   // our one-pass kernels are done: hand the owners' locks back
     return COMEX_SUCCESS;
 }
 
@@ -2475,8 +2561,11 @@ int comex_fence_all(comex_group_t group) {
     Runtime &r = rt();
     drain_all_jobs();   // every target's chunks posted (side by side), then wait for each
     for (int t = 0; t < r.size; ++t) fence_target(t);
-    std::lock_guard<std::mutex> g(r.launch_mu);
-    sched_sync_all();
+    {
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        sched_sync_all();
+    }
+    one_pass_reap(true);
     return COMEX_SUCCESS;
 }
 
@@ -2611,6 +2700,7 @@ int comex_wait_all(comex_group_t group) {
         std::lock_guard<std::mutex> g(r.launch_mu);
         sched_sync_all();
     }
+    one_pass_reap(true);
     for (int i = 0; i < kMaxNb; ++i) r.nb_used[i] = false;
     return COMEX_SUCCESS;
 }
