@@ -1141,9 +1141,12 @@ static int64_t row_bytes_of(int op, int count0) {
 //     (own_write_guard, from sched_pick) and keeps it while such writes may be in
 //     flight; its progress thread gives it up when a requester waits (mem_want):
 //     every stream of the owner drained first (sched_sync_all);
-//   * a requester takes the owner's lock, launches, waits for its kernel, and
-//     releases it -- so the owner's next write (ordered after the host-observed
+//   * a requester takes the owner's lock, launches, and releases it once its
+//     kernels' events completed (its progress thread, or a blocking call / wait /
+//     fence) -- so the owner's next write (ordered after the host-observed
 //     completion, one device: kernel-boundary coherence) sees the update.
+// Lock holders never wait for another memory lock while holding launch_mu, and a
+// requester's lock is released by event completion alone, so no wait cycle forms.
 // A requester never writes its own segments while it holds another rank's lock
 // (the one-pass launch writes only the remote view), so no cycle of locks forms.
 // Across GPUs there is no one-pass route: the owner applies.
@@ -1571,7 +1574,7 @@ static char *iov_host_scratch(size_t bytes) {   // pinned upload staging; caller
     if (bytes <= g_iov_host_bytes) return g_iov_host;
     if (g_iov_host) GA_HIP(hipHostFree(g_iov_host));
     g_iov_host_bytes = std::max<size_t>(bytes, 1 << 20);
-    GA_HIP(hipHostMalloc((void **)&g_iov_host, g_iov_host_bytes, hipHostMallocDefault));
+    GA_HIP(hipHostMalloc((void **)&g_iov_host, g_iov_host_bytes, hipHostMallocMapped));
     return g_iov_host;
 }
 
@@ -1906,7 +1909,14 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     ds.lo = dst_listed ? (int64_t)dlo : (int64_t)(uintptr_t)(dev + o_res);
     ds.hi = dst_listed ? (int64_t)dhi : ds.lo + (int64_t)pk;
     const int si = sched_pick(ss, ds);
-    GA_HIP(hipMemcpyAsync(dev, up, o_res, hipMemcpyHostToDevice, r.streams[si]));
+    // the upload: the copy kernel reading the mapped pinned buffer (no DMA engine
+    // round trip before the first io-vector kernel), or the runtime's copy
+    static const bool kernel_upload = [] {
+        const char *e = getenv("COMEX_AMD_IOV_KERNEL_UPLOAD");
+        return !e || atoi(e) != 0;
+    }();
+    if (kernel_upload) upload_pinned(dev, up, o_res, r.streams[si]);
+    else GA_HIP(hipMemcpyAsync(dev, up, o_res, hipMemcpyHostToDevice, r.streams[si]));
     const int rc = runs ? launch_iov_runs(cop, scale, d, align_or, dlo, (dhi - dlo) / (uint64_t)bytes + 1,
                                           dev + o_work, work, r.streams[si], src_peer)
                         : launch_iov(cop, scale, d, align_or, serial, r.streams[si], src_peer);

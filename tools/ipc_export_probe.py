@@ -15,6 +15,12 @@ counts refusals:
   export_twice       A exports the same block twice
   mixed_sizes        interleaved 64 MiB / 1 GiB blocks, the bench's C5 pattern
                      (1 GiB GA blocks and sources, then a 64 MiB check GA)
+  fd_growth          open file descriptors of the exporter after each export and
+                     each free, and of the importer after each open and close
+                     (dmabuf IPC: an export is a file descriptor)
+  fd_limit           the exporter's RLIMIT_NOFILE lowered to a few descriptors above
+                     its current count: does running out of descriptors make
+                     hipIpcGetMemHandle refuse, and with which error
 
 Usage: python tools/ipc_export_probe.py [rounds]  -> one JSON line per scenario.
 """
@@ -66,6 +72,10 @@ def open_h(L, raw):
     return rc, p.value
 
 
+def nfds():
+    return len(os.listdir("/proc/self/fd"))
+
+
 def worker(role, q_in, q_out, rounds):
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     L = hip()
@@ -106,6 +116,41 @@ def worker(role, q_in, q_out, rounds):
                 rc2, raw2 = export(L, p)
                 q_out.put(("twice", rc1, rc2, raw1 == raw2))
                 assert L.hipFree(ctypes.c_void_p(p)) == 0
+            elif name == "fd_growth":
+                trace = []
+                for i in range(args):
+                    f0 = nfds()
+                    p = alloc(L, 64 * MB)
+                    rc, raw = export(L, p)
+                    f1 = nfds()
+                    q_out.put(("handle", rc, raw, p))
+                    q_in.get()                  # B opened and closed it
+                    assert L.hipFree(ctypes.c_void_p(p)) == 0
+                    trace.append((f0, f1, nfds(), rc))
+                q_out.put(("fd_growth", trace))
+            elif name == "fd_limit":
+                import resource
+                soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+                base = nfds()
+                resource.setrlimit(resource.RLIMIT_NOFILE, (base + 6, hard))
+                got, ps = [], []
+                for i in range(24):
+                    try:
+                        p = alloc(L, 64 * MB)
+                    except AssertionError:
+                        got.append(("alloc_refused", nfds()))
+                        break
+                    ps.append(p)
+                    rc, _ = export(L, p)
+                    got.append((rc, L.hipGetErrorString(rc).decode() if rc else "", nfds()))
+                    if rc:
+                        break
+                resource.setrlimit(resource.RLIMIT_NOFILE, (soft, hard))
+                # the same export after the limit is restored
+                rc_after = export(L, ps[-1])[0] if ps else None
+                for p in ps:
+                    L.hipFree(ctypes.c_void_p(p))
+                q_out.put(("fd_limit", base, soft, hard, got, rc_after))
             elif name == "mixed":
                 sizes = args
                 ps = []
@@ -139,6 +184,17 @@ def worker(role, q_in, q_out, rounds):
                 erc, _ = export(L, mine)
                 assert L.hipFree(ctypes.c_void_p(mine)) == 0
                 q_out.put(("import_va_reuse", orc, mine == v, erc))
+            elif name == "fd_growth":
+                trace = []
+                for i in range(args):
+                    _, rc, raw, p = q_in.get()
+                    f0 = nfds()
+                    orc, v = open_h(L, raw)
+                    f1 = nfds()
+                    L.hipIpcCloseMemHandle(ctypes.c_void_p(v))
+                    trace.append((f0, f1, nfds(), orc))
+                    q_out.put(("opened",))
+                q_out.put(("fd_growth_b", trace))
             elif name == "mixed":
                 _, rcs, raws = q_in.get()
                 vs = []
@@ -250,6 +306,27 @@ def main():
         assert qa_out.get()[0] == "done" and qb_out.get()[0] == "done"
         stats["rounds"] += 1
     results["mixed_sizes"] = stats
+    # descriptors per export / open, and after free / close
+    nfd = max(4, rounds)
+    qa_in.put(("fd_growth", nfd))
+    qb_in.put(("fd_growth", nfd))
+    for _ in range(nfd):
+        qb_in.put(qa_out.get())
+        qb_out.get()
+        qa_in.put("go")
+    ta = qa_out.get()[1]
+    tb = qb_out.get()[1]
+    assert qa_out.get()[0] == "done" and qb_out.get()[0] == "done"
+    results["fd_growth"] = {"rounds": nfd, "exporter_fds_before_export_after_export_after_free": ta[:4] + ta[-2:],
+                            "exporter_fd_leak_per_round": (ta[-1][2] - ta[0][0]) / nfd,
+                            "importer_fds_before_open_after_open_after_close": tb[:4] + tb[-2:],
+                            "importer_fd_leak_per_round": (tb[-1][2] - tb[0][0]) / nfd}
+    qa_in.put(("fd_limit", 0))
+    qb_in.put(("noop", 0))
+    fl = qa_out.get()
+    assert qa_out.get()[0] == "done" and qb_out.get()[0] == "done"
+    results["fd_limit"] = {"fds_at_start": fl[1], "nofile_soft": fl[2], "nofile_hard": fl[3],
+                           "exports_rc_errstr_fds": fl[4], "export_after_limit_restored_rc": fl[5]}
     qa_in.put(None)
     qb_in.put(None)
     A.join(60)
