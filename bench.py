@@ -425,16 +425,29 @@ def run_gpu(args, dist, finalize=True):
     L.comex_barrier(0)
     dist.barrier()
     ga_amd.sync()
+    # BENCH_STAMPS=1 (diagnostic runs only, never the driver's): the library's host
+    # stamps (gaamd_stamps, CLOCK_BOOTTIME) of the first call and of the closing wait,
+    # read after the region, for tools/region_edges.py to place on a kernel trace
+    stamps_on = os.environ.get("BENCH_STAMPS") == "1"
+    st_buf = (ctypes.c_ulonglong * 8)()
+
     def value_region(first):
+        first_stamps = None
+        if stamps_on:
+            L.gaamd_stamps(1, None)
         b0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
         t0 = time.perf_counter()
         step(first)
         t_first = time.perf_counter()
+        if stamps_on:
+            L.gaamd_stamps(-1, st_buf)
+            first_stamps = list(st_buf[:5])
         for i in range(1, args.steps):
             step(first + i)
         t_enq = time.perf_counter()
         # every step's kernel has finished: comex_wait_all synchronises every library
         # stream (hipStreamSynchronize each), i.e. all GPU work of this rank
+        bw = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
         hd.drain()
         if seg_dst:
             L.comex_fence_all(0)            # remote completion: the owner has applied every request
@@ -442,9 +455,14 @@ def run_gpu(args, dist, finalize=True):
         b1 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
         # boottime_ns: the region's ends on the clock rocprofv3 stamps kernels with,
         # so a profiled run can place the first kernel's start and the last one's end
-        return t1 - t0, {"first_call_us": round((t_first - t0) * 1e6, 1),
-                         "enqueue_all_us": round((t_enq - t0) * 1e6, 1), "total_us": round((t1 - t0) * 1e6, 1),
-                         "boottime_ns": [b0, b1]}
+        prof = {"first_call_us": round((t_first - t0) * 1e6, 1),
+                "enqueue_all_us": round((t_enq - t0) * 1e6, 1), "total_us": round((t1 - t0) * 1e6, 1),
+                "boottime_ns": [b0, b1]}
+        if stamps_on:
+            L.gaamd_stamps(0, st_buf)
+            prof["stamps_ns"] = {"region_start": b0, "first_call": first_stamps, "wait_call_py": bw,
+                                 "wait": list(st_buf[5:8]), "region_end": b1}
+        return t1 - t0, prof
 
     elapsed, region_profile = value_region(nxt)
     gc.enable()

@@ -165,6 +165,13 @@ def route_counts():
     return {"packed": c[0], "direct_src": c[1], "iov": c[2], "rmw": c[3], "one_pass": lib().gaamd_one_pass_count()}
 
 
+def toggle_counts():
+    """operations that took the reference's PACKED / IOV / GET_SELF+SMP toggle routes"""
+    c = (ctypes.c_ulonglong * 3)()
+    lib().gaamd_toggle_counts(c)
+    return {"rows": c[0], "pairs": c[1], "owner_gets": c[2]}
+
+
 def owner_counts():
     """requests this rank's progress thread applied, by kind"""
     c = (ctypes.c_ulonglong * 4)()

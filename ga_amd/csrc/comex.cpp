@@ -532,6 +532,43 @@ static void post_request_direct(int t, int op, const void *scale, uint64_t dst_a
     q.state.store(2, std::memory_order_release);
 }
 
+// kind 4: a get through the owner (COMEX_ENABLE_GET_SELF/SMP=0): the owner packs
+// rows rb..re of its patch into our staging at `off` (nb_get's OP_GET message to the
+// progress rank, comex.c:6188-6214)
+static void post_request_get(int t, uint64_t src_addr, const int *src_stride, const int *count, int levels,
+                             uint64_t off, uint64_t len, uint64_t rb, uint64_t re) {
+    Runtime &r = rt();
+    Inbox *ib = inbox_of(r.shm, r.li(t));
+    const uint64_t ticket = ib->tail.fetch_add(1, std::memory_order_acq_rel);
+    Request &q = ib->slot[ticket % kInboxSlots];
+    for (unsigned spins = 0; ib->head.load(std::memory_order_acquire) + kInboxSlots <= ticket; ++spins)
+        if (spins > 256) sched_yield();
+    for (unsigned spins = 0;; ++spins) {
+        uint32_t expect = 0;
+        if (q.state.compare_exchange_weak(expect, 1, std::memory_order_acq_rel)) break;
+        if (spins > 256) sched_yield();
+    }
+    q.src_rank = r.rank;
+    q.op = kOpCopy;
+    q.levels = levels;
+    memset(q.count, 0, sizeof(q.count));
+    memset(q.dst_stride, 0, sizeof(q.dst_stride));
+    memset(q.src_stride, 0, sizeof(q.src_stride));
+    for (int j = 0; j <= levels; ++j) q.count[j] = count[j];
+    for (int j = 0; j < levels; ++j) q.src_stride[j] = src_stride[j];
+    q.src_addr = src_addr;
+    q.dst_addr = 0;
+    q.staging_off = off;
+    q.bytes = len;
+    q.seq = (rb << 32) | (re & 0xffffffffull);
+    memset(q.scale, 0, sizeof(q.scale));
+    q.kind = 4;
+    q.iov_serial = 0;
+    q.iov_align = 0;
+    q.dst_hi = 0;
+    q.state.store(2, std::memory_order_release);
+}
+
 static uint64_t iov_list_off(int n, int bytes) { return (((uint64_t)n * (uint64_t)bytes) + 15) & ~15ull; }
 
 static bool own_release_if_wanted();   // one-pass memory lock (below)
@@ -614,7 +651,7 @@ static void progress_loop() {
         // the kind tests fall through to the last branch as a packed one (an
         // io-vector request applied as an 8-byte unpack-acc: a whole request lost)
         const bool ready = q.state.load(std::memory_order_acquire) == 2;
-        if (ready && q.kind != 0 && q.kind != 1 && q.kind != 2 && q.kind != 3)
+        if (ready && (q.kind < 0 || q.kind > 4))
             fatal("inbox request of unknown kind %d from rank %d", (int)q.kind, (int)q.src_rank);
         if (ready && q.kind == 1) {
             // io-vector accumulate (the _acc_iov_handler analogue, comex.c:4284-4397)
@@ -742,6 +779,37 @@ static void progress_loop() {
             }
             inflight.push_back({ev, src, false});
             g_owned[3].fetch_add(1, std::memory_order_relaxed);
+            q.state.store(0, std::memory_order_release);
+            ib->head.store(h + 1, std::memory_order_release);
+            worked = true;
+        } else if (ready && q.kind == 4) {
+            // a get through us: rows rb..re of our patch packed into the requester's
+            // staging (a rank on this GPU, or ourselves: the requester never routes a
+            // get from another GPU here -- no rank writes another GPU's HBM)
+            const int src = q.src_rank;
+            const uint64_t rb = q.seq >> 32, re = q.seq & 0xffffffffull;
+            int pstride[8];
+            {
+                int64_t acc = q.count[0];
+                for (int j = 0; j < q.levels; ++j) { pstride[j] = (int)acc; acc *= q.count[j + 1]; }
+            }
+            char *stage = const_cast<char *>(peer_staging_or_die(src)) + q.staging_off;
+            char *stage0 = stage - (int64_t)rb * q.count[0];
+            int64_t slo = 0, shi = 0;
+            side_span_host(q.src_stride, q.count, q.levels, q.count[0], &slo, &shi);
+            hipEvent_t ev;
+            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            else { ev = pool.back(); pool.pop_back(); }
+            {
+                std::lock_guard<std::mutex> g(r.launch_mu);
+                const int si = sched_pick(span_of((void *)q.src_addr, slo, shi), span_of(stage, 0, (int64_t)q.bytes));
+                const int rc = launch_strided(kOpCopy, nullptr, (const char *)q.src_addr, q.src_stride, stage0, pstride,
+                                              q.count, q.levels, r.streams[si], nullptr, rb, re);
+                if (rc) fatal("get pack launch failed (%d)", rc);
+                GA_HIP(hipEventRecord(ev, r.streams[si]));
+            }
+            inflight.push_back({ev, src, false});
+            g_owned[0].fetch_add(1, std::memory_order_relaxed);
             q.state.store(0, std::memory_order_release);
             ib->head.store(h + 1, std::memory_order_release);
             worked = true;
@@ -1353,8 +1421,154 @@ static int get_via_scratch(const char *src, const int *ss, char *dst, const int 
     return rc;
 }
 
+// ---- host-side stamps (diagnostic) -----------------------------------------
+// CLOCK_BOOTTIME ns (the clock rocprofv3 stamps kernels with) at fixed points of the
+// last strided call and the last comex_wait_all, for placing the bench's value
+// region edges on a kernel trace.  Off unless gaamd_stamps(1).
+static std::atomic<bool> g_stamp_on{false};
+static uint64_t g_stamp[8];
+static inline void stamp(int i) {
+    if (!g_stamp_on.load(std::memory_order_relaxed)) return;
+    timespec ts;
+    clock_gettime(CLOCK_BOOTTIME, &ts);
+    g_stamp[i] = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+// ---- the reference's route toggles beyond SELF/SMP --------------------------
+static std::atomic<unsigned long long> g_toggle[3];   // gaamd_toggle_counts: rows, pairs, owner gets
+
+// the reference's self/SMP test (comex.c:6365-6377, 6634-6647, 6910-6913,
+// 7120-7122, 7224-7226, 7336-7338): true when the self or SMP route applies to an
+// operation on `world`; only otherwise are the PACKED / IOV toggles consulted
+static bool self_smp_route(Xfer kind, int world) {
+    Runtime &r = rt();
+    const bool self = kind == X_ACC ? r.acc_self_direct : (kind == X_PUT ? r.put_self_direct : r.get_self_direct);
+    const bool smp = kind == X_ACC ? r.acc_smp_direct : (kind == X_PUT ? r.put_smp_direct : r.get_smp_direct);
+    return world == r.rank ? self : (smp && r.same_node(world));
+}
+
+static int xfer_contig(Xfer kind, int op, void *scale, void *src, void *dst, int bytes, int proc, int group,
+                       comex_request_t *hdl);
+
+// contiguous operations issued non-blocking, at most 32 outstanding (the handle
+// table holds kMaxNb), all complete when the window is flushed
+struct ContigWindow {
+    std::deque<comex_request_t> h;
+    void issue(Xfer kind, int op, void *scale, void *src, void *dst, int bytes, int proc, int group) {
+        comex_request_t x = -1;
+        xfer_contig(kind, op, scale, src, dst, bytes, proc, group, &x);
+        h.push_back(x);
+        if (h.size() >= 32) {
+            comex_wait(&h.front());
+            h.pop_front();
+        }
+    }
+    void flush() {
+        for (comex_request_t &x : h) comex_wait(&x);
+        h.clear();
+    }
+};
+
+// COMEX_ENABLE_{ACC,PUT,GET}_PACKED=0: the patch row by row, each row a contiguous
+// operation, in the odometer order of nb_accs / nb_puts / nb_gets (comex.c:6918-6961)
+static int xfer_rows(Xfer kind, int op, void *scale, char *src, const int *ss, char *dst, const int *ds,
+                     const int *count, int levels, int proc, int group, comex_request_t *hdl) {
+    uint64_t rows = 1;
+    for (int j = 1; j <= levels; ++j) rows *= (uint64_t)count[j];
+    int idx[8] = {0};
+    ContigWindow w;
+    for (uint64_t i = 0; i < rows; ++i) {
+        int64_t so = 0, dof = 0;
+        for (int j = 1; j <= levels; ++j) {
+            so += (int64_t)idx[j] * ss[j - 1];
+            dof += (int64_t)idx[j] * ds[j - 1];
+        }
+        w.issue(kind, op, scale, src + so, dst + dof, count[0], proc, group);
+        for (int j = 1; j <= levels; ++j) {
+            if (++idx[j] < count[j]) break;
+            idx[j] = 0;
+        }
+    }
+    w.flush();
+    g_toggle[0].fetch_add(1, std::memory_order_relaxed);
+    if (hdl) nb_complete_now(hdl);
+    return COMEX_SUCCESS;
+}
+
+// COMEX_ENABLE_GET_SELF/SMP=0: a get from a rank on this GPU (or from ourselves)
+// through the owner.  Row ranges of at most half the staging sub-ring for t: we
+// reserve the slice, post a kind-4 request, the owner's progress thread packs the
+// rows into it and counts the request done, we unpack the slice into dst.  One
+// range at a time (this is the reference's test route, not a fast path).
+static void get_via_owner(int t, char *src, const int *ss, char *dst, const int *ds, const int *count, int levels) {
+    Runtime &r = rt();
+    const uint64_t sub = sub_ring_bytes();
+    const uint64_t row = (uint64_t)count[0];
+    if (row > sub / 2) {
+        // pieces of a long row become one more level (they lie back to back on both
+        // sides), the rows' tails a second patch
+        if (levels + 1 >= kMaxLevels) fatal("get of %lu-byte rows at %d levels exceeds the staging ring", (unsigned long)row, levels);
+        const uint64_t piece = std::max<uint64_t>(16, (sub / 2) / 16 * 16);
+        const uint64_t k = row / piece, tail = row - k * piece;
+        int cb[8], ssb[8], dsb[8];
+        cb[0] = (int)piece;
+        cb[1] = (int)k;
+        ssb[0] = dsb[0] = (int)piece;
+        for (int j = 0; j < levels; ++j) {
+            cb[j + 2] = count[j + 1];
+            ssb[j + 1] = ss[j];
+            dsb[j + 1] = ds[j];
+        }
+        get_via_owner(t, src, ssb, dst, dsb, cb, levels + 1);
+        if (tail) {
+            int ct[8];
+            for (int j = 0; j <= levels; ++j) ct[j] = count[j];
+            ct[0] = (int)tail;
+            get_via_owner(t, src + k * piece, ss, dst + k * piece, ds, ct, levels);
+        }
+        return;
+    }
+    uint64_t rows = 1;
+    for (int j = 1; j <= levels; ++j) rows *= (uint64_t)count[j];
+    int64_t slo = 0, shi = 0, dlo = 0, dhi = 0;
+    side_span_host(ss, count, levels, (int64_t)row, &slo, &shi);
+    side_span_host(ds, count, levels, (int64_t)row, &dlo, &dhi);
+    check_remote(t, src, slo, shi);
+    drain_target(t);   // our earlier chunks to t are posted first: its done counter stays in order
+    View dv = local_view(dst, dlo, dhi, true);
+    const bool host_side = needs_sync(dv);
+    int pstride[8];
+    {
+        int64_t acc = (int64_t)row;
+        for (int j = 0; j < levels; ++j) { pstride[j] = (int)acc; acc *= count[j + 1]; }
+    }
+    const uint64_t per = std::max<uint64_t>(1, (sub / 2) / row);
+    for (uint64_t rb = 0; rb < rows; rb += per) {
+        const uint64_t re = std::min(rows, rb + per), len = (re - rb) * row;
+        const uint64_t off = stage_alloc(t, ring_len(len));
+        const uint64_t seq = ++r.posted[t];
+        g_pend[t].push_back({seq, off, ring_len(len)});
+        r.stage_head[t] = off + ring_len(len);
+        post_request_get(t, (uint64_t)(uintptr_t)src, ss, count, levels, (uint64_t)t * sub + off, len, rb, re);
+        wait_done(t, seq);   // the owner's pack kernel has completed
+        const char *stage0 = r.staging + (size_t)t * sub + off - (int64_t)(rb * row);
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        int si = 0;
+        if (host_side) sched_join();
+        else si = sched_pick(span_of(stage0, (int64_t)(rb * row), (int64_t)(re * row)), span_of(dv.dev, dlo, dhi),
+                             len);
+        const int rc = launch_strided(kOpCopy, nullptr, stage0, pstride, dv.dev, ds, count, levels, r.streams[si],
+                                      nullptr, rb, re);
+        if (rc) fatal("get unpack launch failed (%d)", rc);
+        GA_HIP(hipStreamSynchronize(r.streams[si]));   // the slice is free for the next request
+    }
+    release_view(dv);
+    g_toggle[2].fetch_add(1, std::memory_order_relaxed);
+}
+
 static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, int *ds, int *count,
                 int levels, int proc, int group, comex_request_t *hdl) {
+    stamp(0);
     ensure_init();
     Runtime &r = rt();
     progress_jobs();   // pending remote accumulates advance on every call
@@ -1378,6 +1592,9 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         if (hdl) nb_complete_now(hdl);
         return COMEX_SUCCESS;
     }
+    if (levels > 0 && !(kind == X_ACC ? r.acc_packed : (kind == X_PUT ? r.put_packed : r.get_packed)) &&
+        !self_smp_route(kind, world))
+        return xfer_rows(kind, op, scale, (char *)src, ss, (char *)dst, ds, count, levels, proc, group, hdl);
 
     if (world != r.rank && !r.same_node(world)) {
         // another node: the message protocol (wire.cpp)
@@ -1443,6 +1660,14 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     if (kind == X_ACC && world != r.rank &&
         one_pass_acc(world, op, scale, src, ss, dst, ds, count, levels, row_bytes_of(op, count[0]), hdl))
         return COMEX_SUCCESS;
+    // a get through the owner (COMEX_ENABLE_GET_SELF/SMP=0) from a rank on this GPU or
+    // ourselves; from another GPU the get stays a direct read (system-scope loads):
+    // the owner could only answer by writing our HBM
+    if (kind == X_GET && !self_smp_route(X_GET, world) && !r.peer_src(world)) {
+        get_via_owner(world, (char *)src, ss, (char *)dst, ds, count, levels);
+        if (hdl) nb_complete_now(hdl);
+        return COMEX_SUCCESS;
+    }
     // the packed route: remote accumulates on this node, and -- under the
     // COMEX_ENABLE_* toggles -- accumulates / puts to self or same-node puts
     // a put into another GPU's memory is applied by its owner too (no rank writes
@@ -1524,11 +1749,14 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     hipStream_t st;
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
+        stamp(1);
         if (host_side) sched_join();   // staged copies sit on stream 0: run there, after everything
         else si = sched_pick(span_of(sv.dev, slo, shi), span_of(dv.dev, dlo, dhi), payload_bytes(rb, count, levels));
         st = r.streams[si];
+        stamp(2);
         int rc = launch_strided(cop, scale, sv.dev, ss, dv.dev, ds, count, levels, st, last_launch_info(), 0, ~0ull,
                                 false, peer);
+        stamp(3);
         if (rc == kErrPeerOrdered) rc = get_via_scratch(sv.dev, ss, dv.dev, ds, count, levels, st);
         if (rc) fatal("strided %s launch failed (code %d): misaligned elements or bad descriptor",
                       kind == X_ACC ? "acc" : (kind == X_PUT ? "put" : "get"), rc);
@@ -1549,6 +1777,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         release_view(dv);
     }
     if (hdl) nb_complete_now(hdl, si, true);
+    stamp(4);
     return COMEX_SUCCESS;
 }
 
@@ -1940,6 +2169,15 @@ static int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len,
         const int n = darr[k].count, bytes = darr[k].bytes;
         if (n <= 0) continue;
         if (bytes <= 0) fatal("io-vector of %d bytes", bytes);
+        if (!(kind == X_ACC ? r.acc_iov : (kind == X_PUT ? r.put_iov : r.get_iov)) && !self_smp_route(kind, world)) {
+            // COMEX_ENABLE_*_IOV=0: pair by pair as contiguous operations (nb_accv's
+            // loop, comex.c:7342-7351)
+            ContigWindow w;
+            for (int i = 0; i < n; ++i) w.issue(kind, op, scale, darr[k].src[i], darr[k].dst[i], bytes, proc, group);
+            w.flush();
+            g_toggle[1].fetch_add(1, std::memory_order_relaxed);
+            continue;
+        }
         const bool remote_side_is_dst = (kind != X_GET);
         // the owner applies it (staging + inbox request): every remote accumulate, and
         // a put into another GPU's memory (no rank writes another GPU's HBM)
@@ -2402,10 +2640,18 @@ int comex_init() {
         r.acc_self_direct = flag("COMEX_ENABLE_ACC_SELF") || r.acc_smp_direct;
         r.put_smp_direct = flag("COMEX_ENABLE_PUT_SMP");
         r.put_self_direct = flag("COMEX_ENABLE_PUT_SELF") || r.put_smp_direct;
+        r.get_smp_direct = flag("COMEX_ENABLE_GET_SMP");
+        r.get_self_direct = flag("COMEX_ENABLE_GET_SELF") || r.get_smp_direct;
+        r.acc_packed = flag("COMEX_ENABLE_ACC_PACKED");
+        r.put_packed = flag("COMEX_ENABLE_PUT_PACKED");
+        r.get_packed = flag("COMEX_ENABLE_GET_PACKED");
+        r.acc_iov = flag("COMEX_ENABLE_ACC_IOV");
+        r.put_iov = flag("COMEX_ENABLE_PUT_IOV");
+        r.get_iov = flag("COMEX_ENABLE_GET_IOV");
     }
     const char *dbg = getenv("COMEX_AMD_DEBUG");
     r.debug = dbg ? atoi(dbg) : 0;
-    if (r.size > 1 || !r.acc_self_direct || !r.put_self_direct) {
+    if (r.size > 1 || !r.acc_self_direct || !r.put_self_direct || !r.get_self_direct) {
         // staging HBM for remote accumulates, exported to every local rank
         const char *mb = getenv("COMEX_AMD_STAGING_MB");
         r.staging_bytes = (size_t)(mb ? atol(mb) : 256) << 20;
@@ -2696,6 +2942,7 @@ int comex_test(comex_request_t *h, int *status) {
 }
 
 int comex_wait_all(comex_group_t group) {
+    stamp(5);
     ensure_init();
     (void)group;
     Runtime &r = rt();
@@ -2708,7 +2955,9 @@ int comex_wait_all(comex_group_t group) {
     }
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
+        stamp(6);
         sched_sync_all();
+        stamp(7);
     }
     one_pass_reap(true);
     for (int i = 0; i < kMaxNb; ++i) r.nb_used[i] = false;
@@ -3027,6 +3276,21 @@ int gaamd_peers_unmapped(void) {
     for (int q = 0; q < r.size && q < (int)r.peer_staging.size(); ++q)
         if (q != r.rank && r.same_node(q) && !r.peer_staging[q]) ++n;
     return n;
+}
+
+int gaamd_stamps(int on, unsigned long long out[8]) {
+    if (out)
+        for (int k = 0; k < 8; ++k) out[k] = g_stamp[k];
+    if (on >= 0) {
+        if (on) memset(g_stamp, 0, sizeof(g_stamp));
+        g_stamp_on.store(on != 0, std::memory_order_relaxed);
+    }
+    return 0;
+}
+
+int gaamd_toggle_counts(unsigned long long counts[3]) {
+    for (int k = 0; k < 3; ++k) counts[k] = g_toggle[k].load(std::memory_order_relaxed);
+    return 0;
 }
 
 int gaamd_route_counts(unsigned long long counts[4]) {

@@ -57,12 +57,14 @@ struct alignas(64) Request {
     uint64_t seq;                    // strided: row range (begin << 32 | end)
     uint8_t scale[16];
     int32_t kind;                    // 0 strided (count/dst_stride), 1 io-vector, 2 rmw,
-                                     // 3 strided read straight from src_rank's segment
+                                     // 3 strided read straight from src_rank's segment,
+                                     // 4 get: our patch (src_addr/src_stride) packed into
+                                     //   src_rank's staging at staging_off (row range in seq)
     int32_t iov_serial;              // io-vector: destinations overlap -> in order
     uint64_t iov_align;              // io-vector: OR of the destination addresses
     uint64_t dst_hi;                 // io-vector: [dst_addr, dst_hi) covers every pair
-    int32_t src_stride[8];           // kind 3: the source patch in src_rank's segment
-    uint64_t src_addr;               // kind 3: src_rank's address space
+    int32_t src_stride[8];           // kind 3: the source patch in src_rank's segment; kind 4: ours
+    uint64_t src_addr;               // kind 3: src_rank's address space; kind 4: ours
 };
 
 struct alignas(64) Inbox {
@@ -147,6 +149,16 @@ struct Runtime {
     // ACC_SMP off also turns the direct-source route off (a same-node accumulate
     // then always packs, comex.c:6911-6915)
     bool acc_self_direct = true, acc_smp_direct = true, put_self_direct = true, put_smp_direct = true;
+    // COMEX_ENABLE_GET_{SELF,SMP} (comex.c:444-465, nb_get 6157-6214): with both off a
+    // get from this rank, with SMP off a get from a rank sharing this GPU, goes
+    // through the owner (kind 4: its progress thread packs the patch into our
+    // staging, we unpack it) instead of reading the owner's memory directly
+    bool get_self_direct = true, get_smp_direct = true;
+    // COMEX_ENABLE_{ACC,PUT,GET}_PACKED and _IOV (comex.c:474-531): off, a strided /
+    // io-vector operation that does not take the self/SMP route goes row by row /
+    // pair by pair as contiguous operations (nb_accs 6918-6961, nb_accv 7342-7351)
+    bool acc_packed = true, put_packed = true, get_packed = true;
+    bool acc_iov = true, put_iov = true, get_iov = true;
     // COMEX_AMD_DIRECT_SRC (default 1): a same-node accumulate whose source lies
     // in one of this rank's HBM segments is applied by the owner straight from
     // that segment (its IPC mapping) -- no pack pass, no staging

@@ -85,6 +85,17 @@ int gaamd_kernel_counts(unsigned long long counts[5]);
  * {packed chunks (pack -> staging -> owner unpack), direct-source (owner reads
  * our segment), io-vector, rmw} */
 int gaamd_route_counts(unsigned long long counts[4]);
+/* Operations that took the reference's route toggles beyond SELF/SMP, since init:
+ * [0] strided operations split row by row (COMEX_ENABLE_{ACC,PUT,GET}_PACKED=0),
+ * [1] io-vector descriptors split pair by pair (COMEX_ENABLE_{ACC,PUT,GET}_IOV=0),
+ * [2] gets through the owner (COMEX_ENABLE_GET_SELF/SMP=0). */
+int gaamd_toggle_counts(unsigned long long counts[3]);
+/* Diagnostic host stamps (CLOCK_BOOTTIME ns) of the last strided call and the last
+ * comex_wait_all: [0] call entry, [1] route decided (launch lock held), [2] stream
+ * picked, [3] kernel launched, [4] call return, [5] wait entry, [6] streams about
+ * to be synchronised, [7] synchronised.  out (may be NULL) receives the current
+ * stamps; on = 1 clears them and turns stamping on, 0 off, -1 leaves it. */
+int gaamd_stamps(int on, unsigned long long out[8]);
 /* one-pass accumulates this rank applied into the segment of a rank on the same GPU */
 unsigned long long gaamd_one_pass_count(void);
 /* same-node peers whose staging buffer this rank could not map by IPC at

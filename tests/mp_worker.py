@@ -275,6 +275,11 @@ def remote_test(L, rank, size):
     ga_amd.comex_barrier()
     assert ga_amd.comex_free(seg2[rank]) == 0
     assert ga_amd.comex_free(seg[rank]) == 0
+    if os.environ.get("TEST_EXPECT_TOGGLES"):
+        # COMEX_ENABLE_*_PACKED / _IOV / GET_SELF+SMP = 0: the routes they select ran
+        tc = ga_amd.toggle_counts()
+        assert tc["rows"] > 0 and tc["pairs"] > 0 and tc["owner_gets"] > 0, (rank, tc)
+        say(rank, f"toggle routes {tc}")
     ga_amd.comex_finalize()
 
 

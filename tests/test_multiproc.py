@@ -299,6 +299,25 @@ def test_packed_route_forced_by_comex_enable_toggles(n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2])
+def test_reference_route_toggles_packed_iov_get(n):
+    """The rest of the reference's route toggles (comex.c:413-573): with SELF/SMP off
+    for accumulates, puts and gets, COMEX_ENABLE_{ACC,PUT,GET}_PACKED=0 sends every
+    strided operation row by row as contiguous ones (nb_accs 6918-6961),
+    COMEX_ENABLE_{ACC,PUT,GET}_IOV=0 every io-vector pair by pair (nb_accv 7342-7351),
+    and gets go through the owner (nb_get's OP_GET, 6188-6214: the owner packs into the
+    requester's staging).  The whole remote suite stays exact against the oracle,
+    and each of the three routes ran (gaamd_toggle_counts)."""
+    toggles = {k: "0" for k in ("COMEX_ENABLE_ACC_SELF", "COMEX_ENABLE_ACC_SMP", "COMEX_ENABLE_PUT_SELF",
+                                "COMEX_ENABLE_PUT_SMP", "COMEX_ENABLE_GET_SELF", "COMEX_ENABLE_GET_SMP",
+                                "COMEX_ENABLE_ACC_PACKED", "COMEX_ENABLE_PUT_PACKED", "COMEX_ENABLE_GET_PACKED",
+                                "COMEX_ENABLE_ACC_IOV", "COMEX_ENABLE_PUT_IOV", "COMEX_ENABLE_GET_IOV")}
+    toggles["TEST_EXPECT_TOGGLES"] = "1"
+    outs = launch("remote", n=n, timeout=180, extra_env=toggles)
+    assert "toggle routes" in outs[0], outs[0][-2000:]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,one_pass", [(2, "1"), (4, "1"), (3, "0")])
 def test_one_pass_same_gpu_exchange(n, one_pass):
     """Ranks sharing this GPU accumulate from plain device buffers into every

@@ -1,0 +1,147 @@
+// completion_probe.hip -- how much of the headline region's closing edge is the
+// runtime's completion path?  The bench region ends when
+// hipStreamSynchronize returns on both library streams after the last of K
+// accumulate kernels; profiled, that return comes 23-35 us after the last kernel
+// ends.  Here the same shape (K = 20 launches of a 64 MiB f64 axpy, 1 KiB per
+// one-wave block, 65536 blocks, two streams alternating) runs with a completion
+// counter: every block, after its stores, bumps a per-launch device counter
+// (agent-scope release first); the block that completes the launch stores the
+// launch number into pinned host memory (system-scope release).  The host spins
+// on that word, stamps when the last launch's number appears, then calls
+// hipStreamSynchronize on both streams and stamps again.  Reported per region:
+//   flag_us  -- region start to the host seeing the last launch's flag
+//   sync_us  -- region start to both synchronizations returning (the bench's end)
+//   gap_us   -- sync_us - flag_us: what a flag-polling wait would save
+// and the same region without the counter (plain_us), the counter's own cost.
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/completion_probe.hip -o tools/completion_probe
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <time.h>
+#include <algorithm>
+#include <vector>
+
+#define CK(x)                                                                                         \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) {                                                                       \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));                 \
+            exit(1);                                                                                  \
+        }                                                                                             \
+    } while (0)
+
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+#pragma clang fp contract(off)
+template <bool FLAG>
+__global__ __launch_bounds__(64) void k_axpy(const v2d *a, v2d *b, double s, unsigned long long *count,
+                                             unsigned long long target, unsigned int *host_flag, unsigned int tag) {
+    const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+    const v2d x = __builtin_nontemporal_load(a + i);
+    const v2d y = __builtin_nontemporal_load(b + i);
+    v2d r;
+    r.x = y.x + s * x.x;
+    r.y = y.y + s * x.y;
+    __builtin_nontemporal_store(r, b + i);
+    if (FLAG) {
+        __syncthreads();   // every lane's store issued and complete (vmcnt) before the count
+        if (threadIdx.x == 0) {
+            __atomic_thread_fence(__ATOMIC_RELEASE);   // agent scope by default: the block's stores first
+            const unsigned long long old = atomicAdd(count, 1ull);
+            if (host_flag && old + 1 == target) {
+                __atomic_thread_fence(__ATOMIC_SEQ_CST);
+                __hip_atomic_store(host_flag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+}
+
+static double now_us() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
+
+int main(int argc, char **argv) {
+    const int K = argc > 1 ? atoi(argv[1]) : 20;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 40;
+    const size_t n2 = (64ull << 20) / 16;   // v2d per 64 MiB
+    const int blocks = (int)(n2 / 64);
+    const int sets = 8;                     // rotate buffers as the bench does (MALL cannot hold them)
+    std::vector<v2d *> A(sets), B(sets);
+    for (int k = 0; k < sets; ++k) {
+        CK(hipMalloc((void **)&A[k], n2 * 16));
+        CK(hipMalloc((void **)&B[k], n2 * 16));
+        CK(hipMemset(A[k], 0, n2 * 16));
+        CK(hipMemset(B[k], 0, n2 * 16));
+    }
+    unsigned long long *cnt;
+    CK(hipMalloc((void **)&cnt, 8));
+    CK(hipMemset(cnt, 0, 8));
+    unsigned int *flag_h, *flag_d;
+    CK(hipHostMalloc((void **)&flag_h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    CK(hipHostGetDevicePointer((void **)&flag_d, flag_h, 0));
+    *(volatile unsigned int *)flag_h = 0;
+    hipStream_t st[2];
+    CK(hipStreamCreateWithFlags(&st[0], hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&st[1], hipStreamNonBlocking));
+    unsigned long long launched = 0;   // launches with the counter so far (the counter's target)
+    unsigned int tag = 0;
+    int it = 0;
+    auto region = [&](bool flag, double *flag_us, double *sync_us) {
+        CK(hipStreamSynchronize(st[0]));
+        CK(hipStreamSynchronize(st[1]));
+        const double t0 = now_us();
+        unsigned int last = 0;
+        for (int k = 0; k < K; ++k, ++it) {
+            const int s = it % sets;
+            if (flag) {
+                ++launched;
+                last = ++tag;
+                // one counter shared by all launches: launch number m completes when the
+                // count reaches m * blocks (launches on two streams can overlap, so the
+                // count only says "m launches' worth of blocks finished"; the flag of
+                // the K-th launch of a region is written once all K are done; only the
+                // region's last launch writes it)
+                k_axpy<true><<<blocks, 64, 0, st[k & 1]>>>(A[s], B[s], 0.5, cnt, launched * (unsigned long long)blocks,
+                                                          k == K - 1 ? flag_d : nullptr, last);
+            } else {
+                k_axpy<false><<<blocks, 64, 0, st[k & 1]>>>(A[s], B[s], 0.5, nullptr, 0, nullptr, 0);
+            }
+        }
+        if (flag) {
+            const double give_up = now_us() + 1e6;
+            while (__atomic_load_n((volatile unsigned int *)flag_h, __ATOMIC_ACQUIRE) != last) {
+                if (now_us() > give_up) {
+                    fprintf(stderr, "flag %u never arrived (saw %u)\n", last, *(volatile unsigned int *)flag_h);
+                    exit(2);
+                }
+            }
+            *flag_us = now_us() - t0;
+        }
+        CK(hipStreamSynchronize(st[0]));
+        CK(hipStreamSynchronize(st[1]));
+        *sync_us = now_us() - t0;
+    };
+    double f, s;
+    for (int w = 0; w < 10; ++w) { region(true, &f, &s); region(false, &f, &s); }
+    std::vector<double> fl, sy, pl;
+    for (int r = 0; r < rounds; ++r) {
+        region(true, &f, &s);
+        fl.push_back(f);
+        sy.push_back(s);
+        region(false, &f, &s);
+        pl.push_back(s);
+    }
+    auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+    std::vector<double> gap(fl.size());
+    for (size_t k = 0; k < fl.size(); ++k) gap[k] = sy[k] - fl[k];
+    const double bytes = 3.0 * 64 * (1 << 20) * K;
+    printf("{\"probe\": \"completion\", \"launches\": %d, \"rounds\": %d, \"flag_us\": %.2f, \"sync_us\": %.2f, "
+           "\"gap_us\": %.2f, \"gap_min_us\": %.2f, \"plain_us\": %.2f, \"frac_at_flag\": %.4f, \"frac_at_sync\": %.4f, "
+           "\"frac_plain\": %.4f}\n",
+           K, rounds, med(fl), med(sy), med(gap), *std::min_element(gap.begin(), gap.end()), med(pl),
+           bytes / (med(fl) * 1e-6) / 8e12, bytes / (med(sy) * 1e-6) / 8e12, bytes / (med(pl) * 1e-6) / 8e12);
+    return 0;
+}

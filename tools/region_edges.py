@@ -52,6 +52,26 @@ def main():
         "first_call_us": line["value_region"]["first_call_us"],
         "enqueue_all_us": line["value_region"]["enqueue_all_us"],
     }
+    st = line["value_region"].get("stamps_ns")
+    if st:
+        # BENCH_STAMPS=1: the library's own host stamps on the same clock
+        f, w = st["first_call"], st["wait"]
+        us = lambda a, b: round((b - a) / 1e3, 2)
+        out["first_call_breakdown_us"] = {
+            "python_to_library_entry": us(b0, f[0]),
+            "entry_to_route_decided": us(f[0], f[1]),
+            "stream_pick": us(f[1], f[2]),
+            "plan_and_hip_launch": us(f[2], f[3]),
+            "launch_to_call_return": us(f[3], f[4]),
+            "launch_return_to_first_kernel_start": us(f[3], first_start),
+        }
+        out["close_breakdown_us"] = {
+            "python_wait_call_to_library_wait_entry": us(st["wait_call_py"], w[0]),
+            "wait_entry_to_stream_sync": us(w[0], w[1]),
+            "stream_sync_begin_after_last_kernel_end": us(last_end, w[1]),
+            "last_kernel_end_to_sync_return": us(last_end, w[2]),
+            "sync_return_to_region_end": us(w[2], b1),
+        }
     print(json.dumps(out, indent=1))
 
 
