@@ -172,6 +172,13 @@ def toggle_counts():
     return {"rows": c[0], "pairs": c[1], "owner_gets": c[2]}
 
 
+def iov_path_counts():
+    """local io-vector launches with repeated-destination ordering, by path"""
+    c = (ctypes.c_ulonglong * 3)()
+    lib().gaamd_iov_path_counts(c)
+    return {"hashed": c[0], "hashed_then_radix": c[1], "radix": c[2]}
+
+
 def owner_counts():
     """requests this rank's progress thread applied, by kind"""
     c = (ctypes.c_ulonglong * 4)()

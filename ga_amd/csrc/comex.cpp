@@ -1795,6 +1795,9 @@ static int xfer_contig(Xfer kind, int op, void *scale, void *src, void *dst, int
 // scatter-acc duplicates) run one by one in order.
 static char *g_iov_scratch = nullptr;
 static size_t g_iov_scratch_bytes = 0;
+// gaamd_iov_path_counts: local io-vector launches with repeated-destination
+// ordering, by path: hashed, hashed + radix fallback (conflicts overflowed), radix
+static std::atomic<unsigned long long> g_iov_path[3];
 
 static char *g_iov_host = nullptr;
 static size_t g_iov_host_bytes = 0;
@@ -2146,9 +2149,38 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     }();
     if (kernel_upload) upload_pinned(dev, up, o_res, r.streams[si]);
     else GA_HIP(hipMemcpyAsync(dev, up, o_res, hipMemcpyHostToDevice, r.streams[si]));
-    const int rc = runs ? launch_iov_runs(cop, scale, d, align_or, dlo, (dhi - dlo) / (uint64_t)bytes + 1,
-                                          dev + o_work, work, r.streams[si], src_peer)
-                        : launch_iov(cop, scale, d, align_or, serial, r.streams[si], src_peer);
+    const uint64_t units = runs ? (dhi - dlo) / (uint64_t)bytes + 1 : 0;
+    int rc;
+    if (runs) {
+        // repeated destinations: the hashed path (sorts only the pairs that share a
+        // destination), or the radix path above 2^19 pairs / with COMEX_AMD_IOV_HASH=0
+        static const bool hash_on = [] {
+            const char *e = getenv("COMEX_AMD_IOV_HASH");
+            return !e || atoi(e) != 0;
+        }();
+        static IovHash *g_hash = nullptr;
+        rc = 1;
+        if (hash_on) {
+            if (!g_hash) g_hash = iov_hash_create();
+            rc = launch_iov_hashed(g_hash, cop, scale, d, align_or, dlo, units, r.streams[si], src_peer);
+            if (rc == 0) {
+                // more repeated destinations than the hashed launch orders in LDS: after
+                // it completed, the radix path applies the pairs it left (the rest masked)
+                GA_HIP(hipStreamSynchronize(r.streams[si]));
+                const bool over = iov_hash_overflowed(g_hash);
+                g_iov_path[over ? 1 : 0].fetch_add(1, std::memory_order_relaxed);
+                if (over)
+                    rc = launch_iov_runs(cop, scale, d, align_or, dlo, units, dev + o_work, work, r.streams[si],
+                                         src_peer, g_hash);
+            }
+        }
+        if (rc == 1) {
+            g_iov_path[2].fetch_add(1, std::memory_order_relaxed);
+            rc = launch_iov_runs(cop, scale, d, align_or, dlo, units, dev + o_work, work, r.streams[si], src_peer);
+        }
+    } else {
+        rc = launch_iov(cop, scale, d, align_or, serial, r.streams[si], src_peer);
+    }
     if (rc) fatal("io-vector launch failed (%d): misaligned elements?", rc);
     if (!dst_listed) {
         GA_HIP(hipStreamSynchronize(r.streams[si]));
@@ -3285,6 +3317,11 @@ int gaamd_stamps(int on, unsigned long long out[8]) {
         if (on) memset(g_stamp, 0, sizeof(g_stamp));
         g_stamp_on.store(on != 0, std::memory_order_relaxed);
     }
+    return 0;
+}
+
+int gaamd_iov_path_counts(unsigned long long counts[3]) {
+    for (int k = 0; k < 3; ++k) counts[k] = g_iov_path[k].load(std::memory_order_relaxed);
     return 0;
 }
 

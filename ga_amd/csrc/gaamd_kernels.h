@@ -138,7 +138,23 @@ int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool ser
 // < 2^32, d.bytes <= kIovRunsMaxBytes, and no source inside a destination.
 constexpr int kIovRunsMaxBytes = 256;
 size_t iov_runs_work_bytes(uint32_t n);
+struct IovHash;   // the hashed path's table (one per calling thread; kept across calls)
+// mask: the table of a hashed launch whose conflicts overflowed (iov_hash_overflowed):
+// the pairs it applied already are skipped
 int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
-                    void *work, size_t work_bytes, hipStream_t stream, bool src_peer = false);
+                    void *work, size_t work_bytes, hipStream_t stream, bool src_peer = false,
+                    const IovHash *mask = nullptr);
+// The same contract as launch_iov_runs without the sort for up to 2^19 pairs: a
+// hash table finds the destinations with more than one pair; pairs alone on
+// theirs are applied at once, the rest (up to 8192) sorted by (destination,
+// index) in one workgroup's LDS and applied in index order.  Returns 1 when n is
+// outside its range (use launch_iov_runs).  After the stream has completed the
+// launch, iov_hash_overflowed(h) true means more conflicting pairs than the LDS
+// holds: none of those was applied -- run launch_iov_runs(..., mask = h) next.
+// The caller serialises its launches on one IovHash (the table is reused).
+IovHash *iov_hash_create();
+int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo,
+                      uint64_t units, hipStream_t stream, bool src_peer = false);
+bool iov_hash_overflowed(const IovHash *h);
 
 }  // namespace gaamd

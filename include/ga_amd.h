@@ -90,6 +90,11 @@ int gaamd_route_counts(unsigned long long counts[4]);
  * [1] io-vector descriptors split pair by pair (COMEX_ENABLE_{ACC,PUT,GET}_IOV=0),
  * [2] gets through the owner (COMEX_ENABLE_GET_SELF/SMP=0). */
 int gaamd_toggle_counts(unsigned long long counts[3]);
+/* Local io-vector launches whose destinations may repeat (>= 4096 pairs), by path:
+ * [0] hashed (only pairs sharing a destination sorted, in LDS), [1] hashed, then
+ * the radix path for the pairs it could not order (more than 8192 such pairs),
+ * [2] the radix path (over 2^19 pairs, or COMEX_AMD_IOV_HASH=0). */
+int gaamd_iov_path_counts(unsigned long long counts[3]);
 /* Diagnostic host stamps (CLOCK_BOOTTIME ns) of the last strided call and the last
  * comex_wait_all: [0] call entry, [1] route decided (launch lock held), [2] stream
  * picked, [3] kernel launched, [4] call return, [5] wait entry, [6] streams about

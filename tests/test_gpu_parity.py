@@ -573,12 +573,21 @@ def test_accv_large_repeated_destinations(gpu_lib, oracle, op, nbytes, slots, sh
         do[rng.random(n) < 0.01] += shift
     g = _giov_np(so + np.uint64(sb.ptr), do + np.uint64(db.ptr), nbytes)
     keep, sp = ga_amd.scale_buffer(op, C.SCALE[op])
+    paths0 = ga_amd.iov_path_counts()
     assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
     ga_amd.comex_fence_all()
+    paths1 = ga_amd.iov_path_counts()
     want = dst.copy()
     _oracle_acc_pairs(oracle, op, C.SCALE[op], src, want, list(zip(so.tolist(), do.tolist())), nbytes)
     got = db.download(np.uint8, dst.size)
     assert same_bits_nan_aware(got, want, op)
+    if nbytes <= 256 and not shift:
+        # the hashed path orders the pairs that share a destination: up to 8192 of them
+        # in LDS (1e6 slots: ~800 such pairs), more (every pair repeats) through the
+        # radix path for what the hashed launch left
+        conflicting = n - int(np.sum(np.unique(do, return_counts=True)[1] == 1))
+        key = "hashed" if conflicting <= 8192 else "hashed_then_radix"
+        assert paths1[key] == paths0[key] + 1, (conflicting, paths0, paths1)
 
 
 @pytest.mark.parametrize("n", [50, 20000, 200000])

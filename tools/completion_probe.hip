@@ -13,6 +13,9 @@
 //   sync_us  -- region start to both synchronizations returning (the bench's end)
 //   gap_us   -- sync_us - flag_us: what a flag-polling wait would save
 // and the same region without the counter (plain_us), the counter's own cost.
+// argv: K rounds [h]: with a third argument 1, instead the bare-HIP region of the
+// headline H shape (2-D, ld 8192): what a program with no library around the
+// kernel reads on the bench's clock.
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/completion_probe.hip -o tools/completion_probe
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -55,6 +58,19 @@ __global__ __launch_bounds__(64) void k_axpy(const v2d *a, v2d *b, double s, uns
             }
         }
     }
+}
+
+// the headline H shape: 2048 rows of 32 KiB (f64), row pitch 64 KiB on both sides,
+// one 1 KiB chunk per one-wave block (32 blocks per row), as the library's k_rows2d
+__global__ __launch_bounds__(64) void k_axpy2d(const v2d *a, v2d *b, double s) {
+    const size_t row = blockIdx.x >> 5, chunk = blockIdx.x & 31;
+    const size_t i = row * 4096 + chunk * 64 + threadIdx.x;   // 4096 v2d = 64 KiB pitch
+    const v2d x = __builtin_nontemporal_load(a + i);
+    const v2d y = __builtin_nontemporal_load(b + i);
+    v2d r;
+    r.x = y.x + s * x.x;
+    r.y = y.y + s * x.y;
+    __builtin_nontemporal_store(r, b + i);
 }
 
 static double now_us() {
@@ -124,6 +140,41 @@ int main(int argc, char **argv) {
         CK(hipStreamSynchronize(st[1]));
         *sync_us = now_us() - t0;
     };
+    // the bare-HIP region of the headline shape: K launches of the 2-D kernel over 8
+    // buffer sets of 2 x 128 MiB (H: src and dst both ld 8192 f64), two streams,
+    // barrier-free: host clock from the first launch to both synchronizations
+    const int reg2d = argc > 3 ? atoi(argv[3]) : 0;
+    if (reg2d) {
+        std::vector<v2d *> A2(sets), B2(sets);
+        for (int k = 0; k < sets; ++k) {
+            CK(hipMalloc((void **)&A2[k], 128ull << 20));
+            CK(hipMalloc((void **)&B2[k], 128ull << 20));
+            CK(hipMemset(A2[k], 0, 128ull << 20));
+            CK(hipMemset(B2[k], 0, 128ull << 20));
+        }
+        int j = 0;
+        auto reg = [&]() {
+            CK(hipStreamSynchronize(st[0]));
+            CK(hipStreamSynchronize(st[1]));
+            const double t0 = now_us();
+            for (int k = 0; k < K; ++k, ++j)
+                k_axpy2d<<<65536, 64, 0, st[k & 1]>>>(A2[j % sets], B2[j % sets], 0.5);
+            CK(hipStreamSynchronize(st[0]));
+            CK(hipStreamSynchronize(st[1]));
+            return now_us() - t0;
+        };
+        const double warm_until = now_us() + 500e3;   // the bench's time-based warm-up
+        while (now_us() < warm_until) reg();
+        std::vector<double> v;
+        for (int r = 0; r < rounds; ++r) v.push_back(reg());
+        std::sort(v.begin(), v.end());
+        const double bytes = 3.0 * 64 * (1 << 20) * K;
+        printf("{\"probe\": \"bare_region_H\", \"launches\": %d, \"rounds\": %d, \"min_us\": %.2f, \"median_us\": %.2f, "
+               "\"max_us\": %.2f, \"frac_median\": %.4f, \"frac_best\": %.4f}\n",
+               K, rounds, v[0], v[v.size() / 2], v.back(), bytes / (v[v.size() / 2] * 1e-6) / 8e12,
+               bytes / (v[0] * 1e-6) / 8e12);
+        return 0;
+    }
     double f, s;
     for (int w = 0; w < 10; ++w) { region(true, &f, &s); region(false, &f, &s); }
     std::vector<double> fl, sy, pl;
