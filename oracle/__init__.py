@@ -12,6 +12,10 @@ package; the product library (ga_amd/libga_amd.so) never links or calls it.
   reference tree exists; the .so travels to the GPU box).
 * ``LegacyRef``: _ref/libref_legacy_acc.so, the legacy ARMCI accumulate loops
   (armci/src/xfer/caccumulate.c) compiled as they lie.
+* ``IterRef``: _ref/libref_iterator.so, ComEx-ARMCI's stride iterator
+  (comex/src-armci/iterator.c) compiled as it lies: armci_write_strided (strided
+  -> contiguous, the reference's pack in odometer order) and armci_read_strided
+  (its unpack).
 """
 import ctypes
 import os
@@ -22,6 +26,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libref_acc.so")
 LEGACY_SO = os.path.join(HERE, "_ref", "libref_legacy_acc.so")
+ITER_SO = os.path.join(HERE, "_ref", "libref_iterator.so")
 
 _ip = ctypes.POINTER(ctypes.c_int)
 _vp = ctypes.c_void_p
@@ -191,6 +196,36 @@ class LegacyRef:
         fn.restype = None
         r = ctypes.c_int(rows)
         fn(_ptr(s), _ptr(A), _ptr(B), ctypes.byref(r))
+
+
+class IterRef:
+    """The reference's stride iterator: armci_write_strided / armci_read_strided
+    (iterator.c:156-194).  Its descriptors are the non-overlapping ones the
+    iterator asserts (stride[0] >= count[0], stride[i] >= stride[i-1] * count[i])."""
+
+    def __init__(self, path=ITER_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        L = ctypes.CDLL(path)
+        for n in ("armci_write_strided", "armci_read_strided"):
+            f = getattr(L, n)
+            f.restype = None
+            f.argtypes = [_vp, ctypes.c_int, _ip, _ip, _vp]
+        self.L = L
+
+    def write_strided(self, src, src_off, src_stride, count, levels, packed_size):
+        """strided bytes of `src` (numpy uint8) -> a new contiguous buffer"""
+        out = np.zeros(max(1, packed_size), dtype=np.uint8)
+        self.L.armci_write_strided(_vp(src.ctypes.data + src_off), levels, _ints(src_stride), _ints(count), _ptr(out))
+        return out[:packed_size]
+
+    def read_strided(self, packed, dst, dst_off, dst_stride, count, levels):
+        """contiguous `packed` -> the strided bytes of `dst` (in place)"""
+        self.L.armci_read_strided(_vp(dst.ctypes.data + dst_off), levels, _ints(dst_stride), _ints(count), _ptr(packed))
+
+
+def iter_ref_available():
+    return os.path.exists(ITER_SO)
 
 
 def legacy_ref_available():
