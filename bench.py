@@ -530,7 +530,7 @@ def run_gpu(args, dist, finalize=True):
     return res
 
 
-def c5_extras(args, dist):
+def c5_extras(args, dist, wd=None):
     """N > 1: C5 in the same job -- M1, every rank NGA_Acc's its
     own block (owner-aligned, HBM-bound), and M2, every rank NGA_Acc's the whole
     array, (p-1)/p of it through the remote path (pack into exported staging HBM,
@@ -543,6 +543,8 @@ def c5_extras(args, dist):
                                            ("M2_src_in_segment", True, m2, True)):
         if args.verbose:
             print(f"rank {dist.rank}: C5 {mode} starts", file=sys.stderr, flush=True)
+        if wd is not None:
+            wd.phase = mode
         args.src_seg = src_seg
         r = run_ga(args, dist, exchange=exchange, steps=steps, warmup_ms=0.0, terminate=False)
         args.src_seg = saved
@@ -565,6 +567,8 @@ def c5_extras(args, dist):
         out[mode] = d
     # the exactness check runs at the configured GA size, not a reduced one
     n_chk = args.ga_dims if args.ga_dims else GA_DIMS[0]
+    if wd is not None:
+        wd.phase = "exchange_check"
     out["exchange_check"] = {route: c5_exchange_check(dist, src_seg, n=n_chk) for route, src_seg in
                              (("buffer_src", False), ("segment_src", True))}
     ga_amd_lib().GA_Terminate()
@@ -832,6 +836,8 @@ def main():
     ap.add_argument("--ga-dims", type=int, default=0, help="C5: square GA of this size instead of 32768^2")
     ap.add_argument("--c5-steps", type=int, default=4, help="N>1: timed C5 M1 steps (M2: half as many)")
     ap.add_argument("--no-extras", action="store_true", help="N>1: skip the C5 M1/M2 measurements")
+    ap.add_argument("--extras-timeout", type=float, default=300.0,
+                    help="N>1: seconds the C5 extras may take before the headline line is printed without them")
     ap.add_argument("--verbose", action="store_true", help="progress lines on stderr")
     args = ap.parse_args()
     if os.environ.get("BENCH_STACK_DUMP_S"):   # diagnostics: where a hung rank is stuck
@@ -856,8 +862,11 @@ def main():
     dist = Dist(args.gpus)
     extras_on = dist.size > 1 and not args.no_extras and args.workload != "C5"
     r = run_gpu(args, dist, finalize=not extras_on)
-    c5 = None
+    # the headline line is complete before the extras start: should the extras (the
+    # first cross-GPU exchange of a job) not finish, the watchdog still prints it
+    line = make_line(args, dist, r, ga_amd) if dist.rank == 0 else None
     if extras_on:
+        wd = ExtrasWatchdog(args.extras_timeout, dist.rank, line)
         # the C5 exchange needs every same-node peer mapped by IPC; a rank that could not
         # map one would abort there, so the extras are skipped (by every rank) instead
         unmapped = int(dist.max(float(ga_amd.lib().gaamd_peers_unmapped())))
@@ -865,9 +874,46 @@ def main():
             ga_amd.lib().comex_finalize()
             c5 = {"skipped": f"a rank could not map {unmapped} same-node peer(s) by IPC at comex_init"}
         else:
-            c5 = c5_extras(args, dist)
-    if dist.rank != 0:
-        return
+            c5 = c5_extras(args, dist, wd)
+        wd.cancel()
+        if line is not None:
+            line["c5"] = c5
+    if line is not None:
+        print(json.dumps(line), flush=True)
+
+
+class ExtrasWatchdog:
+    """N > 1: the C5 extras run after the headline is measured.  If they have not
+    finished after `seconds` (a hang in an exchange no one-GPU box could rehearse),
+    rank 0 prints the headline line with the extras marked as timed out, every rank
+    dumps its Python stacks to stderr and leaves with status 0 -- the headline was
+    measured and is reported; the extras' failure is stated in the line."""
+
+    def __init__(self, seconds, rank, line):
+        import threading
+        self.phase = "start"
+        self.rank, self.line = rank, line
+        self.t = threading.Timer(seconds, self.fire, args=(seconds,))
+        self.t.daemon = True
+        self.t.start()
+
+    def fire(self, seconds):
+        import faulthandler
+        print(f"rank {self.rank}: C5 extras still in phase {self.phase!r} after {seconds:.0f} s; stacks:",
+              file=sys.stderr, flush=True)
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+        if self.line is not None:
+            self.line["c5"] = {"timed_out": f"C5 extras did not finish within {seconds:.0f} s "
+                                            f"(phase {self.phase!r} on rank 0); the headline above was "
+                                            "measured before they started"}
+            print(json.dumps(self.line), flush=True)
+        os._exit(0)
+
+    def cancel(self):
+        self.t.cancel()
+
+
+def make_line(args, dist, r, ga_amd):
     n = dist.size
     alg = r["alg_bytes"]
     value = n * args.steps * alg / r["elapsed"] / 2 ** 30
@@ -925,8 +971,6 @@ def main():
         line["diag_regions"] = r["diag_regions"]
     if r.get("blocking"):
         line["blocking_api"] = r["blocking"]   # same K steps through the blocking call, after the value region
-    if c5:
-        line["c5"] = c5
     if r.get("xfer", "acc") != "acc":
         line["metric"] = f"GiB/s device-resident strided f64 {r['xfer']} (comex_{r['xfer']}s), not the headline metric"
         line["config"]["step"] = f"comex_{r['xfer']}s of the patch; algorithmic bytes = 2 x payload (read + write)"
@@ -953,7 +997,7 @@ def main():
         line["exchange_achieved_GBps_per_rank"] = round(achieved, 1)
     if "host" in r:
         line["host_inclusive_GiB_per_s"] = {k: round(v, 2) for k, v in r["host"].items()}
-    print(json.dumps(line), flush=True)
+    return line
 
 
 if __name__ == "__main__":

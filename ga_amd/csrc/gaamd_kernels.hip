@@ -32,7 +32,6 @@
 #pragma clang fp contract(off)
 
 #include "gaamd_kernels.h"
-#include <hipcub/device/device_radix_sort.hpp>
 #include <string.h>
 #include <algorithm>
 #include <type_traits>
@@ -1483,11 +1482,130 @@ int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool ser
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// ---------------------------------------------------------------------------
+// stable LSD radix sort of (key, value) u32 pairs for the io-vector run path,
+// 8-bit digits over bits [0, end_bit).  Per pass three launches:
+//   k_rs_hist    one workgroup per tile of 4096 keys: digit counts in LDS,
+//                stored digit-major (counts[digit * ntiles + tile])
+//   k_rs_scan    one workgroup per digit: exclusive prefix of its row of tile
+//                counts, the digit's total to totals[digit]
+//   k_rs_scatter one workgroup per tile: the 256 digit bases (exclusive scan of
+//                the totals) + the tile's offsets; the tile's keys in 16 rounds
+//                of 256 (input order), each key's rank among equal digits of
+//                its round from wave ballots (8 of them: the lanes whose digit
+//                matches) and per-wave counts in LDS -- equal keys keep their
+//                input order, which the run kernel's order relies on.
+// A hand-written sort rather than a library one: one instantiation, three
+// kernels, no per-architecture dispatch code in the shipped object.
+constexpr int kRsThreads = 256, kRsRounds = 16, kRsTile = kRsThreads * kRsRounds;
+
+__global__ __launch_bounds__(256) void k_rs_hist(const uint32_t *keys, uint32_t n, uint32_t shift, uint32_t ntiles,
+                                                 uint32_t *counts) {
+    __shared__ uint32_t h[256];
+    const uint32_t t = threadIdx.x, tile = blockIdx.x;
+    h[t] = 0;
+    __syncthreads();
+    const uint32_t base = tile * (uint32_t)kRsTile;
+#pragma unroll 4
+    for (int j = 0; j < kRsRounds; ++j) {
+        const uint32_t i = base + (uint32_t)j * kRsThreads + t;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    counts[(size_t)t * ntiles + tile] = h[t];
+}
+
+// exclusive scan of one digit's tile counts (in place); its total to totals[digit]
+__global__ __launch_bounds__(256) void k_rs_scan(uint32_t *counts, uint32_t ntiles, uint32_t *totals) {
+    __shared__ uint32_t part[256];
+    const uint32_t t = threadIdx.x;
+    uint32_t *row = counts + (size_t)blockIdx.x * ntiles;
+    const uint32_t per = (ntiles + 255u) / 256u, lo = min(ntiles, t * per), hi = min(ntiles, lo + per);
+    uint32_t sum = 0;
+    for (uint32_t k = lo; k < hi; ++k) sum += row[k];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {   // inclusive Hillis-Steele scan of the partial sums
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    for (uint32_t k = lo; k < hi; ++k) {
+        const uint32_t c = row[k];
+        row[k] = run;
+        run += c;
+    }
+    if (t == 255) totals[blockIdx.x] = part[255];
+}
+
+__global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t *kin, const uint32_t *vin, uint32_t *kout,
+                                                    uint32_t *vout, uint32_t n, uint32_t shift, uint32_t ntiles,
+                                                    const uint32_t *counts, const uint32_t *totals) {
+    __shared__ uint32_t base[256];
+    __shared__ uint32_t wcnt[4][256];
+    const uint32_t t = threadIdx.x, tile = blockIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t tot = totals[t];
+    base[t] = tot;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {
+        const uint32_t v = t >= off ? base[t - off] : 0u;
+        __syncthreads();
+        base[t] += v;
+        __syncthreads();
+    }
+    const uint32_t mine = base[t] - tot + counts[(size_t)t * ntiles + tile];   // exclusive + the tile's offset
+    __syncthreads();
+    base[t] = mine;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int j = 0; j < kRsRounds; ++j) {
+        wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
+        __syncthreads();
+        const uint32_t i = tile * (uint32_t)kRsTile + (uint32_t)j * kRsThreads + t;
+        const bool valid = i < n;
+        const uint32_t key = valid ? kin[i] : 0u;
+        const uint32_t dg = (key >> shift) & 255u;
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (dg >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(m & lt);
+        if (valid && rank == 0) wcnt[w][dg] = (uint32_t)__popcll(m);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = base[dg] + rank;
+            for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][dg];
+            kout[pos] = key;
+            vout[pos] = vin[i];
+        }
+        __syncthreads();
+        base[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+    }
+}
+
 static size_t iov_sort_temp_bytes(uint32_t n) {
-    size_t t = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                             (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0, 32);
-    return t;
+    const size_t ntiles = ((size_t)n + kRsTile - 1) / kRsTile;
+    return (256 * ntiles + 256) * 4;
+}
+
+// sorts (k[0], v[0]), (k[1], v[1]) the other half of the ping-pong; returns the index
+// of the pair of buffers that holds the result
+static int radix_sort_pairs(uint32_t *const k[2], uint32_t *const v[2], uint32_t n, int end_bit, void *temp,
+                            hipStream_t stream) {
+    const uint32_t ntiles = (n + kRsTile - 1) / kRsTile;
+    uint32_t *counts = (uint32_t *)temp, *totals = counts + (size_t)256 * ntiles;
+    int cur = 0;
+    for (int shift = 0; shift < end_bit; shift += 8, cur ^= 1) {
+        hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(256), 0, stream, k[cur], n, (uint32_t)shift, ntiles, counts);
+        hipLaunchKernelGGL(k_rs_scan, dim3(256), dim3(256), 0, stream, counts, ntiles, totals);
+        hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(256), 0, stream, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], n,
+                           (uint32_t)shift, ntiles, counts, totals);
+    }
+    return cur;
 }
 
 size_t iov_runs_work_bytes(uint32_t n) { return 4 * align256((size_t)n * 4) + align256(iov_sort_temp_bytes(n)); }
@@ -1517,7 +1635,6 @@ int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uin
     uint32_t *kin = (uint32_t *)w, *kout = (uint32_t *)(w + q), *vin = (uint32_t *)(w + 2 * q),
              *vout = (uint32_t *)(w + 3 * q);
     void *temp = w + 4 * q;
-    size_t temp_bytes = work_bytes - 4 * q;
     int end_bit = 1;
     while (end_bit < 32 && (1ull << end_bit) < units) ++end_bit;
     if (mask) {
@@ -1535,10 +1652,12 @@ int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uin
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return -100 - (int)e;
-    e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, kin, kout, vin, vout, (int)d.n, 0, end_bit, stream);
+    uint32_t *const kb[2] = {kin, kout}, *const vb[2] = {vin, vout};
+    const int r = radix_sort_pairs(kb, vb, d.n, end_bit, temp, stream);
+    e = hipGetLastError();
     if (e != hipSuccess) return -100 - (int)e;
-    d.run_key = kout;
-    d.run_perm = vout;
+    d.run_key = kb[r];
+    d.run_perm = vb[r];
     return iov_dispatch(op, scale, W, d, false, src_peer, stream);
 }
 

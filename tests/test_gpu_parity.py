@@ -590,6 +590,34 @@ def test_accv_large_repeated_destinations(gpu_lib, oracle, op, nbytes, slots, sh
         assert paths1[key] == paths0[key] + 1, (conflicting, paths0, paths1)
 
 
+@pytest.mark.parametrize("op,nbytes,slots,n", [(C.DBL, 8, 150000, 600037), (C.FLT, 4, 900, 530001),
+                                               (C.LNG, 8, 70000, 4 * 2 ** 18 + 5)])
+def test_accv_radix_path(gpu_lib, oracle, op, nbytes, slots, n):
+    """Above 2^19 pairs the hashed path is skipped: every destination is sorted on the
+    GPU by the library's own stable LSD radix sort (k_rs_*; 8-bit digits, 2 passes at
+    900 slots, 3 at 70 000 and 150 000; ragged last tile) and each destination's pairs
+    applied in input order -- bit-exact against the pairs applied one by one."""
+    rng = np.random.default_rng(n)
+    src = C.fill_bytes(op, n * nbytes, 11)
+    dst = C.fill_bytes(op, slots * nbytes, 12)
+    sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+    sb.upload(src)
+    db.upload(dst)
+    so = np.arange(n, dtype=np.uint64) * nbytes
+    do = rng.integers(0, slots, n).astype(np.uint64) * nbytes
+    g = _giov_np(so + np.uint64(sb.ptr), do + np.uint64(db.ptr), nbytes)
+    keep, sp = ga_amd.scale_buffer(op, C.SCALE[op])
+    paths0 = ga_amd.iov_path_counts()
+    assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
+    ga_amd.comex_fence_all()
+    paths1 = ga_amd.iov_path_counts()
+    assert paths1["radix"] == paths0["radix"] + 1, (paths0, paths1)
+    want = dst.copy()
+    _oracle_acc_pairs(oracle, op, C.SCALE[op], src, want, zip(so.tolist(), do.tolist()), nbytes)
+    got = db.download(np.uint8, dst.size)
+    assert same_bits_nan_aware(got, want, op)
+
+
 @pytest.mark.parametrize("n", [50, 20000, 200000])
 def test_accv_host_sources_packed(gpu_lib, oracle, n):
     """Pageable host sources (GA's MA buffer `v` of NGA_Scatter_acc) are gathered on the

@@ -388,3 +388,23 @@ def test_bench_two_ranks_exchange_exact():
     chk = line["c5"]["exchange_check"]
     assert chk["buffer_src"]["result"] == "exact" and chk["segment_src"]["result"] == "exact", chk
     assert chk["buffer_src"]["array"] == "8192x8192 f64", chk   # at --ga-dims, not a fixed 4096
+
+
+@pytest.mark.gpu
+def test_bench_extras_watchdog_keeps_headline():
+    """If the N > 1 extras (the cross-GPU exchange) do not finish in time, rank 0
+    still prints the headline line -- measured before the extras -- with the extras
+    marked as timed out, and the job ends with status 0."""
+    import json
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+                        "--warmup-ms", "0", "--no-cpu", "--ga-dims", "8192", "--c5-steps", "2",
+                        "--extras-timeout", "0.05"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert "timed_out" in line["c5"], line["c5"]

@@ -73,6 +73,39 @@ __global__ __launch_bounds__(64) void k_axpy2d(const v2d *a, v2d *b, double s) {
     __builtin_nontemporal_store(r, b + i);
 }
 
+// the same kernel with a chosen store policy (mode 2): does the end-of-launch release
+// (which writes back the dirty L2 lines before the completion signal) shorten when the
+// stores leave nothing dirty in L2?  0 = nt (the library's), 1 = sc0 sc1 (system scope:
+// written through), 2 = sc0 sc1 nt, 3 = plain, 4 = sc1 (agent scope: written through,
+// the line dropped from L2), 5 = sc1 nt
+template <int POL>
+__global__ __launch_bounds__(64) void k_axpy2d_pol(const v2d *a, v2d *b, double s) {
+    const size_t row = blockIdx.x >> 5, chunk = blockIdx.x & 31;
+    const size_t i = row * 4096 + chunk * 64 + threadIdx.x;
+    const v2d x = __builtin_nontemporal_load(a + i);
+    const v2d y = __builtin_nontemporal_load(b + i);
+    v2d r;
+    r.x = y.x + s * x.x;
+    r.y = y.y + s * x.y;
+    if (POL == 0) __builtin_nontemporal_store(r, b + i);
+    else if (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(b + i), "v"(r) : "memory");
+    else if (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(b + i), "v"(r) : "memory");
+    else if (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(b + i), "v"(r) : "memory");
+    else if (POL == 5) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(b + i), "v"(r) : "memory");
+    else b[i] = r;
+}
+
+static void launch_pol(int pol, int blocks, hipStream_t st, const v2d *a, v2d *b) {
+    switch (pol) {
+    case 1: k_axpy2d_pol<1><<<blocks, 64, 0, st>>>(a, b, 0.5); break;
+    case 2: k_axpy2d_pol<2><<<blocks, 64, 0, st>>>(a, b, 0.5); break;
+    case 3: k_axpy2d_pol<3><<<blocks, 64, 0, st>>>(a, b, 0.5); break;
+    case 4: k_axpy2d_pol<4><<<blocks, 64, 0, st>>>(a, b, 0.5); break;
+    case 5: k_axpy2d_pol<5><<<blocks, 64, 0, st>>>(a, b, 0.5); break;
+    default: k_axpy2d_pol<0><<<blocks, 64, 0, st>>>(a, b, 0.5); break;
+    }
+}
+
 static double now_us() {
     timespec t;
     clock_gettime(CLOCK_MONOTONIC, &t);
@@ -144,6 +177,51 @@ int main(int argc, char **argv) {
     // buffer sets of 2 x 128 MiB (H: src and dst both ld 8192 f64), two streams,
     // barrier-free: host clock from the first launch to both synchronizations
     const int reg2d = argc > 3 ? atoi(argv[3]) : 0;
+    if (reg2d == 2) {
+        // store-policy sweep, interleaved: configs (policy of every launch, policy of the
+        // region's last launch); regions of K and 2K launches, so that per config the
+        // slope is the per-launch time and the intercept the region's two edges
+        std::vector<v2d *> A2(sets), B2(sets);
+        for (int k = 0; k < sets; ++k) {
+            CK(hipMalloc((void **)&A2[k], 128ull << 20));
+            CK(hipMalloc((void **)&B2[k], 128ull << 20));
+            CK(hipMemset(A2[k], 0, 128ull << 20));
+            CK(hipMemset(B2[k], 0, 128ull << 20));
+        }
+        const int cfg[][2] = {{0, 0}, {1, 1}, {2, 2}, {3, 3}, {4, 4}, {5, 5}, {0, 4}};
+        const int ncfg = sizeof(cfg) / sizeof(cfg[0]);
+        int j = 0;
+        auto reg = [&](int c, int k_launches) {
+            CK(hipStreamSynchronize(st[0]));
+            CK(hipStreamSynchronize(st[1]));
+            const double t0 = now_us();
+            for (int k = 0; k < k_launches; ++k, ++j)
+                launch_pol(k == k_launches - 1 ? cfg[c][1] : cfg[c][0], 65536, st[k & 1], A2[j % sets], B2[j % sets]);
+            CK(hipStreamSynchronize(st[0]));
+            CK(hipStreamSynchronize(st[1]));
+            return now_us() - t0;
+        };
+        const double warm_until = now_us() + 500e3;
+        while (now_us() < warm_until)
+            for (int c = 0; c < ncfg; ++c) reg(c, K);
+        std::vector<std::vector<double>> v1(ncfg), v2(ncfg);
+        for (int r = 0; r < rounds; ++r)
+            for (int c = 0; c < ncfg; ++c) {
+                v1[c].push_back(reg(c, K));
+                v2[c].push_back(reg(c, 2 * K));
+            }
+        auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+        for (int c = 0; c < ncfg; ++c) {
+            const double m1 = med(v1[c]), m2 = med(v2[c]);
+            const double per = (m2 - m1) / K, edges = m1 - K * per;
+            const double bytes = 3.0 * 64 * (1 << 20) * K;
+            printf("{\"probe\": \"store_policy\", \"policy_all\": %d, \"policy_last\": %d, \"launches\": %d, "
+                   "\"rounds\": %d, \"median_us\": %.2f, \"median_2k_us\": %.2f, \"per_launch_us\": %.3f, "
+                   "\"edges_us\": %.2f, \"frac_median\": %.4f}\n",
+                   cfg[c][0], cfg[c][1], K, rounds, m1, m2, per, edges, bytes / (m1 * 1e-6) / 8e12);
+        }
+        return 0;
+    }
     if (reg2d) {
         std::vector<v2d *> A2(sets), B2(sets);
         for (int k = 0; k < sets; ++k) {
