@@ -23,6 +23,7 @@
 #include <stdlib.h>
 #include <time.h>
 #include <algorithm>
+#include <array>
 #include <vector>
 
 #define CK(x)                                                                                         \
@@ -188,8 +189,18 @@ int main(int argc, char **argv) {
             CK(hipMemset(A2[k], 0, 128ull << 20));
             CK(hipMemset(B2[k], 0, 128ull << 20));
         }
-        const int cfg[][2] = {{0, 0}, {1, 1}, {2, 2}, {3, 3}, {4, 4}, {5, 5}, {0, 4}};
-        const int ncfg = sizeof(cfg) / sizeof(cfg[0]);
+        // configs "all:last,all:last,..." (argv[4]); default every policy once plus the
+        // library's nt with a write-through last launch
+        std::vector<std::array<int, 2>> cfg;
+        const char *spec = argc > 4 ? argv[4] : "0:0,1:1,2:2,3:3,4:4,5:5,0:4";
+        for (const char *p = spec; *p;) {
+            int a = 0, b = 0, used = 0;
+            if (sscanf(p, "%d:%d%n", &a, &b, &used) != 2) break;
+            cfg.push_back({a, b});
+            p += used;
+            if (*p == ',') ++p;
+        }
+        const int ncfg = (int)cfg.size();
         int j = 0;
         auto reg = [&](int c, int k_launches) {
             CK(hipStreamSynchronize(st[0]));
@@ -206,9 +217,15 @@ int main(int argc, char **argv) {
             for (int c = 0; c < ncfg; ++c) reg(c, K);
         std::vector<std::vector<double>> v1(ncfg), v2(ncfg);
         for (int r = 0; r < rounds; ++r)
-            for (int c = 0; c < ncfg; ++c) {
-                v1[c].push_back(reg(c, K));
-                v2[c].push_back(reg(c, 2 * K));
+            for (int q = 0; q < ncfg; ++q) {   // the order rotates every round: no config always follows another
+                const int c = (q + r) % ncfg;
+                if (r & 1) {
+                    v2[c].push_back(reg(c, 2 * K));
+                    v1[c].push_back(reg(c, K));
+                } else {
+                    v1[c].push_back(reg(c, K));
+                    v2[c].push_back(reg(c, 2 * K));
+                }
             }
         auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
         for (int c = 0; c < ncfg; ++c) {
