@@ -69,7 +69,6 @@ struct Tuning {
     int align = 1;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses (misaligned rows)
     int flat_line_min = 40; // rows off 128 B lines on both sides with at least this many vectors: rows kernel (0 = off)
     int ordered_cols = 1;   // ordered rows sharing bytes only column-wise: column-sliced many-workgroup kernel
-    int store_wt = 1;       // streaming kernels store write-through (sc1) instead of nt: no dirty L2 lines at launch end
 };
 Tuning &tuning();
 

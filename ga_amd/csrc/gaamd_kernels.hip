@@ -119,30 +119,6 @@ __device__ __forceinline__ void vstore(char *p, typename Vec<W>::T v) {
     else *reinterpret_cast<V *>(p) = v;
 }
 
-// Write-through store for the streaming kernels (every byte written once, never
-// re-read by the kernel): `global_store_* sc1`, agent scope, which the XCD's L2
-// passes on to memory and does not keep (MI355X_MICROARCH.md, "stores of each
-// flavour").  An nt store leaves the line dirty in L2 and the end-of-launch
-// release has to write those lines back before the completion signal; after
-// write-through stores there is nothing to write back.  Bare-HIP headline region
-// (tools/completion_probe mode 2, 300 interleaved rounds): 20 launches 623 us vs
-// 635 us with nt stores, the same 30.1 us per launch (profiles/r03/s14).
-// The asm store is issued after every load of the lane and nothing after it reads
-// the address in the same kernel, so the compiler's wait counts need not see it.
-template <int W>
-__device__ __forceinline__ void vstore_wt(char *p, typename Vec<W>::T v) {
-    if constexpr (W == 16) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-    else if constexpr (W == 8) asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-    else if constexpr (W == 4) asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-    else if constexpr (W == 2) asm volatile("global_store_short %0, %1, off sc1" ::"v"(p), "v"((uint32_t)v) : "memory");
-    else asm volatile("global_store_byte %0, %1, off sc1" ::"v"(p), "v"((uint32_t)v) : "memory");
-}
-template <int W, bool WT>
-__device__ __forceinline__ void vstore_stream(char *p, typename Vec<W>::T v) {
-    if constexpr (WT) vstore_wt<W>(p, v);
-    else vstore<W, true>(p, v);
-}
-
 // ---------------------------------------------------------------------------
 // element operations on one W-byte vector
 // Each op also has serial_elem(dp, sp): one element through memory, for the
@@ -256,7 +232,7 @@ __device__ __forceinline__ void row_offsets(const Desc &d, uint32_t r, int64_t &
 // `full` (wave-uniform) says the whole chunk lies inside the row, so the
 // vectors need no predicate and their addresses fold into immediate offsets.
 // SYS: the source lies in a peer GPU's memory -> system-scope source loads
-template <class OP, int W, int U, int BS, bool SYS = false, bool WT = false>
+template <class OP, int W, int U, int BS, bool SYS = false>
 __device__ __forceinline__ void chunk_op(const char *sp, char *dp, int64_t v0, uint32_t nvec, bool full,
                                          const OP &op) {
     typedef typename Vec<W>::T V;
@@ -271,7 +247,7 @@ __device__ __forceinline__ void chunk_op(const char *sp, char *dp, int64_t v0, u
             if constexpr (OP::kReadsDst) b[k] = vload<W, true>(d0 + k * BS * W);
         }
 #pragma unroll
-        for (int k = 0; k < U; ++k) vstore_stream<W, WT>(d0 + k * BS * W, op.template apply<W>(b[k], a[k]));
+        for (int k = 0; k < U; ++k) vstore<W, true>(d0 + k * BS * W, op.template apply<W>(b[k], a[k]));
         return;
     }
     // row head/tail: one vector at a time (keeps the register budget of the full path)
@@ -282,7 +258,7 @@ __device__ __forceinline__ void chunk_op(const char *sp, char *dp, int64_t v0, u
         else x = vload<W, true>(s0 + k * BS * W);
         y = x;
         if constexpr (OP::kReadsDst) y = vload<W, true>(d0 + k * BS * W);
-        vstore_stream<W, WT>(d0 + k * BS * W, op.template apply<W>(y, x));
+        vstore<W, true>(d0 + k * BS * W, op.template apply<W>(y, x));
     }
 }
 
@@ -313,7 +289,7 @@ struct Desc2 {
     uint32_t align_mask;   // != 0: chunk boundaries at dst addresses = 0 mod (mask+1)
 };
 
-template <class OP, int W, int U, int BS, bool WT>
+template <class OP, int W, int U, int BS>
 __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
     for (uint32_t w = blockIdx.x; w < d.items; w += gridDim.x) {
         const uint32_t rl = d.chunk_div.div(w);
@@ -325,7 +301,7 @@ __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
         const int64_t shift = (int64_t)(((uintptr_t)dp & d.align_mask) / W);
         const int64_t c0 = (int64_t)chunk * (BS * U) - shift;
         const bool full = c0 >= 0 && c0 + BS * U <= (int64_t)d.nvec;
-        chunk_op<OP, W, U, BS, false, WT>(sp, dp, c0 + threadIdx.x, d.nvec, full, op);
+        chunk_op<OP, W, U, BS>(sp, dp, c0 + threadIdx.x, d.nvec, full, op);
     }
 }
 
@@ -344,7 +320,7 @@ struct Desc2D {
     uint32_t row0;
 };
 
-template <class OP, int W, int BS, bool WT>
+template <class OP, int W, int BS>
 __global__ __launch_bounds__(BS) void k_rows2d(const Desc2D d, const OP op) {
     const uint32_t w = blockIdx.x;
     const uint32_t rl = d.chunk_div.div(w);
@@ -355,7 +331,7 @@ __global__ __launch_bounds__(BS) void k_rows2d(const Desc2D d, const OP op) {
     char *dp = d.dst + r * d.d_str + v * W;
     typename Vec<W>::T a = vload<W, true>(sp), b = a;
     if constexpr (OP::kReadsDst) b = vload<W, true>(dp);
-    vstore_stream<W, WT>(dp, op.template apply<W>(b, a));
+    vstore<W, true>(dp, op.template apply<W>(b, a));
 }
 
 // DIRECT N-D kernel (2 or 3 stride levels, every row whole chunks): as
@@ -371,7 +347,7 @@ struct DescND {
     uint32_t row0;
 };
 
-template <class OP, int W, int BS, int LV, bool WT>
+template <class OP, int W, int BS, int LV>
 __global__ __launch_bounds__(BS) void k_rowsnd(const DescND<LV> d, const OP op) {
     const uint32_t w = blockIdx.x;
     const uint32_t rl = d.chunk_div.div(w);
@@ -391,12 +367,12 @@ __global__ __launch_bounds__(BS) void k_rowsnd(const DescND<LV> d, const OP op) 
     char *dp = d.dst + dof + v * W;
     typename Vec<W>::T a = vload<W, true>(sp), b = a;
     if constexpr (OP::kReadsDst) b = vload<W, true>(dp);
-    vstore_stream<W, WT>(dp, op.template apply<W>(b, a));
+    vstore<W, true>(dp, op.template apply<W>(b, a));
 }
 
 // FLAT kernel: vectors of all rows flattened, each lane decodes its own row;
 // non-temporal accesses (+12-24 % on 64 B-1 KiB rows, profiles/r01/flat_nt_ab.jsonl).
-template <class OP, int W, int U, int BS, int LV, bool WT>
+template <class OP, int W, int U, int BS, int LV>
 __global__ __launch_bounds__(BS) void k_flat(const Desc d, const OP op) {
     constexpr bool NT = true;
     typedef typename Vec<W>::T V;
@@ -420,7 +396,7 @@ __global__ __launch_bounds__(BS) void k_flat(const Desc d, const OP op) {
         }
 #pragma unroll
         for (int k = 0; k < U; ++k)
-            if (dps[k]) vstore_stream<W, WT>(dps[k], op.template apply<W>(b[k], a[k]));
+            if (dps[k]) vstore<W, NT>(dps[k], op.template apply<W>(b[k], a[k]));
     }
 }
 
@@ -604,17 +580,11 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, hipStre
             f.d_str = e.d_str;
             f.chunk_div = d.chunk_div;
             f.row0 = d.row0;
-            if (tuning().store_wt)
-                hipLaunchKernelGGL((k_rows2d<OP, W, BS, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
-            else
-                hipLaunchKernelGGL((k_rows2d<OP, W, BS, false>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
+            hipLaunchKernelGGL((k_rows2d<OP, W, BS>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
             return hipGetLastError();
         }
     }
-    if (tuning().store_wt)
-        hipLaunchKernelGGL((k_rows2<OP, W, U, BS, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
-    else
-        hipLaunchKernelGGL((k_rows2<OP, W, U, BS, false>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
+    hipLaunchKernelGGL((k_rows2<OP, W, U, BS>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
     return hipGetLastError();
 }
 
@@ -633,10 +603,7 @@ static hipError_t go_rows_nd(const Desc &d, const OP &op, uint64_t blocks, hipSt
             }
             f.chunk_div = d.chunk_div;
             f.row0 = d.row0;
-            if (tuning().store_wt)
-                hipLaunchKernelGGL((k_rowsnd<OP, W, BS, LV, true>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
-            else
-                hipLaunchKernelGGL((k_rowsnd<OP, W, BS, LV, false>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
+            hipLaunchKernelGGL((k_rowsnd<OP, W, BS, LV>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
             return hipGetLastError();
         }
     }
@@ -677,21 +644,12 @@ static hipError_t dispatch_w(const Plan &p, const Desc &d, const OP &op, uint64_
         if (p.kind == KK_FLAT) {
             constexpr int UF = (W == 16) ? 1 : 4;
             constexpr int FB = (W == 16) ? 64 : 256;
-            if (tuning().store_wt) {
-                if (d.levels == 1)
-                    hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 1, true>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
-                else if (d.levels == 2)
-                    hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 2, true>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
-                else
-                    hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 0, true>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
-            } else {
-                if (d.levels == 1)
-                    hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 1, false>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
-                else if (d.levels == 2)
-                    hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 2, false>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
-                else
-                    hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 0, false>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
-            }
+            if (d.levels == 1)
+                hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 1>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
+            else if (d.levels == 2)
+                hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 2>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
+            else
+                hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 0>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
             return hipGetLastError();
         }
         if (d.levels == 2) return go_rows_nd<OP, W, 2>(d, op, blocks, p.BS, st);

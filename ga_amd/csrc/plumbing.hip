@@ -138,7 +138,6 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "align")) return &t.align;
     if (!strcmp(key, "flat_line_min")) return &t.flat_line_min;
     if (!strcmp(key, "ordered_cols")) return &t.ordered_cols;
-    if (!strcmp(key, "store_wt")) return &t.store_wt;
     return nullptr;
 }
 

@@ -69,8 +69,7 @@ def test_golden_cases_armci_and_nb(gpu_lib, manifest, golden):
 
 
 @pytest.mark.parametrize("knob", [("kind", 1), ("kind", 2), ("kind", 3), ("kind", 4), ("block", 128), ("block", 64),
-                                  ("align", 0), ("align", 1), ("flat_line_min", 0), ("ordered_cols", 0),
-                                  ("store_wt", 0)])
+                                  ("align", 0), ("align", 1), ("flat_line_min", 0), ("ordered_cols", 0)])
 def test_kernel_variants_identical(gpu_lib, manifest, golden, knob):
     """Every shipped kernel family / tuning gives the same bits as the reference
     (ordered_cols 0: the coinciding-row golden cases on the one-workgroup kernel)."""
@@ -287,7 +286,7 @@ def test_empty_patches_are_noops(gpu_lib):
 
 
 @pytest.mark.parametrize("knobs", [{}, {"align": 0}, {"align": 1, "block": 128}, {"block": 64},
-                                   {"streams": 1}, {"kind": 4}, {"store_wt": 0}, {"store_wt": 0, "kind": 4}])
+                                   {"streams": 1}, {"kind": 4}])
 def test_wide_rows_odd_strides_all_knobs(gpu_lib, oracle, knobs):
     """Rows of 8-40 KiB (several chunks per row) at odd leading dimensions and
     offsets, so chunk splitting, the aligned-chunk grid and row tails are all
