@@ -1279,18 +1279,41 @@ static bool own_release_if_wanted() {
 
 static std::atomic<unsigned long long> g_one_pass{0};   // gaamd_route_counts: one-pass accumulates issued
 
-// The requester's side of the lock: per target, whether we hold its memory lock
-// and the events of our one-pass kernels still writing its segment.  A
-// non-blocking one-pass returns after the launch; the lock is released once every
-// such kernel has completed -- by our progress thread (one_pass_reap each pass),
-// or by a blocking call / wait / fence that waited for them.  Further one-pass
-// accumulates into the same target while we hold its lock go straight on (stream
-// order and sched_pick's range dependencies order them among themselves), unless
-// someone else waits for the lock (mem_want): then ours finish and it goes first.
-struct OnePassHold { bool held = false; std::vector<hipEvent_t> evs; };
+// The requester's side of the lock: per target, whether we hold its memory lock,
+// the library streams our one-pass kernels into its segment were launched on since
+// the last completion mark (`pending`), and the marks (events) recorded after them.
+// A non-blocking one-pass returns after the launch and records nothing: an event
+// per launch puts a marker packet between every two kernels of the stream (the
+// cost the sparse completion marks of sched.cpp avoid).  The lock stays with us
+// while nobody else wants it; when someone does (mem_want: the owner writing its
+// own segment, or another requester), our progress thread marks the pending
+// streams, and releases the lock once those marks completed.  A blocking call, a
+// wait or a fence marks and waits at once.  Further one-pass accumulates into the
+// same target while we hold its lock go straight on (stream order and sched_pick's
+// range dependencies order them among themselves), unless someone else waits for
+// the lock: then ours finish and it goes first.
+struct OnePassHold { bool held = false; uint32_t pending = 0; std::vector<hipEvent_t> evs; };
 static std::mutex g_op_mu;   // g_op_hold, g_op_pool; never held while waiting for a memory lock
 static std::vector<OnePassHold> g_op_hold;
 static std::vector<hipEvent_t> g_op_pool;
+
+// record a completion mark on every stream with unmarked one-pass launches into
+// this target (caller holds g_op_mu; takes launch_mu: the lock order is g_op_mu,
+// then launch_mu, everywhere)
+static void one_pass_mark(OnePassHold &h) {
+    if (!h.pending) return;
+    Runtime &r = rt();
+    std::lock_guard<std::mutex> g(r.launch_mu);
+    for (int si = 0; si < 32 && si < (int)r.streams.size(); ++si) {
+        if (!(h.pending >> si & 1u)) continue;
+        hipEvent_t ev;
+        if (g_op_pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        else { ev = g_op_pool.back(); g_op_pool.pop_back(); }
+        GA_HIP(hipEventRecord(ev, r.streams[si]));
+        h.evs.push_back(ev);
+    }
+    h.pending = 0;
+}
 
 static void one_pass_release(int t, OnePassHold &h) {   // caller holds g_op_mu; every event completed
     Runtime &r = rt();
@@ -1300,14 +1323,20 @@ static void one_pass_release(int t, OnePassHold &h) {   // caller holds g_op_mu;
     r.shm->mem_lock[r.li(t)].store(0, std::memory_order_release);
 }
 
-// release the locks whose kernels have all completed (wait: wait for them first);
+// release the locks whose kernels have all completed (wait: mark and wait for them
+// first; otherwise a lock nobody waits for stays with us until it is wanted);
 // true if one was released
 static bool one_pass_reap(bool wait) {
     bool any = false;
+    Runtime &r = rt();
     std::lock_guard<std::mutex> g(g_op_mu);
     for (size_t t = 0; t < g_op_hold.size(); ++t) {
         OnePassHold &h = g_op_hold[t];
         if (!h.held) continue;
+        if (h.pending) {
+            if (!wait && !r.shm->mem_want[r.li((int)t)].load(std::memory_order_acquire)) continue;
+            one_pass_mark(h);
+        }
         bool done = true;
         for (hipEvent_t e : h.evs) {
             const hipError_t x = wait ? hipEventSynchronize(e) : hipEventQuery(e);
@@ -1347,6 +1376,7 @@ static bool one_pass_acc(int t, int op, void *scale, void *src, const int *ss, v
     if (g_op_hold.size() != (size_t)r.size) g_op_hold.resize(r.size);
     if (g_op_hold[t].held && want.load(std::memory_order_acquire) > 0) {
         // someone waits for t's memory: let ours finish and hand it over first
+        one_pass_mark(g_op_hold[t]);
         for (hipEvent_t e : g_op_hold[t].evs) GA_HIP(hipEventSynchronize(e));
         one_pass_release(t, g_op_hold[t]);
     }
@@ -1362,25 +1392,24 @@ static bool one_pass_acc(int t, int op, void *scale, void *src, const int *ss, v
         og.lock();
         g_op_hold[t].held = true;
     }
-    hipEvent_t ev;
-    if (g_op_pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    else { ev = g_op_pool.back(); g_op_pool.pop_back(); }
     int si;
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
         si = sched_pick(span_of(sdev, slo, shi), span_of(dview, dlo, dhi), payload_bytes(rbd, count, levels));
         const int rc = launch_strided(op, scale, sdev, ss, dview, ds, count, levels, r.streams[si], last_launch_info());
         if (rc) fatal("one-pass accumulate launch failed (%d)", rc);
-        GA_HIP(hipEventRecord(ev, r.streams[si]));
     }
-    g_op_hold[t].evs.push_back(ev);
-    og.unlock();
+    g_op_hold[t].pending |= 1u << si;
     g_one_pass.fetch_add(1, std::memory_order_relaxed);
     if (hdl) {
+        og.unlock();
         nb_complete_now(hdl, si, true);
     } else {
-        GA_HIP(hipEventSynchronize(ev));   // blocking: the source is reusable on return
-        one_pass_reap(false);
+        // blocking: the source is reusable on return -- mark, wait, and hand the lock back
+        one_pass_mark(g_op_hold[t]);
+        for (hipEvent_t e : g_op_hold[t].evs) GA_HIP(hipEventSynchronize(e));
+        one_pass_release(t, g_op_hold[t]);
+        og.unlock();
     }
     return true;
 }
