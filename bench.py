@@ -557,8 +557,9 @@ def c5_extras(args, dist, wd=None):
             xgmi = (p - 1) * r["block_bytes"]
             d["xgmi_GBps_per_gpu"] = round(xgmi / t / 1e9, 1)
             d["note"] = ("whole-array accumulate by every rank; value counts 3 x payload of HBM-side traffic per rank; "
-                         + ("the local buffer lies in the rank's comex segment: owners accumulate straight from it "
-                            "(direct-source route, no pack)" if src_seg else
+                         + ("the local buffer lies in the rank's comex segment: owners on other GPUs accumulate "
+                            "straight from it (direct-source route, no pack); ranks sharing a GPU the one-pass route"
+                            if src_seg else
                             "the local buffer is a plain device buffer: owners on other GPUs pack -> staging -> owner "
                             "unpack-acc; ranks sharing a GPU the one-pass route"))
             d["routes"] = r.get("routes")
@@ -587,7 +588,7 @@ def c5_exchange_check(dist, src_seg, n=4096):
     exactly 2**p - 1 afterwards -- a lost, doubled or stale contribution shows as a
     wrong element and its value says whose.  The source is a plain device buffer
     (packed route to other GPUs, one-pass to ranks on the same GPU) or lies in the
-    rank's segment (direct-source route)."""
+    rank's segment (direct-source route to other GPUs, one-pass on the same GPU)."""
     import ga_amd
     L = ga_amd.lib()
     ia = ga_amd.int_array

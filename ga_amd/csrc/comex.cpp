@@ -1648,6 +1648,13 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         return COMEX_SUCCESS;
     }
 
+    // an owner on this GPU: the one-pass route (our kernel writes its segment under its
+    // memory lock), whether or not the source lies in one of our segments -- no host
+    // drain of our streams and no hand-off to the owner's progress thread, which the
+    // direct-source route below needs
+    if (kind == X_ACC && world != r.rank &&
+        one_pass_acc(world, op, scale, src, ss, dst, ds, count, levels, row_bytes_of(op, count[0]), hdl))
+        return COMEX_SUCCESS;
     // the direct-source route is a direct (SMP) route: COMEX_ENABLE_ACC_SMP=0 sends
     // same-node accumulates down the packed route, as the reference (comex.c:6911-6915)
     if (kind == X_ACC && world != r.rank && r.direct_src && r.acc_smp_direct && r.same_node(world)) {
@@ -1686,9 +1693,6 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
             return COMEX_SUCCESS;
         }
     }
-    if (kind == X_ACC && world != r.rank &&
-        one_pass_acc(world, op, scale, src, ss, dst, ds, count, levels, row_bytes_of(op, count[0]), hdl))
-        return COMEX_SUCCESS;
     // a get through the owner (COMEX_ENABLE_GET_SELF/SMP=0) from a rank on this GPU or
     // ourselves; from another GPU the get stays a direct read (system-scope loads):
     // the owner could only answer by writing our HBM

@@ -360,12 +360,15 @@ def test_direct_ops_on_self_after_packed_self_traffic(n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [2, 3])
-def test_direct_source_remote_accumulate(n):
+@pytest.mark.parametrize("n,one_pass", [(2, "0"), (3, "0"), (3, "1")])
+def test_direct_source_remote_accumulate(n, one_pass):
     """Source in the caller's segment: the owner accumulates straight from it
     (no pack, no staging), bit-exact against the oracle; smaller patches keep
-    the packed route."""
-    launch("directsrc", n=n, timeout=120)
+    the packed route.  An owner on the caller's GPU takes the
+    one-pass route instead unless COMEX_AMD_ONE_PASS=0 (the ranks of this test
+    share one GPU; with the route off they exercise the direct-source route, as
+    owners on other GPUs do)."""
+    launch("directsrc", n=n, timeout=120, extra_env={"COMEX_AMD_ONE_PASS": one_pass})
 
 
 @pytest.mark.gpu
