@@ -866,6 +866,14 @@ def armci_misc_test(L, rank, size):
         gb = (c_int * 2)(rank, rank)
         L.armci_msg_group_bcast_scope(333, gb, 8, evens[-1], byref(g))
         assert list(gb) == [evens[-1]] * 2
+        # GA's gai_get_shmem (base.c:3494-3512) on a group: ptr_arr[group rank] set, the
+        # rest zero, then armci_exchange_address_grp fills every member's entry in
+        # group-rank order (the reference's ComEx ARMCI aborts there, message.c:694-713,
+        # whose disabled MPI_Allgather this implements)
+        ga_addr = (vp * len(evens))()
+        ga_addr[gr.value] = 0x5000 + 0x100 * rank
+        L.armci_exchange_address_grp(ga_addr, len(evens), byref(g))
+        assert [a or 0 for a in ga_addr] == [0x5000 + 0x100 * q for q in evens], list(ga_addr)
         gseg = (vp * len(evens))()
         assert L.ARMCI_Malloc_group(gseg, 4096, byref(g)) == 0
         peer = evens[(gr.value + 1) % len(evens)]
