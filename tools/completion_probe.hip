@@ -96,6 +96,12 @@ __global__ __launch_bounds__(64) void k_axpy2d_pol(const v2d *a, v2d *b, double 
     else b[i] = r;
 }
 
+// mode 3: a one-lane tail kernel that stores a tag into pinned host memory with a
+// system-scope release; stream order starts it only after the kernel before it ended
+__global__ void k_tail_flag(unsigned int *flag, unsigned int tag) {
+    __hip_atomic_store(flag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 static void launch_pol(int pol, int blocks, hipStream_t st, const v2d *a, v2d *b) {
     switch (pol) {
     case 1: k_axpy2d_pol<1><<<blocks, 64, 0, st>>>(a, b, 0.5); break;
@@ -178,6 +184,53 @@ int main(int argc, char **argv) {
     // buffer sets of 2 x 128 MiB (H: src and dst both ld 8192 f64), two streams,
     // barrier-free: host clock from the first launch to both synchronizations
     const int reg2d = argc > 3 ? atoi(argv[3]) : 0;
+    if (reg2d == 3) {
+        // blocking-call completion: K launches of the H-shape kernel on one stream, then
+        // (a) hipStreamSynchronize, or (b) a tail flag kernel and a host spin on the flag
+        // (then hipStreamSynchronize, outside the time).  K = 1 is a blocking comex_accs;
+        // K = 20 the value region's close.  Interleaved, `rounds` each.
+        std::vector<v2d *> A2(sets), B2(sets);
+        for (int k = 0; k < sets; ++k) {
+            CK(hipMalloc((void **)&A2[k], 128ull << 20));
+            CK(hipMalloc((void **)&B2[k], 128ull << 20));
+            CK(hipMemset(A2[k], 0, 128ull << 20));
+            CK(hipMemset(B2[k], 0, 128ull << 20));
+        }
+        int j = 0;
+        auto reg = [&](int k_launches, bool tail, double *flag_us) {
+            CK(hipStreamSynchronize(st[0]));
+            const double t0 = now_us();
+            for (int k = 0; k < k_launches; ++k, ++j) launch_pol(0, 65536, st[0], A2[j % sets], B2[j % sets]);
+            if (tail) {
+                const unsigned int want = ++tag;
+                k_tail_flag<<<1, 1, 0, st[0]>>>(flag_d, want);
+                const double give_up = now_us() + 1e6;
+                while (__atomic_load_n((volatile unsigned int *)flag_h, __ATOMIC_ACQUIRE) != want)
+                    if (now_us() > give_up) { fprintf(stderr, "tail flag never arrived\n"); exit(2); }
+                *flag_us = now_us() - t0;
+                CK(hipStreamSynchronize(st[0]));
+                return now_us() - t0;
+            }
+            CK(hipStreamSynchronize(st[0]));
+            return now_us() - t0;
+        };
+        double f = 0;
+        const double warm_until = now_us() + 500e3;
+        while (now_us() < warm_until) { reg(1, false, &f); reg(1, true, &f); }
+        for (int kl : {1, 20}) {
+            std::vector<double> vs, vf, vfs;
+            for (int r = 0; r < rounds; ++r) {
+                vs.push_back(reg(kl, false, &f));
+                vfs.push_back(reg(kl, true, &f));
+                vf.push_back(f);
+            }
+            auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+            printf("{\"probe\": \"tail_flag\", \"launches\": %d, \"rounds\": %d, \"sync_us\": %.2f, "
+                   "\"tail_flag_seen_us\": %.2f, \"tail_then_sync_us\": %.2f}\n",
+                   kl, rounds, med(vs), med(vf), med(vfs));
+        }
+        return 0;
+    }
     if (reg2d == 2) {
         // store-policy sweep, interleaved: configs (policy of every launch, policy of the
         // region's last launch); regions of K and 2K launches, so that per config the
