@@ -1218,7 +1218,15 @@ static int64_t row_bytes_of(int op, int count0) {
 // A requester never writes its own segments while it holds another rank's lock
 // (the one-pass launch writes only the remote view), so no cycle of locks forms.
 // Across GPUs there is no one-pass route: the owner applies.
-constexpr uint64_t kOnePassMin = 1ull << 20;   // smaller patches keep the asynchronous packed route
+// smaller patches keep the asynchronous packed route (COMEX_AMD_ONE_PASS_MIN bytes; tests
+// lower it so that random programs of small patches exercise the lock hand-offs)
+static uint64_t one_pass_min() {
+    static const uint64_t v = [] {
+        const char *e = getenv("COMEX_AMD_ONE_PASS_MIN");
+        return e ? (uint64_t)strtoull(e, nullptr, 10) : (1ull << 20);
+    }();
+    return v;
+}
 
 static bool in_own_segment(const Span &d) {
     Runtime &r = rt();
@@ -1239,6 +1247,8 @@ static bool in_own_segment(const Span &d) {
 // across the wait, eight ranks accumulating into each other could close one:
 // rank A's progress thread holding A's launch_mu waiting for A's lock held by C,
 // C waiting for its launch_mu held by its progress thread waiting for C's lock...).
+static bool one_pass_reap_try();
+
 void own_write_guard(const Span &dst) {
     Runtime &r = rt();
     if (!r.one_pass || r.own_holds || dst.lo >= dst.hi || !in_own_segment(dst)) return;
@@ -1254,6 +1264,10 @@ void own_write_guard(const Span &dst) {
             waiting = true;
         }
         r.launch_mu.unlock();
+        // while we wait for our own memory, hand back the locks of others we hold and
+        // someone wants: the holder of ours may be waiting, in this same loop, for one
+        // of them (locks are released on demand, so a waiter must never stop reaping)
+        one_pass_reap_try();
         if (spins > 64) sched_yield();
         r.launch_mu.lock();
         if (r.own_holds) {   // another thread of this process took it meanwhile
@@ -1325,11 +1339,10 @@ static void one_pass_release(int t, OnePassHold &h) {   // caller holds g_op_mu;
 
 // release the locks whose kernels have all completed (wait: mark and wait for them
 // first; otherwise a lock nobody waits for stays with us until it is wanted);
-// true if one was released
-static bool one_pass_reap(bool wait) {
+// true if one was released.  Caller holds g_op_mu.
+static bool one_pass_reap_locked(bool wait) {
     bool any = false;
     Runtime &r = rt();
-    std::lock_guard<std::mutex> g(g_op_mu);
     for (size_t t = 0; t < g_op_hold.size(); ++t) {
         OnePassHold &h = g_op_hold[t];
         if (!h.held) continue;
@@ -1351,13 +1364,27 @@ static bool one_pass_reap(bool wait) {
     return any;
 }
 
+static bool one_pass_reap(bool wait) {
+    std::lock_guard<std::mutex> g(g_op_mu);
+    return one_pass_reap_locked(wait);
+}
+
+// from a memory-lock wait loop: reap what others want unless another thread of this
+// process is in the bookkeeping (it reaps then, or it is the one-pass launch that
+// holds g_op_mu only across a launch and an event wait)
+static bool one_pass_reap_try() {
+    std::unique_lock<std::mutex> g(g_op_mu, std::try_to_lock);
+    if (!g.owns_lock()) return false;
+    return one_pass_reap_locked(false);
+}
+
 // true: launched (blocking: complete on return; else `hdl` tracks it);
 // false: not eligible (the caller takes another route)
 static bool one_pass_acc(int t, int op, void *scale, void *src, const int *ss, void *dst, const int *ds,
                          const int *count, int levels, int64_t rbd, comex_request_t *hdl) {
     Runtime &r = rt();
     if (!r.one_pass || t == r.rank || !r.same_node(t) || !r.acc_smp_direct || r.peer_src(t)) return false;
-    if (rbd <= 0 || payload_bytes(rbd, count, levels) < kOnePassMin) return false;
+    if (rbd <= 0 || payload_bytes(rbd, count, levels) < one_pass_min()) return false;
     int64_t slo = 0, shi = 0, dlo = 0, dhi = 0;
     side_span_host(ss, count, levels, rbd, &slo, &shi);
     side_span_host(ds, count, levels, rbd, &dlo, &dhi);
@@ -1386,6 +1413,7 @@ static bool one_pass_acc(int t, int op, void *scale, void *src, const int *ss, v
         for (unsigned spins = 0;; ++spins) {
             uint32_t e = 0;
             if (lk.compare_exchange_weak(e, me, std::memory_order_acq_rel)) break;
+            if ((spins & 63) == 63) one_pass_reap_try();   // never stop handing back what others want
             if (spins > 64) sched_yield();
         }
         want.fetch_sub(1, std::memory_order_acq_rel);

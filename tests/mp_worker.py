@@ -1415,6 +1415,9 @@ def stress_test(L, rank, size):
     assert bad.size == 0, f"rank {rank}: {bad.size} accumulate-zone elements differ, first {bad[:5]}"
     assert np.array_equal(out[ST_ACC:].reshape(size, ST_ZONE), zones), f"rank {rank}: put zones differ"
     assert ga_amd.kernel_counts()["serial"] == serial0, f"rank {rank}: a serial kernel ran"
+    if os.environ.get("COMEX_AMD_ONE_PASS_MIN") and size > 1 and one_pass_expected():
+        # the test's point: small device-source accumulates into ranks of this GPU one-pass
+        assert ga_amd.route_counts()["one_pass"] > 0, ga_amd.route_counts()
     ga_amd.comex_barrier()
     for b in keep:
         b.free()

@@ -206,6 +206,18 @@ def test_stress_random_programs(mode, n, nodes, staging):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,seed", [(3, "0"), (4, "5"), (4, "11"), (3, "17")])
+def test_stress_random_programs_one_pass_everywhere(n, seed):
+    """The same random programs with the one-pass route taken by every device-source
+    accumulate into a rank of this GPU, however small (COMEX_AMD_ONE_PASS_MIN=1):
+    hundreds of memory-lock hand-offs per rank between requesters and owners that
+    accumulate into their own segments, on-demand completion marks, non-blocking
+    waits and fences interleaved with puts and gets -- exact."""
+    launch("stress", n=n, timeout=150, extra_env={"COMEX_AMD_ONE_PASS_MIN": "1", "STRESS_SEED": seed,
+                                                  "STRESS_OPS": "800"})
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [1, 3])
 def test_comex_test_acc_restated(n):
     """comex/testing/test.c test_acc + test_cplx_acc (1028-1235) for ndim 1..7:
