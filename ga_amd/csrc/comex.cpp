@@ -21,6 +21,7 @@
 // Host (non-HBM) buffers are accepted everywhere: pinned memory is used in
 // place (device-mapped), pageable memory is registered for the call.  All
 // arithmetic runs on the GPU; there is no CPU compute path.
+#include <chrono>
 #include "runtime.hpp"
 #include "../../include/ga_amd.h"
 #include "gaamd_kernels.h"
@@ -1219,11 +1220,16 @@ static int64_t row_bytes_of(int op, int count0) {
 // (the one-pass launch writes only the remote view), so no cycle of locks forms.
 // Across GPUs there is no one-pass route: the owner applies.
 // smaller patches keep the asynchronous packed route (COMEX_AMD_ONE_PASS_MIN bytes; tests
-// lower it so that random programs of small patches exercise the lock hand-offs)
+// lower it so that random programs of small patches exercise the lock hand-offs).
+// 64 KiB: one-pass beats the packed route from there up, alone (2 ranks of one GPU,
+// tools/remote_sweep.py: latency 16.5 vs 43 us, pipelined 7.7 vs 18-20 us per call)
+// and with every other rank accumulating into the same owner (39 vs 68 us per call
+// at 64-256 KiB on 3 ranks, 79-83 vs 147-152 on 5; profiles/r03/s24, s25); below it
+// the contended case was not better on the one-pass route.
 static uint64_t one_pass_min() {
     static const uint64_t v = [] {
         const char *e = getenv("COMEX_AMD_ONE_PASS_MIN");
-        return e ? (uint64_t)strtoull(e, nullptr, 10) : (1ull << 20);
+        return e ? (uint64_t)strtoull(e, nullptr, 10) : (64ull << 10);
     }();
     return v;
 }
@@ -1306,7 +1312,27 @@ static std::atomic<unsigned long long> g_one_pass{0};   // gaamd_route_counts: o
 // same target while we hold its lock go straight on (stream order and sched_pick's
 // range dependencies order them among themselves), unless someone else waits for
 // the lock: then ours finish and it goes first.
-struct OnePassHold { bool held = false; uint32_t pending = 0; std::vector<hipEvent_t> evs; };
+struct OnePassHold {
+    bool held = false;
+    uint32_t pending = 0;
+    double since = 0;   // steady-clock seconds at which we took the lock
+    std::vector<hipEvent_t> evs;
+};
+// A holder with launches in flight keeps a wanted lock for up to this long after it
+// took it (COMEX_AMD_ONE_PASS_LEASE_US): requesters streaming accumulates into one
+// owner then hand the lock over once per lease instead of once per call, each
+// hand-over costing a completion wait and a dispatch (tens of us against a few us
+// of enqueue per call); the wait a requester sees stays bounded by the lease.
+static double one_pass_lease_s() {
+    static const double v = [] {
+        const char *e = getenv("COMEX_AMD_ONE_PASS_LEASE_US");
+        return (e ? atof(e) : 0.0) * 1e-6;
+    }();
+    return v;
+}
+static double steady_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 static std::mutex g_op_mu;   // g_op_hold, g_op_pool; never held while waiting for a memory lock
 static std::vector<OnePassHold> g_op_hold;
 static std::vector<hipEvent_t> g_op_pool;
@@ -1347,7 +1373,9 @@ static bool one_pass_reap_locked(bool wait) {
         OnePassHold &h = g_op_hold[t];
         if (!h.held) continue;
         if (h.pending) {
-            if (!wait && !r.shm->mem_want[r.li((int)t)].load(std::memory_order_acquire)) continue;
+            if (!wait && (!r.shm->mem_want[r.li((int)t)].load(std::memory_order_acquire) ||
+                          steady_s() - h.since < one_pass_lease_s()))
+                continue;
             one_pass_mark(h);
         }
         bool done = true;
@@ -1401,7 +1429,8 @@ static bool one_pass_acc(int t, int op, void *scale, void *src, const int *ss, v
     const uint32_t me = 1 + (uint32_t)r.li(r.rank);
     std::unique_lock<std::mutex> og(g_op_mu);
     if (g_op_hold.size() != (size_t)r.size) g_op_hold.resize(r.size);
-    if (g_op_hold[t].held && want.load(std::memory_order_acquire) > 0) {
+    if (g_op_hold[t].held && want.load(std::memory_order_acquire) > 0 &&
+        steady_s() - g_op_hold[t].since >= one_pass_lease_s()) {
         // someone waits for t's memory: let ours finish and hand it over first
         one_pass_mark(g_op_hold[t]);
         for (hipEvent_t e : g_op_hold[t].evs) GA_HIP(hipEventSynchronize(e));
@@ -1419,6 +1448,7 @@ static bool one_pass_acc(int t, int op, void *scale, void *src, const int *ss, v
         want.fetch_sub(1, std::memory_order_acq_rel);
         og.lock();
         g_op_hold[t].held = true;
+        g_op_hold[t].since = steady_s();
     }
     int si;
     {

@@ -653,11 +653,14 @@ def direct_src_test(L, rank, size):
         say(rank, f"direct-source case {it} checked")
     counts = ga_amd.route_counts()
     if size > 1:
-        # the 64-column case is packed; the others take the direct-source route -- or, with
-        # the owner on this GPU, the one-pass route (the caller's kernel, no owner hand-off)
-        key = "one_pass" if one_pass_expected() else "direct_src"
-        assert counts[key] - counts0[key] == 3, (counts0, counts)
-        assert counts["packed"] > counts0["packed"]
+        # with the owner on this GPU every case takes the one-pass route (the caller's
+        # kernel, no owner hand-off; its floor is 64 KiB); otherwise the 64-column case
+        # (256 KiB) is below the direct-source route's 1 MiB floor and packs
+        if one_pass_expected():
+            assert counts["one_pass"] - counts0["one_pass"] == 4, (counts0, counts)
+        else:
+            assert counts["direct_src"] - counts0["direct_src"] == 3, (counts0, counts)
+            assert counts["packed"] > counts0["packed"]
     ga_amd.comex_barrier()
     assert ga_amd.comex_free(seg[rank]) == 0
     ga_amd.comex_finalize()
