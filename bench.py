@@ -572,6 +572,20 @@ def c5_extras(args, dist, wd=None):
         wd.phase = "exchange_check"
     out["exchange_check"] = {route: c5_exchange_check(dist, src_seg, n=n_chk) for route, src_seg in
                              (("buffer_src", False), ("segment_src", True))}
+    # diagnostics only (BENCH_CHECK_LOOPS=n): the exchange check n more times per route,
+    # with the first mismatch's details (never the driver's runs)
+    loops = int(os.environ.get("BENCH_CHECK_LOOPS", "0"))
+    if loops:
+        rep = {}
+        for route, src_seg in (("buffer_src", False), ("segment_src", True)):
+            bad, first = 0, None
+            for _ in range(loops):
+                r = c5_exchange_check(dist, src_seg, n=n_chk)
+                if r["result"] != "exact":
+                    bad += 1
+                    first = first or r
+            rep[route] = {"loops": loops, "mismatches": bad, "first_mismatch": first}
+        out["exchange_check_loops"] = rep
     ga_amd_lib().GA_Terminate()
     return out
 
@@ -629,8 +643,13 @@ def c5_exchange_check(dist, src_seg, n=4096):
     worst = int(dist.max(float(bad)))
     res = {"array": f"{n}x{n} f64", "expect_every_element": want, "wrong_elements_max_over_ranks": worst,
            "result": "exact" if worst == 0 else "MISMATCH", "routes_rank": routes}
-    if bad:
-        res["first_wrong_value_this_rank"] = sample
+    if worst:
+        # which rank's block, and what its first wrong element reads (2^p - 1 minus a
+        # missing contribution 2^k, or plus a doubled one, says whose)
+        bad_rank = int(dist.max(float(dist.rank) if bad else -1.0))
+        res["a_rank_with_wrong_elements"] = bad_rank
+        res["its_wrong_elements"] = int(dist.max(float(bad) if dist.rank == bad_rank else -1.0))
+        res["its_first_wrong_value"] = dist.max(sample if dist.rank == bad_rank else -1e300)
     return res
 
 

@@ -127,6 +127,8 @@ void addr_event(char kind, const void *p, size_t bytes, int peer) {
     g_addr_log.push_back({kind, (uintptr_t)p, (uintptr_t)p + bytes, peer});
     if (g_addr_log.size() > 4096) g_addr_log.pop_front();
 }
+static std::vector<void *> g_quarantine;   // blocks whose IPC export was refused (freed at finalize)
+
 static void addr_history(const void *p, size_t bytes) {
     std::lock_guard<std::mutex> g(g_addr_mu);
     const uintptr_t lo = (uintptr_t)p, hi = lo + bytes;
@@ -135,7 +137,7 @@ static void addr_history(const void *p, size_t bytes) {
         if (e.lo < hi && lo < e.hi) {
             fprintf(stderr, "[ga_amd %d]   earlier %s [%p, %p) %s%d\n", rt().rank,
                     e.kind == 'x' ? "export" : e.kind == 'o' ? "IPC map" : e.kind == 'c' ? "IPC unmap" :
-                    e.kind == 'f' ? "free" : e.kind == 'a' ? "alloc" : "?",
+                    e.kind == 'f' ? "free" : e.kind == 'a' ? "alloc" : e.kind == 'r' ? "reuse (cached block)" : "?",
                     (void *)e.lo, (void *)e.hi, e.peer >= 0 ? "of rank " : "", e.peer);
             ++n;
         }
@@ -2871,6 +2873,9 @@ int comex_finalize() {
     if (r.staging) addr_event('f', r.staging, r.staging_bytes, -1);
     if (r.staging) (void)hipFree(r.staging);
     r.staging = nullptr;
+    segment_cache_flush();
+    for (void *q : g_quarantine) (void)hipFree(q);
+    g_quarantine.clear();
     sched_sync_all();
     sched_fini();
     if (g_get_scratch) (void)hipFree(g_get_scratch);
@@ -3106,6 +3111,8 @@ int comex_wait_proc(int proc, comex_group_t group) {
 // export, IPC map/unmap, alloc and free this process made over that address range
 // (addr_history), then allocates another block while holding the refused one, up
 // to 4 times; COMEX_AMD_IPC_RETRY=0 makes the first refusal fatal instead.
+static void *device_alloc(size_t bytes);
+
 static void export_alloc(void **p, size_t bytes, hipIpcMemHandle_t *h, const char *what) {
     Runtime &r = rt();
     static const bool retry = [] {
@@ -3122,16 +3129,100 @@ static void export_alloc(void **p, size_t bytes, hipIpcMemHandle_t *h, const cha
         if (!retry) break;
         fprintf(stderr, "[ga_amd %d]   allocating another block (COMEX_AMD_IPC_RETRY=0: abort instead)\n", r.rank);
         held.push_back(*p);
-        GA_HIP(hipMalloc(p, bytes));
+        *p = device_alloc(bytes);
         addr_event('a', *p, bytes, -1);
         e = hipIpcGetMemHandle(h, *p);
     }
-    for (void *q : held) {
-        addr_event('f', q, bytes, -1);
-        GA_HIP(hipFree(q));
-    }
+    // a refused block is kept, not freed, until comex_finalize: freed, its address
+    // would come back from hipMalloc and be refused again
+    for (void *q : held) g_quarantine.push_back(q);
     if (e != hipSuccess) fatal("hipIpcGetMemHandle of a %zu-byte %s failed: %s", bytes, what, hipGetErrorString(e));
     addr_event('x', *p, bytes, -1);
+}
+
+// Freed device segments are kept for the next comex_malloc of the same size, with
+// their IPC export, instead of going back to hipFree (COMEX_AMD_SEGMENT_CACHE_MB,
+// default 16 GiB per rank; 0 disables).  GA creates and destroys arrays of the same
+// shapes over and over; every hipFree + hipMalloc + export cycle recycles addresses
+// and descriptors, and the runtime refuses, now and then, to export a fresh block at
+// a recycled address (profiles/r03/s19, s20, s27-s29: 1-4 refusals in most runs of
+// eight ranks on one GPU).  A cached block is exported once, for good, and a reused
+// one is opened again by the peers from the same handle.
+struct CachedBlock {
+    void *p;
+    size_t bytes;
+    bool exported;
+    hipIpcMemHandle_t h;
+};
+static std::deque<CachedBlock> g_blocks;   // oldest first
+static size_t g_blocks_bytes = 0;
+static std::atomic<unsigned long long> g_block_reuse{0};
+
+static size_t block_cache_cap() {
+    static const size_t v = [] {
+        const char *e = getenv("COMEX_AMD_SEGMENT_CACHE_MB");
+        return (size_t)(e ? atof(e) : 16384.0) << 20;
+    }();
+    return v;
+}
+
+static void block_free_one(const CachedBlock &b) {
+    addr_event('f', b.p, b.bytes, -1);
+    GA_HIP(hipFree(b.p));
+}
+
+static void block_flush() {
+    for (const CachedBlock &b : g_blocks) block_free_one(b);
+    g_blocks.clear();
+    g_blocks_bytes = 0;
+}
+
+
+
+extern "C" unsigned long long gaamd_segment_cache_reuse(void) { return g_block_reuse.load(); }
+
+static void block_put(void *p, size_t bytes, bool exported, const hipIpcMemHandle_t &h) {
+    const size_t cap = block_cache_cap();
+    if (bytes > cap) {
+        block_free_one({p, bytes, exported, h});
+        return;
+    }
+    while (g_blocks_bytes + bytes > cap && !g_blocks.empty()) {
+        block_free_one(g_blocks.front());
+        g_blocks_bytes -= g_blocks.front().bytes;
+        g_blocks.pop_front();
+    }
+    g_blocks.push_back({p, bytes, exported, h});
+    g_blocks_bytes += bytes;
+}
+
+// a cached block of exactly `bytes`; its export in *h when it has one
+static bool block_take(size_t bytes, void **p, bool *exported, hipIpcMemHandle_t *h) {
+    for (auto it = g_blocks.begin(); it != g_blocks.end(); ++it) {
+        if (it->bytes != bytes) continue;
+        *p = it->p;
+        *exported = it->exported;
+        if (it->exported) *h = it->h;
+        g_blocks_bytes -= bytes;
+        g_blocks.erase(it);
+        g_block_reuse.fetch_add(1, std::memory_order_relaxed);
+        addr_event('r', *p, bytes, -1);
+        return true;
+    }
+    return false;
+}
+
+// hipMalloc, giving the cached blocks back first when the device is full
+static void *device_alloc(size_t bytes) {
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipErrorOutOfMemory && !g_blocks.empty()) {
+        (void)hipGetLastError();
+        block_flush();
+        e = hipMalloc(&p, bytes);
+    }
+    if (e != hipSuccess) fatal("hipMalloc of %zu bytes failed: %s", bytes, hipGetErrorString(e));
+    return p;
 }
 
 static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool device) {
@@ -3145,10 +3236,13 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     struct Info { uint64_t base, bytes; hipIpcMemHandle_t h; int32_t device, pad; } mine;
     memset(&mine, 0, sizeof(mine));
     void *p = nullptr;
+    bool exported = false;
     if (bytes) {
         if (device) {
-            GA_HIP(hipMalloc(&p, bytes));
-            addr_event('a', p, bytes, -1);
+            if (!block_take(bytes, &p, &exported, &mine.h)) {
+                p = device_alloc(bytes);
+                addr_event('a', p, bytes, -1);
+            }
             if (r.debug) {
                 void *base = nullptr;
                 size_t sz = 0;
@@ -3156,7 +3250,10 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
                 fprintf(stderr, "[ga_amd %d] segment %p (%zu B): allocation base %p size %zu\n", r.rank, p,
                         bytes, base, sz);
             }
-            if (r.size > 1) export_alloc(&p, bytes, &mine.h, "segment");
+            if (r.size > 1 && !exported) {
+                export_alloc(&p, bytes, &mine.h, "segment");
+                exported = true;
+            }
         } else {
             GA_HIP(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
         }
@@ -3180,6 +3277,9 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     s.live = true;
     s.device = device;
     s.local = p;
+    s.local_bytes = bytes;
+    s.exported = exported;
+    if (exported) s.handle = mine.h;
     for (int q = 0; q < r.size; ++q) {
         s.peer[q].base = all[q].base;
         s.peer[q].bytes = all[q].bytes;
@@ -3222,7 +3322,10 @@ int comex_free(void *ptr, comex_group_t group) {
     for (size_t k = 0; k < members.size(); ++k) all[members[k]] = gathered[k];
     members_barrier(members, group);   // nobody still reads the segment
     void *local = nullptr;
-    bool device = true, found = false;
+    bool device = true, found = false, exported = false;
+    size_t local_bytes = 0;
+    hipIpcMemHandle_t handle;
+    memset(&handle, 0, sizeof(handle));
     {
         std::lock_guard<std::mutex> g(r.seg_mu);
         for (Segment &s : r.segs) {
@@ -3234,6 +3337,9 @@ int comex_free(void *ptr, comex_group_t group) {
                 if (q != r.rank && s.peer[q].mapped) ipc_close(s.peer[q].mapped, q);
             local = s.local;
             device = s.device;
+            local_bytes = s.local_bytes;
+            exported = s.exported;
+            if (exported) handle = s.handle;
             s.live = false;
             s.local = nullptr;
             found = true;
@@ -3246,8 +3352,12 @@ int comex_free(void *ptr, comex_group_t group) {
     // refuses to export a new allocation it hands out at the same address
     // (hipIpcGetMemHandle: invalid argument in the next comex_malloc)
     members_barrier(members, group);
-    if (local && device) addr_event('f', local, mapped_size(local), -1);
-    if (local) GA_HIP(device ? hipFree(local) : hipHostFree(local));
+    if (local && device) {
+        if (block_cache_cap()) block_put(local, local_bytes, exported, handle);   // kept for the next comex_malloc
+        else block_free_one({local, local_bytes, exported, handle});
+    } else if (local) {
+        GA_HIP(hipHostFree(local));
+    }
     return COMEX_SUCCESS;
 }
 
@@ -3432,3 +3542,7 @@ int gaamd_route_counts(unsigned long long counts[4]) {
 unsigned long long gaamd_one_pass_count(void) { return g_one_pass.load(std::memory_order_relaxed); }
 
 }  // extern "C"
+
+namespace gaamd {
+void segment_cache_flush() { block_flush(); }
+}  // namespace gaamd

@@ -182,7 +182,11 @@ void *gaamd_stream_at(int i) {
 
 void *gaamd_dev_malloc(size_t bytes) {
     void *p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        segment_cache_flush();   // freed segments kept for reuse go back first
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    }
     addr_event('a', p, bytes, -1);
     return p;
 }

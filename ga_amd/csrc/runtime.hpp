@@ -121,6 +121,9 @@ struct Segment {
     bool live = false;
     bool device = true;
     void *local = nullptr;
+    size_t local_bytes = 0;      // bytes of the local block
+    bool exported = false;       // `handle` is the local block's IPC export
+    hipIpcMemHandle_t handle;
     std::vector<PeerMap> peer;   // indexed by world rank
 };
 
@@ -222,6 +225,8 @@ void boot_barrier();
 void boot_finalize();
 
 // sched.cpp (callers hold launch_mu)
+// give the freed device segments kept for reuse (comex.cpp) back to the runtime
+void segment_cache_flush();
 void sched_init(int nstreams, int pull_streams = 0);
 void sched_fini();
 void sched_resize(int nstreams);

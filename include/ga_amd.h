@@ -103,6 +103,8 @@ int gaamd_iov_path_counts(unsigned long long counts[3]);
 int gaamd_stamps(int on, unsigned long long out[8]);
 /* one-pass accumulates this rank applied into the segment of a rank on the same GPU */
 unsigned long long gaamd_one_pass_count(void);
+/* comex_malloc calls served by a freed segment block kept for reuse (with its IPC export) */
+unsigned long long gaamd_segment_cache_reuse(void);
 /* same-node peers whose staging buffer this rank could not map by IPC at
  * comex_init (remote accumulates to or from them would abort); -1 before init */
 int gaamd_peers_unmapped(void);

@@ -106,6 +106,8 @@ def main():
         c5_full_test(L, rank, size)
     elif mode == "directsrc":
         direct_src_test(L, rank, size)
+    elif mode == "segcache":
+        segment_cache_test(L, rank, size)
     elif mode in ("armcimisc", "armcimisc-gloo"):
         armci_misc_test(L, rank, size)
     else:
@@ -598,6 +600,49 @@ def self_order_test(L, rank, size):
         assert ga_amd.comex_free(src2[rank]) == 0
     ga_amd.comex_barrier()
     assert ga_amd.comex_free(me) == 0
+    ga_amd.comex_finalize()
+
+
+def segment_cache_test(L, rank, size):
+    """comex_malloc / remote accumulates / comex_free of same-size segments, over and
+    over (GA creating and destroying arrays): a freed block is kept with its IPC export
+    and serves the next comex_malloc of its size, the peers opening it again from the
+    same handle.  Every round: zero, every rank accumulates 2**rank into the next
+    rank's block (one-pass or packed route) and into its own, barrier, exact check.
+    A different size every third round takes a fresh block."""
+    import ga_amd
+    assert ga_amd.comex_init() == 0
+    cache_on = os.environ.get("COMEX_AMD_SEGMENT_CACHE_MB", "1") != "0"
+    reuse0 = L.gaamd_segment_cache_reuse()
+    one = ctypes.c_double(1.0)
+    for it in range(9):
+        n = (1 << 18) if it % 3 != 2 else (1 << 18) + 512 * it   # f64 elements
+        seg = ga_amd.comex_malloc(n * 8, size)
+        L.gaamd_memset(ctypes.c_void_p(seg[rank]), 0, n * 8)
+        ga_amd.sync()
+        ga_amd.comex_barrier()
+        src = ga_amd.DeviceBuffer(n * 8)
+        ga_amd.fill_const(src.ptr, n * 8, float(2 ** rank))
+        ga_amd.sync()
+        for t in {rank, (rank + 1) % size}:
+            assert L.comex_acc(38, ctypes.byref(one), ctypes.c_void_p(src.ptr), ctypes.c_void_p(seg[t]), n * 8, t,
+                               0) == 0
+        ga_amd.comex_barrier()
+        got = np.zeros(n)
+        assert L.comex_get(ctypes.c_void_p(seg[rank]), got.ctypes.data_as(ctypes.c_void_p), n * 8, rank, 0) == 0
+        prv = (rank - 1) % size
+        want = float(2 ** rank + (2 ** prv if prv != rank else 0))
+        bad = int(np.count_nonzero(got != want))
+        assert bad == 0, f"rank {rank} round {it}: {bad} wrong, e.g. {got[np.nonzero(got != want)[0][0]]} != {want}"
+        src.free()
+        ga_amd.comex_barrier()
+        assert ga_amd.comex_free(seg[rank]) == 0
+    reused = L.gaamd_segment_cache_reuse() - reuse0
+    if cache_on:
+        assert reused >= 5, f"rank {rank}: {reused} segments served from the cache"
+    else:
+        assert reused == 0, reused
+    say(rank, f"segment cache: {reused} of 9 comex_malloc served by a kept block")
     ga_amd.comex_finalize()
 
 

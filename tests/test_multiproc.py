@@ -423,3 +423,12 @@ def test_bench_extras_watchdog_keeps_headline():
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["value"] > 0
     assert "timed_out" in line["c5"], line["c5"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,cache", [(2, "16384"), (3, "16384"), (3, "0")])
+def test_segment_cache_reuse(n, cache):
+    """Freed segments are kept with their IPC export and serve the next comex_malloc of
+    their size; remote accumulates into reused segments stay exact (and with the cache
+    off, every segment is a fresh block)."""
+    launch("segcache", n=n, timeout=120, extra_env={"COMEX_AMD_SEGMENT_CACHE_MB": cache})
