@@ -3157,6 +3157,7 @@ struct CachedBlock {
 static std::deque<CachedBlock> g_blocks;   // oldest first
 static size_t g_blocks_bytes = 0;
 static std::atomic<unsigned long long> g_block_reuse{0};
+static std::atomic<unsigned long long> g_remapped{0};   // segments replaced after a stale peer mapping
 
 static size_t block_cache_cap() {
     static const size_t v = [] {
@@ -3180,6 +3181,7 @@ static void block_flush() {
 
 
 extern "C" unsigned long long gaamd_segment_cache_reuse(void) { return g_block_reuse.load(); }
+extern "C" unsigned long long gaamd_segment_remaps(void) { return g_remapped.load(); }
 
 static void block_put(void *p, size_t bytes, bool exported, const hipIpcMemHandle_t &h) {
     const size_t cap = block_cache_cap();
@@ -3225,6 +3227,19 @@ static void *device_alloc(size_t bytes) {
     return p;
 }
 
+// Every segment gets a per-rank, per-allocation tag in its first and last 8 bytes
+// before its handle goes out, and every peer reads both through its fresh mapping.
+// Eight ranks on one GPU (profiles/r03/s32), with freed blocks going back to the
+// runtime: in 2 of 30 runs, after the runtime had refused an export and a new block
+// was exported instead, EVERY peer's mapping of that rank's new block reached other
+// memory -- the block later read only its owner's own contribution, nobody else's,
+// with no error anywhere.  A mapping that does not read the tags is therefore
+// closed, the owner's block set aside (quarantined) and replaced, and the exchange
+// repeated (all ranks, collectively), up to 4 times.
+static uint64_t seg_tag(int rank, uint64_t gen, int end) {
+    return 0x67614d4453454700ull ^ ((uint64_t)rank << 40) ^ (gen << 1) ^ (uint64_t)end;
+}
+
 static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool device) {
     ensure_init();
     Runtime &r = rt();
@@ -3233,8 +3248,9 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     const std::vector<int> members = group_members(group);
     const bool trace = r.debug >= 2;
     if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc(%zu, group %d): enter\n", r.rank, bytes, group);
-    struct Info { uint64_t base, bytes; hipIpcMemHandle_t h; int32_t device, pad; } mine;
+    struct Info { uint64_t base, bytes; hipIpcMemHandle_t h; int32_t device, pad; uint64_t gen; } mine;
     memset(&mine, 0, sizeof(mine));
+    static uint64_t gen = 0;   // this rank's allocation counter (the tags)
     void *p = nullptr;
     bool exported = false;
     if (bytes) {
@@ -3258,18 +3274,70 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
             GA_HIP(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
         }
     }
-    mine.base = (uint64_t)(uintptr_t)p;
-    mine.bytes = bytes;
-    mine.device = r.device;
-    if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: allocated %p, allgather\n", r.rank, p);
-    std::vector<Info> gathered(members.size());
-    members_allgather(members, group, &mine, gathered.data(), sizeof(Info));
-    if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: allgather done, opening peers\n", r.rank);
+    const bool tagged = device && bytes >= 16;
     std::vector<Info> all(r.size);
-    memset(all.data(), 0, sizeof(Info) * all.size());
-    for (size_t k = 0; k < members.size(); ++k) {
-        all[members[k]] = gathered[k];
-        ptr_arr[k] = (void *)(uintptr_t)gathered[k].base;
+    std::vector<void *> mapped(r.size, nullptr);
+    for (int attempt = 0;; ++attempt) {
+        mine.base = (uint64_t)(uintptr_t)p;
+        mine.bytes = bytes;
+        mine.device = r.device;
+        mine.gen = ++gen;
+        if (tagged) {
+            const uint64_t t0 = seg_tag(r.rank, mine.gen, 0), t1 = seg_tag(r.rank, mine.gen, 1);
+            GA_HIP(hipMemcpy(p, &t0, 8, hipMemcpyHostToDevice));
+            GA_HIP(hipMemcpy((char *)p + bytes - 8, &t1, 8, hipMemcpyHostToDevice));
+        }
+        if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: allocated %p, allgather\n", r.rank, p);
+        std::vector<Info> gathered(members.size());
+        members_allgather(members, group, &mine, gathered.data(), sizeof(Info));
+        if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: allgather done, opening peers\n", r.rank);
+        memset(all.data(), 0, sizeof(Info) * all.size());
+        for (size_t k = 0; k < members.size(); ++k) {
+            all[members[k]] = gathered[k];
+            ptr_arr[k] = (void *)(uintptr_t)gathered[k].base;
+        }
+        // open, and check that each mapping reads its owner's tags
+        std::vector<uint8_t> stale(r.size, 0);
+        for (int q = 0; q < r.size; ++q) {
+            mapped[q] = nullptr;
+            if (q == r.rank || !all[q].bytes || !r.same_node(q)) continue;
+            if (!device) fatal("host-memory segments are rank-private (use device segments for remote access)");
+            mapped[q] = ipc_open(all[q].h, q, "segment");
+            if (!mapped[q] || all[q].bytes < 16) continue;
+            uint64_t t[2] = {0, 0};
+            GA_HIP(hipMemcpy(&t[0], mapped[q], 8, hipMemcpyDeviceToHost));
+            GA_HIP(hipMemcpy(&t[1], (char *)mapped[q] + all[q].bytes - 8, 8, hipMemcpyDeviceToHost));
+            if (t[0] != seg_tag(q, all[q].gen, 0) || t[1] != seg_tag(q, all[q].gen, 1)) {
+                stale[q] = 1;
+                fprintf(stderr, "[ga_amd %d] the IPC mapping of rank %d's new %zu-byte segment (%p in its space) "
+                        "reads %#llx / %#llx, not its tags: another allocation's memory\n", r.rank, q,
+                        (size_t)all[q].bytes, (void *)(uintptr_t)all[q].base, (unsigned long long)t[0],
+                        (unsigned long long)t[1]);
+            }
+        }
+        std::vector<uint8_t> seen(members.size() * (size_t)r.size);
+        members_allgather(members, group, stale.data(), seen.data(), (size_t)r.size);
+        bool any = false, mine_stale = false;
+        for (size_t k = 0; k < members.size(); ++k)
+            for (int q = 0; q < r.size; ++q)
+                if (seen[k * (size_t)r.size + q]) {
+                    any = true;
+                    if (q == r.rank) mine_stale = true;
+                }
+        if (!any) break;
+        if (attempt >= 3) fatal("IPC mappings of a new segment keep reaching other memory (4 attempts)");
+        for (int q = 0; q < r.size; ++q)
+            if (mapped[q]) ipc_close(mapped[q], q);
+        if (mine_stale) {
+            // set the block aside for good and export a fresh one
+            addr_history(p, bytes);
+            g_quarantine.push_back(p);
+            p = device_alloc(bytes);
+            addr_event('a', p, bytes, -1);
+            export_alloc(&p, bytes, &mine.h, "segment");
+            g_remapped.fetch_add(1, std::memory_order_relaxed);
+        }
+        members_barrier(members, group);   // every stale mapping closed before the next round
     }
     Segment s;
     s.peer.resize(r.size);
@@ -3283,12 +3351,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     for (int q = 0; q < r.size; ++q) {
         s.peer[q].base = all[q].base;
         s.peer[q].bytes = all[q].bytes;
-        if (q == r.rank) {
-            s.peer[q].mapped = (char *)p;
-        } else if (all[q].bytes && r.same_node(q)) {
-            if (!device) fatal("host-memory segments are rank-private (use device segments for remote access)");
-            s.peer[q].mapped = (char *)ipc_open(all[q].h, q, "segment");
-        }
+        s.peer[q].mapped = q == r.rank ? (char *)p : (char *)mapped[q];
     }
     {
         std::lock_guard<std::mutex> g(r.seg_mu);

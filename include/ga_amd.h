@@ -105,6 +105,8 @@ int gaamd_stamps(int on, unsigned long long out[8]);
 unsigned long long gaamd_one_pass_count(void);
 /* comex_malloc calls served by a freed segment block kept for reuse (with its IPC export) */
 unsigned long long gaamd_segment_cache_reuse(void);
+/* segments this rank replaced because a peer's fresh IPC mapping did not read their tags */
+unsigned long long gaamd_segment_remaps(void);
 /* same-node peers whose staging buffer this rank could not map by IPC at
  * comex_init (remote accumulates to or from them would abort); -1 before init */
 int gaamd_peers_unmapped(void);
