@@ -127,6 +127,11 @@ void addr_event(char kind, const void *p, size_t bytes, int peer) {
     g_addr_log.push_back({kind, (uintptr_t)p, (uintptr_t)p + bytes, peer});
     if (g_addr_log.size() > 4096) g_addr_log.pop_front();
 }
+// the tag a rank writes into a new exported block (do_malloc, the staging buffer)
+static uint64_t seg_tag(int rank, uint64_t gen, int end) {
+    return 0x67614d4453454700ull ^ ((uint64_t)rank << 40) ^ (gen << 1) ^ (uint64_t)end;
+}
+
 static std::vector<void *> g_quarantine;   // blocks whose IPC export was refused (freed at finalize)
 
 static void addr_history(const void *p, size_t bytes) {
@@ -2789,6 +2794,10 @@ int comex_init() {
         memset(&mine, 0, sizeof(mine));
         export_alloc((void **)&r.staging, r.staging_bytes, &mine.h, "staging buffer");
         mine.bytes = r.staging_bytes;
+        {
+            const uint64_t t = seg_tag(r.rank, 0, 0);   // checked by every peer below
+            GA_HIP(hipMemcpy(r.staging, &t, 8, hipMemcpyHostToDevice));
+        }
         std::vector<char> buf(sizeof(mine) * (size_t)r.size);
         boot_allgather(&mine, buf.data(), sizeof(mine));
         all = reinterpret_cast<decltype(all)>(buf.data());
@@ -2798,6 +2807,19 @@ int comex_init() {
             if (!r.same_node(q)) continue;   // another node: reached through wire.cpp
             r.peer_staging[q] = (char *)ipc_open(all[q].h, q, "staging buffer");
         }
+        // as for segments (do_malloc): every staging mapping must read its owner's tag
+        // (written before the exchange below the allgather's barrier) -- a mapping of
+        // the wrong allocation would hand the owners other bytes to accumulate
+        boot_barrier();
+        for (int q = 0; q < r.size; ++q) {
+            if (q == r.rank || !r.peer_staging[q] || all[q].bytes < 8) continue;
+            uint64_t t = 0;
+            GA_HIP(hipMemcpy(&t, r.peer_staging[q], 8, hipMemcpyDeviceToHost));
+            if (t != seg_tag(q, 0, 0))
+                fatal("the IPC mapping of rank %d's staging buffer reads %#llx, not its tag: another allocation's "
+                      "memory", q, (unsigned long long)t);
+        }
+        boot_barrier();   // nobody reads a tag any more: the rings may be written
         r.posted.assign(r.size, 0);
         r.stage_head.assign(r.size, 0);
         r.direct_pending.assign(r.size, 0);
@@ -3236,9 +3258,7 @@ static void *device_alloc(size_t bytes) {
 // with no error anywhere.  A mapping that does not read the tags is therefore
 // closed, the owner's block set aside (quarantined) and replaced, and the exchange
 // repeated (all ranks, collectively), up to 4 times.
-static uint64_t seg_tag(int rank, uint64_t gen, int end) {
-    return 0x67614d4453454700ull ^ ((uint64_t)rank << 40) ^ (gen << 1) ^ (uint64_t)end;
-}
+
 
 static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool device) {
     ensure_init();
