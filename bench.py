@@ -856,7 +856,7 @@ def main():
     ap.add_argument("--ga-dims", type=int, default=0, help="C5: square GA of this size instead of 32768^2")
     ap.add_argument("--c5-steps", type=int, default=4, help="N>1: timed C5 M1 steps (M2: half as many)")
     ap.add_argument("--no-extras", action="store_true", help="N>1: skip the C5 M1/M2 measurements")
-    ap.add_argument("--extras-timeout", type=float, default=300.0,
+    ap.add_argument("--extras-timeout", type=float, default=180.0,
                     help="N>1: seconds the C5 extras may take before the headline line is printed without them")
     ap.add_argument("--verbose", action="store_true", help="progress lines on stderr")
     args = ap.parse_args()
