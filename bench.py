@@ -895,42 +895,61 @@ def main():
             c5 = {"skipped": f"a rank could not map {unmapped} same-node peer(s) by IPC at comex_init"}
         else:
             c5 = c5_extras(args, dist, wd)
-        wd.cancel()
+        if not wd.cancel():
+            time.sleep(3600)   # the watchdog owns the line and the exit status
         if line is not None:
             line["c5"] = c5
     if line is not None:
         print(json.dumps(line), flush=True)
 
 
+EXTRAS_TIMEOUT_STATUS = 3
+
+
 class ExtrasWatchdog:
     """N > 1: the C5 extras run after the headline is measured.  If they have not
     finished after `seconds` (a hang in an exchange no one-GPU box could rehearse),
     rank 0 prints the headline line with the extras marked as timed out, every rank
-    dumps its Python stacks to stderr and leaves with status 0 -- the headline was
-    measured and is reported; the extras' failure is stated in the line."""
+    dumps its Python stacks to stderr and the job ends with status
+    EXTRAS_TIMEOUT_STATUS (3): the headline was measured and is reported, and the
+    hang is a failure the caller sees, not a success with a note.
+    The line is printed exactly once: cancel() and fire() settle it under a lock."""
 
     def __init__(self, seconds, rank, line):
         import threading
         self.phase = "start"
         self.rank, self.line = rank, line
+        self.lock = threading.Lock()
+        self.settled = False
         self.t = threading.Timer(seconds, self.fire, args=(seconds,))
         self.t.daemon = True
         self.t.start()
 
     def fire(self, seconds):
         import faulthandler
-        print(f"rank {self.rank}: C5 extras still in phase {self.phase!r} after {seconds:.0f} s; stacks:",
-              file=sys.stderr, flush=True)
-        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
-        if self.line is not None:
-            self.line["c5"] = {"timed_out": f"C5 extras did not finish within {seconds:.0f} s "
-                                            f"(phase {self.phase!r} on rank 0); the headline above was "
-                                            "measured before they started"}
-            print(json.dumps(self.line), flush=True)
-        os._exit(0)
+        with self.lock:
+            if self.settled:        # the extras finished first: main prints the line
+                return
+            self.settled = True
+            print(f"rank {self.rank}: C5 extras still in phase {self.phase!r} after {seconds:.0f} s; stacks:",
+                  file=sys.stderr, flush=True)
+            faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+            if self.line is not None:
+                self.line["c5"] = {"timed_out": f"C5 extras did not finish within {seconds:.0f} s "
+                                                f"(phase {self.phase!r} on rank 0); the headline above was "
+                                                "measured before they started"}
+                print(json.dumps(self.line), flush=True)
+            os._exit(EXTRAS_TIMEOUT_STATUS)
 
     def cancel(self):
-        self.t.cancel()
+        """True: the extras finished in time and the caller prints the line; False:
+        the watchdog fired (and is ending the process)."""
+        with self.lock:
+            self.t.cancel()
+            if self.settled:
+                return False
+            self.settled = True
+            return True
 
 
 def make_line(args, dist, r, ga_amd):

@@ -68,7 +68,10 @@ struct Tuning {
     int flat_max_nvec = 127;// rows with at most this many vectors use the flat kernel
     int align = 1;          // 2-D rows kernel: start chunks on chunk-aligned dst addresses (misaligned rows)
     int flat_line_min = 40; // rows off 128 B lines on both sides with at least this many vectors: rows kernel (0 = off)
-    int ordered_cols = 1;   // ordered rows sharing bytes only column-wise: column-sliced many-workgroup kernel
+    // ordered rows sharing bytes only column-wise: 2 (default) column slices, rows loaded by
+    // every wave of a workgroup and applied in order from LDS (k_ordered_cols_lds); 1 one lane
+    // per column slice loading its own rows (k_ordered_cols); 0 the one-workgroup kernel
+    int ordered_cols = 2;
 };
 Tuning &tuning();
 

@@ -90,13 +90,17 @@ __device__ __forceinline__ typename Vec<W>::T vload(const char *p) {
 }
 
 // System-scope loads for bytes that live in ANOTHER GPU's HBM (a peer's staging
-// or segment reached through its IPC mapping).  A relaxed system-scope atomic
-// load lowers to `global_load_* sc0 sc1` on gfx950 (LLVM's AMDGPU memory model,
-// the GFX942 family: the same lowering as a system-scope atomic load), which the
-// L2 serves coherently at system scope -- a line of the peer's memory this GPU's
-// L2 still holds from an earlier read (MTYPE NC) is not returned stale.  One
-// dword (or the element's own 1/2 bytes) per load: every vector the launcher
-// builds is dword-aligned at W >= 4, so each load is naturally aligned.
+// or segment reached through its IPC mapping).  They must be served coherently at
+// system scope: a line of the peer's memory this GPU's L2 still holds from an
+// earlier read (MTYPE NC) must not be returned stale.  On gfx950 (LLVM's AMDGPU
+// memory model, the GFX942 family) both a relaxed system-scope atomic load and a
+// volatile load lower to `global_load_* sc0 sc1`; only the volatile form comes
+// in every width, so W = 4/8/16 is ONE `global_load_dword{,x2,x4} ... sc0 sc1`
+// (round 3 issued a system-scope dword per 4 bytes).  The
+// memory model follows a volatile load with `s_waitcnt vmcnt(0)` (volatile
+// accesses keep their order), so callers issue their other loads BEFORE the
+// system-scope one: they are then in flight together.  Every vector the launcher
+// builds is naturally aligned at its width W.  1/2-byte vectors stay atomic loads.
 template <int W>
 __device__ __forceinline__ typename Vec<W>::T vload_sys(const char *p) {
     typedef typename Vec<W>::T V;
@@ -105,11 +109,9 @@ __device__ __forceinline__ typename Vec<W>::T vload_sys(const char *p) {
     } else if constexpr (W == 2) {
         return __hip_atomic_load(reinterpret_cast<const uint16_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     } else {
-        union { V v; uint32_t w[W / 4]; } u;
-        const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
-#pragma unroll
-        for (int i = 0; i < W / 4; ++i) u.w[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return u.v;
+        // through a global (addrspace 1) pointer: a generic one becomes flat_load
+        typedef const volatile __attribute__((address_space(1))) V GV;
+        return *(GV *)(p);
     }
 }
 template <int W, bool NT>
@@ -240,11 +242,21 @@ __device__ __forceinline__ void chunk_op(const char *sp, char *dp, int64_t v0, u
     const char *s0 = sp + v0 * W;
     char *d0 = dp + v0 * W;
     if (full) {
+        if constexpr (SYS) {
+            // the local dst loads first: each system-scope (volatile) source load is
+            // followed by a wait for every load in flight (vload_sys)
+            if constexpr (OP::kReadsDst) {
 #pragma unroll
-        for (int k = 0; k < U; ++k) {
-            if constexpr (SYS) a[k] = vload_sys<W>(s0 + k * BS * W);
-            else a[k] = vload<W, true>(s0 + k * BS * W);
-            if constexpr (OP::kReadsDst) b[k] = vload<W, true>(d0 + k * BS * W);
+                for (int k = 0; k < U; ++k) b[k] = vload<W, true>(d0 + k * BS * W);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) a[k] = vload_sys<W>(s0 + k * BS * W);
+        } else {
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                a[k] = vload<W, true>(s0 + k * BS * W);
+                if constexpr (OP::kReadsDst) b[k] = vload<W, true>(d0 + k * BS * W);
+            }
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) vstore<W, true>(d0 + k * BS * W, op.template apply<W>(b[k], a[k]));
@@ -254,10 +266,10 @@ __device__ __forceinline__ void chunk_op(const char *sp, char *dp, int64_t v0, u
     for (int k = 0; k < U; ++k) {
         if ((uint64_t)(v0 + k * BS) >= (uint64_t)nvec) continue;   // negative or past the row
         V x, y;
+        if constexpr (OP::kReadsDst) y = vload<W, true>(d0 + k * BS * W);
         if constexpr (SYS) x = vload_sys<W>(s0 + k * BS * W);
         else x = vload<W, true>(s0 + k * BS * W);
-        y = x;
-        if constexpr (OP::kReadsDst) y = vload<W, true>(d0 + k * BS * W);
+        if constexpr (!OP::kReadsDst) y = x;
         vstore<W, true>(d0 + k * BS * W, op.template apply<W>(y, x));
     }
 }
@@ -527,6 +539,94 @@ __global__ __launch_bounds__(64) void k_ordered_cols(const Desc d, const OP op) 
     }
 }
 
+// COLUMN-ORDERED, LDS-staged (the PIPE geometries).  The
+// one-lane-per-column kernel above is latency-bound: a column reduction has only
+// row-width / W lanes (8192 at 64 KiB rows: one wave per two CUs), each with at
+// most 63 loads in flight (vmcnt) -- 0.62-0.65 TB/s of real HBM traffic.  Here a
+// workgroup of KC_NW waves owns CW column slices (CW*W contiguous bytes of every
+// row), and ALL its waves load rows: wave w's k-th load instruction fetches rows
+// (w*P + k)*RPI .. +RPI-1 of the tile (RPI = 64/CW rows per instruction, CW lanes
+// each), so a workgroup keeps KC_NW*P instructions in flight.  The tile goes to
+// LDS, and the first CW lanes of wave 0 walk its rows IN ORDER, applying each to
+// the column value held in a register (stored when the dst run changes and at the
+// end) -- the reference's operations in its order per column (comex.c:6936-6961,
+// acc.h:137-143) -- while the next tile's loads are in flight.  A row's dst offset
+// is the same for every lane, so the run test is wave-uniform.
+constexpr int KC_NW = 4;                 // waves per workgroup
+template <int W> struct KcRows { static constexpr int P = W >= 16 ? 16 : 32; };   // load instructions per wave per tile
+template <class OP, int W, int LV, int CW>
+__global__ __launch_bounds__(KC_NW * 64) void k_ordered_cols_lds(const Desc d, const OP op) {
+    typedef typename Vec<W>::T V;
+    constexpr int P = KcRows<W>::P;
+    constexpr int RPI = 64 / CW;                 // rows per load instruction
+    constexpr int T = KC_NW * P * RPI;           // rows per tile
+    __shared__ V tile[T * CW];                   // [row][column], KC_NW*P*64 vectors
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t col = blockIdx.x * (uint32_t)CW + (lane % CW);
+    const bool live = col < d.nvec;
+    const int64_t xo = (int64_t)col * W;
+    const uint32_t sub = lane / CW;              // which row of an instruction's RPI this lane loads
+    // lanes past the row's last column or the last row load a valid clamped address
+    // (their values are never applied): every load is unconditional, so the P loads
+    // of a wave issue back to back (conditional loads each got an s_waitcnt vmcnt(0))
+    const int64_t xl = (int64_t)min(col, d.nvec - 1u) * W;
+    V s[P];
+    auto load_tile = [&](uint32_t r0) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const uint32_t r = min(r0 + (wave * P + (uint32_t)k) * RPI + sub, d.rows - 1u);
+            int64_t so, dof;
+            row_offsets<LV>(d, d.row0 + r, so, dof);
+            s[k] = vload<W, true>(d.src + so + xl);
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int k = 0; k < P; ++k) tile[(wave * P + (uint32_t)k) * 64 + lane] = s[k];
+    };
+    V acc = {};
+    int64_t cur = 0;
+    bool held = false;
+    load_tile(0);
+    store_tile();
+    __syncthreads();
+    for (uint32_t r0 = 0; r0 < d.rows; r0 += T) {
+        if (r0 + T < d.rows) load_tile(r0 + T);   // in flight while the tile below is applied
+        if (wave == 0 && lane < (uint32_t)CW && live) {
+            const uint32_t n = min((uint32_t)T, d.rows - r0);
+            constexpr int B = 8;                  // LDS reads issued ahead of the dependent chain
+            for (uint32_t t = 0; t < n; t += B) {
+                V x[B];
+                int64_t dofs[B];
+#pragma unroll
+                for (int j = 0; j < B; ++j) {
+                    if (t + j < n) {
+                        int64_t so;
+                        row_offsets<LV>(d, d.row0 + r0 + t + j, so, dofs[j]);
+                        x[j] = tile[(t + j) * CW + lane];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < B; ++j) {
+                    if (t + j >= n) break;
+                    if (!held || dofs[j] != cur) {
+                        if (held) vstore<W, false>(d.dst + cur + xo, acc);
+                        cur = dofs[j];
+                        held = true;
+                        acc = x[j];
+                        if constexpr (OP::kReadsDst) acc = vload<W, false>(d.dst + cur + xo);
+                    }
+                    acc = op.template apply<W>(acc, x[j]);
+                }
+            }
+        }
+        __syncthreads();                          // the tile has been read
+        if (r0 + T < d.rows) store_tile();
+        __syncthreads();
+    }
+    if (held) vstore<W, false>(d.dst + cur + xo, acc);
+}
+
 // ---------------------------------------------------------------------------
 // host launch plumbing
 //
@@ -543,7 +643,32 @@ struct Plan {
     int W, U, BS;
     int variant;     // KK_ORDERED: 0 one workgroup, 1 column slices (pipelined), 2 column slices (in place)
     bool sys;        // KK_ROWS: source in a peer GPU's memory (system-scope loads)
+    int cw;          // variant 1: columns per workgroup of the LDS-staged kernel (0: one lane per column)
 };
+
+// LDS-staged column kernel: column slices per workgroup -- 64 when that still
+// gives >= 256 workgroups (one per CU), else the narrow form: one 128-byte line
+// per row segment (16 slices of 8 B, 32 of 4 B; a 16-byte element keeps 16).
+// Built for W = 4/8 and for 16-byte elements (W = 16); the column path never uses
+// 16-byte vectors for smaller elements, and W = 1/2 keep one lane per column.
+static int cols_per_group(uint32_t nvec, int W) {
+    if (W != 4 && W != 8 && W != 16) return 0;
+    if ((nvec + 63u) / 64u >= 256u) return 64;
+    return W == 4 ? 32 : 16;
+}
+
+template <class OP, int W, int LV>
+static void go_cols_lds(const Desc &d, const OP &op, int cw, uint64_t blocks, hipStream_t st) {
+    constexpr int NARROW = W == 4 ? 32 : 16;
+    if constexpr ((W == 4 || W == 8) || (W == 16 && OP::kElem == 16)) {
+        if (cw == 64)
+            hipLaunchKernelGGL((k_ordered_cols_lds<OP, W, LV, 64>), dim3((uint32_t)blocks), dim3(KC_NW * 64), 0, st, d,
+                               op);
+        else
+            hipLaunchKernelGGL((k_ordered_cols_lds<OP, W, LV, NARROW>), dim3((uint32_t)blocks), dim3(KC_NW * 64), 0,
+                               st, d, op);
+    }
+}
 
 // flat kernel shape: one-wave blocks of one 16-byte vector per lane (+3.5-5 % on
 // 128 B-1 KiB rows over 256 x 2, profiles/r01/sweep_flat_shape.jsonl); narrower
@@ -626,6 +751,11 @@ static hipError_t dispatch_w(const Plan &p, const Desc &d, const OP &op, uint64_
             return hipGetLastError();
         }
         if (p.kind == KK_ORDERED) {
+            if (p.variant == 1 && p.cw) {   // LDS-staged column slices
+                if (d.levels == 1) go_cols_lds<OP, W, 1>(d, op, p.cw, blocks, st);
+                else go_cols_lds<OP, W, 0>(d, op, p.cw, blocks, st);
+                return hipGetLastError();
+            }
             if (p.variant == 1 && d.levels == 1)   // 2-D: the row offset is one multiply
                 hipLaunchKernelGGL((k_ordered_cols<OP, W, true, 1>), dim3((uint32_t)blocks), dim3(64), 0, st, d, op);
             else if (p.variant == 1)
@@ -1071,6 +1201,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     p.BS = BS;
     p.sys = src_peer;
     p.variant = (kind == KK_ORDERED && cols) ? (ov == OV_COLS ? 1 : 2) : 0;
+    p.cw = (p.variant == 1 && tn.ordered_cols == 2 && (W <= 8 || esz == 16)) ? cols_per_group(d.nvec, W) : 0;
     const uint32_t per_chunk = (uint32_t)BS * (uint32_t)U;
     d.align_mask = 0;
     if (tn.align && kind == KK_ROWS && !src_peer && L <= 1 && d.nvec >= 2 * per_chunk) {
@@ -1107,7 +1238,8 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
             blocks = (d.items + per - 1) / per;
         } else {
             d.items = nr;
-            if (p.variant) blocks = (d.nvec + 63u) / 64u;   // one wave per 64 column slices
+            if (p.cw) blocks = (d.nvec + (uint32_t)p.cw - 1) / (uint32_t)p.cw;   // CW column slices per workgroup
+            else if (p.variant) blocks = (d.nvec + 63u) / 64u;                   // one wave per 64 column slices
         }
         if (blocks > lim) blocks = lim;
         if (!plan_only) {
@@ -1125,7 +1257,8 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         info->launches = launches;
         info->blocks = total_blocks;
         info->block = (kind == KK_ROWS) ? BS
-                      : (kind == KK_FLAT ? flat_block_threads(W) : ((kind == KK_ORDERED && !p.variant) ? kOrderedBS : 64));
+                      : (kind == KK_FLAT ? flat_block_threads(W)
+                                         : ((kind == KK_ORDERED && !p.variant) ? kOrderedBS : (p.cw ? KC_NW * 64 : 64)));
         info->levels = L;
         info->aligned = d.align_mask ? 1 : 0;
         info->sys = src_peer ? 1 : 0;

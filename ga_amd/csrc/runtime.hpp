@@ -238,6 +238,9 @@ void own_write_guard(const Span &dst);
 // op with no dependency (owner pulls from a peer GPU: one stream per source rank)
 int sched_pick(const Span &src, const Span &dst, uint64_t payload = 0, int prefer = -1);
 void sched_join();
+// sched_join before a launch that writes `dst` (own_write_guard first); a span of
+// unknown extent is Span{0, INT64_MAX}
+void sched_join_write(const Span &dst);
 void sched_sync_all();
 // completion marks (user thread): sequence number of an op just enqueued on
 // stream s; whether op `seq` of stream s has completed (waiting for it if `wait`)

@@ -186,6 +186,15 @@ void sched_join() {
     g_base = -1;
 }
 
+// A join before a launch on stream 0 that writes `dst` (host-side operands,
+// staged copies, wire unpacks): like sched_pick, it first takes this rank's
+// memory lock when dst may be one of its segments -- a same-GPU peer's one-pass
+// kernel may otherwise be writing the same bytes.
+void sched_join_write(const Span &dst) {
+    own_write_guard(dst);
+    sched_join();
+}
+
 void sched_sync_all() {
     Runtime &r = rt();
     // (polling hipStreamQuery instead measured the same ≈13 µs acc + fence

@@ -767,7 +767,12 @@ void wire_get_strided(uint64_t src, const int *ss, char *dst_dev, const int *ds,
         recv_all(p.fd, b.host, f.length);
         {
             std::lock_guard<std::mutex> g(r.launch_mu);
-            sched_join();
+            int64_t dlo = 0, dhi = 0;
+            side_span_host(ds, count, levels, (int64_t)rowb, &dlo, &dhi);
+            Span dsp;
+            dsp.lo = (int64_t)(uintptr_t)dst_dev + dlo;
+            dsp.hi = (int64_t)(uintptr_t)dst_dev + dhi;
+            sched_join_write(dsp);   // dst may be one of our segments
             const int rc = launch_strided(kOpCopy, nullptr, b.dev - (int64_t)rb * (int64_t)rowb, pstride, dst_dev, ds,
                                           count, levels, r.streams[0], nullptr, rb, re);
             if (rc) fatal("wire: unpack launch failed (%d)", rc);
@@ -848,7 +853,14 @@ void wire_get_iov(const uint64_t *src, const uint64_t *dst_dev, int n, int bytes
         d.n = (uint32_t)m;
         {
             std::lock_guard<std::mutex> g(r.launch_mu);
-            sched_join();
+            Span dsp;   // the listed destinations may lie in our segments
+            dsp.lo = INT64_MAX;
+            dsp.hi = 0;
+            for (int i = 0; i < m; ++i) {
+                dsp.lo = std::min(dsp.lo, (int64_t)dst_dev[i0 + i]);
+                dsp.hi = std::max(dsp.hi, (int64_t)dst_dev[i0 + i] + bytes);
+            }
+            sched_join_write(dsp);
             const int rc = launch_iov(kOpCopy, nullptr, d, dalign, false, r.streams[0]);
             if (rc) fatal("wire: io-vector scatter failed (%d)", rc);
         }

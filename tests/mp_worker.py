@@ -102,6 +102,8 @@ def main():
         c1_test(L, rank, size)
     elif mode == "onepass":
         one_pass_test(L, rank, size)
+    elif mode == "hostself":
+        host_self_test(L, rank, size)
     elif mode == "c5full":
         c5_full_test(L, rank, size)
     elif mode == "directsrc":
@@ -384,6 +386,64 @@ def one_pass_test(L, rank, size):
         assert r1["one_pass"] - r0["one_pass"] == rounds * (size - 1), (r0, r1)
     say(rank, f"one-pass exchange exact; routes {dict((k, r1[k] - r0[k]) for k in r1)}")
     src.free()
+    ga_amd.comex_barrier()
+    assert ga_amd.comex_free(seg[rank]) == 0
+    ga_amd.comex_finalize()
+
+
+def host_self_test(L, rank, size):
+    """an owner accumulating into its OWN block from pageable host
+    memory (the host-side route: its pages are registered for the call and the launch
+    joins every library stream) while same-GPU peers accumulate large device-buffer
+    patches into the same elements on the one-pass route (their kernels write the
+    owner's segment under the owner's memory lock).  The owner's host-side launch
+    must take its own memory lock too, or two read-modify-write kernels run on the
+    same bytes at once and updates are lost.  Every rank adds 2**rank into rank 0's
+    4 MiB block ROUNDS times with no barrier in between; each element must read
+    exactly ROUNDS * (2**size - 1)."""
+    import ga_amd
+    DBL = 38
+    assert ga_amd.comex_init() == 0
+    n = 1 << 19                               # 4 MiB of f64: every peer call >= 64 KiB (one-pass)
+    rounds = 24
+    seg = ga_amd.comex_malloc(n * 8, size)
+    zero = np.zeros(n)
+    assert L.comex_put(zero.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(seg[rank]), n * 8, rank, 0) == 0
+    ga_amd.comex_barrier()
+    one = ctypes.c_double(1.0)
+    r0 = ga_amd.route_counts()
+    if rank == 0:
+        for it in range(rounds):
+            # a fresh pageable buffer each time: registered for the call only
+            h = np.full(n, float(2 ** rank))
+            assert L.comex_acc(DBL, ctypes.byref(one), h.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(seg[0]),
+                               n * 8, 0, 0) == 0
+    else:
+        src = ga_amd.DeviceBuffer(n * 8)
+        ga_amd.fill_const(src.ptr, n * 8, float(2 ** rank))
+        ga_amd.sync()
+        handles = []
+        for it in range(rounds):
+            h = ctypes.c_int(-1)
+            assert L.comex_nbacc(DBL, ctypes.byref(one), ctypes.c_void_p(src.ptr), ctypes.c_void_p(seg[0]), n * 8,
+                                 0, 0, ctypes.byref(h)) == 0
+            handles.append(h)
+            if len(handles) > 4:
+                assert L.comex_wait(ctypes.byref(handles.pop(0))) == 0
+        for h in handles:
+            assert L.comex_wait(ctypes.byref(h)) == 0
+        src.free()
+    ga_amd.comex_barrier()
+    r1 = ga_amd.route_counts()
+    if rank == 0:
+        got = np.zeros(n)
+        assert L.comex_get(ctypes.c_void_p(seg[0]), got.ctypes.data_as(ctypes.c_void_p), n * 8, 0, 0) == 0
+        want = float(rounds * (2 ** size - 1))
+        bad = int(np.count_nonzero(got != want))
+        assert bad == 0, f"owner block: {bad} wrong, e.g. {got[np.nonzero(got != want)[0][0]]} != {want}"
+    elif one_pass_expected():
+        assert r1["one_pass"] - r0["one_pass"] == rounds, (r0, r1)
+    say(rank, "host-source self accumulates vs one-pass peers exact")
     ga_amd.comex_barrier()
     assert ga_amd.comex_free(seg[rank]) == 0
     ga_amd.comex_finalize()
