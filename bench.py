@@ -69,6 +69,12 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s device-resident 2-D strided f64 accumulate, 64 MiB patch; % HBM peak"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md chip table (8.0 TB/s)
+# xGMI: 7 links per MI355X at 153.6 GB/s each counting both directions (the task
+# brief's "7 links x ~153 GB/s"; MI355X_MICROARCH.md has no xGMI figure), so
+# 76.8 GB/s per link per direction.  An owner pulling its peers' contributions
+# (M2) is bound by the links INTO it: min(7, p - 1) x 76.8 GB/s.
+XGMI_LINKS = 7
+XGMI_LINK_GBS_PER_DIRECTION = 76.8
 DBL, DCP = 38, 41
 
 WORKLOADS = {
@@ -310,6 +316,7 @@ def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True
         region_ms, _ = event_region(L, step, steps, nxt + steps)
         avg_kernel_s = dist.max(region_ms / 1e3 / steps)
     routes = ga_amd.route_counts()
+    topology = ga_amd.device_topology()
     if src is not None:
         src.free()
     L.GA_Sync()
@@ -322,7 +329,8 @@ def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True
             + ("every rank the whole array (M2)" if exchange else f"own {rows}x{cols} block (M1)"))
     return dict(op=DBL, desc=desc, payload=payload, alg_bytes=3 * payload, elems=rows * cols, elapsed=elapsed,
                 avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), exchange=exchange,
-                steps=steps, block_bytes=block_bytes, array_bytes=dims[0] * dims[1] * 8, routes=routes)
+                steps=steps, block_bytes=block_bytes, array_bytes=dims[0] * dims[1] * 8, routes=routes,
+                topology=topology)
 
 
 def run_gpu(args, dist, finalize=True):
@@ -525,6 +533,7 @@ def run_gpu(args, dist, finalize=True):
     res["exchange"] = exchange
     res["self_packed"] = self_packed
     res["routes"] = routes
+    res["topology"] = ga_amd.device_topology()
     if finalize:
         ga_amd.comex_finalize()
     return res
@@ -553,9 +562,30 @@ def c5_extras(args, dist, wd=None):
         d = {"desc": r["desc"], "steps": steps, "ms_per_step": round(t * 1e3, 3),
              "GiB_per_s_job": round(p * r["alg_bytes"] / t / 2 ** 30, 1)}
         if exchange:
-            # each owner receives (p-1) blocks' worth of packed rows from its peers per step
-            xgmi = (p - 1) * r["block_bytes"]
-            d["xgmi_GBps_per_gpu"] = round(xgmi / t / 1e9, 1)
+            # each owner receives (p-1) blocks' worth of its peers' contributions per step
+            # (packed rows, or their sources read in place); they cross xGMI only when
+            # the ranks sit on different GPUs (say which)
+            inbound = (p - 1) * r["block_bytes"]
+            rate = inbound / t / 1e9
+            topo = r.get("topology") or {}
+            gpus, per_gpu = topo.get("gpus_on_node", 1), topo.get("ranks_on_gpu", p)
+            if gpus == p and topo.get("peer_loads") != "off":
+                links = min(XGMI_LINKS, p - 1)
+                peak = links * XGMI_LINK_GBS_PER_DIRECTION
+                d["xgmi_GBps_per_gpu"] = round(rate, 1)
+                d["roofline"] = {"bound": "xgmi", "achieved": round(rate, 1), "peak": round(peak, 1),
+                                 "unit": "GB/s", "frac": round(rate / peak, 4),
+                                 "peak_basis": f"{links} links into each owner x {XGMI_LINK_GBS_PER_DIRECTION} GB/s "
+                                               "per direction (153.6 GB/s per link, both directions)",
+                                 "achieved_basis": "(p-1) x owner block bytes per GPU per step / step time"}
+            else:
+                # ranks share GPUs: the peers' bytes are read from the same HBM, not over xGMI
+                d["inter_rank_GBps_per_gpu"] = round(rate, 1)
+                d["roofline"] = None
+                d["xgmi_note"] = (f"{p} ranks on {gpus} GPU(s) ({per_gpu} per GPU): "
+                                  + ("no byte crossed xGMI" if gpus == 1 else
+                                     "part of the traffic stays on one GPU") + "; no xGMI roofline")
+            d["devices_distinct"] = gpus
             d["note"] = ("whole-array accumulate by every rank; value counts 3 x payload of HBM-side traffic per rank; "
                          + ("the local buffer lies in the rank's comex segment: owners on other GPUs accumulate "
                             "straight from it (direct-source route, no pack); ranks sharing a GPU the one-pass route"
@@ -978,9 +1008,11 @@ def make_line(args, dist, r, ga_amd):
         "data": "synthetic (splitmix64, SURVEY.md 8(d)); device-resident src+dst, %d rotating buffer sets" % args.sets,
         "config": {"workload": args.workload, "patch": r["desc"], "payload_bytes": r["payload"],
                    "algorithmic_bytes_per_step": alg,
-                   "parallelism": (("GA_Acc of the whole array by every rank: pack + owner unpack-acc over xGMI"
+                   "parallelism": (("GA_Acc of the whole array by every rank: remote owners apply the "
+                                    "contributions (over xGMI when the ranks sit on different GPUs)"
                                     if args.workload == "C5" else
-                                    f"exchange x{n}: rank r -> rank r+1, pack + owner unpack-acc over xGMI")
+                                    f"exchange x{n}: rank r -> rank r+1 through the owner's route "
+                                    "(over xGMI when the ranks sit on different GPUs)")
                                    if r["exchange"] else f"owner-aligned x{n} (no collective)"),
                    "kernel": r["launch"]},
         "payload_GiB_per_s": round(value / (3 if r.get("xfer", "acc") == "acc" else 2), 2),
@@ -1004,6 +1036,16 @@ def make_line(args, dist, r, ga_amd):
                 else "comex_accs per step (blocking: returns after its kernel)"),
     }
     line["hip_runtime"] = ga_amd.lib().gaamd_hip_runtime().decode()
+    topo = r.get("topology")
+    if n > 1 and topo:
+        # how the ranks sat on the node's GPUs (a one-GPU rehearsal must not
+        # read as an xGMI run), the C5 entries say the same per measurement
+        line["topology"] = dict(topo, ranks=n)
+        if topo["ranks_on_gpu"] > 1:
+            line["roofline"]["note"] = (f"{topo['ranks_on_gpu']} ranks share each GPU: a rank's kernel time "
+                                        "includes the other ranks' traffic on the same HBM")
+    if n > 1:
+        line["cpu_baseline_note"] = "the CPU baseline is measured at N = 1 only (rank 0), per the bench contract"
     if r.get("region_profile"):
         line["value_region"] = r["region_profile"]   # host-clock marks inside the timed region
     if r.get("diag_regions"):

@@ -158,6 +158,16 @@ def kernel_counts():
     return {"rows": c[1], "flat": c[2], "serial": c[3], "ordered": c[4]}
 
 
+def device_topology():
+    """after comex_init: ranks on this rank's GPU (itself included), distinct GPUs among
+    this node's ranks, and the peer-load mode (0 auto, 1 all peers as other GPUs, 2 off)"""
+    a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    if lib().gaamd_device_topology(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)) != 0:
+        return None
+    return {"ranks_on_gpu": a.value, "gpus_on_node": b.value,
+            "peer_loads": {0: "auto", 1: "all", 2: "off"}.get(c.value, c.value)}
+
+
 def route_counts():
     """requests this rank posted to same-node owners, by route"""
     c = (ctypes.c_ulonglong * 4)()

@@ -295,3 +295,14 @@ extern "C" int gaamd_bootstrap_selftest(int rounds) {
 extern "C" int gaamd_rank(void) { return rt().rank; }
 extern "C" int gaamd_size(void) { return rt().size; }
 extern "C" int gaamd_device(void) { return rt().device; }
+
+extern "C" int gaamd_device_topology(int *ranks_on_gpu, int *gpus_on_node, int *peer_loads) {
+    Runtime &r = rt();
+    if (!r.initialized) return -1;
+    int same = 0;
+    for (uint8_t d : r.same_dev) same += d ? 1 : 0;
+    if (ranks_on_gpu) *ranks_on_gpu = same;
+    if (gpus_on_node) *gpus_on_node = r.node_gpus;
+    if (peer_loads) *peer_loads = r.peer_loads;
+    return 0;
+}

@@ -627,6 +627,14 @@ int comex_init() {
         r.same_dev.assign(r.size, 0);
         for (int q = 0; q < r.size; ++q)
             r.same_dev[q] = devs[q].node == r.node && !strcmp(devs[q].bus, mine_dev.bus);
+        r.node_gpus = 0;   // distinct bus ids among this node's ranks
+        for (int q = 0; q < r.size; ++q) {
+            if (devs[q].node != r.node) continue;
+            bool first = true;
+            for (int k = 0; k < q && first; ++k)
+                first = !(devs[k].node == r.node && !strcmp(devs[k].bus, devs[q].bus));
+            if (first) ++r.node_gpus;
+        }
         const char *pl = getenv("COMEX_AMD_PEER_LOADS");
         r.peer_loads = (pl && !strcmp(pl, "all")) ? 1 : ((pl && !strcmp(pl, "off")) ? 2 : 0);
         int peers = 0;   // same-node ranks whose memory is read as another GPU's

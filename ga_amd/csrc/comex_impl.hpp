@@ -79,8 +79,12 @@ char *remote_view(int owner, const void *p, int64_t lo, int64_t hi);
 bool src_segment_shared(const void *p, int64_t lo, int64_t hi, int t);
 // d meets one of our segments that same-GPU ranks may write (one-pass route)
 bool in_own_segment(const Span &d);
+// rank `owner`'s segment holding p (owner's address space): 0 none, 1 HBM, 2 host
+int segment_kind_of(int owner, const void *p);
 // the tag a rank writes into a new exported block (segments, the staging buffer)
 uint64_t seg_tag(int rank, uint64_t gen, int end);
+// the IPC handle table a stale mapping is reported against (rank, allocation number)
+void handle_seen(int rank, uint64_t gen, uint64_t base, uint64_t bytes, const hipIpcMemHandle_t &h);
 void *ipc_open(hipIpcMemHandle_t h, int q, const char *what);
 void ipc_close(void *mapped, int peer);
 // IPC handle of a fresh hipMalloc block *p (another block if the export is refused)

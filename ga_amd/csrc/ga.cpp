@@ -235,6 +235,14 @@ static long block_elems(const GArray &a, int proc, long *lo, long *hi) {
     return n;
 }
 
+// a rank's own block: HBM is zeroed on the device; a host segment (COMEX_AMD_SEGMENT=host)
+// the way pnga_zero does it, memset through the host pointer (global.nalg.c:94-129)
+static void zero_block(void *p, size_t bytes) {
+    if (!bytes) return;
+    if (segment_kind(p) == 2) memset(p, 0, bytes);
+    else GA_HIP(hipMemsetAsync(p, 0, bytes, rt().stream));
+}
+
 static int allocate(GArray &a) {
     Runtime &r = rt();
     long lo[GA_MAX_DIM], hi[GA_MAX_DIM];
@@ -244,7 +252,7 @@ static int allocate(GArray &a) {
     const long n = block_elems(a, r.rank, lo, hi);
     a.ptr.assign(r.size, nullptr);
     if (comex_malloc(a.ptr.data(), (size_t)n * a.elemsize, COMEX_GROUP_WORLD) != COMEX_SUCCESS) return 0;
-    if (n) GA_HIP(hipMemsetAsync(a.ptr[r.rank], 0, (size_t)n * a.elemsize, r.stream));
+    zero_block(a.ptr[r.rank], (size_t)n * a.elemsize);
     comex_barrier(COMEX_GROUP_WORLD);
     a.live = true;
     g_arrays.push_back(a);
@@ -651,7 +659,7 @@ void GA_Zero(int g_a) {
     // pnga_zero (global.nalg.c:60-90) is collective and syncs first: no rank may
     // zero its block while another still reads or writes it
     comex_barrier(COMEX_GROUP_WORLD);
-    if (n) GA_HIP(hipMemsetAsync(a.ptr[r.rank], 0, (size_t)n * a.elemsize, r.stream));
+    zero_block(a.ptr[r.rank], (size_t)n * a.elemsize);
     comex_barrier(COMEX_GROUP_WORLD);   // fences (syncs every library stream) + barrier
 }
 

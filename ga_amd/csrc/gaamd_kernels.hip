@@ -301,7 +301,7 @@ struct Desc2 {
     uint32_t align_mask;   // != 0: chunk boundaries at dst addresses = 0 mod (mask+1)
 };
 
-template <class OP, int W, int U, int BS>
+template <class OP, int W, int U, int BS, bool SYS = false>
 __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
     for (uint32_t w = blockIdx.x; w < d.items; w += gridDim.x) {
         const uint32_t rl = d.chunk_div.div(w);
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(BS) void k_rows2(const Desc2 d, const OP op) {
         const int64_t shift = (int64_t)(((uintptr_t)dp & d.align_mask) / W);
         const int64_t c0 = (int64_t)chunk * (BS * U) - shift;
         const bool full = c0 >= 0 && c0 + BS * U <= (int64_t)d.nvec;
-        chunk_op<OP, W, U, BS>(sp, dp, c0 + threadIdx.x, d.nvec, full, op);
+        chunk_op<OP, W, U, BS, SYS>(sp, dp, c0 + threadIdx.x, d.nvec, full, op);
     }
 }
 
@@ -332,7 +332,9 @@ struct Desc2D {
     uint32_t row0;
 };
 
-template <class OP, int W, int BS>
+// SYS: the source lies in a peer GPU's memory (the owner's direct-source route):
+// one system-scope load per lane, issued after the local dst load (vload_sys)
+template <class OP, int W, int BS, bool SYS = false>
 __global__ __launch_bounds__(BS) void k_rows2d(const Desc2D d, const OP op) {
     const uint32_t w = blockIdx.x;
     const uint32_t rl = d.chunk_div.div(w);
@@ -341,8 +343,16 @@ __global__ __launch_bounds__(BS) void k_rows2d(const Desc2D d, const OP op) {
     const int64_t v = (int64_t)chunk * BS + threadIdx.x;
     const char *sp = d.src + r * d.s_str + v * W;
     char *dp = d.dst + r * d.d_str + v * W;
-    typename Vec<W>::T a = vload<W, true>(sp), b = a;
-    if constexpr (OP::kReadsDst) b = vload<W, true>(dp);
+    typename Vec<W>::T a, b;
+    if constexpr (SYS) {
+        if constexpr (OP::kReadsDst) b = vload<W, true>(dp);
+        a = vload_sys<W>(sp);
+        if constexpr (!OP::kReadsDst) b = a;
+    } else {
+        a = vload<W, true>(sp);
+        b = a;
+        if constexpr (OP::kReadsDst) b = vload<W, true>(dp);
+    }
     vstore<W, true>(dp, op.template apply<W>(b, a));
 }
 
@@ -681,7 +691,7 @@ template <int W> struct DefaultU { static constexpr int value = W == 16 ? 1 : (W
 static int unroll_for(int W) { return W >= 16 ? 1 : 16 / W; }
 constexpr int kSysBS = 256;   // peer-source rows kernel block
 
-template <class OP, int W, int BS>
+template <class OP, int W, int BS, bool SYS = false>
 static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, hipStream_t st) {
     constexpr int U = DefaultU<W>::value;
     Desc2 e;
@@ -705,11 +715,11 @@ static hipError_t go_rows2(const Desc &d, const OP &op, uint64_t blocks, hipStre
             f.d_str = e.d_str;
             f.chunk_div = d.chunk_div;
             f.row0 = d.row0;
-            hipLaunchKernelGGL((k_rows2d<OP, W, BS>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
+            hipLaunchKernelGGL((k_rows2d<OP, W, BS, SYS>), dim3((uint32_t)blocks), dim3(BS), 0, st, f, op);
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((k_rows2<OP, W, U, BS>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
+    hipLaunchKernelGGL((k_rows2<OP, W, U, BS, SYS>), dim3((uint32_t)blocks), dim3(BS), 0, st, e, op);
     return hipGetLastError();
 }
 
@@ -767,6 +777,12 @@ static hipError_t dispatch_w(const Plan &p, const Desc &d, const OP &op, uint64_
             return hipGetLastError();
         }
         if (p.sys) {
+            // <= 1 stride level (GA 2-D patches, packed chunks): the 2-D kernels with
+            // system-scope source loads; deeper patches the generic rows kernel
+            if (d.levels <= 1) {
+                if (p.BS == 64) return go_rows2<OP, W, 64, true>(d, op, blocks, st);
+                return go_rows2<OP, W, 128, true>(d, op, blocks, st);
+            }
             hipLaunchKernelGGL((k_rows<OP, W, DefaultU<W>::value, kSysBS, 0, true>), dim3((uint32_t)blocks),
                                dim3(kSysBS), 0, st, d, op);
             return hipGetLastError();
@@ -1194,7 +1210,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         block = (al & 4095) ? 128 : 64;
     }
     // the (U, BS) the dispatcher will pick -- chunking must agree with it
-    const int U = unroll_for(W), BS = src_peer ? kSysBS : block;
+    const int U = unroll_for(W), BS = (src_peer && L > 1) ? kSysBS : block;
     p.kind = kind;
     p.W = W;
     p.U = U;
@@ -1204,7 +1220,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     p.cw = (p.variant == 1 && tn.ordered_cols == 2 && (W <= 8 || esz == 16)) ? cols_per_group(d.nvec, W) : 0;
     const uint32_t per_chunk = (uint32_t)BS * (uint32_t)U;
     d.align_mask = 0;
-    if (tn.align && kind == KK_ROWS && !src_peer && L <= 1 && d.nvec >= 2 * per_chunk) {
+    if (tn.align && kind == KK_ROWS && L <= 1 && d.nvec >= 2 * per_chunk) {
         d.align_mask = per_chunk * (uint32_t)W - 1;   // a chunk spans per_chunk*W bytes
         // rows whose start is not chunk-aligned need one more (partial) chunk
         bool any = ((uintptr_t)dst & d.align_mask) != 0;
@@ -1231,7 +1247,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         if (kind == KK_ROWS) {
             d.items = nr * d.chunks;
             blocks = d.items;
-            if (src_peer && blocks > 65536) blocks = 65536;   // grid-stride loop
+            if (src_peer && L > 1 && blocks > 65536) blocks = 65536;   // grid-stride loop
         } else if (kind == KK_FLAT) {
             d.items = nr * d.nvec;
             const uint64_t per = flat_block_items(W);

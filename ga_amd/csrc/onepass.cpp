@@ -244,6 +244,9 @@ bool one_pass_acc(int t, int op, void *scale, void *src, const int *ss, void *ds
     memset(&at, 0, sizeof(at));
     if (hipPointerGetAttributes(&at, src) == hipSuccess && at.type == hipMemoryTypeHost) return false;
     (void)hipGetLastError();
+    // HBM segments only: a host segment's owner keeps no memory lock (own_write_guard
+    // covers its HBM segments), so accumulates into it go through the owner
+    if (segment_kind_of(t, (const char *)dst + dlo) != 1) return false;
     char *dview = remote_view(t, dst, dlo, dhi);
     fence_target(t);   // our earlier packed chunks / direct-source requests to t are applied first
     std::atomic<uint32_t> &lk = r.shm->mem_lock[r.li(t)];

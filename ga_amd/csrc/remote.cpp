@@ -826,6 +826,7 @@ void remote_init() {
     boot_allgather(&mine, buf.data(), sizeof(mine));
     all = reinterpret_cast<decltype(all)>(buf.data());
     r.peer_staging.assign(r.size, nullptr);
+    for (int q = 0; q < r.size; ++q) handle_seen(q, 0, 0, all[q].bytes, all[q].h);   // allocation 0: staging
     for (int q = 0; q < r.size; ++q) {
         if (q == r.rank) { r.peer_staging[q] = r.staging; continue; }
         if (!r.same_node(q)) continue;   // another node: reached through wire.cpp

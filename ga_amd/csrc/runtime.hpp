@@ -113,13 +113,18 @@ struct Span {
 struct PeerMap {
     uintptr_t base = 0;   // segment address in the owner's address space
     size_t bytes = 0;
-    char *mapped = nullptr;   // same bytes as seen from this process
+    char *mapped = nullptr;   // same bytes as seen from this process (device-accessible)
     bool member = false;      // the rank took part in the segment's comex_malloc
+    // host segments: this process's mapping of the owner's node shm object (page-
+    // rounded bytes), registered with HIP; `mapped` is its device view (the same
+    // address: do_malloc checks it)
+    char *host_map = nullptr;
+    size_t map_bytes = 0;
 };
 
 struct Segment {
     bool live = false;
-    bool device = true;
+    bool device = true;          // HBM (IPC-exported) or a host segment in node shm
     void *local = nullptr;
     size_t local_bytes = 0;      // bytes of the local block
     bool exported = false;       // `handle` is the local block's IPC export
@@ -203,6 +208,7 @@ struct Runtime {
     // COMEX_AMD_PEER_LOADS: auto (default: per device), all (every other rank's
     // memory as if on another GPU -- exercises that path on one GPU), off.
     std::vector<uint8_t> same_dev;
+    int node_gpus = 1;                  // distinct physical GPUs among this node's ranks
     int peer_loads = 0;                 // 0 auto, 1 all, 2 off
     bool peer_src(int q) const {
         if (q == rank || peer_loads == 2) return false;
@@ -275,7 +281,9 @@ uint64_t rmw_local(int swap, void *addr, int bytes, uint64_t val);
 bool mutex_try_local(int owner, int mutex);
 void mutex_release_local(int owner, int mutex);
 bool segment_of_rank(int owner, uint64_t p, int64_t lo, int64_t hi);   // comex.cpp (reg_cache_find)
-bool segment_local(const void *p, int64_t lo, int64_t hi);              // comex.cpp
+bool segment_local(const void *p, int64_t lo, int64_t hi);              // segments.cpp
+// 0: not in one of our segments, 1: in an HBM segment, 2: in a host (node shm) segment
+int segment_kind(const void *p);
 // comex.cpp: the device-address history a refused IPC export prints (kind: a alloc,
 // f free, x export, o IPC map, c IPC unmap; peer = the other rank, -1 none)
 void addr_event(char kind, const void *p, size_t bytes, int peer);

@@ -14,6 +14,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <deque>
 #include <mutex>
 #include <algorithm>
@@ -205,13 +208,19 @@ void export_alloc(void **p, size_t bytes, hipIpcMemHandle_t *h, const char *what
 }
 
 // Freed device segments are kept for the next comex_malloc of the same size, with
-// their IPC export, instead of going back to hipFree (COMEX_AMD_SEGMENT_CACHE_MB,
-// default 16 GiB per rank; 0 disables).  GA creates and destroys arrays of the same
-// shapes over and over; every hipFree + hipMalloc + export cycle recycles addresses
-// and descriptors, and the runtime refuses, now and then, to export a fresh block at
-// a recycled address (profiles/r03/s19, s20, s27-s29: 1-4 refusals in most runs of
-// eight ranks on one GPU).  A cached block is exported once, for good, and a reused
-// one is opened again by the peers from the same handle.
+// their IPC export, instead of going back to hipFree.  GA creates and destroys
+// arrays of the same shapes over and over; every hipFree + hipMalloc + export cycle
+// recycles addresses and descriptors, and the runtime refuses, now and then, to
+// export a fresh block at a recycled address (profiles/r03/s19, s20, s27-s29: 1-4
+// refusals in most runs of eight ranks on one GPU).  A cached block is exported
+// once, for good, and a reused one is opened again by the peers from the same
+// handle.  The cache must not starve other allocators: its default cap
+// is an eighth of the device's memory shared among the ranks on that GPU (at most
+// 16 GiB; COMEX_AMD_SEGMENT_CACHE_MB overrides, 0 disables), and it is given back
+// -- by every rank of the GPU, each seeing the device's free memory -- whenever a
+// new segment would leave less than COMEX_AMD_SEGMENT_FREE_MIN_MB free (default
+// 1/16 of the device), before a freed block would be cached below that watermark,
+// and when any allocation of this library fails.
 struct CachedBlock {
     void *p;
     size_t bytes;
@@ -222,11 +231,45 @@ static std::deque<CachedBlock> g_blocks;   // oldest first
 static size_t g_blocks_bytes = 0;
 static std::atomic<unsigned long long> g_block_reuse{0};
 static std::atomic<unsigned long long> g_remapped{0};   // segments replaced after a stale peer mapping
+static std::atomic<unsigned long long> g_cache_trims{0};   // cache given back under memory pressure
+
+static size_t device_total() {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return tot;
+}
+
+static size_t device_free() {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return fr;
+}
+
+static int ranks_on_this_gpu() {
+    int n = 0;
+    for (uint8_t d : rt().same_dev) n += d ? 1 : 0;
+    return n > 0 ? n : 1;
+}
 
 static size_t block_cache_cap() {
     static const size_t v = [] {
-        const char *e = getenv("COMEX_AMD_SEGMENT_CACHE_MB");
-        return (size_t)(e ? atof(e) : 16384.0) << 20;
+        if (const char *e = getenv("COMEX_AMD_SEGMENT_CACHE_MB")) return (size_t)atof(e) << 20;
+        const size_t share = device_total() / 8 / (size_t)ranks_on_this_gpu();
+        return std::min<size_t>(share, 16ull << 30);
+    }();
+    return v;
+}
+
+static size_t free_watermark() {
+    static const size_t v = [] {
+        if (const char *e = getenv("COMEX_AMD_SEGMENT_FREE_MIN_MB")) return (size_t)atof(e) << 20;
+        return device_total() / 16;
     }();
     return v;
 }
@@ -244,8 +287,13 @@ static void block_flush() {
 
 static void block_put(void *p, size_t bytes, bool exported, const hipIpcMemHandle_t &h) {
     const size_t cap = block_cache_cap();
-    if (bytes > cap) {
+    if (bytes > cap || device_free() < free_watermark()) {
+        // too big to keep, or the device is short of memory: give it back now
         block_free_one({p, bytes, exported, h});
+        if (!g_blocks.empty() && device_free() < free_watermark()) {
+            g_cache_trims.fetch_add(1, std::memory_order_relaxed);
+            block_flush();
+        }
         return;
     }
     while (g_blocks_bytes + bytes > cap && !g_blocks.empty()) {
@@ -273,17 +321,128 @@ static bool block_take(size_t bytes, void **p, bool *exported, hipIpcMemHandle_t
     return false;
 }
 
+// Before a new device segment of `bytes` per rank: every rank of this GPU makes
+// the same call at the same point of the collective comex_malloc and sees the
+// same device-wide free memory, so when the GPU's ranks together would drop below
+// the watermark each one gives its cache back -- another rank's allocation (or the
+// application's) is not refused for memory this library only keeps for reuse.
+static void block_trim_for(size_t bytes) {
+    if (g_blocks.empty()) return;
+    const size_t need = bytes * (size_t)ranks_on_this_gpu() + free_watermark();
+    if (device_free() < need) {
+        g_cache_trims.fetch_add(1, std::memory_order_relaxed);
+        block_flush();
+    }
+}
+
 // hipMalloc, giving the cached blocks back first when the device is full
 static void *device_alloc(size_t bytes) {
     void *p = nullptr;
     hipError_t e = hipMalloc(&p, bytes);
     if (e == hipErrorOutOfMemory && !g_blocks.empty()) {
         (void)hipGetLastError();
+        g_cache_trims.fetch_add(1, std::memory_order_relaxed);
         block_flush();
         e = hipMalloc(&p, bytes);
     }
     if (e != hipSuccess) fatal("hipMalloc of %zu bytes failed: %s", bytes, hipGetErrorString(e));
     return p;
+}
+
+// ---- IPC handle table ------------------------------------
+// Every IPC handle this process exported or was handed (a segment's, a staging
+// buffer's): whose, which allocation (the tag number), the owner's base and size,
+// and the handle's 64 bytes.  A mapping that fails its tag check is reported with
+// its handle and every earlier handle with the same bytes, and with the handle of
+// the allocation its tags say it reached -- which earlier export, and whose, it
+// really resolved to.
+struct HandleSeen {
+    int rank;
+    uint64_t gen, base, bytes;
+    hipIpcMemHandle_t h;
+};
+static std::mutex g_hs_mu;
+static std::deque<HandleSeen> g_handles;   // newest last, at most 4096
+
+static uint64_t handle_hash(const hipIpcMemHandle_t &h) {
+    uint64_t x = 1469598103934665603ull;
+    const unsigned char *b = reinterpret_cast<const unsigned char *>(&h);
+    for (size_t i = 0; i < sizeof(h); ++i) x = (x ^ b[i]) * 1099511628211ull;
+    return x;
+}
+
+void handle_seen(int rank, uint64_t gen, uint64_t base, uint64_t bytes, const hipIpcMemHandle_t &h) {
+    std::lock_guard<std::mutex> g(g_hs_mu);
+    g_handles.push_back({rank, gen, base, bytes, h});
+    if (g_handles.size() > 4096) g_handles.pop_front();
+}
+
+static void print_handle(const char *what, const hipIpcMemHandle_t &h) {
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(&h);
+    fprintf(stderr, "[ga_amd %d]     %s (hash %016llx):", rt().rank, what, (unsigned long long)handle_hash(h));
+    for (size_t i = 0; i < sizeof(h) / 8; ++i) fprintf(stderr, " %016llx", (unsigned long long)w[i]);
+    fprintf(stderr, "\n");
+}
+
+// a stale mapping of rank q's segment (its handle h, allocation gen) read `tag`
+static void report_stale(int q, uint64_t gen, uint64_t base, uint64_t bytes, const hipIpcMemHandle_t &h,
+                         uint64_t tag) {
+    std::lock_guard<std::mutex> g(g_hs_mu);
+    const uint64_t x = tag ^ seg_tag(0, 0, 0);
+    const int trank = (int)(x >> 40);
+    const uint64_t tgen = (x & ((1ull << 40) - 1)) >> 1;
+    const bool is_tag = (x >> 40) < (uint64_t)kMaxRanks * 64 && !(x & 1);
+    fprintf(stderr, "[ga_amd %d]   stale mapping of rank %d's allocation %llu (base %#llx, %llu B): it reads ",
+            rt().rank, q, (unsigned long long)gen, (unsigned long long)base, (unsigned long long)bytes);
+    if (is_tag) fprintf(stderr, "the tag of rank %d's allocation %llu\n", trank, (unsigned long long)tgen);
+    else fprintf(stderr, "no tag (%#llx)\n", (unsigned long long)tag);
+    print_handle("handle opened", h);
+    const uint64_t hh = handle_hash(h);
+    int same = 0;
+    for (const HandleSeen &e : g_handles) {
+        if (handle_hash(e.h) == hh && !(e.rank == q && e.gen == gen)) {
+            fprintf(stderr, "[ga_amd %d]     equal to the handle rank %d sent for its allocation %llu (base %#llx, "
+                    "%llu B)\n", rt().rank, e.rank, (unsigned long long)e.gen, (unsigned long long)e.base,
+                    (unsigned long long)e.bytes);
+            ++same;
+        }
+        if (is_tag && e.rank == trank && e.gen == tgen) print_handle("handle of the allocation it reached", e.h);
+    }
+    if (!same) fprintf(stderr, "[ga_amd %d]     no earlier handle has the same bytes\n", rt().rank);
+}
+
+// ---- host segments in node shared memory ----------------
+// COMEX_AMD_SEGMENT=host / comex_malloc_mem_dev(..., "host"): the reference's own
+// segment kind -- a POSIX shm object per rank, mmap'ed by every rank of the node
+// (_comex_malloc_local / _shm_attach, comex.c:1465-1524, 4968-5290) -- registered
+// with HIP in every process that maps it, so kernels on any of the node's GPUs reach
+// it through a device pointer and the host can touch it directly: GA's host-side
+// local operations (pnga_access_ptr + memset in pnga_zero, global.nalg.c:94-129)
+// work on it.  Registered host memory is fine-grained (PCIe / system memory), so it
+// needs no cache maintenance between a host write and a peer's kernel.
+static size_t page_round(size_t n) { return (n + (size_t)kPage - 1) & ~(size_t)(kPage - 1); }
+
+static char *shm_map_registered(const char *name, size_t map_bytes, bool create) {
+    const int fd = shm_open(name, O_RDWR | (create ? (O_CREAT | O_EXCL) : 0), 0600);
+    if (fd < 0) fatal("host segment: shm_open(%s) failed: %s", name, strerror(errno));
+    if (create && ftruncate(fd, (off_t)map_bytes) != 0) fatal("host segment: ftruncate(%s) failed", name);
+    void *p = mmap(nullptr, map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) fatal("host segment: mmap(%s, %zu) failed: %s", name, map_bytes, strerror(errno));
+    GA_HIP(hipHostRegister(p, map_bytes, hipHostRegisterMapped));
+    void *d = nullptr;
+    GA_HIP(hipHostGetDevicePointer(&d, p, 0));
+    // every address computation of the library (a rank's own segment addresses,
+    // the owner addresses in requests) assumes the device view of this process's
+    // mapping is the mapping itself, as it is for registered memory on this runtime
+    if (d != p) fatal("host segment: the device view %p of registered memory differs from its address %p", d, p);
+    return (char *)p;
+}
+
+static void shm_unmap_registered(char *p, size_t map_bytes) {
+    if (!p) return;
+    (void)hipHostUnregister(p);
+    munmap(p, map_bytes);
 }
 
 // Every segment gets a per-rank, per-allocation tag in its first and last 8 bytes
@@ -295,7 +454,6 @@ static void *device_alloc(size_t bytes) {
 // with no error anywhere.  A mapping that does not read the tags is therefore
 // closed, the owner's block set aside (quarantined) and replaced, and the exchange
 // repeated (all ranks, collectively), up to 4 times.
-
 static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool device) {
     ensure_init();
     Runtime &r = rt();
@@ -304,13 +462,21 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     const std::vector<int> members = group_members(group);
     const bool trace = r.debug >= 2;
     if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc(%zu, group %d): enter\n", r.rank, bytes, group);
-    struct Info { uint64_t base, bytes; hipIpcMemHandle_t h; int32_t device, pad; uint64_t gen; } mine;
+    struct Info {
+        uint64_t base, bytes;
+        hipIpcMemHandle_t h;
+        int32_t device, host;    // host: a node shm segment, `name` below
+        uint64_t gen;
+        char name[64];
+    } mine;
     memset(&mine, 0, sizeof(mine));
-    static uint64_t gen = 0;   // this rank's allocation counter (the tags)
+    static uint64_t gen = 0;   // this rank's allocation counter (the tags, the shm names)
     void *p = nullptr;
     bool exported = false;
+    const size_t map_bytes = page_round(bytes);
     if (bytes) {
         if (device) {
+            block_trim_for(bytes);
             if (!block_take(bytes, &p, &exported, &mine.h)) {
                 p = device_alloc(bytes);
                 addr_event('a', p, bytes, -1);
@@ -327,7 +493,11 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
                 exported = true;
             }
         } else {
-            GA_HIP(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
+            const char *job = getenv("COMEX_AMD_JOBID");
+            snprintf(mine.name, sizeof(mine.name), "/gaamd_seg_%d_%d_%s_%d_%llu", (int)getuid(), (int)getpid(),
+                     job ? job : "0", r.rank, (unsigned long long)(gen + 1));
+            p = shm_map_registered(mine.name, map_bytes, true);
+            mine.host = 1;
         }
     }
     const bool tagged = device && bytes >= 16;
@@ -351,13 +521,19 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         for (size_t k = 0; k < members.size(); ++k) {
             all[members[k]] = gathered[k];
             ptr_arr[k] = (void *)(uintptr_t)gathered[k].base;
+            if (gathered[k].bytes && !gathered[k].host)
+                handle_seen(members[k], gathered[k].gen, gathered[k].base, gathered[k].bytes, gathered[k].h);
         }
-        // open, and check that each mapping reads its owner's tags
+        // open, and check that each IPC mapping reads its owner's tags
         std::vector<uint8_t> stale(r.size, 0);
         for (int q = 0; q < r.size; ++q) {
             mapped[q] = nullptr;
             if (q == r.rank || !all[q].bytes || !r.same_node(q)) continue;
-            if (!device) fatal("host-memory segments are rank-private (use device segments for remote access)");
+            if (all[q].host) {   // a host segment: map the owner's shm object
+                all[q].name[sizeof(all[q].name) - 1] = 0;
+                mapped[q] = shm_map_registered(all[q].name, page_round(all[q].bytes), false);
+                continue;
+            }
             mapped[q] = ipc_open(all[q].h, q, "segment");
             if (!mapped[q] || all[q].bytes < 16) continue;
             uint64_t t[2] = {0, 0};
@@ -369,6 +545,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
                         "reads %#llx / %#llx, not its tags: another allocation's memory\n", r.rank, q,
                         (size_t)all[q].bytes, (void *)(uintptr_t)all[q].base, (unsigned long long)t[0],
                         (unsigned long long)t[1]);
+                report_stale(q, all[q].gen, all[q].base, all[q].bytes, all[q].h, t[0]);
             }
         }
         std::vector<uint8_t> seen(members.size() * (size_t)r.size);
@@ -386,6 +563,9 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
             if (mapped[q]) ipc_close(mapped[q], q);
         if (mine_stale) {
             // set the block aside for good and export a fresh one
+            fprintf(stderr, "[ga_amd %d]   my new segment's mapping was stale; its handle and address history:\n",
+                    r.rank);
+            print_handle("handle exported", mine.h);
             addr_history(p, bytes);
             g_quarantine.push_back(p);
             p = device_alloc(bytes);
@@ -408,6 +588,10 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         s.peer[q].base = all[q].base;
         s.peer[q].bytes = all[q].bytes;
         s.peer[q].mapped = q == r.rank ? (char *)p : (char *)mapped[q];
+        if (all[q].host && s.peer[q].mapped) {
+            s.peer[q].host_map = s.peer[q].mapped;
+            s.peer[q].map_bytes = page_round(all[q].bytes);
+        }
     }
     {
         std::lock_guard<std::mutex> g(r.seg_mu);
@@ -415,10 +599,32 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     }
     if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: peers mapped, barrier\n", r.rank);
     members_barrier(members, group);
+    // every member has mapped the shm object: its name can go (the mappings stay)
+    if (!device && bytes) shm_unlink(mine.name);
     if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: done\n", r.rank);
     return COMEX_SUCCESS;
 }
 
+// close this process's view of a segment's peer q (IPC mapping or shm mapping)
+static void close_peer(PeerMap &m, int q) {
+    if (m.host_map) shm_unmap_registered(m.host_map, m.map_bytes);
+    else if (m.mapped) ipc_close(m.mapped, q);
+    m.mapped = m.host_map = nullptr;
+}
+
+int segment_kind_of(int owner, const void *p) {
+    Runtime &r = rt();
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> g(r.seg_mu);
+    for (const Segment &s : r.segs) {
+        if (!s.live || s.peer.empty()) continue;
+        const PeerMap &m = s.peer[owner];
+        if (m.bytes && a >= m.base && a < m.base + m.bytes) return s.device ? 1 : 2;
+    }
+    return 0;
+}
+
+int segment_kind(const void *p) { return segment_kind_of(rt().rank, p); }
 
 // comex_finalize, after the last barrier: every live segment's mappings closed and
 // its block freed, then the cached and quarantined blocks
@@ -427,9 +633,10 @@ void segments_finalize() {
     for (Segment &s : r.segs) {
         if (!s.live) continue;
         for (int q = 0; q < (int)s.peer.size(); ++q)
-            if (q != r.rank && s.peer[q].mapped) ipc_close(s.peer[q].mapped, q);
+            if (q != r.rank) close_peer(s.peer[q], q);
         if (s.local && s.device) addr_event('f', s.local, s.peer[r.rank].bytes, -1);
-        if (s.local) (void)(s.device ? hipFree(s.local) : hipHostFree(s.local));
+        if (s.local && s.device) (void)hipFree(s.local);
+        else if (s.local) shm_unmap_registered((char *)s.local, s.peer[r.rank].map_bytes);
         s.live = false;
     }
     r.segs.clear();
@@ -472,7 +679,7 @@ int comex_free(void *ptr, comex_group_t group) {
     members_barrier(members, group);   // nobody still reads the segment
     void *local = nullptr;
     bool device = true, found = false, exported = false;
-    size_t local_bytes = 0;
+    size_t local_bytes = 0, local_map_bytes = 0;
     hipIpcMemHandle_t handle;
     memset(&handle, 0, sizeof(handle));
     {
@@ -483,9 +690,10 @@ int comex_free(void *ptr, comex_group_t group) {
             for (int q = 0; q < r.size; ++q) if (s.peer[q].base != all[q]) { match = false; break; }
             if (!match) continue;
             for (int q = 0; q < r.size; ++q)
-                if (q != r.rank && s.peer[q].mapped) ipc_close(s.peer[q].mapped, q);
+                if (q != r.rank) close_peer(s.peer[q], q);
             local = s.local;
             device = s.device;
+            local_map_bytes = s.peer[r.rank].map_bytes;
             local_bytes = s.local_bytes;
             exported = s.exported;
             if (exported) handle = s.handle;
@@ -505,7 +713,7 @@ int comex_free(void *ptr, comex_group_t group) {
         if (block_cache_cap()) block_put(local, local_bytes, exported, handle);   // kept for the next comex_malloc
         else block_free_one({local, local_bytes, exported, handle});
     } else if (local) {
-        GA_HIP(hipHostFree(local));
+        shm_unmap_registered((char *)local, local_map_bytes);
     }
     return COMEX_SUCCESS;
 }
@@ -528,5 +736,7 @@ int comex_free_local(void *ptr) {
 
 unsigned long long gaamd_segment_cache_reuse(void) { return g_block_reuse.load(); }
 unsigned long long gaamd_segment_remaps(void) { return g_remapped.load(); }
+unsigned long long gaamd_segment_cache_trims(void) { return g_cache_trims.load(); }
+int gaamd_segment_kind(const void *p) { return rt().initialized ? segment_kind(p) : 0; }
 
 }  // extern "C"

@@ -49,6 +49,12 @@ int gaamd_rank(void);
 int gaamd_size(void);
 /* HIP device of this rank after comex_init (COMEX_AMD_DEVICE or local rank mod devices) */
 int gaamd_device(void);
+/* after comex_init: ranks (this one included) whose HIP device is this rank's physical
+   GPU (PCI bus id), distinct GPUs among the ranks of this node, and the peer-load mode
+   (COMEX_AMD_PEER_LOADS: 0 auto -- peers on other GPUs read with system-scope loads,
+   1 all -- every peer treated as another GPU, 2 off).  Lets a caller say whether its
+   remote traffic crossed xGMI. */
+int gaamd_device_topology(int *ranks_on_gpu, int *gpus_on_node, int *peer_loads);
 /* nodes: ranks sharing a host (or the same COMEX_AMD_NODE value) map each other's
    HBM; ranks on different nodes exchange the MPI-PR messages over TCP (wire.cpp).
    After bootstrap: this rank's node index, the node count, ranks on this node. */
@@ -107,6 +113,11 @@ unsigned long long gaamd_one_pass_count(void);
 unsigned long long gaamd_segment_cache_reuse(void);
 /* segments this rank replaced because a peer's fresh IPC mapping did not read their tags */
 unsigned long long gaamd_segment_remaps(void);
+/* times the freed-segment cache was given back under device-memory pressure */
+unsigned long long gaamd_segment_cache_trims(void);
+/* the kind of this rank's segment holding p: 0 none, 1 HBM, 2 host (node shm,
+   COMEX_AMD_SEGMENT=host: the host may read and write it directly) */
+int gaamd_segment_kind(const void *p);
 /* same-node peers whose staging buffer this rank could not map by IPC at
  * comex_init (remote accumulates to or from them would abort); -1 before init */
 int gaamd_peers_unmapped(void);

@@ -104,6 +104,8 @@ def main():
         one_pass_test(L, rank, size)
     elif mode == "hostself":
         host_self_test(L, rank, size)
+    elif mode == "hostseg-ga":
+        host_segment_ga_test(L, rank, size)
     elif mode == "c5full":
         c5_full_test(L, rank, size)
     elif mode == "directsrc":
@@ -449,6 +451,92 @@ def host_self_test(L, rank, size):
     ga_amd.comex_finalize()
 
 
+def host_segment_ga_test(L, rank, size):
+    """VERDICT r3 item 3, run with COMEX_AMD_SEGMENT=host: GA partitions in host
+    segments (one POSIX shm object per rank, mapped and HIP-registered by every rank
+    of the node), which GA's global/src dereferences on the host -- pnga_zero takes
+    pnga_access_ptr and memsets the block (global.nalg.c:94-129).  Each rank fills its
+    block on the HOST through NGA_Access; every rank reads the whole array back with
+    NGA_Get (remote gets from other ranks' host segments); every rank NGA_Acc's the
+    whole array (remote accumulates into host segments, applied by their owners) and
+    each owner checks its block on the host; then each rank zeroes its block with a
+    host memset through NGA_Access, exactly as pnga_zero, and the peers' NGA_Get must
+    see zeros.  Integer-valued f64: exact."""
+    import ga_amd
+    ia = ga_amd.int_array
+    C_DBL = 1004
+    n, m = 1000, 700
+    assert L.GA_Initialize() == 0
+    g = L.NGA_Create(C_DBL, 2, ia([n, m]), b"hostseg", None)
+    assert g > 0
+    los, his = [], []
+    for q in range(size):
+        lo_, hi_ = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
+        L.NGA_Distribution(g, q, lo_, hi_)
+        los.append(list(lo_))
+        his.append(list(hi_))
+    blo, bhi = ia(los[rank]), ia(his[rank])
+    rows, cols = his[rank][0] - los[rank][0] + 1, his[rank][1] - los[rank][1] + 1
+
+    def access():
+        ptr, ld = ctypes.c_void_p(), (ctypes.c_int * 1)()
+        L.NGA_Access(g, blo, bhi, ctypes.byref(ptr), ld)
+        assert ld[0] == cols, (ld[0], cols)
+        assert L.gaamd_segment_kind(ptr) == 2, "the GA block is not in a host segment"
+        return np.ctypeslib.as_array((ctypes.c_double * (rows * cols)).from_address(ptr.value)).reshape(rows, cols)
+
+    def init_of(q):
+        r_, c_ = his[q][0] - los[q][0] + 1, his[q][1] - los[q][1] + 1
+        return 1000.0 * q + (np.arange(r_ * c_) % 997).reshape(r_, c_)
+
+    def whole():
+        out = np.empty(n * m)
+        L.NGA_Get(g, ia([0, 0]), ia([n - 1, m - 1]), out.ctypes.data_as(ctypes.c_void_p), ia([m]))
+        return out.reshape(n, m)
+
+    blk = access()
+    blk[:] = init_of(rank)               # host writes straight into the segment
+    L.NGA_Release_update(g, blo, bhi)
+    L.GA_Sync()
+    got = whole()
+    for q in range(size):
+        sub = got[los[q][0]:his[q][0] + 1, los[q][1]:his[q][1] + 1]
+        assert np.array_equal(sub, init_of(q)), f"rank {rank}: host-written block of rank {q} not seen by NGA_Get"
+    say(rank, "host-written blocks read back through NGA_Get")
+    # every rank accumulates the whole array: a device source of 2**rank and a pageable one of 3
+    src = ga_amd.DeviceBuffer(n * m * 8)
+    ga_amd.fill_const(src.ptr, n * m * 8, float(2 ** rank))
+    ga_amd.sync()
+    hsrc = np.full(n * m, 3.0)
+    one = ctypes.c_double(1.0)
+    L.NGA_Acc(g, ia([0, 0]), ia([n - 1, m - 1]), ctypes.c_void_p(src.ptr), ia([m]), ctypes.byref(one))
+    L.NGA_Acc(g, ia([0, 0]), ia([n - 1, m - 1]), hsrc.ctypes.data_as(ctypes.c_void_p), ia([m]), ctypes.byref(one))
+    L.GA_Sync()
+    blk = access()                       # read on the host, after the owners applied everything
+    want = init_of(rank) + float(2 ** size - 1) + 3.0 * size
+    bad = int(np.count_nonzero(blk != want))
+    assert bad == 0, f"rank {rank}: {bad} elements of the host block wrong after the accumulates"
+    L.NGA_Release(g, blo, bhi)
+    say(rank, "remote accumulates into host segments exact (checked on the host)")
+    # pnga_zero's way: pnga_access_ptr + memset of the local block, then sync
+    blk = access()
+    ctypes.memset(blk.ctypes.data, 0, rows * cols * 8)
+    L.NGA_Release_update(g, blo, bhi)
+    L.GA_Sync()
+    assert not np.any(whole()), f"rank {rank}: a peer's host memset is not visible through NGA_Get"
+    # and the library's own GA_Zero on host segments after some data
+    L.NGA_Acc(g, ia([0, 0]), ia([n - 1, m - 1]), ctypes.c_void_p(src.ptr), ia([m]), ctypes.byref(one))
+    L.GA_Sync()
+    L.GA_Zero(g)
+    assert not np.any(whole()), f"rank {rank}: GA_Zero left data in a host segment"
+    assert not np.any(access()), f"rank {rank}: GA_Zero not seen on the host"
+    say(rank, "host memset through NGA_Access (pnga_zero) and GA_Zero visible to every rank")
+    src.free()
+    L.GA_Sync()
+    L.GA_Destroy(g)
+    L.GA_Terminate()
+
+
 def c1_test(L, rank, size):
     """BASELINE config C1: 1-D contiguous f64 accumulate of 1 MiB
     (131 072 elements) between ranks, rank r -> rank (r+1) % size, the survey's
@@ -520,11 +608,17 @@ def c5_full_test(L, rank, size):
       M1: every rank NGA_Acc's its own block from a device buffer of the constant
           2**rank (alpha 1): the block must read 2**rank exactly.
       M2: every rank NGA_Acc's the WHOLE array from an 8 GiB source of 2**rank --
-          even ranks from a plain device buffer (packed route: pack -> staging ->
-          owner unpack-acc), odd ranks from their own comex segment (direct-source
-          route: the owner reads it in place) -- so every element must read exactly
-          2**size - 1; a lost, doubled or stale contribution shows as a wrong value
-          that says whose (onesided.c:1387-1440; comex.c:6965-7109, 4133-4281)."""
+          even ranks from a plain device buffer, odd ranks from their own comex
+          segment -- so every element must read exactly 2**size - 1; a lost, doubled
+          or stale contribution shows as a wrong value that says whose
+          (onesided.c:1387-1440; comex.c:6965-7109, 4133-4281).
+    Which route M2 takes depends on where the owners are (asserted below): ranks
+    sharing this GPU -- the one-pass route for every rank (the requester's kernel
+    writes the owner's block under its memory lock); owners on other GPUs, or every
+    peer treated as one (COMEX_AMD_PEER_LOADS=all) -- the packed route for the even
+    ranks (pack -> staging -> the owner's unpack-acc pulling with system-scope loads)
+    and the direct-source route for the odd ones (the owner reads the segment in
+    place with system-scope loads)."""
     import time
     import ga_amd
     ia = ga_amd.int_array
@@ -590,10 +684,10 @@ def c5_full_test(L, rank, size):
     routes = {k: r1[k] - r0[k] for k in r1}
     check_block(float(2 ** size - 1), "M2")
     if size > 1:
-        if use_seg and not one_pass_expected():
-            assert routes["direct_src"] > 0 and routes["packed"] == 0, routes
-        elif one_pass_expected():
+        if one_pass_expected():
             assert routes["one_pass"] > 0 and routes["packed"] == 0 and routes["direct_src"] == 0, routes
+        elif use_seg:
+            assert routes["direct_src"] > 0 and routes["packed"] == 0 and routes["one_pass"] == 0, routes
         else:
             assert routes["packed"] > 0 and routes["direct_src"] == 0 and routes["one_pass"] == 0, routes
     L.GA_Sync()
@@ -601,8 +695,8 @@ def c5_full_test(L, rank, size):
         buf.free()
     assert ga_amd.comex_free(seg[rank]) == 0
     L.GA_Destroy(g)
-    say(rank, f"C5 M2 exact ({'direct-source' if use_seg else 'packed'} route {routes}, {t_m2:.1f} s; "
-              f"total {time.perf_counter() - t0:.1f} s)")
+    route = "one-pass" if one_pass_expected() else ("direct-source" if use_seg else "packed")
+    say(rank, f"C5 M2 exact ({route} route {routes}, {t_m2:.1f} s; total {time.perf_counter() - t0:.1f} s)")
     L.GA_Terminate()
 
 

@@ -350,6 +350,19 @@ def test_owner_host_source_self_acc_vs_one_pass_peers(n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["remote", "hostseg-ga"])
+def test_host_segments_three_ranks(mode):
+    """COMEX_AMD_SEGMENT=host gives every rank a host segment (a
+    POSIX shm object mapped and HIP-registered by every rank of the node, as the
+    reference's _shm_create/_shm_attach), so GA's host-side local operations work with
+    several ranks per node.  `remote`: the whole remote suite (acc/put/get/accv/getv/
+    putv, a chunked remote accumulate) into host segments, exact vs the oracle;
+    `hostseg-ga`: host writes through NGA_Access seen by the peers' NGA_Get, remote
+    NGA_Acc checked on the host, and pnga_zero's NGA_Access + memset visible to all."""
+    launch(mode, n=3, timeout=150, extra_env={"COMEX_AMD_SEGMENT": "host"})
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("one_pass", ["1", "0"])
 def test_config_c1_one_mib_remote_acc_two_ranks(one_pass):
     """BASELINE config C1: a 1-D contiguous f64 accumulate of 1 MiB from rank 0 to
@@ -363,9 +376,26 @@ def test_config_c1_one_mib_remote_acc_two_ranks(one_pass):
 def test_config_c5_full_size_eight_ranks_one_gpu():
     """BASELINE config C5 at its stated size: NGA_Acc into a 32768^2 f64 GA on 8 ranks
     sharing this GPU -- M1 (own 1 GiB block) and M2 (every rank the whole 8 GiB
-    array; half the ranks on the packed route, half on the direct-source route),
-    checked exactly with the 2**rank scheme."""
+    array), checked exactly with the 2**rank scheme.  The owners
+    share the GPU, so EVERY rank's M2 takes the one-pass route (its fused kernel
+    writes each owner's block under the owner's memory lock) -- the worker asserts
+    one_pass > 0 and no packed or direct-source request for every rank.  The routes
+    an 8-GPU node takes are the next test."""
     launch("c5full", n=8, timeout=420, extra_env={"COMEX_AMD_STAGING_MB": "256"})
+
+
+@pytest.mark.gpu
+def test_config_c5_full_size_eight_ranks_cross_device_routes():
+    """C5 at its stated size on the routes an 8-GPU node takes:
+    32768^2 f64 GA, 8 ranks, every other rank's memory treated as another GPU's
+    (COMEX_AMD_PEER_LOADS=all).  M2: even ranks accumulate the whole 8 GiB array from
+    a plain device buffer -- the packed route: pack -> staging -> the owner pulls
+    the chunk with system-scope loads on a pull stream of that source; odd ranks from
+    their own segment -- the direct-source route: the owner's kernel reads the source
+    in place with system-scope loads.  The worker asserts the route counts (packed
+    only on even ranks, direct_src only on odd ones, no one-pass) and checks every
+    element of every block exactly (2**8 - 1)."""
+    launch("c5full", n=8, timeout=420, extra_env={"COMEX_AMD_STAGING_MB": "256", "COMEX_AMD_PEER_LOADS": "all"})
 
 
 @pytest.mark.gpu
