@@ -445,8 +445,10 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         if (kind == X_PUT) {
             sv = local_view(src, slo, shi);
             dv.dev = remote_view(world, dst, dlo, dhi);
+            dv.hbm = segment_kind_of(world, (const char *)dst + dlo) == 1;
         } else {
             sv.dev = remote_view(world, src, slo, shi);
+            sv.hbm = segment_kind_of(world, (const char *)src + slo) == 1;
             dv = local_view(dst, dlo, dhi, true);
         }
     } else {
@@ -477,7 +479,13 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     // blocking call: local completion before returning (src reusable, a get's
     // dst filled) -- the stream the op went to holds it and its dependencies
     const bool synced = host_side || (!hdl && r.blocking_sync);
-    if (!host_side && synced) GA_HIP(hipStreamSynchronize(st));
+    if (!host_side && synced) {
+        // HBM operands only: a completion flag behind the kernel (sched_wait_flag,
+        // ~4 us sooner than the runtime's signal); otherwise the runtime's sync, whose
+        // system-scope release makes a host-memory destination's bytes visible
+        if (sv.hbm && dv.hbm && sched_flag_wait_enabled()) sched_wait_flag(si);
+        else GA_HIP(hipStreamSynchronize(st));
+    }
     if (world != r.rank && !synced && !r.direct_pending.empty()) r.direct_pending[world] = 1;
     if (r.debug)
         fprintf(stderr, "[ga_amd %d] %s -> %d levels %d count0 %d rows %d: src %s dst %s stream %d\n", r.rank,
@@ -726,6 +734,7 @@ int comex_finalize() {
     segments_release_blocks();          // the freed-segment cache and quarantined blocks
     sched_sync_all();
     sched_fini();
+    sched_flag_fini();
     if (g_get_scratch) (void)hipFree(g_get_scratch);
     g_get_scratch = nullptr;
     g_get_scratch_bytes = 0;

@@ -39,9 +39,11 @@ struct View {
     char *host = nullptr;
     int64_t lo = 0, hi = 0;
     bool copy_back = false;
+    bool hbm = false;             // device memory the CPU never touches (HBM segment or hipMalloc)
 };
-// device-visible without help (our segments, HBM, managed, pinned/registered host)
-bool direct_view(void *p, char **dev);
+// device-visible without help (our segments, HBM, managed, pinned/registered host);
+// *hbm (optional): the memory is HBM (not managed, not host)
+bool direct_view(void *p, char **dev, bool *hbm = nullptr);
 // src and dst of one local transfer; a pageable pair whose page ranges overlap is
 // registered once as a union
 void local_views(void *src, int64_t slo, int64_t shi, void *dst, int64_t dlo, int64_t dhi, View &sv, View &dv);

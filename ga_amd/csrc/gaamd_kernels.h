@@ -110,6 +110,8 @@ int elem_size(int op);            // bytes per element for op; 1 for copy; 0 if 
 // comex_rmw: fetch-and-add (swap == 0) or swap of one 4- or 8-byte word at
 // `addr` (device-accessible); the old value lands in *out_dev (8 bytes)
 int launch_rmw(int swap, void *addr, int bytes, uint64_t val, uint64_t *out_dev, hipStream_t stream);
+// one lane stores v into *flag_dev (pinned host memory) after the stream's earlier work
+int launch_flag(uint64_t *flag_dev, uint64_t v, hipStream_t stream);
 LaunchInfo *last_launch_info();   // most recent launch_strided (any caller)
 unsigned long long kernel_count(int kind);   // launch_strided launches so far, by KernelKind (< kKinds)
 

@@ -1303,6 +1303,21 @@ __global__ __launch_bounds__(64) void k_rmw(void *addr, int swap, int bytes, uin
     }
 }
 
+// Completion flag of a blocking call (comex.cpp / sched.cpp sched_wait_flag): after
+// every earlier operation of the stream, one lane stores `v` into pinned host memory
+// with a system-scope release (a vector store), and the host spins on that word --
+// about 4 us sooner than the runtime's completion signal wakes hipStreamSynchronize
+// (tools/completion_probe.hip mode 3, profiles/r03/s21).
+__global__ __launch_bounds__(64) void k_flag(uint64_t *flag, uint64_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int launch_flag(uint64_t *flag_dev, uint64_t v, hipStream_t stream) {
+    hipLaunchKernelGGL(k_flag, dim3(1), dim3(64), 0, stream, flag_dev, v);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
 int launch_rmw(int swap, void *addr, int bytes, uint64_t val, uint64_t *out_dev, hipStream_t stream) {
     if (bytes != 4 && bytes != 8) return -4;
     if (((uintptr_t)addr & (uintptr_t)(bytes - 1)) != 0) return -8;

@@ -26,6 +26,7 @@
 // have their own lock (g_marks_mu): sched_track / sched_complete run outside
 // launch_mu, and a wait on an event is done with the lock released.
 #include "runtime.hpp"
+#include "gaamd_kernels.h"
 #include <string.h>
 #include <stdlib.h>
 #include <deque>
@@ -207,6 +208,63 @@ void sched_sync_all() {
     }
     g_hist.clear();
     g_base = -1;
+}
+
+// ---- blocking-call completion through a flag -----------------
+// A blocking call whose operands are all device memory (HBM) completes locally when
+// its kernel has finished.  hipStreamSynchronize returns some 4 us after the GPU is
+// done (the runtime's completion signal and the host wake-up); a one-lane kernel
+// behind it storing a sequence number into pinned host memory, which the caller
+// spins on, is seen that much sooner.  Only for HBM operands: the CPU never reads
+// them, so nothing but the ORDER of the GPU's work matters; a host-memory
+// destination keeps hipStreamSynchronize (the runtime's system-scope release at
+// the stream's end makes its bytes visible to the CPU).  COMEX_AMD_BLOCKING_WAIT=
+// sync restores hipStreamSynchronize everywhere.
+namespace {
+uint64_t *g_flag_host = nullptr, *g_flag_dev = nullptr;
+std::vector<uint64_t> g_flag_seq;
+}
+
+bool sched_flag_wait_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("COMEX_AMD_BLOCKING_WAIT");
+        return !(e && !strcmp(e, "sync"));
+    }();
+    return on;
+}
+
+void sched_wait_flag(int s) {
+    Runtime &r = rt();
+    uint64_t v;
+    volatile uint64_t *f;
+    {
+        std::lock_guard<std::mutex> g(r.launch_mu);
+        if (!g_flag_host) {
+            GA_HIP(hipHostMalloc((void **)&g_flag_host, 64 * sizeof(uint64_t), hipHostMallocMapped));
+            GA_HIP(hipHostGetDevicePointer((void **)&g_flag_dev, g_flag_host, 0));
+            memset(g_flag_host, 0, 64 * sizeof(uint64_t));
+            g_flag_seq.assign(64, 0);
+        }
+        if (s < 0 || s >= 64) fatal("stream index %d out of range", s);
+        v = ++g_flag_seq[s];
+        const int rc = launch_flag(g_flag_dev + s, v, r.streams[s]);
+        if (rc) fatal("completion flag launch failed (%d)", rc);
+        f = g_flag_host + s;
+    }
+    for (unsigned long spins = 0; __atomic_load_n(f, __ATOMIC_ACQUIRE) < v; ++spins) {
+        if ((spins & 0xfffff) == 0xfffff) {
+            // every ~1M polls: a failed stream reports its error instead of spinning on
+            const hipError_t e = hipStreamQuery(r.streams[s]);
+            if (e != hipSuccess && e != hipErrorNotReady) fatal("stream failed: %s", hipGetErrorString(e));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+void sched_flag_fini() {
+    if (g_flag_host) (void)hipHostFree(g_flag_host);
+    g_flag_host = g_flag_dev = nullptr;
+    g_flag_seq.clear();
 }
 
 // Launches that move at least this many payload bytes stay on the stream of the

@@ -17,13 +17,19 @@ namespace gaamd {
 // addresses, and a later pageable host allocation can land there -- a cached
 // "device" answer then hands the GPU an unmapped host address: a memory-access
 // fault, round 3, test_pageable_sources_sharing_pages_back_to_back.)
-bool direct_view(void *p, char **dev) {
-    if (segment_local(p, 0, 1)) { *dev = (char *)p; return true; }
+bool direct_view(void *p, char **dev, bool *hbm) {
+    if (hbm) *hbm = false;
+    if (const int k = segment_kind(p)) {   // our HBM segment, or a host segment (same address)
+        *dev = (char *)p;
+        if (hbm) *hbm = k == 1;
+        return true;
+    }
     hipPointerAttribute_t at;
     memset(&at, 0, sizeof(at));
     hipError_t e = hipPointerGetAttributes(&at, p);
     if (e == hipSuccess && (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged)) {
         *dev = (char *)p;
+        if (hbm) *hbm = at.type == hipMemoryTypeDevice;
         return true;
     }
     if (e == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer) {
@@ -69,9 +75,9 @@ static void stage_view(View &v, void *p, int64_t lo, int64_t hi, bool is_dst) {
 void local_views(void *src, int64_t slo, int64_t shi, void *dst, int64_t dlo, int64_t dhi,
                         View &sv, View &dv) {
     char *d = nullptr;
-    const bool sd = direct_view(src, &d);
+    const bool sd = direct_view(src, &d, &sv.hbm);
     if (sd) sv.dev = d;
-    const bool dd = direct_view(dst, &d);
+    const bool dd = direct_view(dst, &d, &dv.hbm);
     if (dd) dv.dev = d;
     uintptr_t s0 = 0, s1 = 0, d0 = 0, d1 = 0;
     if (!sd) page_range(src, slo, shi, s0, s1);
@@ -103,7 +109,7 @@ void local_views(void *src, int64_t slo, int64_t shi, void *dst, int64_t dlo, in
 View local_view(void *p, int64_t lo, int64_t hi, bool is_dst) {
     View v;
     char *d = nullptr;
-    if (direct_view(p, &d)) { v.dev = d; return v; }
+    if (direct_view(p, &d, &v.hbm)) { v.dev = d; return v; }
     uintptr_t a0, a1;
     page_range(p, lo, hi, a0, a1);
     char *base = nullptr;

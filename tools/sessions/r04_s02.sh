@@ -25,3 +25,10 @@ print({k: d.get(k) for k in ("value", "hbm_peak_frac", "topology", "cpu_baseline
 for k, v in d.get("c5", {}).items():
     print(k, json.dumps(v)[:600])
 PY
+# blocking API: completion flag (default) vs the runtime's sync, interleaved
+for i in 1 2; do
+  for w in flag sync; do
+    COMEX_AMD_BLOCKING_WAIT=$w timeout -k 10 120 python bench.py --steps 100 --warmup 5 --no-cpu > $O/blk_${w}_$i.json 2> $O/blk_${w}_$i.err || { echo "blk $w failed"; tail $O/blk_${w}_$i.err; exit 1; }
+    python -c "import json;d=json.load(open('$O/blk_${w}_$i.json'));print('blocking $w', d['value'], d['hbm_peak_frac'], d['blocking_api'])"
+  done
+done
