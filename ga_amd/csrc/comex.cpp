@@ -732,6 +732,7 @@ int comex_finalize() {
     boot_barrier();
     remote_free_staging();
     segments_release_blocks();          // the freed-segment cache and quarantined blocks
+    vmm_finalize();                     // the reserved address ranges
     sched_sync_all();
     sched_fini();
     sched_flag_fini();

@@ -94,6 +94,14 @@ void export_alloc(void **p, size_t bytes, hipIpcMemHandle_t *h, const char *what
 void segments_finalize();         // every live segment: peer mappings closed, block freed
 void segments_release_blocks();   // the freed-segment cache and the quarantined blocks
 
+// ---- HBM segments through the virtual-memory API (vmm.cpp) ---------------------
+bool vmm_enabled();                       // COMEX_AMD_SEGMENT_ALLOC=vmm
+size_t vmm_round(size_t bytes);           // to the allocation granularity
+void *vmm_alloc(size_t bytes, VmmBlock *b);                  // this GPU's HBM, exported (b->fd)
+void *vmm_import(int pid, int fd, size_t bytes, int q, VmmBlock *b);   // rank q's block
+void vmm_free(VmmBlock *b);               // unmap + release (the address range is never reused)
+void vmm_finalize();
+
 // ---- remote operations through the owner (remote.cpp) -----------------------
 void remote_init();             // staging buffer, peer mappings, progress thread (collective)
 void remote_finalize();         // after comex_barrier: job bookkeeping freed, progress thread stopped

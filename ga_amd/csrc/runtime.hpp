@@ -122,8 +122,21 @@ struct PeerMap {
     size_t map_bytes = 0;
 };
 
+// an HBM block of the virtual-memory allocator (vmm.cpp): its mapping here, the
+// physical handle and its dmabuf descriptor (an owner's export or a peer's import)
+struct VmmBlock {
+    char *va = nullptr;
+    size_t bytes = 0;                    // mapped bytes (granularity-rounded)
+    hipMemGenericAllocationHandle_t handle{};
+    int fd = -1;
+    bool imported = false;
+};
+
 struct Segment {
     bool live = false;
+    bool vmm = false;            // HBM from vmm.cpp (own block in vmm_local, peers' in vmm_peer)
+    VmmBlock vmm_local;
+    std::vector<VmmBlock> vmm_peer;
     bool device = true;          // HBM (IPC-exported) or a host segment in node shm
     void *local = nullptr;
     size_t local_bytes = 0;      // bytes of the local block

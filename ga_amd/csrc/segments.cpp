@@ -468,14 +468,24 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         int32_t device, host;    // host: a node shm segment, `name` below
         uint64_t gen;
         char name[64];
+        int32_t vmm, pid, fd, pad;   // vmm: HBM from vmm.cpp, descriptor `fd` of process `pid`
+        uint64_t vmm_bytes;
     } mine;
     memset(&mine, 0, sizeof(mine));
     static uint64_t gen = 0;   // this rank's allocation counter (the tags, the shm names)
     void *p = nullptr;
     bool exported = false;
     const size_t map_bytes = page_round(bytes);
+    const bool vmm = device && vmm_enabled();
+    VmmBlock vlocal;
     if (bytes) {
-        if (device) {
+        if (vmm) {
+            p = vmm_alloc(bytes, &vlocal);
+            mine.vmm = 1;
+            mine.pid = (int32_t)getpid();
+            mine.fd = vlocal.fd;
+            mine.vmm_bytes = vlocal.bytes;
+        } else if (device) {
             block_trim_for(bytes);
             if (!block_take(bytes, &p, &exported, &mine.h)) {
                 p = device_alloc(bytes);
@@ -503,6 +513,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     const bool tagged = device && bytes >= 16;
     std::vector<Info> all(r.size);
     std::vector<void *> mapped(r.size, nullptr);
+    std::vector<VmmBlock> vpeer;
     for (int attempt = 0;; ++attempt) {
         mine.base = (uint64_t)(uintptr_t)p;
         mine.bytes = bytes;
@@ -521,7 +532,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         for (size_t k = 0; k < members.size(); ++k) {
             all[members[k]] = gathered[k];
             ptr_arr[k] = (void *)(uintptr_t)gathered[k].base;
-            if (gathered[k].bytes && !gathered[k].host)
+            if (gathered[k].bytes && !gathered[k].host && !gathered[k].vmm)
                 handle_seen(members[k], gathered[k].gen, gathered[k].base, gathered[k].bytes, gathered[k].h);
         }
         // open, and check that each IPC mapping reads its owner's tags
@@ -534,7 +545,12 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
                 mapped[q] = shm_map_registered(all[q].name, page_round(all[q].bytes), false);
                 continue;
             }
-            mapped[q] = ipc_open(all[q].h, q, "segment");
+            if (all[q].vmm) {    // the owner's dmabuf descriptor, mapped at a fresh address here
+                if (vpeer.size() != (size_t)r.size) vpeer.assign(r.size, VmmBlock());
+                mapped[q] = vmm_import(all[q].pid, all[q].fd, all[q].vmm_bytes, q, &vpeer[q]);
+            } else {
+                mapped[q] = ipc_open(all[q].h, q, "segment");
+            }
             if (!mapped[q] || all[q].bytes < 16) continue;
             uint64_t t[2] = {0, 0};
             GA_HIP(hipMemcpy(&t[0], mapped[q], 8, hipMemcpyDeviceToHost));
@@ -558,6 +574,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
                     if (q == r.rank) mine_stale = true;
                 }
         if (!any) break;
+        if (vmm) fatal("a mapping of a new segment of the virtual-memory allocator does not read its owner's tags");
         if (attempt >= 3) fatal("IPC mappings of a new segment keep reaching other memory (4 attempts)");
         for (int q = 0; q < r.size; ++q)
             if (mapped[q]) ipc_close(mapped[q], q);
@@ -580,6 +597,11 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     for (int q : members) s.peer[q].member = true;
     s.live = true;
     s.device = device;
+    s.vmm = vmm;
+    if (vmm) {
+        s.vmm_local = vlocal;
+        s.vmm_peer = vpeer;
+    }
     s.local = p;
     s.local_bytes = bytes;
     s.exported = exported;
@@ -605,9 +627,11 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     return COMEX_SUCCESS;
 }
 
-// close this process's view of a segment's peer q (IPC mapping or shm mapping)
-static void close_peer(PeerMap &m, int q) {
+// close this process's view of a segment's peer q (IPC, shm or vmm mapping)
+static void close_peer(Segment &s, int q) {
+    PeerMap &m = s.peer[q];
     if (m.host_map) shm_unmap_registered(m.host_map, m.map_bytes);
+    else if (s.vmm && q < (int)s.vmm_peer.size() && s.vmm_peer[q].va) vmm_free(&s.vmm_peer[q]);
     else if (m.mapped) ipc_close(m.mapped, q);
     m.mapped = m.host_map = nullptr;
 }
@@ -633,10 +657,14 @@ void segments_finalize() {
     for (Segment &s : r.segs) {
         if (!s.live) continue;
         for (int q = 0; q < (int)s.peer.size(); ++q)
-            if (q != r.rank) close_peer(s.peer[q], q);
-        if (s.local && s.device) addr_event('f', s.local, s.peer[r.rank].bytes, -1);
-        if (s.local && s.device) (void)hipFree(s.local);
-        else if (s.local) shm_unmap_registered((char *)s.local, s.peer[r.rank].map_bytes);
+            if (q != r.rank) close_peer(s, q);
+        if (s.vmm) vmm_free(&s.vmm_local);
+        else if (s.local && s.device) {
+            addr_event('f', s.local, s.peer[r.rank].bytes, -1);
+            (void)hipFree(s.local);
+        } else if (s.local) {
+            shm_unmap_registered((char *)s.local, s.peer[r.rank].map_bytes);
+        }
         s.live = false;
     }
     r.segs.clear();
@@ -680,6 +708,8 @@ int comex_free(void *ptr, comex_group_t group) {
     void *local = nullptr;
     bool device = true, found = false, exported = false;
     size_t local_bytes = 0, local_map_bytes = 0;
+    VmmBlock vblock;
+    bool is_vmm = false;
     hipIpcMemHandle_t handle;
     memset(&handle, 0, sizeof(handle));
     {
@@ -690,10 +720,15 @@ int comex_free(void *ptr, comex_group_t group) {
             for (int q = 0; q < r.size; ++q) if (s.peer[q].base != all[q]) { match = false; break; }
             if (!match) continue;
             for (int q = 0; q < r.size; ++q)
-                if (q != r.rank) close_peer(s.peer[q], q);
+                if (q != r.rank) close_peer(s, q);
             local = s.local;
             device = s.device;
             local_map_bytes = s.peer[r.rank].map_bytes;
+            if (s.vmm) {
+                vblock = s.vmm_local;
+                s.vmm_local = VmmBlock();
+                is_vmm = true;
+            }
             local_bytes = s.local_bytes;
             exported = s.exported;
             if (exported) handle = s.handle;
@@ -709,7 +744,9 @@ int comex_free(void *ptr, comex_group_t group) {
     // refuses to export a new allocation it hands out at the same address
     // (hipIpcGetMemHandle: invalid argument in the next comex_malloc)
     members_barrier(members, group);
-    if (local && device) {
+    if (is_vmm) {
+        vmm_free(&vblock);   // physical memory back now; the address range is never reused
+    } else if (local && device) {
         if (block_cache_cap()) block_put(local, local_bytes, exported, handle);   // kept for the next comex_malloc
         else block_free_one({local, local_bytes, exported, handle});
     } else if (local) {

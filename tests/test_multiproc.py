@@ -350,6 +350,22 @@ def test_owner_host_source_self_acc_vs_one_pass_peers(n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode,n,extra", [("remote", 3, {}), ("onepass", 4, {}), ("directsrc", 3, {}),
+                                          ("segcache", 3, {"COMEX_AMD_SEGMENT_CACHE_MB": "0"}),
+                                          ("stress", 3, {"COMEX_AMD_STAGING_MB": "1"}),
+                                          ("c5full", 8, {"COMEX_AMD_STAGING_MB": "256", "TEST_C5_N": "16384"}),
+                                          ("c5full", 4, {"COMEX_AMD_PEER_LOADS": "all", "TEST_C5_N": "8192"})])
+def test_vmm_segments(mode, n, extra):
+    """HBM segments from the virtual-memory allocator
+    (COMEX_AMD_SEGMENT_ALLOC=vmm, vmm.cpp) -- hipMemCreate + a dmabuf descriptor
+    handed to the peers with pidfd_getfd, every mapping at an address range this
+    process never used before -- under the remote suite, the one-pass and
+    direct-source routes, create/free cycles, random programs and C5 (one GPU, and
+    with every peer treated as another GPU), all exact."""
+    launch(mode, n=n, timeout=300, extra_env=dict(extra, COMEX_AMD_SEGMENT_ALLOC="vmm"))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["remote", "hostseg-ga"])
 def test_host_segments_three_ranks(mode):
     """COMEX_AMD_SEGMENT=host gives every rank a host segment (a
