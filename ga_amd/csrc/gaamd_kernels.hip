@@ -553,88 +553,88 @@ __global__ __launch_bounds__(64) void k_ordered_cols(const Desc d, const OP op) 
 // one-lane-per-column kernel above is latency-bound: a column reduction has only
 // row-width / W lanes (8192 at 64 KiB rows: one wave per two CUs), each with at
 // most 63 loads in flight (vmcnt) -- 0.62-0.65 TB/s of real HBM traffic.  Here a
-// workgroup of KC_NW waves owns CW column slices (CW*W contiguous bytes of every
-// row), and ALL its waves load rows: wave w's k-th load instruction fetches rows
-// (w*P + k)*RPI .. +RPI-1 of the tile (RPI = 64/CW rows per instruction, CW lanes
-// each), so a workgroup keeps KC_NW*P instructions in flight.  The tile goes to
-// LDS, and the first CW lanes of wave 0 walk its rows IN ORDER, applying each to
-// the column value held in a register (stored when the dst run changes and at the
-// end) -- the reference's operations in its order per column (comex.c:6936-6961,
-// acc.h:137-143) -- while the next tile's loads are in flight.  A row's dst offset
-// is the same for every lane, so the run test is wave-uniform.
-constexpr int KC_NW = 4;                 // waves per workgroup
-template <int W> struct KcRows { static constexpr int P = W >= 16 ? 16 : 32; };   // load instructions per wave per tile
+// workgroup owns CW column slices (CW*W contiguous bytes of every row) and splits
+// the work by role:
+//   * waves 1..KC_NW-1 LOAD: each fetches P load instructions of rows per tile
+//     (RPI = 64/CW rows per instruction, CW lanes each), unconditionally (rows
+//     past the last load the last one again: straight-line code, so the P loads
+//     issue back to back), and writes them into one of two LDS tiles;
+//   * wave 0 APPLIES: its first CW lanes walk the other tile's rows IN ORDER,
+//     applying each to the column value held in a register (stored when the dst
+//     run changes and at the end) -- the reference's operations in its order per
+//     column (comex.c:6936-6961, acc.h:137-143).  A row's dst offset is the same
+//     for every lane, so the run test is a scalar branch; rows come in batches of
+//     8 with their LDS reads issued together ahead of the dependent chain.
+// One barrier per tile: the loaders fill tile i+1 while wave 0 applies tile i.
+constexpr int KC_NW = 8;                 // waves per workgroup: 1 applier + 7 loaders
+template <int W> struct KcRows { static constexpr int P = 128 / W; };   // 56 KiB per LDS tile
 template <class OP, int W, int LV, int CW>
 __global__ __launch_bounds__(KC_NW * 64) void k_ordered_cols_lds(const Desc d, const OP op) {
     typedef typename Vec<W>::T V;
     constexpr int P = KcRows<W>::P;
-    constexpr int RPI = 64 / CW;                 // rows per load instruction
-    constexpr int T = KC_NW * P * RPI;           // rows per tile
-    __shared__ V tile[T * CW];                   // [row][column], KC_NW*P*64 vectors
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t col = blockIdx.x * (uint32_t)CW + (lane % CW);
-    const bool live = col < d.nvec;
-    const int64_t xo = (int64_t)col * W;
-    const uint32_t sub = lane / CW;              // which row of an instruction's RPI this lane loads
-    // lanes past the row's last column or the last row load a valid clamped address
-    // (their values are never applied): every load is unconditional, so the P loads
-    // of a wave issue back to back (conditional loads each got an s_waitcnt vmcnt(0))
+    constexpr int RPI = 64 / CW;                     // rows per load instruction
+    constexpr int T = (KC_NW - 1) * P * RPI;         // rows per tile
+    __shared__ V tile[2][T * CW];                    // [buffer][row][column]
+    // the wave index through readfirstlane: the compiler then knows the role branch
+    // (and every value inside the applier's) is wave-uniform -- scalar branches
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t c = lane % CW;                    // this lane's column slice within the workgroup
+    const uint32_t col = blockIdx.x * (uint32_t)CW + c;
+    // every lane works on a valid address (clamped column; its values are never stored)
     const int64_t xl = (int64_t)min(col, d.nvec - 1u) * W;
-    V s[P];
-    auto load_tile = [&](uint32_t r0) {
+    const uint32_t ntiles = (d.rows + (uint32_t)T - 1) / (uint32_t)T;
+    auto load_store = [&](uint32_t tl, int buf) {    // loader waves: tile `tl` into tile[buf]
+        const uint32_t lw = wave - 1, sub = lane / CW;
+        V s[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            const uint32_t r = min(r0 + (wave * P + (uint32_t)k) * RPI + sub, d.rows - 1u);
+            const uint32_t r = min(tl * (uint32_t)T + (lw * P + (uint32_t)k) * RPI + sub, d.rows - 1u);
             int64_t so, dof;
             row_offsets<LV>(d, d.row0 + r, so, dof);
             s[k] = vload<W, true>(d.src + so + xl);
         }
-    };
-    auto store_tile = [&]() {
 #pragma unroll
-        for (int k = 0; k < P; ++k) tile[(wave * P + (uint32_t)k) * 64 + lane] = s[k];
+        for (int k = 0; k < P; ++k) tile[buf][(lw * P + (uint32_t)k) * 64 + lane] = s[k];
     };
+    const bool lane_ok = lane < (uint32_t)CW && col < d.nvec;
     V acc = {};
     int64_t cur = 0;
     bool held = false;
-    load_tile(0);
-    store_tile();
-    __syncthreads();
-    for (uint32_t r0 = 0; r0 < d.rows; r0 += T) {
-        if (r0 + T < d.rows) load_tile(r0 + T);   // in flight while the tile below is applied
-        if (wave == 0 && lane < (uint32_t)CW && live) {
-            const uint32_t n = min((uint32_t)T, d.rows - r0);
-            constexpr int B = 8;                  // LDS reads issued ahead of the dependent chain
-            for (uint32_t t = 0; t < n; t += B) {
-                V x[B];
-                int64_t dofs[B];
-#pragma unroll
-                for (int j = 0; j < B; ++j) {
-                    if (t + j < n) {
-                        int64_t so;
-                        row_offsets<LV>(d, d.row0 + r0 + t + j, so, dofs[j]);
-                        x[j] = tile[(t + j) * CW + lane];
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < B; ++j) {
-                    if (t + j >= n) break;
-                    if (!held || dofs[j] != cur) {
-                        if (held) vstore<W, false>(d.dst + cur + xo, acc);
-                        cur = dofs[j];
-                        held = true;
-                        acc = x[j];
-                        if constexpr (OP::kReadsDst) acc = vload<W, false>(d.dst + cur + xo);
-                    }
-                    acc = op.template apply<W>(acc, x[j]);
-                }
-            }
+    auto apply_row = [&](uint32_t r, const V &x) {   // applier: row r of the patch (wave-uniform)
+        int64_t so, dof;
+        row_offsets<LV>(d, d.row0 + r, so, dof);
+        if (!held || dof != cur) {
+            if (held && lane_ok) vstore<W, false>(d.dst + cur + xl, acc);
+            cur = dof;
+            held = true;
+            acc = x;
+            if constexpr (OP::kReadsDst) acc = vload<W, false>(d.dst + cur + xl);
         }
-        __syncthreads();                          // the tile has been read
-        if (r0 + T < d.rows) store_tile();
+        acc = op.template apply<W>(acc, x);
+    };
+    if (wave != 0) load_store(0, 0);
+    __syncthreads();
+    for (uint32_t i = 0; i < ntiles; ++i) {
+        const int buf = (int)(i & 1);
+        if (wave != 0) {
+            if (i + 1 < ntiles) load_store(i + 1, buf ^ 1);
+        } else {
+            const uint32_t r0 = i * (uint32_t)T;
+            const uint32_t n = min((uint32_t)T, d.rows - r0);
+            constexpr int B = 8;
+            uint32_t t = 0;
+            for (; t + B <= n; t += B) {
+                V x[B];
+#pragma unroll
+                for (int j = 0; j < B; ++j) x[j] = tile[buf][(t + j) * CW + c];
+#pragma unroll
+                for (int j = 0; j < B; ++j) apply_row(r0 + t + j, x[j]);
+            }
+            for (; t < n; ++t) apply_row(r0 + t, tile[buf][t * CW + c]);
+        }
         __syncthreads();
     }
-    if (held) vstore<W, false>(d.dst + cur + xo, acc);
+    if (held && lane_ok) vstore<W, false>(d.dst + cur + xl, acc);
 }
 
 // ---------------------------------------------------------------------------
