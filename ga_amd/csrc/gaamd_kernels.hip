@@ -637,6 +637,50 @@ __global__ __launch_bounds__(KC_NW * 64) void k_ordered_cols_lds(const Desc d, c
     if (held && lane_ok) vstore<W, false>(d.dst + cur + xl, acc);
 }
 
+// COLUMN REDUCTION OF INTEGERS, rows split over workgroups:
+// for COMEX_ACC_INT / _LNG the reference's per-row `A += B*C` wraps (unsigned
+// arithmetic here, -fwrapv in the oracle), so a dst element's final value is its
+// initial value plus the wrapped sum of its rows' products in ANY order.  A
+// workgroup takes R consecutive rows of 256 element columns: the R loads of a
+// lane are issued together (row-major streaming of the source, every row read in
+// full 256-element pieces), the products of consecutive rows hitting the same dst
+// run are summed in a register, and each run's partial goes into dst with one
+// device-scope atomic add (the launcher takes this path only for a dst in HBM).
+constexpr int kColsAtomicRows = 64;
+template <class OP, int LV>
+__global__ __launch_bounds__(256) void k_cols_atomic(const Desc d, const OP op) {
+    typedef decltype(op.s) A;                      // uint32_t (INT) / uint64_t (LNG)
+    constexpr int R = kColsAtomicRows;
+    const uint32_t v = blockIdx.x * 256u + threadIdx.x;
+    if (v >= d.nvec) return;
+    const uint32_t rb = blockIdx.y * (uint32_t)R;
+    const uint32_t n = min((uint32_t)R, d.rows - rb);
+    const int64_t xo = (int64_t)v * sizeof(A);
+    A x[R];
+    int64_t dofs[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {                  // rows past the last load the last one again
+        int64_t so;
+        row_offsets<LV>(d, d.row0 + min(rb + (uint32_t)k, d.rows - 1u), so, dofs[k]);
+        x[k] = __builtin_nontemporal_load(reinterpret_cast<const A *>(d.src + so + xo));
+    }
+    A part = 0;
+    int64_t cur = dofs[0];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        if ((uint32_t)k >= n) break;
+        if (dofs[k] != cur) {
+            __hip_atomic_fetch_add(reinterpret_cast<A *>(d.dst + cur + xo), part, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            cur = dofs[k];
+            part = 0;
+        }
+        A prod = x[k] * op.s;
+        part = part + prod;
+    }
+    __hip_atomic_fetch_add(reinterpret_cast<A *>(d.dst + cur + xo), part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------------------
 // host launch plumbing
 //
@@ -651,7 +695,8 @@ __global__ __launch_bounds__(KC_NW * 64) void k_ordered_cols_lds(const Desc d, c
 struct Plan {
     int kind;        // KK_ROWS / KK_FLAT / KK_SERIAL / KK_ORDERED
     int W, U, BS;
-    int variant;     // KK_ORDERED: 0 one workgroup, 1 column slices (pipelined), 2 column slices (in place)
+    int variant;     // KK_ORDERED: 0 one workgroup, 1 column slices (pipelined), 2 column slices (in place),
+                     // 3 integer column reduction with rows split over workgroups (atomic partials)
     bool sys;        // KK_ROWS: source in a peer GPU's memory (system-scope loads)
     int cw;          // variant 1: columns per workgroup of the LDS-staged kernel (0: one lane per column)
 };
@@ -761,6 +806,17 @@ static hipError_t dispatch_w(const Plan &p, const Desc &d, const OP &op, uint64_
             return hipGetLastError();
         }
         if (p.kind == KK_ORDERED) {
+            if (p.variant == 3) {           // integers: rows split over workgroups, atomic partials
+                if constexpr (std::is_same<OP, AccInt>::value || std::is_same<OP, AccLng>::value) {
+                    if constexpr (W == OP::kElem) {
+                        const dim3 grid((d.nvec + 255u) / 256u, (d.rows + kColsAtomicRows - 1) / kColsAtomicRows);
+                        if (d.levels == 1) hipLaunchKernelGGL((k_cols_atomic<OP, 1>), grid, dim3(256), 0, st, d, op);
+                        else hipLaunchKernelGGL((k_cols_atomic<OP, 0>), grid, dim3(256), 0, st, d, op);
+                        return hipGetLastError();
+                    }
+                }
+                return hipErrorInvalidValue;
+            }
             if (p.variant == 1 && p.cw) {   // LDS-staged column slices
                 if (d.levels == 1) go_cols_lds<OP, W, 1>(d, op, p.cw, blocks, st);
                 else go_cols_lds<OP, W, 0>(d, op, p.cw, blocks, st);
@@ -1163,6 +1219,18 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     // column slices: 8-byte lanes where the element allows (twice the lanes of
     // 16-byte vectors on a column reduction, whose parallelism is the row width)
     if (cols && W > 8 && esz <= 8) W = 8;
+    // integer column reductions (COMEX_ACC_INT / _LNG, coinciding dst rows, no src row
+    // meeting a dst row): rows split over workgroups with atomic partials -- wrapping
+    // integer sums are exact in any order; device-scope atomics need the dst in HBM
+    bool cols_atomic = false;
+    if (cols && ov == OV_COLS && (op == 37 || op == 42) && tn.ordered_cols == 2 &&
+        (row_end - row_begin) <= (uint64_t)kColsAtomicRows * 65535u && ((uint64_t)(uintptr_t)dst & (esz - 1)) == 0) {
+        hipPointerAttribute_t at;
+        memset(&at, 0, sizeof(at));
+        if (hipPointerGetAttributes(&at, dst) == hipSuccess) cols_atomic = at.type == hipMemoryTypeDevice;
+        else (void)hipGetLastError();
+    }
+    if (cols_atomic) W = esz;
 
     Desc d;
     memset(&d, 0, sizeof(d));
@@ -1216,7 +1284,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     p.U = U;
     p.BS = BS;
     p.sys = src_peer;
-    p.variant = (kind == KK_ORDERED && cols) ? (ov == OV_COLS ? 1 : 2) : 0;
+    p.variant = (kind == KK_ORDERED && cols) ? (cols_atomic ? 3 : (ov == OV_COLS ? 1 : 2)) : 0;
     p.cw = (p.variant == 1 && tn.ordered_cols == 2 && (W <= 8 || esz == 16)) ? cols_per_group(d.nvec, W) : 0;
     const uint32_t per_chunk = (uint32_t)BS * (uint32_t)U;
     d.align_mask = 0;
@@ -1254,7 +1322,9 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
             blocks = (d.items + per - 1) / per;
         } else {
             d.items = nr;
-            if (p.cw) blocks = (d.nvec + (uint32_t)p.cw - 1) / (uint32_t)p.cw;   // CW column slices per workgroup
+            if (p.variant == 3)   // (256-column chunks) x (row groups); the dispatcher builds the 2-D grid
+                blocks = (uint64_t)((d.nvec + 255u) / 256u) * ((nr + kColsAtomicRows - 1) / kColsAtomicRows);
+            else if (p.cw) blocks = (d.nvec + (uint32_t)p.cw - 1) / (uint32_t)p.cw;   // CW column slices per workgroup
             else if (p.variant) blocks = (d.nvec + 63u) / 64u;                   // one wave per 64 column slices
         }
         if (blocks > lim) blocks = lim;
@@ -1274,7 +1344,8 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         info->blocks = total_blocks;
         info->block = (kind == KK_ROWS) ? BS
                       : (kind == KK_FLAT ? flat_block_threads(W)
-                                         : ((kind == KK_ORDERED && !p.variant) ? kOrderedBS : (p.cw ? KC_NW * 64 : 64)));
+                                         : ((kind == KK_ORDERED && !p.variant) ? kOrderedBS
+                                            : (p.variant == 3 ? 256 : (p.cw ? KC_NW * 64 : 64))));
         info->levels = L;
         info->aligned = d.align_mask ? 1 : 0;
         info->sys = src_peer ? 1 : 0;
