@@ -681,6 +681,49 @@ __global__ __launch_bounds__(256) void k_cols_atomic(const Desc d, const OP op) 
     __hip_atomic_fetch_add(reinterpret_cast<A *>(d.dst + cur + xo), part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The same for the pure column reduction -- every row into ONE dst run (all dst
+// strides of the row levels zero): a workgroup owns 64 element columns and ALL rows;
+// its 16 waves take rows w, w + 16, w + 32, ... (16 consecutive rows in flight per
+// step, 64 loads per lane), sum their products in registers, the 16 partials of a
+// column are added in LDS, and one lane read-modify-writes the column: no atomics
+// (the atomic form above pays for contention on the 64-byte dst lines).
+constexpr int kColsSumWaves = 16;
+template <class OP, int LV>
+__global__ __launch_bounds__(kColsSumWaves * 64) void k_cols_sum(const Desc d, const OP op) {
+    typedef decltype(op.s) A;
+    constexpr int P = 32;                          // loads in flight per lane
+    __shared__ A red[kColsSumWaves][64];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t v = blockIdx.x * 64u + lane;
+    const int64_t xo = (int64_t)min(v, d.nvec - 1u) * sizeof(A);
+    A part = 0;
+    for (uint32_t r0 = wave; r0 < d.rows; r0 += kColsSumWaves * P) {
+        A x[P];
+#pragma unroll
+        for (int k = 0; k < P; ++k) {              // rows past the last load the last one again
+            int64_t so, dof;
+            row_offsets<LV>(d, d.row0 + min(r0 + (uint32_t)k * kColsSumWaves, d.rows - 1u), so, dof);
+            x[k] = __builtin_nontemporal_load(reinterpret_cast<const A *>(d.src + so + xo));
+        }
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            A prod = x[k] * op.s;
+            if (r0 + (uint32_t)k * kColsSumWaves < d.rows) part = part + prod;
+        }
+    }
+    red[wave][lane] = part;
+    __syncthreads();
+    if (wave == 0 && v < d.nvec) {
+        A t = 0;
+#pragma unroll
+        for (int w = 0; w < kColsSumWaves; ++w) t = t + red[w][lane];
+        int64_t so, dof;
+        row_offsets<LV>(d, d.row0, so, dof);       // the one dst run
+        A *dp = reinterpret_cast<A *>(d.dst + dof + (int64_t)v * sizeof(A));
+        *dp = *dp + t;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host launch plumbing
 //
@@ -696,7 +739,8 @@ struct Plan {
     int kind;        // KK_ROWS / KK_FLAT / KK_SERIAL / KK_ORDERED
     int W, U, BS;
     int variant;     // KK_ORDERED: 0 one workgroup, 1 column slices (pipelined), 2 column slices (in place),
-                     // 3 integer column reduction with rows split over workgroups (atomic partials)
+                     // 3 integer column reduction with rows split over workgroups (atomic partials),
+                     // 4 integer column reduction into one dst run (a workgroup per 64 columns, LDS sum)
     bool sys;        // KK_ROWS: source in a peer GPU's memory (system-scope loads)
     int cw;          // variant 1: columns per workgroup of the LDS-staged kernel (0: one lane per column)
 };
@@ -806,6 +850,17 @@ static hipError_t dispatch_w(const Plan &p, const Desc &d, const OP &op, uint64_
             return hipGetLastError();
         }
         if (p.kind == KK_ORDERED) {
+            if (p.variant == 4) {           // integers into one dst run: per-workgroup LDS sums
+                if constexpr (std::is_same<OP, AccInt>::value || std::is_same<OP, AccLng>::value) {
+                    if constexpr (W == OP::kElem) {
+                        const dim3 grid((d.nvec + 63u) / 64u);
+                        if (d.levels == 1) hipLaunchKernelGGL((k_cols_sum<OP, 1>), grid, dim3(kColsSumWaves * 64), 0, st, d, op);
+                        else hipLaunchKernelGGL((k_cols_sum<OP, 0>), grid, dim3(kColsSumWaves * 64), 0, st, d, op);
+                        return hipGetLastError();
+                    }
+                }
+                return hipErrorInvalidValue;
+            }
             if (p.variant == 3) {           // integers: rows split over workgroups, atomic partials
                 if constexpr (std::is_same<OP, AccInt>::value || std::is_same<OP, AccLng>::value) {
                     if constexpr (W == OP::kElem) {
@@ -1222,8 +1277,15 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     // integer column reductions (COMEX_ACC_INT / _LNG, coinciding dst rows, no src row
     // meeting a dst row): rows split over workgroups with atomic partials -- wrapping
     // integer sums are exact in any order; device-scope atomics need the dst in HBM
-    bool cols_atomic = false;
-    if (cols && ov == OV_COLS && (op == 37 || op == 42) && tn.ordered_cols == 2 &&
+    bool cols_atomic = false, cols_sum = false;
+    if (cols && ov == OV_COLS && (op == 37 || op == 42) && tn.ordered_cols == 2) {
+        // every row into one dst run: the dst strides of all row levels are zero
+        cols_sum = true;
+        for (int j = 0; j < L; ++j) cols_sum = cols_sum && ds[j] == 0;
+        if (cols_sum && ((uint64_t)(uintptr_t)dst & (esz - 1)) == 0) W = esz;
+        else cols_sum = false;
+    }
+    if (!cols_sum && cols && ov == OV_COLS && (op == 37 || op == 42) && tn.ordered_cols == 2 &&
         (row_end - row_begin) <= (uint64_t)kColsAtomicRows * 65535u && ((uint64_t)(uintptr_t)dst & (esz - 1)) == 0) {
         hipPointerAttribute_t at;
         memset(&at, 0, sizeof(at));
@@ -1284,7 +1346,7 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
     p.U = U;
     p.BS = BS;
     p.sys = src_peer;
-    p.variant = (kind == KK_ORDERED && cols) ? (cols_atomic ? 3 : (ov == OV_COLS ? 1 : 2)) : 0;
+    p.variant = (kind == KK_ORDERED && cols) ? (cols_sum ? 4 : (cols_atomic ? 3 : (ov == OV_COLS ? 1 : 2))) : 0;
     p.cw = (p.variant == 1 && tn.ordered_cols == 2 && (W <= 8 || esz == 16)) ? cols_per_group(d.nvec, W) : 0;
     const uint32_t per_chunk = (uint32_t)BS * (uint32_t)U;
     d.align_mask = 0;
@@ -1322,7 +1384,8 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
             blocks = (d.items + per - 1) / per;
         } else {
             d.items = nr;
-            if (p.variant == 3)   // (256-column chunks) x (row groups); the dispatcher builds the 2-D grid
+            if (p.variant == 4) blocks = (d.nvec + 63u) / 64u;   // 64 columns per workgroup, all rows
+            else if (p.variant == 3)   // (256-column chunks) x (row groups); the dispatcher builds the 2-D grid
                 blocks = (uint64_t)((d.nvec + 255u) / 256u) * ((nr + kColsAtomicRows - 1) / kColsAtomicRows);
             else if (p.cw) blocks = (d.nvec + (uint32_t)p.cw - 1) / (uint32_t)p.cw;   // CW column slices per workgroup
             else if (p.variant) blocks = (d.nvec + 63u) / 64u;                   // one wave per 64 column slices
@@ -1345,7 +1408,8 @@ int launch_strided(int op, const void *scale, const void *src, const int *src_st
         info->block = (kind == KK_ROWS) ? BS
                       : (kind == KK_FLAT ? flat_block_threads(W)
                                          : ((kind == KK_ORDERED && !p.variant) ? kOrderedBS
-                                            : (p.variant == 3 ? 256 : (p.cw ? KC_NW * 64 : 64))));
+                                            : (p.variant == 4 ? kColsSumWaves * 64
+                                               : (p.variant == 3 ? 256 : (p.cw ? KC_NW * 64 : 64)))));
         info->levels = L;
         info->aligned = d.align_mask ? 1 : 0;
         info->sys = src_peer ? 1 : 0;

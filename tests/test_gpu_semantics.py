@@ -146,8 +146,8 @@ def test_ordered_kernel_large_overlapping_rows(gpu_lib, oracle):
     column reduction): rows share bytes only column-wise, so each f64 column slice
     is walked in row order by one lane, its rows loaded by seven
     loader waves of the workgroup and applied from LDS by the eighth (VERDICT r3 item
-    5); int64, whose wrapping sums are exact in any order, splits the rows over
-    workgroups and adds their partials atomically.  Bit-exact against the oracle's
+    5); int64, whose wrapping sums are exact in any order, sums each column's rows
+    over the 16 waves of a workgroup and adds them in LDS.  Bit-exact against the oracle's
     sequential order for int64 and f64 (f64 is order-sensitive).  The
     rate counts PHYSICAL bytes -- the 128 MiB of src plus the 64 KiB dst run read and
     written once (the run stays in a register) -- not 3 x payload, for the default
@@ -169,8 +169,8 @@ def test_ordered_kernel_large_overlapping_rows(gpu_lib, oracle):
                 info = ga_amd.last_launch()
                 assert info["kind"] == "ordered", info
                 if variant == 2 and op == C.LNG:
-                    # integers: rows split over workgroups, atomic partials (unroll = variant 3)
-                    assert info["unroll"] == 3 and info["blocks"] == (w // 256) * (rows // 64), info
+                    # integers into one dst run: a 16-wave workgroup per 64 columns (unroll = variant 4)
+                    assert info["unroll"] == 4 and info["blocks"] == w // 64, info
                 else:
                     # 16 column slices per 8-wave LDS-staged workgroup / 64 per one-wave workgroup
                     assert info["unroll"] == 1 and info["blocks"] == w // (16 if variant == 2 else 64), info
