@@ -750,22 +750,30 @@ struct Plan {
 // per row segment (16 slices of 8 B, 32 of 4 B; a 16-byte element keeps 16).
 // Built for W = 4/8 and for 16-byte elements (W = 16); the column path never uses
 // 16-byte vectors for smaller elements, and W = 1/2 keep one lane per column.
+// One workgroup fits a CU (two 56 KiB LDS tiles) and its applier wave walks every
+// row whatever CW is, so a launch takes about ceil(workgroups / CUs) applier
+// passes: CW is the narrowest of 16/32/64 slices that keeps the workgroups within
+// one pass over the 256 CUs (8192 slices of a 64 KiB f64 row: 32), never below one
+// 128-byte line per row segment.
 static int cols_per_group(uint32_t nvec, int W) {
     if (W != 4 && W != 8 && W != 16) return 0;
-    if ((nvec + 63u) / 64u >= 256u) return 64;
-    return W == 4 ? 32 : 16;
+    int cw = W == 4 ? 32 : 16;
+    while (cw < 64 && (nvec + (uint32_t)cw - 1) / (uint32_t)cw > 256u) cw *= 2;
+    return cw;
 }
 
 template <class OP, int W, int LV>
 static void go_cols_lds(const Desc &d, const OP &op, int cw, uint64_t blocks, hipStream_t st) {
-    constexpr int NARROW = W == 4 ? 32 : 16;
     if constexpr ((W == 4 || W == 8) || (W == 16 && OP::kElem == 16)) {
         if (cw == 64)
             hipLaunchKernelGGL((k_ordered_cols_lds<OP, W, LV, 64>), dim3((uint32_t)blocks), dim3(KC_NW * 64), 0, st, d,
                                op);
-        else
-            hipLaunchKernelGGL((k_ordered_cols_lds<OP, W, LV, NARROW>), dim3((uint32_t)blocks), dim3(KC_NW * 64), 0,
-                               st, d, op);
+        else if (cw == 32)
+            hipLaunchKernelGGL((k_ordered_cols_lds<OP, W, LV, 32>), dim3((uint32_t)blocks), dim3(KC_NW * 64), 0, st, d,
+                               op);
+        else if constexpr (W >= 8)
+            hipLaunchKernelGGL((k_ordered_cols_lds<OP, W, LV, 16>), dim3((uint32_t)blocks), dim3(KC_NW * 64), 0, st, d,
+                               op);
     }
 }
 

@@ -172,8 +172,8 @@ def test_ordered_kernel_large_overlapping_rows(gpu_lib, oracle):
                     # integers into one dst run: a 16-wave workgroup per 64 columns (unroll = variant 4)
                     assert info["unroll"] == 4 and info["blocks"] == w // 64, info
                 else:
-                    # 16 column slices per 8-wave LDS-staged workgroup / 64 per one-wave workgroup
-                    assert info["unroll"] == 1 and info["blocks"] == w // (16 if variant == 2 else 64), info
+                    # 32 column slices per 8-wave LDS-staged workgroup / 64 per one-wave workgroup
+                    assert info["unroll"] == 1 and info["blocks"] == w // (32 if variant == 2 else 64), info
                 want = dst.copy()
                 oracle.accs(op, a, src, 0, [w * 8], want, 0, [0], [w * 8, rows], 1)
                 assert np.array_equal(db.download(np.uint8, dst.size), want), (op, variant)

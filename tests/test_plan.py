@@ -49,12 +49,12 @@ def test_coinciding_destination_rows_take_column_slices():
     """Rows that share bytes only at the same offset (a zero dst stride: every row
     into one run, a column reduction): 8-byte column slices, each walked in row order
     by one lane; the rows are loaded by seven loader waves of an
-    eight-wave workgroup and applied from LDS by the eighth: 64
-    slices per workgroup when that gives >= 256 workgroups, else 16 (one 128-byte line
-    per row segment)."""
+    eight-wave workgroup and applied from LDS by the eighth: the
+    narrowest of 16/32/64 slices per workgroup that keeps the workgroups within one
+    pass over the 256 CUs."""
     p = plan(DBL, SRC, [65536], DST, [0], [65536, 2048], 1)
     assert p["kind"] == "ordered" and p["unroll"] == 1 and p["width"] == 8
-    assert p["block"] == 512 and p["blocks"] == 65536 // 8 // 16
+    assert p["block"] == 512 and p["blocks"] == 65536 // 8 // 32
     p = plan(DBL, SRC, [262144], DST, [0], [262144, 64], 1)
     assert p["block"] == 512 and p["blocks"] == 262144 // 8 // 64
     # ordered_cols = 1: one lane per slice loading its own rows, one-wave workgroups
