@@ -98,8 +98,11 @@ void segments_release_blocks();   // the freed-segment cache and the quarantined
 bool vmm_enabled();                       // COMEX_AMD_SEGMENT_ALLOC=vmm
 size_t vmm_round(size_t bytes);           // to the allocation granularity
 void *vmm_alloc(size_t bytes, VmmBlock *b);                  // this GPU's HBM, exported (b->fd)
-void *vmm_import(int pid, int fd, size_t bytes, int q, VmmBlock *b);   // rank q's block
-void vmm_free(VmmBlock *b);               // unmap + release (the address range is never reused)
+void vmm_listen();                        // this process's descriptor socket (before the allgather)
+void vmm_exchange(int fd, int rank, uint64_t gen, const std::vector<int> &to_pids,
+                  const std::vector<std::pair<int, uint64_t>> &from, int *fds);   // SCM_RIGHTS both ways
+void *vmm_import(int myfd, size_t bytes, int q, VmmBlock *b);   // rank q's block
+void vmm_free(VmmBlock *b);               // unmap + release + the virtual range back
 void vmm_finalize();
 
 // ---- remote operations through the owner (remote.cpp) -----------------------

@@ -306,6 +306,7 @@ int segment_kind(const void *p);
 // comex.cpp: the device-address history a refused IPC export prints (kind: a alloc,
 // f free, x export, o IPC map, c IPC unmap; peer = the other rank, -1 none)
 void addr_event(char kind, const void *p, size_t bytes, int peer);
+void addr_history(const void *p, size_t bytes);   // the logged events touching a range, to stderr
 
 // comex.cpp helpers shared with armci.cpp / armci_msg.cpp
 int translate_world(int group, int proc);

@@ -75,7 +75,7 @@ uint64_t seg_tag(int rank, uint64_t gen, int end) {
 
 static std::vector<void *> g_quarantine;   // blocks whose IPC export was refused (freed at finalize)
 
-static void addr_history(const void *p, size_t bytes) {
+void addr_history(const void *p, size_t bytes) {
     std::lock_guard<std::mutex> g(g_addr_mu);
     const uintptr_t lo = (uintptr_t)p, hi = lo + bytes;
     int n = 0;
@@ -468,7 +468,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         int32_t device, host;    // host: a node shm segment, `name` below
         uint64_t gen;
         char name[64];
-        int32_t vmm, pid, fd, pad;   // vmm: HBM from vmm.cpp, descriptor `fd` of process `pid`
+        int32_t vmm, pid, fd, pad;   // vmm: HBM from vmm.cpp; pid: the process its descriptor comes from
         uint64_t vmm_bytes;
     } mine;
     memset(&mine, 0, sizeof(mine));
@@ -478,11 +478,12 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     const size_t map_bytes = page_round(bytes);
     const bool vmm = device && vmm_enabled();
     VmmBlock vlocal;
+    if (vmm) vmm_listen();
+    mine.pid = (int32_t)getpid();
     if (bytes) {
         if (vmm) {
             p = vmm_alloc(bytes, &vlocal);
             mine.vmm = 1;
-            mine.pid = (int32_t)getpid();
             mine.fd = vlocal.fd;
             mine.vmm_bytes = vlocal.bytes;
         } else if (device) {
@@ -535,6 +536,24 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
             if (gathered[k].bytes && !gathered[k].host && !gathered[k].vmm)
                 handle_seen(members[k], gathered[k].gen, gathered[k].base, gathered[k].bytes, gathered[k].h);
         }
+        // vmm: each member's descriptor passed to the other members on this node
+        std::vector<int> vfd(r.size, -1);
+        if (vmm) {
+            std::vector<int> to;
+            std::vector<std::pair<int, uint64_t>> from;
+            std::vector<int> from_rank;
+            for (int q : members) {
+                if (q == r.rank || !r.same_node(q)) continue;
+                if (mine.vmm) to.push_back(all[q].pid);   // zero-byte members map it too
+                if (all[q].vmm && all[q].bytes) {
+                    from.push_back({q, all[q].gen});
+                    from_rank.push_back(q);
+                }
+            }
+            std::vector<int> got(from.size(), -1);
+            vmm_exchange(vlocal.fd, r.rank, mine.gen, to, from, got.data());
+            for (size_t k = 0; k < from.size(); ++k) vfd[from_rank[k]] = got[k];
+        }
         // open, and check that each IPC mapping reads its owner's tags
         std::vector<uint8_t> stale(r.size, 0);
         for (int q = 0; q < r.size; ++q) {
@@ -547,7 +566,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
             }
             if (all[q].vmm) {    // the owner's dmabuf descriptor, mapped at a fresh address here
                 if (vpeer.size() != (size_t)r.size) vpeer.assign(r.size, VmmBlock());
-                mapped[q] = vmm_import(all[q].pid, all[q].fd, all[q].vmm_bytes, q, &vpeer[q]);
+                mapped[q] = vmm_import(vfd[q], all[q].vmm_bytes, q, &vpeer[q]);
             } else {
                 mapped[q] = ipc_open(all[q].h, q, "segment");
             }
@@ -557,11 +576,11 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
             GA_HIP(hipMemcpy(&t[1], (char *)mapped[q] + all[q].bytes - 8, 8, hipMemcpyDeviceToHost));
             if (t[0] != seg_tag(q, all[q].gen, 0) || t[1] != seg_tag(q, all[q].gen, 1)) {
                 stale[q] = 1;
-                fprintf(stderr, "[ga_amd %d] the IPC mapping of rank %d's new %zu-byte segment (%p in its space) "
-                        "reads %#llx / %#llx, not its tags: another allocation's memory\n", r.rank, q,
+                fprintf(stderr, "[ga_amd %d] the %s mapping of rank %d's new %zu-byte segment (%p in its space) "
+                        "reads %#llx / %#llx, not its tags: another allocation's memory\n", r.rank, all[q].vmm ? "vmm" : "IPC", q,
                         (size_t)all[q].bytes, (void *)(uintptr_t)all[q].base, (unsigned long long)t[0],
                         (unsigned long long)t[1]);
-                report_stale(q, all[q].gen, all[q].base, all[q].bytes, all[q].h, t[0]);
+                if (!all[q].vmm) report_stale(q, all[q].gen, all[q].base, all[q].bytes, all[q].h, t[0]);
             }
         }
         std::vector<uint8_t> seen(members.size() * (size_t)r.size);
@@ -574,7 +593,10 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
                     if (q == r.rank) mine_stale = true;
                 }
         if (!any) break;
-        if (vmm) fatal("a mapping of a new segment of the virtual-memory allocator does not read its owner's tags");
+        if (vmm) {
+            if (mine_stale) addr_history(p, bytes);
+            fatal("a mapping of a new segment of the virtual-memory allocator does not read its owner's tags");
+        }
         if (attempt >= 3) fatal("IPC mappings of a new segment keep reaching other memory (4 attempts)");
         for (int q = 0; q < r.size; ++q)
             if (mapped[q]) ipc_close(mapped[q], q);
@@ -745,7 +767,7 @@ int comex_free(void *ptr, comex_group_t group) {
     // (hipIpcGetMemHandle: invalid argument in the next comex_malloc)
     members_barrier(members, group);
     if (is_vmm) {
-        vmm_free(&vblock);   // physical memory back now; the address range is never reused
+        vmm_free(&vblock);   // physical memory back now
     } else if (local && device) {
         if (block_cache_cap()) block_put(local, local_bytes, exported, handle);   // kept for the next comex_malloc
         else block_free_one({local, local_bytes, exported, handle});

@@ -10,37 +10,36 @@
 // away from the runtime:
 //   * physical HBM from hipMemCreate, exported as a dmabuf file descriptor
 //     (hipMemExportToShareableHandle, POSIX fd);
-//   * the descriptor reaches a peer process through pidfd_getfd (the owner's pid
-//     and descriptor number travel in the comex_malloc allgather, as reg_entry_t
-//     does at comex.c:2461) and is imported there (hipMemImportFromShareableHandle);
-//   * every mapping -- the owner's and each peer's -- goes to virtual addresses this
-//     library reserved itself and NEVER hands out twice in the process's life (a bump
-//     allocator over reserved chunks), so no export or import ever meets an address
-//     the runtime has seen before.
+//   * the descriptor reaches each peer process as SCM_RIGHTS ancillary data on a
+//     datagram socket of the abstract namespace, one per process, named after its
+//     pid (the pid and allocation number travel in the comex_malloc allgather, as
+//     reg_entry_t does at comex.c:2461), and is imported there
+//     (hipMemImportFromShareableHandle).  pidfd_getfd was the first carrier; it
+//     needs ptrace rights over the owner, which the box's Yama policy refuses
+//     between sibling ranks (EPERM, gpurun_out r04s03), so it was dropped;
+//   * every mapping -- the owner's and each peer's -- goes to a virtual range this
+//     library reserved for it and does not reserve again afterwards, and what a peer maps is named by the descriptor it
+//     received for (owner rank, allocation number), never by an address: no runtime
+//     bookkeeping keyed by recycled addresses is involved.
 // COMEX_AMD_SEGMENT_ALLOC=vmm selects it (ipc: hipMalloc + hipIpc*, the round-3 path).
 #include "comex_impl.hpp"
 #include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
-#include <sys/syscall.h>
+#include <stddef.h>
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <time.h>
 #include <unistd.h>
+#include <map>
 #include <mutex>
 #include <vector>
-
-#ifndef SYS_pidfd_open
-#define SYS_pidfd_open 434
-#endif
-#ifndef SYS_pidfd_getfd
-#define SYS_pidfd_getfd 438
-#endif
 
 namespace gaamd {
 
 namespace {
 std::mutex g_vmm_mu;
-struct Chunk { char *base; size_t bytes, used; };
-std::vector<Chunk> g_chunks;            // reserved virtual ranges, never released before finalize
 size_t g_gran = 0;
 
 size_t granularity() {
@@ -57,31 +56,134 @@ size_t granularity() {
     return g_gran;
 }
 
-// a fresh virtual range of `bytes` (a multiple of the granularity), never used before
+// Each mapping gets a virtual range of its own, and a range is not reserved again
+// after its mapping is gone: it stays reserved (retired) until the retired total
+// passes COMEX_AMD_VMM_RETAIN_GB (default 16384 = 16 TiB of the 128 TiB user space),
+// oldest first.  Both halves are measured (gpurun_out r04s05): mappings bump-allocated
+// out of one shared 256 GiB reservation failed hipMemSetAccess once a mapping in it
+// had been unmapped, and a fresh mapping at a just-released range read the end of
+// the PREVIOUS mapping there (its first bytes were right) -- the runtime resolves an
+// address to a mapping through bookkeeping that a recycled range confuses.
+struct Retired { char *va; size_t bytes; };
+std::vector<Retired> g_retired;
+size_t g_retired_bytes = 0;
+
+size_t retain_cap() {
+    static const size_t cap = [] {
+        const char *e = getenv("COMEX_AMD_VMM_RETAIN_GB");
+        return (size_t)(e ? atoll(e) : 16384) << 30;
+    }();
+    return cap;
+}
+
 char *va_take(size_t bytes) {
-    std::lock_guard<std::mutex> g(g_vmm_mu);
-    const size_t gr = granularity();
-    for (Chunk &c : g_chunks) {
-        if (c.bytes - c.used >= bytes) {
-            char *p = c.base + c.used;
-            c.used += bytes;   // bump only: a range is never handed out again
-            return p;
-        }
-    }
-    const size_t chunk = std::max<size_t>((bytes + gr - 1) / gr * gr, 256ull << 30);
     void *base = nullptr;
-    GA_HIP(hipMemAddressReserve(&base, chunk, gr, nullptr, 0));
-    g_chunks.push_back({(char *)base, chunk, bytes});
+    GA_HIP(hipMemAddressReserve(&base, bytes, granularity(), nullptr, 0));
     return (char *)base;
 }
 
-void set_access(char *va, size_t bytes) {
+void va_retire(char *va, size_t bytes) {
+    std::lock_guard<std::mutex> g(g_vmm_mu);
+    g_retired.push_back({va, bytes});
+    g_retired_bytes += bytes;
+    size_t k = 0;
+    while (g_retired_bytes > retain_cap() && k < g_retired.size()) {
+        (void)hipMemAddressFree(g_retired[k].va, g_retired[k].bytes);
+        g_retired_bytes -= g_retired[k].bytes;
+        ++k;
+    }
+    g_retired.erase(g_retired.begin(), g_retired.begin() + k);
+}
+
+// the descriptor exchange: one datagram socket per process, abstract namespace
+int g_sock = -1;
+std::map<std::pair<int, uint64_t>, int> g_stash;   // (rank, allocation number) -> descriptor received early
+
+struct FdMsg {
+    int32_t rank, pad;
+    uint64_t gen;
+};
+
+socklen_t sock_addr(int pid, sockaddr_un *a) {
+    memset(a, 0, sizeof(*a));
+    a->sun_family = AF_UNIX;
+    const int n = snprintf(a->sun_path + 1, sizeof(a->sun_path) - 1, "gaamd_vmm_%d_%d", (int)getuid(), pid);
+    return (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + n);
+}
+
+double now_s() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+bool send_fd(int pid, int fd, int rank, uint64_t gen) {
+    sockaddr_un a;
+    const socklen_t alen = sock_addr(pid, &a);
+    FdMsg m{rank, 0, gen};
+    iovec io{&m, sizeof(m)};
+    alignas(cmsghdr) char ctl[CMSG_SPACE(sizeof(int))];
+    memset(ctl, 0, sizeof(ctl));
+    msghdr h;
+    memset(&h, 0, sizeof(h));
+    h.msg_name = &a;
+    h.msg_namelen = alen;
+    h.msg_iov = &io;
+    h.msg_iovlen = 1;
+    h.msg_control = ctl;
+    h.msg_controllen = sizeof(ctl);
+    cmsghdr *c = CMSG_FIRSTHDR(&h);
+    c->cmsg_level = SOL_SOCKET;
+    c->cmsg_type = SCM_RIGHTS;
+    c->cmsg_len = CMSG_LEN(sizeof(int));
+    memcpy(CMSG_DATA(c), &fd, sizeof(int));
+    if (sendmsg(g_sock, &h, MSG_DONTWAIT) == (ssize_t)sizeof(m)) return true;
+    if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) return false;   // the peer's queue is full
+    fatal("sending a segment descriptor to process %d failed: %s", pid, strerror(errno));
+}
+
+// one received descriptor into the stash; false when none is waiting
+bool recv_fd() {
+    FdMsg m;
+    iovec io{&m, sizeof(m)};
+    alignas(cmsghdr) char ctl[CMSG_SPACE(sizeof(int))];
+    msghdr h;
+    memset(&h, 0, sizeof(h));
+    h.msg_iov = &io;
+    h.msg_iovlen = 1;
+    h.msg_control = ctl;
+    h.msg_controllen = sizeof(ctl);
+    const ssize_t n = recvmsg(g_sock, &h, MSG_DONTWAIT | MSG_CMSG_CLOEXEC);
+    if (n < 0) {
+        if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) return false;
+        fatal("receiving a segment descriptor failed: %s", strerror(errno));
+    }
+    int fd = -1;
+    for (cmsghdr *c = CMSG_FIRSTHDR(&h); c; c = CMSG_NXTHDR(&h, c))
+        if (c->cmsg_level == SOL_SOCKET && c->cmsg_type == SCM_RIGHTS) memcpy(&fd, CMSG_DATA(c), sizeof(int));
+    if (n != (ssize_t)sizeof(m) || fd < 0 || (h.msg_flags & MSG_CTRUNC))
+        fatal("a malformed segment-descriptor message (%zd bytes, descriptor %d)", n, fd);
+    const auto key = std::make_pair((int)m.rank, m.gen);
+    if (g_stash.count(key)) fatal("rank %d sent the descriptor of its allocation %llu twice", m.rank,
+                                  (unsigned long long)m.gen);
+    g_stash[key] = fd;
+    return true;
+}
+
+void set_access(char *va, size_t bytes, int q) {
     hipMemAccessDesc d;
     memset(&d, 0, sizeof(d));
     d.location.type = hipMemLocationTypeDevice;
     d.location.id = rt().device;
     d.flags = hipMemAccessFlagsProtReadWrite;
-    GA_HIP(hipMemSetAccess(va, bytes, &d, 1));
+    const hipError_t e = hipMemSetAccess(va, bytes, &d, 1);
+    if (e != hipSuccess) {
+        fprintf(stderr, "[ga_amd %d] hipMemSetAccess(%p, %zu bytes) of %s failed: %s\n", rt().rank, (void *)va,
+                bytes, q < 0 ? "a new block of this rank" : "an imported block", hipGetErrorString(e));
+        if (q >= 0) fprintf(stderr, "[ga_amd %d]   imported from rank %d\n", rt().rank, q);
+        addr_history(va, bytes);
+        fatal("hipMemSetAccess failed");
+    }
 }
 }  // namespace
 
@@ -118,7 +220,7 @@ void *vmm_alloc(size_t bytes, VmmBlock *b) {
     if (e != hipSuccess) fatal("hipMemCreate of %zu bytes failed: %s", n, hipGetErrorString(e));
     char *va = va_take(n);
     GA_HIP(hipMemMap(va, n, 0, h, 0));
-    set_access(va, n);
+    set_access(va, n, -1);
     int fd = -1;
     GA_HIP(hipMemExportToShareableHandle(&fd, h, hipMemHandleTypePosixFileDescriptor, 0));
     b->va = va;
@@ -130,20 +232,72 @@ void *vmm_alloc(size_t bytes, VmmBlock *b) {
     return va;
 }
 
-// rank q's block: descriptor `fd` in process `pid`, `bytes` (granularity-rounded)
-void *vmm_import(int pid, int fd, size_t bytes, int q, VmmBlock *b) {
-    const int pidfd = (int)syscall(SYS_pidfd_open, pid, 0);
-    if (pidfd < 0) fatal("pidfd_open(%d) for rank %d's segment failed: %s", pid, q, strerror(errno));
-    const int myfd = (int)syscall(SYS_pidfd_getfd, pidfd, fd, 0);
-    close(pidfd);
-    if (myfd < 0) fatal("pidfd_getfd(rank %d's descriptor %d) failed: %s", q, fd, strerror(errno));
+// this process's descriptor socket; bound before the comex_malloc allgather, so a
+// peer that has the allgather's result can send to it
+void vmm_listen() {
+    std::lock_guard<std::mutex> g(g_vmm_mu);
+    if (g_sock >= 0) return;
+    g_sock = socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC, 0);
+    if (g_sock < 0) fatal("socket(AF_UNIX) for segment descriptors failed: %s", strerror(errno));
+    sockaddr_un a;
+    const socklen_t alen = sock_addr((int)getpid(), &a);
+    if (bind(g_sock, (sockaddr *)&a, alen) != 0) fatal("binding the segment-descriptor socket failed: %s", strerror(errno));
+}
+
+// send `fd` (allocation `gen` of `rank`) to every process in `to_pids` and receive
+// the descriptor of each (rank, allocation) in `from`, into fds[k]; both sides
+// progress together (non-blocking sends, a full peer queue retried), so no pair of
+// ranks waits on each other
+void vmm_exchange(int fd, int rank, uint64_t gen, const std::vector<int> &to_pids,
+                  const std::vector<std::pair<int, uint64_t>> &from, int *fds) {
+    std::lock_guard<std::mutex> g(g_vmm_mu);
+    if (g_sock < 0) fatal("vmm_exchange before vmm_listen");
+    std::vector<uint8_t> sent(to_pids.size(), 0);
+    size_t nsent = 0, ngot = 0;
+    for (size_t k = 0; k < from.size(); ++k) fds[k] = -1;
+    const double t0 = now_s();
+    for (;;) {
+        bool moved = false;
+        for (size_t k = 0; k < to_pids.size(); ++k)
+            if (!sent[k] && send_fd(to_pids[k], fd, rank, gen)) {
+                sent[k] = 1;
+                ++nsent;
+                moved = true;
+            }
+        while (recv_fd()) moved = true;
+        ngot = 0;
+        for (size_t k = 0; k < from.size(); ++k) {
+            if (fds[k] < 0) {
+                auto it = g_stash.find(from[k]);
+                if (it != g_stash.end()) {
+                    fds[k] = it->second;
+                    g_stash.erase(it);
+                }
+            }
+            ngot += fds[k] >= 0;
+        }
+        if (nsent == to_pids.size() && ngot == from.size()) return;
+        if (now_s() - t0 > 120.0) {
+            for (size_t k = 0; k < from.size(); ++k)
+                if (fds[k] < 0) fprintf(stderr, "[ga_amd %d] no descriptor from rank %d (allocation %llu)\n", rank,
+                                        from[k].first, (unsigned long long)from[k].second);
+            fatal("segment-descriptor exchange: %zu of %zu sent, %zu of %zu received in 120 s", nsent,
+                  to_pids.size(), ngot, from.size());
+        }
+        if (!moved) usleep(20);
+    }
+}
+
+// rank q's block: `myfd` (this process's descriptor of it, from vmm_exchange, owned
+// by b from here on), `bytes` (granularity-rounded)
+void *vmm_import(int myfd, size_t bytes, int q, VmmBlock *b) {
     hipMemGenericAllocationHandle_t h;
     // the descriptor is passed by value, as the POSIX-fd handle type is documented
     // for the driver API this one mirrors
     GA_HIP(hipMemImportFromShareableHandle(&h, (void *)(uintptr_t)myfd, hipMemHandleTypePosixFileDescriptor));
     char *va = va_take(bytes);
     GA_HIP(hipMemMap(va, bytes, 0, h, 0));
-    set_access(va, bytes);
+    set_access(va, bytes, q);
     b->va = va;
     b->bytes = bytes;
     b->handle = h;
@@ -153,22 +307,29 @@ void *vmm_import(int pid, int fd, size_t bytes, int q, VmmBlock *b) {
     return va;
 }
 
-// unmap and release; the virtual range stays reserved (never reused)
+// unmap and release; the virtual range is retired, not reserved again
 void vmm_free(VmmBlock *b) {
     if (!b->va) return;
     addr_event(b->imported ? 'c' : 'f', b->va, b->bytes, -1);
     GA_HIP(hipMemUnmap(b->va, b->bytes));
     GA_HIP(hipMemRelease(b->handle));
+    va_retire(b->va, b->bytes);
     if (b->fd >= 0) close(b->fd);
     b->va = nullptr;
     b->fd = -1;
 }
 
-// comex_finalize: the reserved ranges (every mapping is gone by then)
+// comex_finalize: the retired ranges and the descriptor socket (every mapping is
+// gone by then)
 void vmm_finalize() {
     std::lock_guard<std::mutex> g(g_vmm_mu);
-    for (const Chunk &c : g_chunks) (void)hipMemAddressFree(c.base, c.bytes);
-    g_chunks.clear();
+    for (const Retired &x : g_retired) (void)hipMemAddressFree(x.va, x.bytes);
+    g_retired.clear();
+    g_retired_bytes = 0;
+    for (auto &kv : g_stash) close(kv.second);
+    g_stash.clear();
+    if (g_sock >= 0) close(g_sock);
+    g_sock = -1;
 }
 
 }  // namespace gaamd

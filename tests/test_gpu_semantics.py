@@ -161,6 +161,11 @@ def test_ordered_kernel_large_overlapping_rows(gpu_lib, oracle):
         dst = C.fill_bytes(op, w * 8, 6)
         sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
         sb.upload(src)
+        # three source copies (384 MiB), rotated: the timed launches read HBM, not the
+        # 256 MiB last-level cache
+        rot = [sb] + [ga_amd.DeviceBuffer(src.size) for _ in range(2)]
+        for b in rot[1:]:
+            b.upload(src)
         for variant in (2, 1):
             oldv = ga_amd.set_tuning("ordered_cols", variant)
             try:
@@ -169,8 +174,11 @@ def test_ordered_kernel_large_overlapping_rows(gpu_lib, oracle):
                 info = ga_amd.last_launch()
                 assert info["kind"] == "ordered", info
                 if variant == 2 and op == C.LNG:
-                    # integers into one dst run: a 16-wave workgroup per 64 columns (unroll = variant 4)
-                    assert info["unroll"] == 4 and info["blocks"] == w // 64, info
+                    # integers into one dst run (unroll = variant 4): 4 KiB row pieces per
+                    # workgroup x row slices of >= 32 rows, about 1024 workgroups
+                    gx = -(-w * 8 // 16 // 256)
+                    sl = min(-(-1024 // gx), -(-rows // 32))
+                    assert info["unroll"] == 4 and info["width"] == 16 and info["blocks"] == gx * sl, info
                 else:
                     # 32 column slices per 8-wave LDS-staged workgroup / 64 per one-wave workgroup
                     assert info["unroll"] == 1 and info["blocks"] == w // (32 if variant == 2 else 64), info
@@ -185,10 +193,10 @@ def test_ordered_kernel_large_overlapping_rows(gpu_lib, oracle):
                     ev0, ev1 = L.gaamd_event_create(), L.gaamd_event_create()
                     st = L.gaamd_stream()
                     L.gaamd_event_record(ev0, st)
-                    for _ in range(10):
+                    for i in range(10):
                         h = ctypes.c_int(-1)
-                        assert L.comex_nbaccs(op, sp, ctypes.c_void_p(sb.ptr), ss, ctypes.c_void_p(db.ptr), ds, cnt,
-                                              1, 0, 0, ctypes.byref(h)) == 0
+                        assert L.comex_nbaccs(op, sp, ctypes.c_void_p(rot[i % 3].ptr), ss, ctypes.c_void_p(db.ptr),
+                                              ds, cnt, 1, 0, 0, ctypes.byref(h)) == 0
                     L.gaamd_event_record(ev1, st)
                     assert L.comex_wait_all(0) == 0
                     ms = L.gaamd_event_elapsed_ms(ev0, ev1) / 10
@@ -202,7 +210,8 @@ def test_ordered_kernel_large_overlapping_rows(gpu_lib, oracle):
             rates[(op, variant)] = gbs
             print(f"column-ordered kernel op {op} ordered_cols={variant}: {ms * 1e3:.0f} us per launch = "
                   f"{gbs:.0f} GB/s physical ({3 * rows * w * 8 / (ms * 1e-3) / 1e9:.0f} GB/s as 3 x payload)")
-        sb.free()
+        for b in rot:
+            b.free()
         db.free()
     # int64 >= 4 TB/s physical, f64 >= 2 x the 0.63 TB/s of round 3
     assert rates[(C.LNG, 2)] > 500 and rates[(C.DBL, 2)] > 500, rates
@@ -272,6 +281,51 @@ def test_column_ordered_kernel_geometries(gpu_lib, oracle, op):
                 assert np.array_equal(got, want), (op, cols, count, ss, ds, so, do)
         finally:
             ga_amd.set_tuning("ordered_cols", old)
+
+
+@pytest.mark.parametrize("op", [C.INT, C.LNG])
+def test_integer_column_reductions(gpu_lib, oracle, op):
+    """The integer column paths of ordered_cols = 2 against the
+    oracle's sequential order, bit-exact (wrapping sums): variant 4 -- every row into
+    one dst run, 4 KiB row pieces per workgroup, row slices with atomic partials --
+    on 2-D and 3-D (planes into one run) patches, ragged rows (37, 2049: slices of
+    unequal length), rows narrower than one workgroup (150 lanes of 256); variant 3
+    (rows split over workgroups, atomic partials per dst run) for a source off 16
+    bytes and for planes each summed into a run of its own."""
+    e = C.ESZ[op]
+    rng = np.random.default_rng(900 + op)
+    scale = C.SCALE[op]
+    w = 1000 * e
+    geos = [  # count, src strides, dst strides, src offset, variant
+        ([w, 37], [w + 8 * e], [0], 0, 4),
+        ([w, 6, 5], [w, w * 6], [0, 0], 0, 4),
+        ([2400, 2049], [4096], [0], 0, 4),
+        ([w, 64], [w + 8 * e], [0], e, 3),
+        ([w, 6, 5], [w, w * 6], [0, w + 4 * e], 0, 3),
+    ]
+    old = ga_amd.set_tuning("ordered_cols", 2)
+    try:
+        for count, ss, ds, so, variant in geos:
+            levels = len(ss)
+            sbytes = so + C.span(ss, count, levels)[1] + 64
+            dbytes = C.span(ds, count, levels)[1] + 64
+            src = C.fill_bytes(op, sbytes, int(rng.integers(1, 1 << 30)))
+            dst = C.fill_bytes(op, dbytes, int(rng.integers(1, 1 << 30)))
+            sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+            sb.upload(src)
+            db.upload(dst)
+            assert ga_amd.comex_accs(op, scale, sb.ptr + so, ss, db.ptr, ds, count, levels, 0) == 0
+            info = ga_amd.last_launch()
+            ga_amd.comex_fence_all()
+            want = dst.copy()
+            oracle.accs(op, scale, src, so, ss, want, 0, ds, count, levels)
+            got = db.download(np.uint8, dst.size)
+            sb.free()
+            db.free()
+            assert info["kind"] == "ordered" and info["unroll"] == variant, (info, count, ss, ds, so)
+            assert np.array_equal(got, want), (op, count, ss, ds, so)
+    finally:
+        ga_amd.set_tuning("ordered_cols", old)
 
 
 def test_blocking_accs_returns_after_src_is_consumed(gpu_lib, oracle):

@@ -358,11 +358,11 @@ def test_owner_host_source_self_acc_vs_one_pass_peers(n):
 def test_vmm_segments(mode, n, extra):
     """HBM segments from the virtual-memory allocator
     (COMEX_AMD_SEGMENT_ALLOC=vmm, vmm.cpp) -- hipMemCreate + a dmabuf descriptor
-    handed to the peers with pidfd_getfd, every mapping at an address range this
-    process never used before -- under the remote suite, the one-pass and
+    handed to the peers over a per-process socket (SCM_RIGHTS), keyed by owner rank
+    and allocation number -- under the remote suite, the one-pass and
     direct-source routes, create/free cycles, random programs and C5 (one GPU, and
     with every peer treated as another GPU), all exact."""
-    launch(mode, n=n, timeout=300, extra_env=dict(extra, COMEX_AMD_SEGMENT_ALLOC="vmm"))
+    launch(mode, n=n, timeout=150, extra_env=dict(extra, COMEX_AMD_SEGMENT_ALLOC="vmm"))
 
 
 @pytest.mark.gpu

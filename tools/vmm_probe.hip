@@ -1,0 +1,179 @@
+// vmm_probe.hip -- two processes, HIP's virtual-memory API, segment create/free cycles
+// as GA's create/destroy drives them (the comex_malloc / comex_free of the vmm
+// allocator, ga_amd/csrc/vmm.cpp), every step's result printed.
+//
+// The parent allocates (hipMemCreate + reserve + map + access), writes a tag at both
+// ends, exports a dmabuf descriptor and passes it to the child over a socketpair
+// (SCM_RIGHTS); the child imports, maps, reads both tags, and each side unmaps and
+// releases before the next round.  Variants (argv[1]):
+//   close   the child closes its received descriptor right after the import
+//   keep    the child closes it only when the mapping goes (what vmm.cpp does)
+//   dupfar  the child moves the descriptor to a number it never used before
+//   retain  as keep, and neither side releases its virtual ranges
+//   mix     as retain, each round first doing a hipMalloc + hipFree of the same size
+//           on both sides (GA's scratch buffers between create/destroy cycles)
+// The sockets are made before either process touches the GPU (fork before HIP).
+//
+// hipcc --offload-arch=gfx950 -O2 -o tools/vmm_probe tools/vmm_probe.hip
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#define CK(x)                                                                                    \
+    do {                                                                                         \
+        hipError_t e_ = (x);                                                                     \
+        if (e_ != hipSuccess) {                                                                  \
+            printf("[%s] %s -> %s\n", who, #x, hipGetErrorString(e_));                           \
+            fflush(stdout);                                                                      \
+            ok = false;                                                                          \
+        }                                                                                        \
+    } while (0)
+
+static const char *who = "?";
+static bool ok = true;
+
+static void send_fd(int s, int fd, int round) {
+    char ctl[CMSG_SPACE(sizeof(int))];
+    memset(ctl, 0, sizeof(ctl));
+    iovec io{&round, sizeof(round)};
+    msghdr h{};
+    h.msg_iov = &io;
+    h.msg_iovlen = 1;
+    h.msg_control = ctl;
+    h.msg_controllen = sizeof(ctl);
+    cmsghdr *c = CMSG_FIRSTHDR(&h);
+    c->cmsg_level = SOL_SOCKET;
+    c->cmsg_type = SCM_RIGHTS;
+    c->cmsg_len = CMSG_LEN(sizeof(int));
+    memcpy(CMSG_DATA(c), &fd, sizeof(int));
+    if (sendmsg(s, &h, 0) < 0) perror("sendmsg");
+}
+
+static int recv_fd(int s, int *round) {
+    char ctl[CMSG_SPACE(sizeof(int))];
+    iovec io{round, sizeof(*round)};
+    msghdr h{};
+    h.msg_iov = &io;
+    h.msg_iovlen = 1;
+    h.msg_control = ctl;
+    h.msg_controllen = sizeof(ctl);
+    if (recvmsg(s, &h, 0) <= 0) return -1;
+    int fd = -1;
+    for (cmsghdr *c = CMSG_FIRSTHDR(&h); c; c = CMSG_NXTHDR(&h, c))
+        if (c->cmsg_type == SCM_RIGHTS) memcpy(&fd, CMSG_DATA(c), sizeof(int));
+    return fd;
+}
+
+static hipMemAllocationProp prop_of() {
+    hipMemAllocationProp p;
+    memset(&p, 0, sizeof(p));
+    p.type = hipMemAllocationTypePinned;
+    p.location.type = hipMemLocationTypeDevice;
+    p.location.id = 0;
+    p.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
+    return p;
+}
+
+static void access_rw(void *va, size_t n) {
+    hipMemAccessDesc d;
+    memset(&d, 0, sizeof(d));
+    d.location.type = hipMemLocationTypeDevice;
+    d.location.id = 0;
+    d.flags = hipMemAccessFlagsProtReadWrite;
+    CK(hipMemSetAccess(va, n, &d, 1));
+}
+
+int main(int argc, char **argv) {
+    const char *mode = argc > 1 ? argv[1] : "keep";
+    const int rounds = argc > 2 ? atoi(argv[2]) : 6;
+    const size_t n = argc > 3 ? strtoull(argv[3], nullptr, 0) : (2u << 20);
+    const bool mix = !strcmp(mode, "mix");
+    const bool retain = !strcmp(mode, "retain") || mix;
+    int sv[2], ack[2];
+    if (socketpair(AF_UNIX, SOCK_DGRAM, 0, sv) || socketpair(AF_UNIX, SOCK_DGRAM, 0, ack)) return 2;
+    const pid_t child = fork();
+    if (child < 0) return 2;
+    who = child ? "owner" : "peer";
+    CK(hipSetDevice(0));
+    hipMemAllocationProp prop = prop_of();
+    size_t gran = 0;
+    CK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+    if (child) printf("mode %s, %d rounds of %zu bytes, granularity %zu\n", mode, rounds, n, gran);
+    int far = 900;
+    for (int r = 0; r < rounds; ++r) {
+        if (mix) {
+            void *tmp = nullptr;
+            CK(hipMalloc(&tmp, n));
+            printf("[%s] round %d: hipMalloc scratch at %p (freed)\n", who, r, tmp);
+            CK(hipFree(tmp));
+        }
+        if (child) {
+            hipMemGenericAllocationHandle_t h;
+            CK(hipMemCreate(&h, n, &prop, 0));
+            void *va = nullptr;
+            CK(hipMemAddressReserve(&va, n, gran, nullptr, 0));
+            CK(hipMemMap(va, n, 0, h, 0));
+            access_rw(va, n);
+            const uint64_t t0 = 0x1000 + r, t1 = 0x2000 + r;
+            CK(hipMemcpy(va, &t0, 8, hipMemcpyHostToDevice));
+            CK(hipMemcpy((char *)va + n - 8, &t1, 8, hipMemcpyHostToDevice));
+            int fd = -1;
+            CK(hipMemExportToShareableHandle(&fd, h, hipMemHandleTypePosixFileDescriptor, 0));
+            printf("[owner] round %d: va %p, descriptor %d\n", r, va, fd);
+            fflush(stdout);
+            send_fd(sv[0], fd, r);
+            int a = 0;
+            if (recv(ack[0], &a, sizeof(a), 0) <= 0) break;
+            CK(hipMemUnmap(va, n));
+            CK(hipMemRelease(h));
+            if (!retain) CK(hipMemAddressFree(va, n));
+            close(fd);
+        } else {
+            int rr = -1;
+            int fd = recv_fd(sv[1], &rr);
+            if (fd < 0) break;
+            if (!strcmp(mode, "dupfar")) {
+                const int f2 = fcntl(fd, F_DUPFD_CLOEXEC, far++);
+                close(fd);
+                fd = f2;
+            }
+            hipMemGenericAllocationHandle_t h;
+            CK(hipMemImportFromShareableHandle(&h, (void *)(uintptr_t)fd, hipMemHandleTypePosixFileDescriptor));
+            if (!strcmp(mode, "close")) {
+                close(fd);
+                fd = -1;
+            }
+            void *va = nullptr;
+            CK(hipMemAddressReserve(&va, n, gran, nullptr, 0));
+            CK(hipMemMap(va, n, 0, h, 0));
+            access_rw(va, n);
+            uint64_t t[2] = {0, 0};
+            CK(hipMemcpy(&t[0], va, 8, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(&t[1], (char *)va + n - 8, 8, hipMemcpyDeviceToHost));
+            const bool good = t[0] == 0x1000u + rr && t[1] == 0x2000u + rr;
+            printf("[peer] round %d: descriptor %d, va %p reads %#llx / %#llx %s\n", rr, fd, va,
+                   (unsigned long long)t[0], (unsigned long long)t[1], good ? "ok" : "WRONG");
+            fflush(stdout);
+            if (!good) ok = false;
+            CK(hipMemUnmap(va, n));
+            CK(hipMemRelease(h));
+            if (!retain) CK(hipMemAddressFree(va, n));
+            if (fd >= 0) close(fd);
+            int a = 1;
+            send(ack[1], &a, sizeof(a), 0);
+        }
+    }
+    if (!child) return ok ? 0 : 1;
+    int st = 0;
+    waitpid(child, &st, 0);
+    const bool all = ok && WIFEXITED(st) && WEXITSTATUS(st) == 0;
+    printf("mode %s: %s\n", mode, all ? "PASS" : "FAIL");
+    return all ? 0 : 1;
+}
