@@ -498,13 +498,20 @@ def run_gpu(args, dist, finalize=True):
         # the blocking API beside the headline: the same K steps through
         # comex_accs, each returning after its kernel -- a host round trip per step,
         # the call GA's NGA_Acc makes for its last owner (onesided.c:1421-1438)
+        # the call through a prototype-free function object with every argument already a
+        # ctypes object: no per-argument conversion in the loop (ctypes' argtypes path cost
+        # ~2-3 us of Python per call, 5-7 % of a 38 us step, that a C caller -- GA --
+        # never pays; tools/blocking_lib_probe.cpp times the same call from C)
+        raw = ctypes.CDLL(ga_amd._lib.LIB_PATH).comex_accs
+        raw.restype = ctypes.c_int
+        c_op, c_lv, c_tg, c_zero = ctypes.c_int(op), ctypes.c_int(levels), ctypes.c_int(target), ctypes.c_int(0)
+        bargs = [(c_op, sp, sp_, ss, dp_, ds, cnt, c_lv, c_tg, c_zero) for sp_, dp_ in ptrs]
         L.comex_barrier(0)
         dist.barrier()
         ga_amd.sync()
         tb = time.perf_counter()
         for i in range(args.steps):
-            sp_, dp_ = ptrs[(nxt + i) % len(ptrs)]
-            if L.comex_accs(op, sp, sp_, ss, dp_, ds, cnt, levels, target, 0):
+            if raw(*bargs[(nxt + i) % len(bargs)]):
                 raise RuntimeError("blocking step failed")
         tb = dist.max(time.perf_counter() - tb)
         blocking = {"api": "comex_accs per step (blocking: returns after its kernel)",

@@ -56,17 +56,23 @@ size_t granularity() {
     return g_gran;
 }
 
-// Each mapping gets a virtual range of its own, and a range is not reserved again
-// after its mapping is gone: it stays reserved (retired) until the retired total
-// passes COMEX_AMD_VMM_RETAIN_GB (default 16384 = 16 TiB of the 128 TiB user space),
-// oldest first.  Both halves are measured (gpurun_out r04s05): mappings bump-allocated
-// out of one shared 256 GiB reservation failed hipMemSetAccess once a mapping in it
-// had been unmapped, and a fresh mapping at a just-released range read the end of
-// the PREVIOUS mapping there (its first bytes were right) -- the runtime resolves an
-// address to a mapping through bookkeeping that a recycled range confuses.
+// Each mapping gets a virtual range of its own, taken from a window of the address
+// space no runtime allocation uses (COMEX_AMD_VMM_VA_BASE, default 32 TiB, asked for
+// by address hint, bump-allocated, never handed out twice), and a range is not
+// reserved again after its mapping is gone: it stays reserved (retired) until the
+// retired total passes COMEX_AMD_VMM_RETAIN_GB (default 16384 = 16 TiB), oldest first.
+// Measured (gpurun_out r04s05, tools/vmm_probe.hip): with ranges the runtime chose, a
+// new block's hipMemSetAccess failed (invalid argument) when its range began where a
+// hipMalloc block of another size had been freed, and so did mappings bump-allocated
+// in one shared reservation; a fresh mapping at a just-released range read the end of
+// the PREVIOUS mapping there -- the runtime resolves an address to its allocation
+// through bookkeeping that a recycled range confuses.  Ranges from the private window
+// meet none of that.
 struct Retired { char *va; size_t bytes; };
 std::vector<Retired> g_retired;
 size_t g_retired_bytes = 0;
+uintptr_t g_window = 0;            // next hint in the private window
+bool g_window_warned = false;
 
 size_t retain_cap() {
     static const size_t cap = [] {
@@ -77,8 +83,22 @@ size_t retain_cap() {
 }
 
 char *va_take(size_t bytes) {
+    std::lock_guard<std::mutex> g(g_vmm_mu);
+    constexpr uintptr_t kAlign = 2u << 20;
+    if (!g_window) {
+        const char *e = getenv("COMEX_AMD_VMM_VA_BASE");
+        g_window = e ? (uintptr_t)strtoull(e, nullptr, 0) : (uintptr_t)0x200000000000ull;
+        g_window = (g_window + kAlign - 1) & ~(kAlign - 1);
+    }
+    void *hint = (void *)g_window;
     void *base = nullptr;
-    GA_HIP(hipMemAddressReserve(&base, bytes, granularity(), nullptr, 0));
+    GA_HIP(hipMemAddressReserve(&base, bytes, granularity(), hint, 0));
+    g_window += (bytes + kAlign - 1) & ~(kAlign - 1);
+    if (base != hint && !g_window_warned) {
+        g_window_warned = true;
+        fprintf(stderr, "[ga_amd %d] vmm: the runtime placed a range at %p, not at the requested %p\n", rt().rank,
+                base, hint);
+    }
     return (char *)base;
 }
 

@@ -12,6 +12,13 @@
 //   retain  as keep, and neither side releases its virtual ranges
 //   mix     as retain, each round first doing a hipMalloc + hipFree of the same size
 //           on both sides (GA's scratch buffers between create/destroy cycles)
+// Single-process modes (the virtual-range cases behind the library's failures):
+//   r_malloc  hipMalloc + hipFree a block, then reserve a range AT its address
+//             (hint) and map a new allocation there: map, access, copy
+//   r_chunk   one 1 GiB reservation; map blocks one after another inside it (bump),
+//             unmapping each before mapping the next
+//   r_hint    per-mapping reservations at hinted addresses in a private window far
+//             from the runtime's allocations, with hipMalloc/hipFree churn between
 // The sockets are made before either process touches the GPU (fork before HIP).
 //
 // hipcc --offload-arch=gfx950 -O2 -o tools/vmm_probe tools/vmm_probe.hip
@@ -90,8 +97,62 @@ static void access_rw(void *va, size_t n) {
     CK(hipMemSetAccess(va, n, &d, 1));
 }
 
+static int single(const char *mode, int rounds, size_t n) {
+    who = mode;
+    CK(hipSetDevice(0));
+    hipMemAllocationProp prop = prop_of();
+    size_t gran = 0;
+    CK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+    char *chunk = nullptr;
+    const size_t chunk_bytes = 1ull << 30;
+    if (!strcmp(mode, "r_chunk")) CK(hipMemAddressReserve((void **)&chunk, chunk_bytes, gran, nullptr, 0));
+    uintptr_t window = 0x200000000000ull;   // 32 TiB
+    size_t used = 0;
+    for (int r = 0; r < rounds; ++r) {
+        ok = true;
+        void *hint = nullptr;
+        void *tmp = nullptr;
+        CK(hipMalloc(&tmp, n));
+        CK(hipFree(tmp));
+        void *va = nullptr;
+        bool own_range = true;
+        if (!strcmp(mode, "r_malloc")) {
+            hint = tmp;
+        } else if (!strcmp(mode, "r_hint")) {
+            hint = (void *)(window + used);
+            used += (n + gran - 1) / gran * gran;
+        }
+        if (!strcmp(mode, "r_chunk")) {
+            va = chunk + used;
+            used += (n + gran - 1) / gran * gran;
+            own_range = false;
+        } else {
+            CK(hipMemAddressReserve(&va, n, gran, hint, 0));
+        }
+        hipMemGenericAllocationHandle_t h;
+        CK(hipMemCreate(&h, n, &prop, 0));
+        CK(hipMemMap(va, n, 0, h, 0));
+        access_rw(va, n);
+        const uint64_t t0 = 0x1000 + r, t1 = 0x2000 + r;
+        uint64_t b[2] = {0, 0};
+        CK(hipMemcpy(va, &t0, 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy((char *)va + n - 8, &t1, 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(&b[0], va, 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(&b[1], (char *)va + n - 8, 8, hipMemcpyDeviceToHost));
+        printf("[%s] round %d: scratch %p, hint %p -> va %p, reads %#llx / %#llx %s\n", mode, r, tmp, hint, va,
+               (unsigned long long)b[0], (unsigned long long)b[1], ok && b[0] == t0 && b[1] == t1 ? "ok" : "FAIL");
+        fflush(stdout);
+        CK(hipMemUnmap(va, n));
+        CK(hipMemRelease(h));
+        if (own_range && !strcmp(mode, "r_malloc")) CK(hipMemAddressFree(va, n));
+    }
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const char *mode = argc > 1 ? argv[1] : "keep";
+    if (!strncmp(mode, "r_", 2))
+        return single(mode, argc > 2 ? atoi(argv[2]) : 4, argc > 3 ? strtoull(argv[3], nullptr, 0) : (2u << 20));
     const int rounds = argc > 2 ? atoi(argv[2]) : 6;
     const size_t n = argc > 3 ? strtoull(argv[3], nullptr, 0) : (2u << 20);
     const bool mix = !strcmp(mode, "mix");
