@@ -9,7 +9,8 @@ O=${OUT:-gpurun_out/r04s03}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 [ -n "$SKIP_HOSTSEG" ] || timeout -k 10 300 python -u -m pytest tests/test_multiproc.py -q -k "host_segments" --timeout 200 --timeout-method thread > $O/hostseg.log 2>&1; echo "hostseg rc=$?"; tail -3 $O/hostseg.log
-timeout -k 10 600 python -u -m pytest tests/test_multiproc.py -q -k "vmm_segments" --timeout 300 --timeout-method thread > $O/vmm.log 2>&1; rc=$?; echo "vmm rc=$rc"; tail -3 $O/vmm.log
+rc=0
+[ -n "$SKIP_VMMTEST" ] || { timeout -k 10 600 python -u -m pytest tests/test_multiproc.py -q -k "vmm_segments" --timeout 170 --timeout-method thread > $O/vmm.log 2>&1; rc=$?; echo "vmm rc=$rc"; tail -3 $O/vmm.log; }
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 [ $rc -eq 0 ] || [ -z "$STOP_ON_VMM_FAIL" ] || exit $rc
 REPS=${REPS:-10}
