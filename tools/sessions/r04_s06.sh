@@ -14,4 +14,9 @@ COMEX_AMD_SEGMENT_ALLOC=vmm timeout -k 10 900 python -u -m pytest tests/test_mul
 timeout -k 10 200 python bench.py > $O/bench_n1.json 2> $O/bench_n1.err; rc=$?; echo "bench rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 python -c "import json;d=json.load(open('$O/bench_n1.json'));print(d['value'], d['roofline']['frac'], d.get('blocking_api'))"
+# HBM segments from hipMemCreate vs hipMalloc under the HBM-bound kernel: C5 M1 at N=1 (one 8 GiB block)
+for alloc in ipc vmm ipc vmm; do
+  COMEX_AMD_SEGMENT_ALLOC=$alloc timeout -k 10 200 python bench.py --workload C5 --steps 20 --warmup 3 --no-cpu > $O/c5_$alloc.json 2> $O/c5_$alloc.err || { echo "c5 $alloc failed"; tail -5 $O/c5_$alloc.err; exit 1; }
+  python -c "import json;d=json.load(open('$O/c5_$alloc.json'));print('C5 N=1 $alloc', d['value'], d['hbm_peak_frac'])"
+done
 OUT=$O SKIP_HOSTSEG=1 SKIP_VMMTEST=1 ALLOCS=vmm REPS=${REPS:-8} bash tools/sessions/r04_s03.sh
