@@ -132,6 +132,12 @@ struct CopyOp {
     static constexpr bool kReadsDst = false;
     template <int W>
     __device__ __forceinline__ typename Vec<W>::T apply(typename Vec<W>::T, typename Vec<W>::T s) const { return s; }
+    // apply() split into its source-only part and the combine (k_ordered_cols_lds:
+    // loaders compute pre(src), the applier's chain is add(dst, pre(src)))
+    template <int W>
+    __device__ __forceinline__ typename Vec<W>::T pre(typename Vec<W>::T s) const { return s; }
+    template <int W>
+    __device__ __forceinline__ typename Vec<W>::T add(typename Vec<W>::T, typename Vec<W>::T i) const { return i; }
     __device__ __forceinline__ void serial_elem(char *dp, const char *sp) const { *dp = *sp; }
 };
 
@@ -151,6 +157,25 @@ struct AccReal {
             A prod = b.t[i] * s;
             a.t[i] = a.t[i] + prod;
         }
+        return a.v;
+    }
+    // the same operations split: pre = the products, add = the sums (bit-identical)
+    template <int W>
+    __device__ __forceinline__ typename Vec<W>::T pre(typename Vec<W>::T sv) const {
+        constexpr int N = W / (int)sizeof(T);
+        union { typename Vec<W>::T v; A t[N]; } b;
+        b.v = sv;
+#pragma unroll
+        for (int i = 0; i < N; ++i) b.t[i] = b.t[i] * s;
+        return b.v;
+    }
+    template <int W>
+    __device__ __forceinline__ typename Vec<W>::T add(typename Vec<W>::T dv, typename Vec<W>::T iv) const {
+        constexpr int N = W / (int)sizeof(T);
+        union { typename Vec<W>::T v; A t[N]; } a, b;
+        a.v = dv; b.v = iv;
+#pragma unroll
+        for (int i = 0; i < N; ++i) a.t[i] = a.t[i] + b.t[i];
         return a.v;
     }
     __device__ __forceinline__ void serial_elem(char *dp, const char *sp) const {
@@ -186,6 +211,35 @@ struct AccCplx {
             a.t[2 * i] = a.t[2 * i] + re;
             a.t[2 * i + 1] = a.t[2 * i + 1] + im;
         }
+        return a.v;
+    }
+    // the same operations split: pre = (re, im) of each source element, add = the sums
+    template <int W>
+    __device__ __forceinline__ typename Vec<W>::T pre(typename Vec<W>::T sv) const {
+        constexpr int N = W / (int)(2 * sizeof(R));
+        union { typename Vec<W>::T v; R t[2 * N]; } b;
+        b.v = sv;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const R br = b.t[2 * i], bi = b.t[2 * i + 1];
+            R p1 = br * sr;
+            R p2 = bi * si;
+            R re = p1 - p2;
+            R p3 = br * si;
+            R p4 = bi * sr;
+            R im = p3 + p4;
+            b.t[2 * i] = re;
+            b.t[2 * i + 1] = im;
+        }
+        return b.v;
+    }
+    template <int W>
+    __device__ __forceinline__ typename Vec<W>::T add(typename Vec<W>::T dv, typename Vec<W>::T iv) const {
+        constexpr int N = W / (int)sizeof(R);
+        union { typename Vec<W>::T v; R t[N]; } a, b;
+        a.v = dv; b.v = iv;
+#pragma unroll
+        for (int i = 0; i < N; ++i) a.t[i] = a.t[i] + b.t[i];
         return a.v;
     }
     __device__ __forceinline__ void serial_elem(char *dp, const char *sp) const {
@@ -555,51 +609,92 @@ __global__ __launch_bounds__(64) void k_ordered_cols(const Desc d, const OP op) 
 // most 63 loads in flight (vmcnt) -- 0.62-0.65 TB/s of real HBM traffic.  Here a
 // workgroup owns CW column slices (CW*W contiguous bytes of every row) and splits
 // the work by role:
-//   * waves 1..KC_NW-1 LOAD: each fetches P load instructions of rows per tile
-//     (RPI = 64/CW rows per instruction, CW lanes each), unconditionally (rows
-//     past the last load the last one again: straight-line code, so the P loads
-//     issue back to back), and writes them into one of two LDS tiles;
+//   * waves 1..KC_NW-1 LOAD: each issues KC_P 16-byte loads per lane per tile (a
+//     load instruction covers RPI rows of the workgroup's piece), unconditionally
+//     (rows past the last load the last one again: straight-line code, so the loads
+//     issue back to back), computes the source-only part of the operation (op.pre:
+//     the products a*src, the (re, im) of a complex product) and writes it into
+//     one of two LDS tiles;
 //   * wave 0 APPLIES: its first CW lanes walk the other tile's rows IN ORDER,
-//     applying each to the column value held in a register (stored when the dst
-//     run changes and at the end) -- the reference's operations in its order per
-//     column (comex.c:6936-6961, acc.h:137-143).  A row's dst offset is the same
-//     for every lane, so the run test is a scalar branch; rows come in batches of
-//     8 with their LDS reads issued together ahead of the dependent chain.
+//     adding each row's pre-computed increment to the column value held in a
+//     register (stored when the dst run changes and at the end) -- the reference's
+//     operations, in its order per column (comex.c:6936-6961, acc.h:137-143); pre
+//     then add is the same two roundings as apply.
+// The applier is one wave and walks every row, so its instructions per row set the
+// kernel's time (a 2048-row f64 column reduction at ~100 cycles per row: 90 us).
+// Hence the split of the products onto the loaders, and a fast path for the common
+// geometry -- every row into ONE dst run (all dst strides zero): no per-row offset
+// or run test, one LDS read + one add per row, 16 rows per batch.
 // One barrier per tile: the loaders fill tile i+1 while wave 0 applies tile i.
+// Measured read rate of this access pattern (tools/piece_probe.hip, 256 workgroups
+// each reading 256-byte pieces of 2048 rows with 64 KiB in flight): 5.4 TB/s.
 constexpr int KC_NW = 8;                 // waves per workgroup: 1 applier + 7 loaders
-template <int W> struct KcRows { static constexpr int P = 128 / W; };   // 56 KiB per LDS tile
+constexpr int KC_P = 8;                  // 16-byte loads per loader lane per tile (56 KiB tiles)
 template <class OP, int W, int LV, int CW>
 __global__ __launch_bounds__(KC_NW * 64) void k_ordered_cols_lds(const Desc d, const OP op) {
     typedef typename Vec<W>::T V;
-    constexpr int P = KcRows<W>::P;
-    constexpr int RPI = 64 / CW;                     // rows per load instruction
-    constexpr int T = (KC_NW - 1) * P * RPI;         // rows per tile
-    __shared__ V tile[2][T * CW];                    // [buffer][row][column]
+    typedef typename Vec<16>::T V16;
+    constexpr int SPL = 16 / W;                      // column slices per 16-byte load
+    constexpr int LPR = CW / SPL;                    // loader lanes per row piece
+    constexpr int RPI = 64 / LPR;                    // rows per load instruction
+    constexpr int T = (KC_NW - 1) * KC_P * RPI;      // rows per tile
+    static_assert(CW % SPL == 0 && 64 % LPR == 0, "column group of whole 16-byte loads");
+    __shared__ __attribute__((aligned(16))) V tile[2][T * CW];   // [buffer][row][column]
     // the wave index through readfirstlane: the compiler then knows the role branch
     // (and every value inside the applier's) is wave-uniform -- scalar branches
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint32_t c = lane % CW;                    // this lane's column slice within the workgroup
-    const uint32_t col = blockIdx.x * (uint32_t)CW + c;
+    const uint32_t c = lane % CW;                    // the applier lane's column slice
+    const uint32_t col0 = blockIdx.x * (uint32_t)CW, col = col0 + c;
     // every lane works on a valid address (clamped column; its values are never stored)
     const int64_t xl = (int64_t)min(col, d.nvec - 1u) * W;
     const uint32_t ntiles = (d.rows + (uint32_t)T - 1) / (uint32_t)T;
+    const bool full = col0 + (uint32_t)CW <= d.nvec;   // no partial slice group (workgroup-uniform)
     auto load_store = [&](uint32_t tl, int buf) {    // loader waves: tile `tl` into tile[buf]
-        const uint32_t lw = wave - 1, sub = lane / CW;
-        V s[P];
+        const uint32_t lw = wave - 1, sub = lane / (uint32_t)LPR, s0 = (lane % (uint32_t)LPR) * SPL;
+        if (full) {
+            const int64_t xo = (int64_t)(col0 + s0) * W;
+            V16 s[KC_P];
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-            const uint32_t r = min(tl * (uint32_t)T + (lw * P + (uint32_t)k) * RPI + sub, d.rows - 1u);
-            int64_t so, dof;
-            row_offsets<LV>(d, d.row0 + r, so, dof);
-            s[k] = vload<W, true>(d.src + so + xl);
+            for (int k = 0; k < KC_P; ++k) {
+                const uint32_t r = min(tl * (uint32_t)T + (lw * KC_P + (uint32_t)k) * RPI + sub, d.rows - 1u);
+                int64_t so, dof;
+                row_offsets<LV>(d, d.row0 + r, so, dof);
+                s[k] = vload<16, true>(d.src + so + xo);
+            }
+#pragma unroll
+            for (int k = 0; k < KC_P; ++k)
+                *reinterpret_cast<V16 *>(&tile[buf][((lw * KC_P + (uint32_t)k) * RPI + sub) * CW + s0]) =
+                    op.template pre<16>(s[k]);
+        } else {
+            // the last workgroup of a row whose slice count is not a multiple of CW:
+            // W-byte loads of clamped slices (never past the row's last byte)
+#pragma unroll
+            for (int k = 0; k < KC_P; ++k) {
+                const uint32_t r = min(tl * (uint32_t)T + (lw * KC_P + (uint32_t)k) * RPI + sub, d.rows - 1u);
+                int64_t so, dof;
+                row_offsets<LV>(d, d.row0 + r, so, dof);
+                V v[SPL];
+#pragma unroll
+                for (int j = 0; j < SPL; ++j)
+                    v[j] = vload<W, true>(d.src + so + (int64_t)min(col0 + s0 + (uint32_t)j, d.nvec - 1u) * W);
+#pragma unroll
+                for (int j = 0; j < SPL; ++j)
+                    tile[buf][((lw * KC_P + (uint32_t)k) * RPI + sub) * CW + s0 + j] = op.template pre<W>(v[j]);
+            }
         }
-#pragma unroll
-        for (int k = 0; k < P; ++k) tile[buf][(lw * P + (uint32_t)k) * 64 + lane] = s[k];
     };
     const bool lane_ok = lane < (uint32_t)CW && col < d.nvec;
+    bool one_run = true;                             // every row into one dst run
+    for (int j = 0; j < d.levels; ++j) one_run = one_run && d.d_str[j] == 0;
     V acc = {};
     int64_t cur = 0;
     bool held = false;
+    if (wave == 0 && one_run) {
+        int64_t so;
+        row_offsets<LV>(d, d.row0, so, cur);
+        held = true;
+        if constexpr (OP::kReadsDst) acc = vload<W, false>(d.dst + cur + xl);
+    }
     auto apply_row = [&](uint32_t r, const V &x) {   // applier: row r of the patch (wave-uniform)
         int64_t so, dof;
         row_offsets<LV>(d, d.row0 + r, so, dof);
@@ -610,7 +705,7 @@ __global__ __launch_bounds__(KC_NW * 64) void k_ordered_cols_lds(const Desc d, c
             acc = x;
             if constexpr (OP::kReadsDst) acc = vload<W, false>(d.dst + cur + xl);
         }
-        acc = op.template apply<W>(acc, x);
+        acc = op.template add<W>(acc, x);
     };
     if (wave != 0) load_store(0, 0);
     __syncthreads();
@@ -621,16 +716,28 @@ __global__ __launch_bounds__(KC_NW * 64) void k_ordered_cols_lds(const Desc d, c
         } else {
             const uint32_t r0 = i * (uint32_t)T;
             const uint32_t n = min((uint32_t)T, d.rows - r0);
-            constexpr int B = 8;
             uint32_t t = 0;
-            for (; t + B <= n; t += B) {
-                V x[B];
+            if (one_run) {
+                constexpr int B = 16;
+                for (; t + B <= n; t += B) {
+                    V x[B];
 #pragma unroll
-                for (int j = 0; j < B; ++j) x[j] = tile[buf][(t + j) * CW + c];
+                    for (int j = 0; j < B; ++j) x[j] = tile[buf][(t + j) * CW + c];
 #pragma unroll
-                for (int j = 0; j < B; ++j) apply_row(r0 + t + j, x[j]);
+                    for (int j = 0; j < B; ++j) acc = op.template add<W>(acc, x[j]);
+                }
+                for (; t < n; ++t) acc = op.template add<W>(acc, tile[buf][t * CW + c]);
+            } else {
+                constexpr int B = 8;
+                for (; t + B <= n; t += B) {
+                    V x[B];
+#pragma unroll
+                    for (int j = 0; j < B; ++j) x[j] = tile[buf][(t + j) * CW + c];
+#pragma unroll
+                    for (int j = 0; j < B; ++j) apply_row(r0 + t + j, x[j]);
+                }
+                for (; t < n; ++t) apply_row(r0 + t, tile[buf][t * CW + c]);
             }
-            for (; t < n; ++t) apply_row(r0 + t, tile[buf][t * CW + c]);
         }
         __syncthreads();
     }

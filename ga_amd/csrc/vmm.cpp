@@ -93,7 +93,11 @@ char *va_take(size_t bytes) {
     void *hint = (void *)g_window;
     void *base = nullptr;
     GA_HIP(hipMemAddressReserve(&base, bytes, granularity(), hint, 0));
-    g_window += (bytes + kAlign - 1) & ~(kAlign - 1);
+    // one empty 2 MiB guard after every range: no range starts where another ends
+    // (a new block's hipMemSetAccess failed, invalid argument, when its range began
+    // right at the end of another mapping of a different size: the runtime's
+    // address lookup then finds the neighbour; tools/vmm_probe.hip r_adjacent)
+    g_window += ((bytes + kAlign - 1) & ~(kAlign - 1)) + kAlign;
     if (base != hint && !g_window_warned) {
         g_window_warned = true;
         fprintf(stderr, "[ga_amd %d] vmm: the runtime placed a range at %p, not at the requested %p\n", rt().rank,

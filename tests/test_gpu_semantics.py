@@ -222,8 +222,9 @@ def test_column_ordered_kernel_geometries(gpu_lib, oracle, op):
     """The column-sliced ordered kernel on every op (0 = put: the last row wins)
     against the oracle's sequential order: zero dst stride (2-D), planes into one
     plane (3-D, repeated dst level), a src row that is an earlier dst row, src and
-    dst the same zero-stride run (dst += a*dst per row), and the same with
-    ordered_cols = 0 (one workgroup) for comparison."""
+    dst the same zero-stride run (dst += a*dst per row), for the default kernels
+    (ordered_cols = 2: LDS-staged, or the integer column paths), the one-lane-per-
+    column kernel (1) and one workgroup (0)."""
     e = C.ESZ.get(op, 8)
     rng = np.random.default_rng(71 + op)
     geos = []
@@ -232,7 +233,7 @@ def test_column_ordered_kernel_geometries(gpu_lib, oracle, op):
     geos.append(([w, 6, 5], [w, w * 6], [w + 4 * e, 0], 0, 0, w * 30, (w + 4 * e) * 6, False))   # planes -> one plane
     geos.append(([w, 40], [w + 16 * e], [w + 16 * e], (w + 16 * e) * 3, 0, None, None, True))     # src row i = dst row i+3
     geos.append(([w, 9], [0], [0], 0, 0, None, None, True))                                # dst += a*dst, 9 times
-    for cols in (1, 0):
+    for cols in (2, 1, 0):
         old = ga_amd.set_tuning("ordered_cols", cols)
         try:
             for count, ss, ds, so, do, sbytes, dbytes, alias in geos:

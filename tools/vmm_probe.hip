@@ -19,6 +19,8 @@
 //             unmapping each before mapping the next
 //   r_hint    per-mapping reservations at hinted addresses in a private window far
 //             from the runtime's allocations, with hipMalloc/hipFree churn between
+//   r_adjacent  a 2 MiB mapping kept, then a mapping of n bytes reserved right at its
+//             end (hint), then one 2 MiB further (a gap); each gets hipMemSetAccess
 // The sockets are made before either process touches the GPU (fork before HIP).
 //
 // hipcc --offload-arch=gfx950 -O2 -o tools/vmm_probe tools/vmm_probe.hip
@@ -149,8 +151,34 @@ static int single(const char *mode, int rounds, size_t n) {
     return 0;
 }
 
+static int adjacent(size_t n) {
+    who = "r_adjacent";
+    CK(hipSetDevice(0));
+    hipMemAllocationProp prop = prop_of();
+    size_t gran = 0;
+    CK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+    char *base = (char *)0x210000000000ull;
+    auto map_at = [&](char *hint, size_t bytes, const char *what) {
+        ok = true;
+        void *va = nullptr;
+        CK(hipMemAddressReserve(&va, bytes, gran, hint, 0));
+        hipMemGenericAllocationHandle_t h;
+        CK(hipMemCreate(&h, bytes, &prop, 0));
+        CK(hipMemMap(va, bytes, 0, h, 0));
+        access_rw(va, bytes);
+        printf("[r_adjacent] %s: %zu bytes at %p (asked %p): %s\n", what, bytes, va, hint, ok ? "ok" : "FAILED");
+        fflush(stdout);
+    };
+    map_at(base, 2u << 20, "first (2 MiB)");
+    map_at(base + (2u << 20), n, "right at its end");
+    map_at(base + (8u << 20), n, "2 MiB past the next boundary (gap)");
+    map_at(base + (8u << 20) + ((n + (2u << 20) - 1) & ~((size_t)(2u << 20) - 1)), 2u << 20, "2 MiB right at that one's rounded end");
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const char *mode = argc > 1 ? argv[1] : "keep";
+    if (!strcmp(mode, "r_adjacent")) return adjacent(argc > 3 ? strtoull(argv[3], nullptr, 0) : 0x202000);
     if (!strncmp(mode, "r_", 2))
         return single(mode, argc > 2 ? atoi(argv[2]) : 4, argc > 3 ? strtoull(argv[3], nullptr, 0) : (2u << 20));
     const int rounds = argc > 2 ? atoi(argv[2]) : 6;
