@@ -52,7 +52,11 @@ size_t granularity() {
     prop.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
     size_t g = 0;
     GA_HIP(hipMemGetAllocationGranularity(&g, &prop, hipMemAllocationGranularityRecommended));
-    g_gran = g ? g : (2u << 20);
+    // whole 2 MiB units at least (the runtime reports 4 KiB): sizes off 2 MiB made a
+    // new block's hipMemSetAccess fail now and then (invalid argument: 0x202000 and
+    // 0x208000 bytes in gpurun_out r04s05 / r04s07, never a 2 MiB multiple), and 2 MiB
+    // units map with large pages; the cost is < 2 MiB per segment
+    g_gran = std::max<size_t>(g, 2u << 20);
     return g_gran;
 }
 
@@ -61,13 +65,10 @@ size_t granularity() {
 // by address hint, bump-allocated, never handed out twice), and a range is not
 // reserved again after its mapping is gone: it stays reserved (retired) until the
 // retired total passes COMEX_AMD_VMM_RETAIN_GB (default 16384 = 16 TiB), oldest first.
-// Measured (gpurun_out r04s05, tools/vmm_probe.hip): with ranges the runtime chose, a
-// new block's hipMemSetAccess failed (invalid argument) when its range began where a
-// hipMalloc block of another size had been freed, and so did mappings bump-allocated
-// in one shared reservation; a fresh mapping at a just-released range read the end of
-// the PREVIOUS mapping there -- the runtime resolves an address to its allocation
-// through bookkeeping that a recycled range confuses.  Ranges from the private window
-// meet none of that.
+// Measured (tools/vmm_probe.hip, profiles/r04/s05): two processes exchanging 2 MiB
+// blocks, the importer releasing its range and reserving it again at the same
+// address -- the new mapping read zeros where the owner's tags were, every round
+// after the first; with ranges never reserved twice every round read right.
 struct Retired { char *va; size_t bytes; };
 std::vector<Retired> g_retired;
 size_t g_retired_bytes = 0;
@@ -93,10 +94,8 @@ char *va_take(size_t bytes) {
     void *hint = (void *)g_window;
     void *base = nullptr;
     GA_HIP(hipMemAddressReserve(&base, bytes, granularity(), hint, 0));
-    // one empty 2 MiB guard after every range: no range starts where another ends
-    // (a new block's hipMemSetAccess failed, invalid argument, when its range began
-    // right at the end of another mapping of a different size: the runtime's
-    // address lookup then finds the neighbour; tools/vmm_probe.hip r_adjacent)
+    // one empty 2 MiB guard after every range, so no range starts where another
+    // ends (a precaution: tools/vmm_probe.hip r_adjacent found adjacent ranges fine)
     g_window += ((bytes + kAlign - 1) & ~(kAlign - 1)) + kAlign;
     if (base != hint && !g_window_warned) {
         g_window_warned = true;
