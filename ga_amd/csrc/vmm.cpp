@@ -32,6 +32,7 @@
 #include <sys/un.h>
 #include <time.h>
 #include <unistd.h>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -71,6 +72,7 @@ size_t granularity() {
 // after the first; with ranges never reserved twice every round read right.
 struct Retired { char *va; size_t bytes; };
 std::vector<Retired> g_retired;
+std::atomic<unsigned long long> g_access_retries{0};
 size_t g_retired_bytes = 0;
 uintptr_t g_window = 0;            // next hint in the private window
 bool g_window_warned = false;
@@ -193,19 +195,39 @@ bool recv_fd() {
     return true;
 }
 
-void set_access(char *va, size_t bytes, int q) {
+// map `h` at a fresh range and give this GPU access; the launch lock is held so no
+// other thread of this process issues HIP work meanwhile.  A refused
+// hipMemSetAccess (invalid argument, now and then in the segment-cache test's
+// create/free cycles, gpurun_out r04s05-r04s07) is retried at another fresh range,
+// up to 3 times, each one logged.
+char *map_fresh(hipMemGenericAllocationHandle_t h, size_t bytes, int q) {
+    Runtime &r = rt();
     hipMemAccessDesc d;
     memset(&d, 0, sizeof(d));
     d.location.type = hipMemLocationTypeDevice;
-    d.location.id = rt().device;
+    d.location.id = r.device;
     d.flags = hipMemAccessFlagsProtReadWrite;
-    const hipError_t e = hipMemSetAccess(va, bytes, &d, 1);
-    if (e != hipSuccess) {
-        fprintf(stderr, "[ga_amd %d] hipMemSetAccess(%p, %zu bytes) of %s failed: %s\n", rt().rank, (void *)va,
-                bytes, q < 0 ? "a new block of this rank" : "an imported block", hipGetErrorString(e));
-        if (q >= 0) fprintf(stderr, "[ga_amd %d]   imported from rank %d\n", rt().rank, q);
+    for (int attempt = 0;; ++attempt) {
+        char *va = va_take(bytes);
+        hipError_t e;
+        {
+            std::lock_guard<std::mutex> g(r.launch_mu);
+            GA_HIP(hipMemMap(va, bytes, 0, h, 0));
+            e = hipMemSetAccess(va, bytes, &d, 1);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                GA_HIP(hipMemUnmap(va, bytes));
+            }
+        }
+        if (e == hipSuccess) return va;
+        g_access_retries.fetch_add(1, std::memory_order_relaxed);
+        fprintf(stderr, "[ga_amd %d] hipMemSetAccess(%p, %zu bytes) of %s failed: %s (attempt %d)\n", r.rank,
+                (void *)va, bytes, q < 0 ? "a new block of this rank" : "an imported block", hipGetErrorString(e),
+                attempt + 1);
+        if (q >= 0) fprintf(stderr, "[ga_amd %d]   imported from rank %d\n", r.rank, q);
         addr_history(va, bytes);
-        fatal("hipMemSetAccess failed");
+        va_retire(va, bytes);
+        if (attempt >= 2) fatal("hipMemSetAccess failed 3 times");
     }
 }
 }  // namespace
@@ -241,9 +263,7 @@ void *vmm_alloc(size_t bytes, VmmBlock *b) {
         e = hipMemCreate(&h, n, &prop, 0);
     }
     if (e != hipSuccess) fatal("hipMemCreate of %zu bytes failed: %s", n, hipGetErrorString(e));
-    char *va = va_take(n);
-    GA_HIP(hipMemMap(va, n, 0, h, 0));
-    set_access(va, n, -1);
+    char *va = map_fresh(h, n, -1);
     int fd = -1;
     GA_HIP(hipMemExportToShareableHandle(&fd, h, hipMemHandleTypePosixFileDescriptor, 0));
     b->va = va;
@@ -318,9 +338,7 @@ void *vmm_import(int myfd, size_t bytes, int q, VmmBlock *b) {
     // the descriptor is passed by value, as the POSIX-fd handle type is documented
     // for the driver API this one mirrors
     GA_HIP(hipMemImportFromShareableHandle(&h, (void *)(uintptr_t)myfd, hipMemHandleTypePosixFileDescriptor));
-    char *va = va_take(bytes);
-    GA_HIP(hipMemMap(va, bytes, 0, h, 0));
-    set_access(va, bytes, q);
+    char *va = map_fresh(h, bytes, q);
     b->va = va;
     b->bytes = bytes;
     b->handle = h;
@@ -334,6 +352,8 @@ void *vmm_import(int myfd, size_t bytes, int q, VmmBlock *b) {
 void vmm_free(VmmBlock *b) {
     if (!b->va) return;
     addr_event(b->imported ? 'c' : 'f', b->va, b->bytes, -1);
+    // (no launch lock here: comex_free calls this under seg_mu, and launch_mu is
+    // taken before seg_mu elsewhere)
     GA_HIP(hipMemUnmap(b->va, b->bytes));
     GA_HIP(hipMemRelease(b->handle));
     va_retire(b->va, b->bytes);
@@ -356,3 +376,5 @@ void vmm_finalize() {
 }
 
 }  // namespace gaamd
+
+extern "C" unsigned long long gaamd_vmm_access_retries() { return gaamd::g_access_retries.load(); }

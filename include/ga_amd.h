@@ -118,6 +118,8 @@ unsigned long long gaamd_segment_cache_trims(void);
 /* the kind of this rank's segment holding p: 0 none, 1 HBM, 2 host (node shm,
    COMEX_AMD_SEGMENT=host: the host may read and write it directly) */
 int gaamd_segment_kind(const void *p);
+/* vmm segment allocator: hipMemSetAccess refusals retried at a fresh range (diagnostic) */
+unsigned long long gaamd_vmm_access_retries(void);
 /* same-node peers whose staging buffer this rank could not map by IPC at
  * comex_init (remote accumulates to or from them would abort); -1 before init */
 int gaamd_peers_unmapped(void);
