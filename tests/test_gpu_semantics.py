@@ -213,8 +213,9 @@ def test_ordered_kernel_large_overlapping_rows(gpu_lib, oracle):
         for b in rot:
             b.free()
         db.free()
-    # int64 >= 4 TB/s physical, f64 >= 2 x the 0.63 TB/s of round 3
-    assert rates[(C.LNG, 2)] > 500 and rates[(C.DBL, 2)] > 500, rates
+    # int64 >= 4 TB/s physical, f64 >= 2 x the 0.63 TB/s of round 3;
+    # measured 4175-4251 (int64) and 4601 (f64) GB/s, asserted with room for box spread
+    assert rates[(C.LNG, 2)] > 3400 and rates[(C.DBL, 2)] > 3400, rates
 
 
 @pytest.mark.parametrize("op", [C.DBL, C.DCP, C.FLT, C.INT, C.CPL, C.LNG, 0])
