@@ -804,7 +804,11 @@ constexpr int kColsSumMinRows = 32;    // rows per slice at least
 // row slices for a grid of gx column chunks over `rows` rows (the plan and the
 // dispatcher agree through this)
 static inline uint32_t cols_sum_slices(uint32_t gx, uint32_t rows) {
-    uint32_t s = (kColsSumTarget + gx - 1) / gx;
+    static const uint32_t target = [] {   // EXPERIMENT (A/B of the workgroup target)
+        const char *e = getenv("GAAMD_COLS_SUM_TARGET");
+        return e ? (uint32_t)atoi(e) : (uint32_t)kColsSumTarget;
+    }();
+    uint32_t s = (target + gx - 1) / gx;
     const uint32_t smax = (rows + kColsSumMinRows - 1) / kColsSumMinRows;
     if (s > smax) s = smax;
     if (s > 65535u) s = 65535u;
