@@ -799,16 +799,12 @@ __global__ __launch_bounds__(256) void k_cols_atomic(const Desc d, const OP op) 
 // dst with device-scope atomic adds (wrapping integer sums are exact in any order;
 // the launcher takes this path only for a 16-byte-aligned source and a dst in HBM).
 constexpr int kColsSumP = 16;          // rows in flight per lane
-constexpr int kColsSumTarget = 1024;   // workgroups to aim for
+constexpr int kColsSumTarget = 1024;   // workgroups to aim for (256: 4.53, 512: 4.19, 1024: 4.87-4.91 TB/s)
 constexpr int kColsSumMinRows = 32;    // rows per slice at least
 // row slices for a grid of gx column chunks over `rows` rows (the plan and the
 // dispatcher agree through this)
 static inline uint32_t cols_sum_slices(uint32_t gx, uint32_t rows) {
-    static const uint32_t target = [] {   // EXPERIMENT (A/B of the workgroup target)
-        const char *e = getenv("GAAMD_COLS_SUM_TARGET");
-        return e ? (uint32_t)atoi(e) : (uint32_t)kColsSumTarget;
-    }();
-    uint32_t s = (target + gx - 1) / gx;
+    uint32_t s = (kColsSumTarget + gx - 1) / gx;
     const uint32_t smax = (rows + kColsSumMinRows - 1) / kColsSumMinRows;
     if (s > smax) s = smax;
     if (s > 65535u) s = 65535u;

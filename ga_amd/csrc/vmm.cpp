@@ -216,7 +216,8 @@ char *map_fresh(hipMemGenericAllocationHandle_t h, size_t bytes, int q) {
             e = hipMemSetAccess(va, bytes, &d, 1);
             if (e != hipSuccess) {
                 (void)hipGetLastError();
-                GA_HIP(hipMemUnmap(va, bytes));
+                (void)hipMemUnmap(va, bytes);   // may be refused as well: the range is retired either way
+                (void)hipGetLastError();
             }
         }
         if (e == hipSuccess) return va;

@@ -45,8 +45,7 @@ def rate(op, rows=2048, w=8192, n=20):
         b.free()
     phys = rows * w * 8 + 2 * w * 8
     return {"op": op, "us": round(ms * 1e3, 1), "GBps_physical": round(phys / (ms * 1e-3) / 1e9),
-            "blocks": info["blocks"], "variant": info["unroll"],
-            "target": os.environ.get("GAAMD_COLS_SUM_TARGET", "default")}
+            "blocks": info["blocks"], "variant": info["unroll"]}
 
 
 if __name__ == "__main__":

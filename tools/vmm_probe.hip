@@ -10,6 +10,8 @@
 //   keep    the child closes it only when the mapping goes (what vmm.cpp does)
 //   dupfar  the child moves the descriptor to a number it never used before
 //   retain  as keep, and neither side releases its virtual ranges
+//   fdcheck as retain, printing after each step whether the descriptors are still
+//           open in this process (who owns an exported / imported descriptor)
 //   mix     as retain, each round first doing a hipMalloc + hipFree of the same size
 //           on both sides (GA's scratch buffers between create/destroy cycles)
 // Single-process modes (the virtual-range cases behind the library's failures):
@@ -184,7 +186,9 @@ int main(int argc, char **argv) {
     const int rounds = argc > 2 ? atoi(argv[2]) : 6;
     const size_t n = argc > 3 ? strtoull(argv[3], nullptr, 0) : (2u << 20);
     const bool mix = !strcmp(mode, "mix");
-    const bool retain = !strcmp(mode, "retain") || mix;
+    const bool fdcheck = !strcmp(mode, "fdcheck");
+    const bool retain = !strcmp(mode, "retain") || mix || fdcheck;
+    auto fd_open = [](int f) { return f >= 0 && fcntl(f, F_GETFD) != -1; };
     int sv[2], ack[2];
     if (socketpair(AF_UNIX, SOCK_DGRAM, 0, sv) || socketpair(AF_UNIX, SOCK_DGRAM, 0, ack)) return 2;
     const pid_t child = fork();
@@ -220,8 +224,10 @@ int main(int argc, char **argv) {
             send_fd(sv[0], fd, r);
             int a = 0;
             if (recv(ack[0], &a, sizeof(a), 0) <= 0) break;
+            if (fdcheck) printf("[owner] round %d: export descriptor %d open after send: %d\n", r, fd, fd_open(fd));
             CK(hipMemUnmap(va, n));
             CK(hipMemRelease(h));
+            if (fdcheck) printf("[owner] round %d: export descriptor %d open after hipMemRelease: %d\n", r, fd, fd_open(fd));
             if (!retain) CK(hipMemAddressFree(va, n));
             close(fd);
         } else {
@@ -235,6 +241,7 @@ int main(int argc, char **argv) {
             }
             hipMemGenericAllocationHandle_t h;
             CK(hipMemImportFromShareableHandle(&h, (void *)(uintptr_t)fd, hipMemHandleTypePosixFileDescriptor));
+            if (fdcheck) printf("[peer] round %d: received descriptor %d open after import: %d\n", rr, fd, fd_open(fd));
             if (!strcmp(mode, "close")) {
                 close(fd);
                 fd = -1;
@@ -253,6 +260,7 @@ int main(int argc, char **argv) {
             if (!good) ok = false;
             CK(hipMemUnmap(va, n));
             CK(hipMemRelease(h));
+            if (fdcheck) printf("[peer] round %d: received descriptor %d open after hipMemRelease: %d\n", rr, fd, fd_open(fd));
             if (!retain) CK(hipMemAddressFree(va, n));
             if (fd >= 0) close(fd);
             int a = 1;
