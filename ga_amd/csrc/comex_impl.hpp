@@ -102,6 +102,7 @@ void vmm_listen();                        // this process's descriptor socket (b
 void vmm_exchange(int fd, int rank, uint64_t gen, const std::vector<int> &to_pids,
                   const std::vector<std::pair<int, uint64_t>> &from, int *fds);   // SCM_RIGHTS both ways
 void *vmm_import(int myfd, size_t bytes, int q, VmmBlock *b);   // rank q's block
+void vmm_quarantine(VmmBlock *b);        // a block whose peers' mappings read other memory: set aside
 void vmm_free(VmmBlock *b);               // unmap + release + the virtual range back
 void vmm_finalize();
 

@@ -593,11 +593,24 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
                     if (q == r.rank) mine_stale = true;
                 }
         if (!any) break;
+        if (attempt >= 3) fatal("mappings of a new segment keep reaching other memory (4 attempts)");
         if (vmm) {
-            if (mine_stale) addr_history(p, bytes);
-            fatal("a mapping of a new segment of the virtual-memory allocator does not read its owner's tags");
+            // every member drops its imports of this round; the owner of a stale block sets
+            // it aside and creates another (vmm.cpp: the runtime can bind a new block's
+            // descriptor to another process's block), then the exchange repeats
+            for (int q = 0; q < r.size; ++q)
+                if (q < (int)vpeer.size() && vpeer[q].va) vmm_free(&vpeer[q]);
+            if (mine_stale) {
+                fprintf(stderr, "[ga_amd %d]   my new vmm block's mappings were stale; replacing it\n", r.rank);
+                vmm_quarantine(&vlocal);
+                p = vmm_alloc(bytes, &vlocal);
+                mine.fd = vlocal.fd;
+                mine.vmm_bytes = vlocal.bytes;
+                g_remapped.fetch_add(1, std::memory_order_relaxed);
+            }
+            members_barrier(members, group);
+            continue;
         }
-        if (attempt >= 3) fatal("IPC mappings of a new segment keep reaching other memory (4 attempts)");
         for (int q = 0; q < r.size; ++q)
             if (mapped[q]) ipc_close(mapped[q], q);
         if (mine_stale) {

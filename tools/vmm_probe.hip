@@ -23,6 +23,15 @@
 //             from the runtime's allocations, with hipMalloc/hipFree churn between
 //   r_adjacent  a 2 MiB mapping kept, then a mapping of n bytes reserved right at its
 //             end (hint), then one 2 MiB further (a gap); each gets hipMemSetAccess
+//   samevva / distinctva  three processes: 0 and 1 each allocate a block (at the SAME
+//             virtual address in their own spaces, or at different ones), write their
+//             tags and send the descriptor to the other two; each imports the other
+//             two blocks at fresh ranges and reads the tags (GA's collective
+//             comex_malloc makes every rank's allocation sequence the same, so the
+//             ranks' blocks coincide in address unless told otherwise); with the
+//             suffix _keep no block is released before the last round; with _serial
+//             the allocation steps (reserve, create, map, access, export) of the three
+//             processes take turns under a file lock
 // The sockets are made before either process touches the GPU (fork before HIP).
 //
 // hipcc --offload-arch=gfx950 -O2 -o tools/vmm_probe tools/vmm_probe.hip
@@ -33,9 +42,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/file.h>
 #include <sys/socket.h>
 #include <sys/wait.h>
 #include <unistd.h>
+#include <vector>
 
 #define CK(x)                                                                                    \
     do {                                                                                         \
@@ -178,8 +189,111 @@ static int adjacent(size_t n) {
     return 0;
 }
 
+// three processes, each with one datagram socketpair end per peer
+static int three(bool same, bool keep, bool serial, int rounds) {
+    std::vector<std::pair<void *, hipMemGenericAllocationHandle_t>> kept;
+    int sp[3][3][2];   // sp[a][b]: a sends to b on sp[a][b][0], b receives on sp[a][b][1]
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b)
+            if (a != b && socketpair(AF_UNIX, SOCK_DGRAM, 0, sp[a][b])) return 2;
+    int me = 0;
+    pid_t kids[2] = {0, 0};
+    for (int k = 1; k < 3; ++k) {
+        const pid_t p = fork();
+        if (p == 0) { me = k; break; }
+        kids[k - 1] = p;
+    }
+    static char name[16];
+    snprintf(name, sizeof(name), "proc%d", me);
+    who = name;
+    CK(hipSetDevice(0));
+    hipMemAllocationProp prop = prop_of();
+    size_t gran = 0;
+    CK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+    const size_t n = 2u << 20;
+    uintptr_t next = 0x220000000000ull + (same ? 0 : (uintptr_t)me << 40);
+    int bad = 0;
+    for (int r = 0; r < rounds; ++r) {
+        void *va = nullptr;
+        const int lk = serial ? open("/tmp/vmm_probe_alloc.lock", O_CREAT | O_RDWR, 0600) : -1;
+        if (lk >= 0) flock(lk, LOCK_EX);   // _serial: one process of the GPU allocates at a time
+        CK(hipMemAddressReserve(&va, n, gran, (void *)next, 0));
+        next += 4u << 20;
+        hipMemGenericAllocationHandle_t h;
+        CK(hipMemCreate(&h, n, &prop, 0));
+        CK(hipMemMap(va, n, 0, h, 0));
+        access_rw(va, n);
+        const uint64_t tag = 0xabc000 + 0x100 * me + r;
+        CK(hipMemcpy(va, &tag, 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy((char *)va + n - 8, &tag, 8, hipMemcpyHostToDevice));
+        CK(hipDeviceSynchronize());
+        int fd = -1;
+        CK(hipMemExportToShareableHandle(&fd, h, hipMemHandleTypePosixFileDescriptor, 0));
+        if (lk >= 0) {
+            flock(lk, LOCK_UN);
+            close(lk);
+        }
+        for (int b = 0; b < 3; ++b)
+            if (b != me) send_fd(sp[me][b][0], fd, r);
+        for (int a = 0; a < 3; ++a) {
+            if (a == me) continue;
+            int rr = -1;
+            const int f = recv_fd(sp[a][me][1], &rr);
+            hipMemGenericAllocationHandle_t ih;
+            CK(hipMemImportFromShareableHandle(&ih, (void *)(uintptr_t)f, hipMemHandleTypePosixFileDescriptor));
+            void *iva = nullptr;
+            CK(hipMemAddressReserve(&iva, n, gran, (void *)next, 0));
+            next += 4u << 20;
+            CK(hipMemMap(iva, n, 0, ih, 0));
+            access_rw(iva, n);
+            uint64_t t[2] = {0, 0};
+            CK(hipMemcpy(&t[0], iva, 8, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(&t[1], (char *)iva + n - 8, 8, hipMemcpyDeviceToHost));
+            const uint64_t want = 0xabc000 + 0x100 * a + r;
+            const bool good = t[0] == want && t[1] == want;
+            bad += !good;
+            printf("[%s] round %d: own block at %p; proc%d's block mapped at %p reads %#llx / %#llx (want %#llx) %s\n",
+                   name, r, va, a, iva, (unsigned long long)t[0], (unsigned long long)t[1], (unsigned long long)want,
+                   good ? "ok" : "WRONG");
+            fflush(stdout);
+            CK(hipMemUnmap(iva, n));
+            CK(hipMemRelease(ih));
+            close(f);
+        }
+        // everyone done reading before anyone frees (one byte to each peer and back)
+        for (int b = 0; b < 3; ++b)
+            if (b != me) send(sp[me][b][0], &r, sizeof(r), 0);
+        for (int a = 0; a < 3; ++a)
+            if (a != me) { int x; recv(sp[a][me][1], &x, sizeof(x), 0); }
+        if (keep) {
+            kept.push_back({va, h});
+        } else {
+            CK(hipMemUnmap(va, n));
+            CK(hipMemRelease(h));
+        }
+        close(fd);
+    }
+    for (auto &k : kept) {
+        CK(hipMemUnmap(k.first, n));
+        CK(hipMemRelease(k.second));
+    }
+    if (me) return bad ? 1 : 0;
+    int all_ok = !bad;
+    for (pid_t k : kids) {
+        int st = 0;
+        waitpid(k, &st, 0);
+        all_ok = all_ok && WIFEXITED(st) && WEXITSTATUS(st) == 0;
+    }
+    printf("mode %s%s%s: %s\n", same ? "samevva" : "distinctva", keep ? "_keep" : "", serial ? "_serial" : "",
+           all_ok ? "PASS" : "FAIL");
+    return all_ok ? 0 : 1;
+}
+
 int main(int argc, char **argv) {
     const char *mode = argc > 1 ? argv[1] : "keep";
+    if (!strncmp(mode, "samevva", 7) || !strncmp(mode, "distinctva", 10))
+        return three(!strncmp(mode, "samevva", 7), strstr(mode, "_keep") != nullptr, strstr(mode, "_serial") != nullptr,
+                     argc > 2 ? atoi(argv[2]) : 3);
     if (!strcmp(mode, "r_adjacent")) return adjacent(argc > 3 ? strtoull(argv[3], nullptr, 0) : 0x202000);
     if (!strncmp(mode, "r_", 2))
         return single(mode, argc > 2 ? atoi(argv[2]) : 4, argc > 3 ? strtoull(argv[3], nullptr, 0) : (2u << 20));
