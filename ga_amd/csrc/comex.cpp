@@ -1101,6 +1101,24 @@ int gaamd_stamps(int on, unsigned long long out[8]) {
     return 0;
 }
 
+// Diagnostic: `steps` blocking comex_accs calls issued from C, the k-th on pointer
+// set k % nsets (srcs[k], dsts[k]); returns the elapsed wall-clock ns (0 on a failed
+// call).  The bench's blocking_api line times the same calls from Python, whose
+// per-call cost is the interpreter's, not the library's: this is the figure a C or
+// Fortran caller (GA's NGA_Acc -> ARMCI_AccS) sees.
+unsigned long long gaamd_time_blocking_accs(int op, void *scale, void *const *srcs, int *ss, void *const *dsts, int *ds,
+                                            int *count, int levels, int proc, int nsets, int steps) {
+    if (nsets <= 0 || steps <= 0) return 0;
+    timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < steps; ++i)
+        if (comex_accs(op, scale, srcs[i % nsets], ss, dsts[i % nsets], ds, count, levels, proc, COMEX_GROUP_WORLD) !=
+            COMEX_SUCCESS)
+            return 0;
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (unsigned long long)(t1.tv_sec - t0.tv_sec) * 1000000000ull + (unsigned long long)(t1.tv_nsec - t0.tv_nsec);
+}
+
 int gaamd_iov_path_counts(unsigned long long counts[3]) {
     for (int k = 0; k < 3; ++k) counts[k] = g_iov_path[k].load(std::memory_order_relaxed);
     return 0;

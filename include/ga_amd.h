@@ -107,6 +107,10 @@ int gaamd_iov_path_counts(unsigned long long counts[3]);
  * to be synchronised, [7] synchronised.  out (may be NULL) receives the current
  * stamps; on = 1 clears them and turns stamping on, 0 off, -1 leaves it. */
 int gaamd_stamps(int on, unsigned long long out[8]);
+/* diagnostic: `steps` blocking comex_accs calls from C over `nsets` (src, dst) pointer
+   sets; elapsed wall-clock ns, 0 if a call failed (the bench's C-caller blocking rate) */
+unsigned long long gaamd_time_blocking_accs(int op, void *scale, void *const *srcs, int *ss, void *const *dsts,
+                                            int *ds, int *count, int levels, int proc, int nsets, int steps);
 /* one-pass accumulates this rank applied into the segment of a rank on the same GPU */
 unsigned long long gaamd_one_pass_count(void);
 /* comex_malloc calls served by a freed segment block kept for reuse (with its IPC export) */
