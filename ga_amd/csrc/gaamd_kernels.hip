@@ -1582,11 +1582,16 @@ __global__ __launch_bounds__(64) void k_rmw(void *addr, int swap, int bytes, uin
 
 // Completion flag of a blocking call (comex.cpp / sched.cpp sched_wait_flag): after
 // every earlier operation of the stream, one lane stores `v` into pinned host memory
-// with a system-scope release (a vector store), and the host spins on that word --
-// about 4 us sooner than the runtime's completion signal wakes hipStreamSynchronize
-// (tools/completion_probe.hip mode 3, profiles/r03/s21).
+// with a system-scope store (a vector store, `global_store_dwordx2 … sc0 sc1`), and
+// the host spins on that word -- about 4 us sooner than the runtime's completion
+// signal wakes hipStreamSynchronize (tools/completion_probe.hip mode 3,
+// profiles/r03/s21).  The store is relaxed: stream order already puts it after the
+// previous kernel's end (whose end-of-kernel release made its writes visible), and
+// the flag only says "that kernel has finished" (its source is consumed).  A release
+// here cost the flag kernel an L2 write-back: 4.2 us of GPU time per blocking call
+// (profiles/r04/final/rocprofv3_kernel_stats_H_1stream.csv).
 __global__ __launch_bounds__(64) void k_flag(uint64_t *flag, uint64_t v) {
-    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 int launch_flag(uint64_t *flag_dev, uint64_t v, hipStream_t stream) {

@@ -15,6 +15,10 @@
 //           pinned host memory -- no second dispatch; each count a release at agent
 //           scope (every workgroup's stores visible first)
 //   fused_relaxed  the same with relaxed counts (loads done, stores maybe in flight)
+//   event   launch + hipEventRecord, the host spinning on hipEventQuery
+//   flag_relaxed  as flag with a relaxed system-scope store (no L2 write-back)
+// argv[2] = "spin": hipSetDeviceFlags(hipDeviceScheduleSpin) first (the runtime's own
+// waits spin instead of yielding / sleeping on an interrupt)
 // Three buffer sets rotate (MALL defeat).  Prints per-call medians and the fraction
 // of the 8 TB/s HBM peak.
 //
@@ -75,6 +79,9 @@ __global__ __launch_bounds__(64) void k_acc(const double *src, double *dst, doub
 __global__ __launch_bounds__(64) void k_flag(uint64_t *flag, uint64_t v) {
     if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__global__ __launch_bounds__(64) void k_flag_relaxed(uint64_t *flag, uint64_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 static double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -82,6 +89,8 @@ static double now_us() {
 
 int main(int argc, char **argv) {
     const int calls = argc > 1 ? atoi(argv[1]) : 200;
+    if (argc > 2 && !strcmp(argv[2], "spin")) CK(hipSetDeviceFlags(hipDeviceScheduleSpin));
+    hipEvent_t ev;
     const size_t bytes = (size_t)kRows * kLd * 8;
     double *src[3], *dst[3];
     for (int k = 0; k < 3; ++k) {
@@ -99,15 +108,17 @@ int main(int argc, char **argv) {
     *flag_h = 0;
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     const dim3 grid(kRows * kChunks), blk(64);
     const double alg = 3.0 * kRows * kCols * 8;
     uint64_t seq = 0;
     auto spin = [&](uint64_t v) {
         while (__atomic_load_n((volatile uint64_t *)flag_h, __ATOMIC_ACQUIRE) < v) __builtin_ia32_pause();
     };
-    const char *modes[] = {"stream", "sync", "flag", "fused", "fused_relaxed"};
+    const char *modes[] = {"stream", "sync", "flag", "fused", "fused_relaxed", "event", "flag_relaxed"};
     for (int rep = 0; rep < 2; ++rep) {
-        for (int m = 0; m < 5; ++m) {
+        for (int m = 0; m < 7; ++m) {
+            if (m == 3 || m == 4) continue;   // the fused forms: measured once, 164-1660 us per call
             std::vector<double> t;
             // warm-up
             for (int i = 0; i < 5; ++i)
@@ -132,9 +143,17 @@ int main(int argc, char **argv) {
                     } else if (m == 3) {
                         hipLaunchKernelGGL(k_acc<1>, grid, blk, 0, st, src[i % 3], dst[i % 3], 1.5, ctr, flag_d, ++seq);
                         spin(seq);
-                    } else {
+                    } else if (m == 4) {
                         hipLaunchKernelGGL(k_acc<2>, grid, blk, 0, st, src[i % 3], dst[i % 3], 1.5, ctr, flag_d, ++seq);
                         spin(seq);
+                    } else if (m == 6) {
+                        hipLaunchKernelGGL(k_acc<0>, grid, blk, 0, st, src[i % 3], dst[i % 3], 1.5, ctr, flag_d, 0);
+                        hipLaunchKernelGGL(k_flag_relaxed, dim3(1), dim3(64), 0, st, flag_d, ++seq);
+                        spin(seq);
+                    } else {
+                        hipLaunchKernelGGL(k_acc<0>, grid, blk, 0, st, src[i % 3], dst[i % 3], 1.5, ctr, flag_d, 0);
+                        CK(hipEventRecord(ev, st));
+                        while (hipEventQuery(ev) == hipErrorNotReady) __builtin_ia32_pause();
                     }
                     t.push_back(now_us() - t0);
                 }
@@ -142,8 +161,8 @@ int main(int argc, char **argv) {
             CK(hipStreamSynchronize(st));
             std::sort(t.begin(), t.end());
             const double med = t[t.size() / 2], p10 = t[t.size() / 10], p90 = t[t.size() * 9 / 10];
-            printf("{\"mode\": \"%s\", \"rep\": %d, \"us_median\": %.2f, \"us_p10\": %.2f, \"us_p90\": %.2f, "
-                   "\"frac_of_8TBs\": %.4f}\n", modes[m], rep, med, p10, p90, alg / (med * 1e-6) / 8e12);
+            printf("{\"mode\": \"%s\", \"spin_flag\": %d, \"rep\": %d, \"us_median\": %.2f, \"us_p10\": %.2f, \"us_p90\": %.2f, "
+                   "\"frac_of_8TBs\": %.4f}\n", modes[m], argc > 2 && !strcmp(argv[2], "spin"), rep, med, p10, p90, alg / (med * 1e-6) / 8e12);
             fflush(stdout);
         }
     }
