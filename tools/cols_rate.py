@@ -3,7 +3,7 @@ tests/test_gpu_semantics.py::test_ordered_kernel_large_overlapping_rows), three
 rotating source copies, 20 launches between events on the library's primary stream;
 prints one JSON line per op with GB/s of physical bytes (src once + the dst run read
 and written once).  Tuning evidence, not product code.
-    python tools/cols_rate.py [ops...]   (ops: 42 = long, 38 = double; default both)
+    python tools/cols_rate.py [ops...]   (comex op codes 37..42; default 42 and 38)
 """
 import ctypes
 import json
@@ -17,8 +17,12 @@ import ga_amd  # noqa: E402
 L = ga_amd._lib.load()
 
 
-def rate(op, rows=2048, w=8192, n=20):
-    a = -3 if op == 42 else 0.7071067811865476
+ESZ = {37: 4, 38: 8, 39: 4, 40: 8, 41: 16, 42: 8}
+
+
+def rate(op, rows=2048, row_bytes=65536, n=20):
+    w = row_bytes // 8
+    a = -3 if op in (37, 42) else 0.7071067811865476
     srcs = [ga_amd.DeviceBuffer(rows * w * 8) for _ in range(3)]
     dst = ga_amd.DeviceBuffer(w * 8)
     for b in srcs + [dst]:
@@ -44,7 +48,7 @@ def rate(op, rows=2048, w=8192, n=20):
     for b in srcs + [dst]:
         b.free()
     phys = rows * w * 8 + 2 * w * 8
-    return {"op": op, "us": round(ms * 1e3, 1), "GBps_physical": round(phys / (ms * 1e-3) / 1e9),
+    return {"op": op, "elem_bytes": ESZ[op], "us": round(ms * 1e3, 1), "GBps_physical": round(phys / (ms * 1e-3) / 1e9),
             "blocks": info["blocks"], "variant": info["unroll"]}
 
 
