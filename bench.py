@@ -519,6 +519,10 @@ def run_gpu(args, dist, finalize=True):
         # Fortran NGA_Acc -> ARMCI_AccS sees, without the interpreter's per-call cost
         srcs = (ctypes.c_void_p * len(ptrs))(*[p_[0].value for p_ in ptrs])
         dsts = (ctypes.c_void_p * len(ptrs))(*[p_[1].value for p_ in ptrs])
+        # W untimed calls of the C loop first, as every timed region here has a warm-up
+        if args.warmup and not L.gaamd_time_blocking_accs(op, sp, srcs, ss, dsts, ds, cnt, levels, target, len(ptrs),
+                                                          args.warmup):
+            raise RuntimeError("blocking warm-up (C loop) failed")
         L.comex_barrier(0)
         dist.barrier()
         ga_amd.sync()
