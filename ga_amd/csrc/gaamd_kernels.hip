@@ -625,8 +625,7 @@ __global__ __launch_bounds__(64) void k_ordered_cols(const Desc d, const OP op) 
 // Hence the split of the products onto the loaders, and a fast path for the common
 // geometry -- every row into ONE dst run (all dst strides zero): no per-row offset
 // or run test, one LDS read + one add per row, 16 rows per batch.
-// One barrier per tile: the loaders fill tile i+1 while wave 0 applies tile i, with
-// the loads of tile i+2 already in flight across the barrier.
+// One barrier per tile: the loaders fill tile i+1 while wave 0 applies tile i.
 // Measured read rate of this access pattern (tools/piece_probe.hip, 256 workgroups
 // each reading 256-byte pieces of 2048 rows with 64 KiB in flight): 5.4 TB/s.
 constexpr int KC_NW = 8;                 // waves per workgroup: 1 applier + 7 loaders
@@ -650,48 +649,40 @@ __global__ __launch_bounds__(KC_NW * 64) void k_ordered_cols_lds(const Desc d, c
     const int64_t xl = (int64_t)min(col, d.nvec - 1u) * W;
     const uint32_t ntiles = (d.rows + (uint32_t)T - 1) / (uint32_t)T;
     const bool full = col0 + (uint32_t)CW <= d.nvec;   // no partial slice group (workgroup-uniform)
-    const uint32_t lw = wave - 1, sub = lane / (uint32_t)LPR, s0 = (lane % (uint32_t)LPR) * SPL;
-    // full column groups: the next tile's 16-byte loads live in registers from one
-    // barrier to the next (issued before the barrier, stored into LDS after it), so
-    // every loader lane has KC_P loads in flight while the workgroup synchronises
-    V16 nxt[KC_P];
-    auto issue = [&](uint32_t tl) {
-        const int64_t xo = (int64_t)(col0 + s0) * W;
+    auto load_store = [&](uint32_t tl, int buf) {    // loader waves: tile `tl` into tile[buf]
+        const uint32_t lw = wave - 1, sub = lane / (uint32_t)LPR, s0 = (lane % (uint32_t)LPR) * SPL;
+        if (full) {
+            const int64_t xo = (int64_t)(col0 + s0) * W;
+            V16 s[KC_P];
 #pragma unroll
-        for (int k = 0; k < KC_P; ++k) {
-            const uint32_t r = min(tl * (uint32_t)T + (lw * KC_P + (uint32_t)k) * RPI + sub, d.rows - 1u);
-            int64_t so, dof;
-            row_offsets<LV>(d, d.row0 + r, so, dof);
-            nxt[k] = vload<16, true>(d.src + so + xo);
+            for (int k = 0; k < KC_P; ++k) {
+                const uint32_t r = min(tl * (uint32_t)T + (lw * KC_P + (uint32_t)k) * RPI + sub, d.rows - 1u);
+                int64_t so, dof;
+                row_offsets<LV>(d, d.row0 + r, so, dof);
+                s[k] = vload<16, true>(d.src + so + xo);
+            }
+#pragma unroll
+            for (int k = 0; k < KC_P; ++k)
+                *reinterpret_cast<V16 *>(&tile[buf][((lw * KC_P + (uint32_t)k) * RPI + sub) * CW + s0]) =
+                    op.template pre<16>(s[k]);
+        } else {
+            // the last workgroup of a row whose slice count is not a multiple of CW:
+            // W-byte loads of clamped slices (never past the row's last byte)
+#pragma unroll
+            for (int k = 0; k < KC_P; ++k) {
+                const uint32_t r = min(tl * (uint32_t)T + (lw * KC_P + (uint32_t)k) * RPI + sub, d.rows - 1u);
+                int64_t so, dof;
+                row_offsets<LV>(d, d.row0 + r, so, dof);
+                V v[SPL];
+#pragma unroll
+                for (int j = 0; j < SPL; ++j)
+                    v[j] = vload<W, true>(d.src + so + (int64_t)min(col0 + s0 + (uint32_t)j, d.nvec - 1u) * W);
+#pragma unroll
+                for (int j = 0; j < SPL; ++j)
+                    tile[buf][((lw * KC_P + (uint32_t)k) * RPI + sub) * CW + s0 + j] = op.template pre<W>(v[j]);
+            }
         }
     };
-    auto store = [&](int buf) {
-#pragma unroll
-        for (int k = 0; k < KC_P; ++k)
-            *reinterpret_cast<V16 *>(&tile[buf][((lw * KC_P + (uint32_t)k) * RPI + sub) * CW + s0]) =
-                op.template pre<16>(nxt[k]);
-    };
-    // the last workgroup of a row whose slice count is not a multiple of CW: W-byte
-    // loads of clamped slices (never past the row's last byte), loaded and stored
-    // within one step
-    auto load_store_partial = [&](uint32_t tl, int buf) {
-#pragma unroll
-        for (int k = 0; k < KC_P; ++k) {
-            const uint32_t r = min(tl * (uint32_t)T + (lw * KC_P + (uint32_t)k) * RPI + sub, d.rows - 1u);
-            int64_t so, dof;
-            row_offsets<LV>(d, d.row0 + r, so, dof);
-            V v[SPL];
-#pragma unroll
-            for (int j = 0; j < SPL; ++j)
-                v[j] = vload<W, true>(d.src + so + (int64_t)min(col0 + s0 + (uint32_t)j, d.nvec - 1u) * W);
-#pragma unroll
-            for (int j = 0; j < SPL; ++j)
-                tile[buf][((lw * KC_P + (uint32_t)k) * RPI + sub) * CW + s0 + j] = op.template pre<W>(v[j]);
-        }
-    };
-    // workgroup barrier that waits for this wave's LDS accesses only: __syncthreads'
-    // workgroup-scope fence would also wait for the loads in flight (vmcnt(0))
-    auto barrier_lds = [] { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
     const bool lane_ok = lane < (uint32_t)CW && col < d.nvec;
     bool one_run = true;                             // every row into one dst run
     for (int j = 0; j < d.levels; ++j) one_run = one_run && d.d_str[j] == 0;
@@ -716,27 +707,12 @@ __global__ __launch_bounds__(KC_NW * 64) void k_ordered_cols_lds(const Desc d, c
         }
         acc = op.template add<W>(acc, x);
     };
-    if (wave != 0) {
-        if (full) {
-            issue(0);
-            store(0);
-            if (ntiles > 1) issue(1);
-        } else {
-            load_store_partial(0, 0);
-        }
-    }
-    barrier_lds();
+    if (wave != 0) load_store(0, 0);
+    __syncthreads();
     for (uint32_t i = 0; i < ntiles; ++i) {
         const int buf = (int)(i & 1);
         if (wave != 0) {
-            if (i + 1 < ntiles) {
-                if (full) {
-                    store(buf ^ 1);
-                    if (i + 2 < ntiles) issue(i + 2);
-                } else {
-                    load_store_partial(i + 1, buf ^ 1);
-                }
-            }
+            if (i + 1 < ntiles) load_store(i + 1, buf ^ 1);
         } else {
             const uint32_t r0 = i * (uint32_t)T;
             const uint32_t n = min((uint32_t)T, d.rows - r0);
@@ -763,7 +739,7 @@ __global__ __launch_bounds__(KC_NW * 64) void k_ordered_cols_lds(const Desc d, c
                 for (; t < n; ++t) apply_row(r0 + t, tile[buf][t * CW + c]);
             }
         }
-        barrier_lds();
+        __syncthreads();
     }
     if (held && lane_ok) vstore<W, false>(d.dst + cur + xl, acc);
 }
