@@ -16,14 +16,16 @@ rc=0
 REPS=${REPS:-10}
 for alloc in ${ALLOCS:-ipc vmm}; do
   for i in $(seq 1 $REPS); do
-    COMEX_AMD_SEGMENT_ALLOC=$alloc COMEX_AMD_SEGMENT_CACHE_MB=0 COMEX_AMD_ONE_PASS_LEASE_US=0 BENCH_CHECK_LOOPS=2 timeout -k 10 150 \
+    if [ -n "$DEFAULTS" ]; then cfg=""; else cfg="COMEX_AMD_SEGMENT_CACHE_MB=0 COMEX_AMD_ONE_PASS_LEASE_US=0"; fi
+    env COMEX_AMD_SEGMENT_ALLOC=$alloc $cfg BENCH_CHECK_LOOPS=2 timeout -k 10 150 \
       python bench.py --gpus 8 --steps 2 --warmup 1 --warmup-ms 0 --no-cpu --ga-dims 16384 --c5-steps 2 \
       > $O/${alloc}_$i.json 2> $O/${alloc}_$i.err
     rc=$?
     ref=$(grep -c "hipIpcGetMemHandle of a" $O/${alloc}_$i.err)
     st=$(grep -c "not its tags" $O/${alloc}_$i.err)
+    sa=$(grep -c "hipMemSetAccess.*refused" $O/${alloc}_$i.err)
     mm=$(python -c "import json;d=json.load(open('$O/${alloc}_$i.json'));c=d['c5'];print(sum(v['mismatches'] for v in c['exchange_check_loops'].values())+sum(v['result']!='exact' for v in c['exchange_check'].values()))" 2>/dev/null || echo "?")
-    echo "${alloc}_$i rc $rc refusals $ref stale $st mismatches $mm" | tee -a $O/summary.txt
+    echo "${alloc}_$i ${DEFAULTS:+defaults }rc $rc refusals $ref access_refused $sa stale $st mismatches $mm" | tee -a $O/summary.txt
     [ $rc -eq 0 ] || exit $rc
   done
 done
