@@ -226,6 +226,8 @@ struct CachedBlock {
     size_t bytes;
     bool exported;
     hipIpcMemHandle_t h;
+    bool vmm = false;   // a block of the vmm allocator: kept with its handle, mapping and descriptor
+    VmmBlock vb;
 };
 static std::deque<CachedBlock> g_blocks;   // oldest first
 static size_t g_blocks_bytes = 0;
@@ -275,6 +277,11 @@ static size_t free_watermark() {
 }
 
 static void block_free_one(const CachedBlock &b) {
+    if (b.vmm) {
+        VmmBlock v = b.vb;
+        vmm_free(&v);
+        return;
+    }
     addr_event('f', b.p, b.bytes, -1);
     GA_HIP(hipFree(b.p));
 }
@@ -285,11 +292,11 @@ static void block_flush() {
     g_blocks_bytes = 0;
 }
 
-static void block_put(void *p, size_t bytes, bool exported, const hipIpcMemHandle_t &h) {
-    const size_t cap = block_cache_cap();
+static void block_put(const CachedBlock &nb) {
+    const size_t bytes = nb.bytes, cap = block_cache_cap();
     if (bytes > cap || device_free() < free_watermark()) {
         // too big to keep, or the device is short of memory: give it back now
-        block_free_one({p, bytes, exported, h});
+        block_free_one(nb);
         if (!g_blocks.empty() && device_free() < free_watermark()) {
             g_cache_trims.fetch_add(1, std::memory_order_relaxed);
             block_flush();
@@ -301,14 +308,23 @@ static void block_put(void *p, size_t bytes, bool exported, const hipIpcMemHandl
         g_blocks_bytes -= g_blocks.front().bytes;
         g_blocks.pop_front();
     }
-    g_blocks.push_back({p, bytes, exported, h});
+    g_blocks.push_back(nb);
     g_blocks_bytes += bytes;
+}
+
+static void block_put(void *p, size_t bytes, bool exported, const hipIpcMemHandle_t &h) {
+    CachedBlock b;
+    b.p = p;
+    b.bytes = bytes;
+    b.exported = exported;
+    b.h = h;
+    block_put(b);
 }
 
 // a cached block of exactly `bytes`; its export in *h when it has one
 static bool block_take(size_t bytes, void **p, bool *exported, hipIpcMemHandle_t *h) {
     for (auto it = g_blocks.begin(); it != g_blocks.end(); ++it) {
-        if (it->bytes != bytes) continue;
+        if (it->bytes != bytes || it->vmm) continue;
         *p = it->p;
         *exported = it->exported;
         if (it->exported) *h = it->h;
@@ -316,6 +332,22 @@ static bool block_take(size_t bytes, void **p, bool *exported, hipIpcMemHandle_t
         g_blocks.erase(it);
         g_block_reuse.fetch_add(1, std::memory_order_relaxed);
         addr_event('r', *p, bytes, -1);
+        return true;
+    }
+    return false;
+}
+
+// the vmm allocator's counterpart: a cached block of exactly `bytes`, with its handle,
+// mapping and descriptor (a reused block is a known-good one: the runtime defect of
+// vmm.cpp strikes new blocks, so GA's create/destroy cycles then create none)
+static bool block_take_vmm(size_t bytes, VmmBlock *v) {
+    for (auto it = g_blocks.begin(); it != g_blocks.end(); ++it) {
+        if (it->bytes != bytes || !it->vmm) continue;
+        *v = it->vb;
+        g_blocks_bytes -= bytes;
+        g_blocks.erase(it);
+        g_block_reuse.fetch_add(1, std::memory_order_relaxed);
+        addr_event('r', v->va, bytes, -1);
         return true;
     }
     return false;
@@ -482,7 +514,8 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     mine.pid = (int32_t)getpid();
     if (bytes) {
         if (vmm) {
-            p = vmm_alloc(bytes, &vlocal);
+            block_trim_for(bytes);
+            p = block_take_vmm(bytes, &vlocal) ? vlocal.va : vmm_alloc(bytes, &vlocal);
             mine.vmm = 1;
             mine.fd = vlocal.fd;
             mine.vmm_bytes = vlocal.bytes;
@@ -780,7 +813,18 @@ int comex_free(void *ptr, comex_group_t group) {
     // (hipIpcGetMemHandle: invalid argument in the next comex_malloc)
     members_barrier(members, group);
     if (is_vmm) {
-        vmm_free(&vblock);   // physical memory back now
+        if (block_cache_cap()) {   // kept, with its descriptor, for the next comex_malloc
+            CachedBlock b;
+            b.p = vblock.va;
+            b.bytes = local_bytes;
+            b.exported = false;
+            memset(&b.h, 0, sizeof(b.h));
+            b.vmm = true;
+            b.vb = vblock;
+            block_put(b);
+        } else {
+            vmm_free(&vblock);   // physical memory back now
+        }
     } else if (local && device) {
         if (block_cache_cap()) block_put(local, local_bytes, exported, handle);   // kept for the next comex_malloc
         else block_free_one({local, local_bytes, exported, handle});

@@ -766,9 +766,7 @@ def segment_cache_test(L, rank, size):
     A different size every third round takes a fresh block."""
     import ga_amd
     assert ga_amd.comex_init() == 0
-    # the cache holds IPC-exported blocks; the vmm allocator frees at once
-    cache_on = (os.environ.get("COMEX_AMD_SEGMENT_CACHE_MB", "1") != "0"
-                and os.environ.get("COMEX_AMD_SEGMENT_ALLOC", "ipc") != "vmm")
+    cache_on = os.environ.get("COMEX_AMD_SEGMENT_CACHE_MB", "1") != "0"   # both allocators cache
     reuse0 = L.gaamd_segment_cache_reuse()
     one = ctypes.c_double(1.0)
     for it in range(9):

@@ -351,7 +351,7 @@ def test_owner_host_source_self_acc_vs_one_pass_peers(n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode,n,extra", [("remote", 3, {}), ("onepass", 4, {}), ("directsrc", 3, {}),
-                                          ("segcache", 3, {"COMEX_AMD_SEGMENT_CACHE_MB": "0"}),
+                                          ("segcache", 3, {"COMEX_AMD_SEGMENT_CACHE_MB": "0"}), ("segcache", 3, {}),
                                           ("stress", 3, {"COMEX_AMD_STAGING_MB": "1"}),
                                           ("c5full", 8, {"COMEX_AMD_STAGING_MB": "256", "TEST_C5_N": "16384"}),
                                           ("c5full", 4, {"COMEX_AMD_PEER_LOADS": "all", "TEST_C5_N": "8192"})])
