@@ -486,6 +486,16 @@ static void shm_unmap_registered(char *p, size_t map_bytes) {
 // with no error anywhere.  A mapping that does not read the tags is therefore
 // closed, the owner's block set aside (quarantined) and replaced, and the exchange
 // repeated (all ranks, collectively), up to 4 times.
+// COMEX_AMD_TEST_STALE_GEN=N (tests only): every peer treats its first mapping of each
+// rank's N-th allocation as stale
+static uint64_t test_stale_gen() {
+    static const uint64_t v = [] {
+        const char *e = getenv("COMEX_AMD_TEST_STALE_GEN");
+        return e ? (uint64_t)strtoull(e, nullptr, 10) : 0ull;
+    }();
+    return v;
+}
+
 static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool device) {
     ensure_init();
     Runtime &r = rt();
@@ -607,7 +617,13 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
             uint64_t t[2] = {0, 0};
             GA_HIP(hipMemcpy(&t[0], mapped[q], 8, hipMemcpyDeviceToHost));
             GA_HIP(hipMemcpy(&t[1], (char *)mapped[q] + all[q].bytes - 8, 8, hipMemcpyDeviceToHost));
-            if (t[0] != seg_tag(q, all[q].gen, 0) || t[1] != seg_tag(q, all[q].gen, 1)) {
+            if (attempt == 0 && all[q].gen == test_stale_gen()) {
+                // test hook: this round's mappings of allocation N are treated as stale, so the
+                // replacement path (set aside, new block, repeated exchange) runs on demand
+                fprintf(stderr, "[ga_amd %d] COMEX_AMD_TEST_STALE_GEN: treating rank %d's allocation %llu as stale\n",
+                        r.rank, q, (unsigned long long)all[q].gen);
+                stale[q] = 1;
+            } else if (t[0] != seg_tag(q, all[q].gen, 0) || t[1] != seg_tag(q, all[q].gen, 1)) {
                 stale[q] = 1;
                 fprintf(stderr, "[ga_amd %d] the %s mapping of rank %d's new %zu-byte segment (%p in its space) "
                         "reads %#llx / %#llx, not its tags: another allocation's memory\n", r.rank, all[q].vmm ? "vmm" : "IPC", q,

@@ -112,6 +112,8 @@ def main():
         direct_src_test(L, rank, size)
     elif mode == "segcache":
         segment_cache_test(L, rank, size)
+    elif mode == "stalefix":
+        stale_fix_test(L, rank, size)
     elif mode in ("armcimisc", "armcimisc-gloo"):
         armci_misc_test(L, rank, size)
     else:
@@ -755,6 +757,46 @@ def self_order_test(L, rank, size):
     ga_amd.comex_barrier()
     assert ga_amd.comex_free(me) == 0
     ga_amd.comex_finalize()
+
+
+def stale_fix_test(L, rank, size):
+    """Run with COMEX_AMD_TEST_STALE_GEN=2: every peer treats its first mapping of each
+    rank's second segment as stale (the runtime binding a new block to other memory,
+    DESIGN.md section 6), so every owner sets that block aside, allocates another and the
+    exchange repeats.  Three segments, each accumulated into by its owner and the
+    previous rank, checked exactly; the remap counter must show the replacement."""
+    import ga_amd
+    assert ga_amd.comex_init() == 0
+    r0 = L.gaamd_segment_remaps()
+    one = ctypes.c_double(1.0)
+    n = 1 << 18
+    segs = []
+    for it in range(3):
+        seg = ga_amd.comex_malloc(n * 8, size)
+        segs.append(seg)
+        L.gaamd_memset(ctypes.c_void_p(seg[rank]), 0, n * 8)
+        ga_amd.sync()
+        ga_amd.comex_barrier()
+        src = ga_amd.DeviceBuffer(n * 8)
+        ga_amd.fill_const(src.ptr, n * 8, float(2 ** rank))
+        ga_amd.sync()
+        for t in {rank, (rank + 1) % size}:
+            assert L.comex_acc(38, ctypes.byref(one), ctypes.c_void_p(src.ptr), ctypes.c_void_p(seg[t]), n * 8, t,
+                               0) == 0
+        ga_amd.comex_barrier()
+        got = np.zeros(n)
+        assert L.comex_get(ctypes.c_void_p(seg[rank]), got.ctypes.data_as(ctypes.c_void_p), n * 8, rank, 0) == 0
+        prv = (rank - 1) % size
+        want = float(2 ** rank + (2 ** prv if prv != rank else 0))
+        bad = int(np.count_nonzero(got != want))
+        assert bad == 0, f"rank {rank} segment {it}: {bad} wrong"
+        src.free()
+        ga_amd.comex_barrier()
+    remaps = L.gaamd_segment_remaps() - r0
+    assert remaps >= 1, f"rank {rank}: no segment replaced"
+    for seg in segs:
+        assert ga_amd.comex_free(seg[rank]) == 0
+    say(rank, f"stale segment replaced ({remaps} remap), all exact")
 
 
 def segment_cache_test(L, rank, size):

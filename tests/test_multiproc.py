@@ -366,6 +366,18 @@ def test_vmm_segments(mode, n, extra):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("alloc", ["ipc", "vmm"])
+def test_stale_segment_replaced(alloc):
+    """The replacement path for a new segment whose peer mappings read other memory
+    (the runtime defect of DESIGN.md section 6), forced on demand
+    (COMEX_AMD_TEST_STALE_GEN=2): the owner sets the block aside, allocates another, the
+    exchange repeats, and every accumulate into the segments is exact, on both segment
+    allocators."""
+    launch("stalefix", n=3, timeout=120,
+           extra_env={"COMEX_AMD_TEST_STALE_GEN": "2", "COMEX_AMD_SEGMENT_ALLOC": alloc})
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["remote", "hostseg-ga"])
 def test_host_segments_three_ranks(mode):
     """COMEX_AMD_SEGMENT=host gives every rank a host segment (a
