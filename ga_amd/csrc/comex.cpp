@@ -575,7 +575,7 @@ extern "C" {
 static void exit_without_finalize() {
     Runtime &r = rt();
     if (!r.initialized) return;
-    if (r.progress.joinable()) r.progress.detach();
+    progress_stop_at_exit(0.2);
     wire_detach();
 }
 

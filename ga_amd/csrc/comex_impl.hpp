@@ -108,7 +108,8 @@ void vmm_finalize();
 
 // ---- remote operations through the owner (remote.cpp) -----------------------
 void remote_init();             // staging buffer, peer mappings, progress thread (collective)
-void remote_finalize();         // after comex_barrier: job bookkeeping freed, progress thread stopped
+void remote_finalize();
+void progress_stop_at_exit(double wait_s);   // exit without comex_finalize: join an idle progress thread         // after comex_barrier: job bookkeeping freed, progress thread stopped
 void remote_release_staging();  // the peers' staging mappings closed
 void remote_free_staging();     // our staging freed (after a barrier: nobody maps it)
 uint64_t sub_ring_bytes();

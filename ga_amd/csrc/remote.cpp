@@ -197,6 +197,8 @@ void post_request_rmw(int t, int swap, uint64_t addr, int bytes, uint64_t val) {
 }
 
 // owner side: drain the inbox in ticket order
+static std::atomic<bool> g_progress_exited{false};
+
 static void progress_loop() {
     Runtime &r = rt();
     GA_HIP(hipSetDevice(r.device));
@@ -526,6 +528,25 @@ static void progress_loop() {
     }
     if (prog_work) (void)hipFree(prog_work);
     if (rmw_host) (void)hipHostFree(rmw_host);
+    g_progress_exited.store(true, std::memory_order_release);
+}
+
+// a process leaving without comex_finalize (exit_without_finalize, comex.cpp): stop the
+// progress thread if it is idle within `wait_s` and join it, so it is not inside a HIP
+// call while the runtime tears down; otherwise leave it detached
+void progress_stop_at_exit(double wait_s) {
+    Runtime &r = rt();
+    if (!r.progress.joinable()) return;
+    r.stop.store(true, std::memory_order_release);
+    auto now_s = [] {
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        return ts.tv_sec + 1e-9 * ts.tv_nsec;
+    };
+    const double t0 = now_s();
+    while (!g_progress_exited.load(std::memory_order_acquire) && now_s() - t0 < wait_s) sched_yield();
+    if (g_progress_exited.load(std::memory_order_acquire)) r.progress.join();
+    else r.progress.detach();
 }
 
 // ---- asynchronous remote accumulate ---------------------------------------

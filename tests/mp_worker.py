@@ -797,6 +797,10 @@ def stale_fix_test(L, rank, size):
     for seg in segs:
         assert ga_amd.comex_free(seg[rank]) == 0
     say(rank, f"stale segment replaced ({remaps} remap), all exact")
+    # the set-aside blocks go back at comex_finalize (GA_Terminate's path); without it the
+    # process leaves through the exit hook (STALEFIX_NO_FINALIZE=1)
+    if os.environ.get("STALEFIX_NO_FINALIZE") != "1":
+        assert ga_amd.comex_finalize() == 0
 
 
 def segment_cache_test(L, rank, size):

@@ -366,15 +366,17 @@ def test_vmm_segments(mode, n, extra):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("alloc", ["ipc", "vmm"])
-def test_stale_segment_replaced(alloc):
+@pytest.mark.parametrize("alloc,finalize", [("ipc", True), ("vmm", True), ("ipc", False), ("vmm", False)])
+def test_stale_segment_replaced(alloc, finalize):
     """The replacement path for a new segment whose peer mappings read other memory
     (the runtime defect of DESIGN.md section 6), forced on demand
     (COMEX_AMD_TEST_STALE_GEN=2): the owner sets the block aside, allocates another, the
     exchange repeats, and every accumulate into the segments is exact, on both segment
-    allocators."""
+    allocators; with comex_finalize and without (the exit hook then joins the idle
+    progress thread: a process exiting with set-aside blocks once crashed there)."""
     launch("stalefix", n=3, timeout=120,
-           extra_env={"COMEX_AMD_TEST_STALE_GEN": "2", "COMEX_AMD_SEGMENT_ALLOC": alloc})
+           extra_env={"COMEX_AMD_TEST_STALE_GEN": "2", "COMEX_AMD_SEGMENT_ALLOC": alloc,
+                      "STALEFIX_NO_FINALIZE": "0" if finalize else "1"})
 
 
 @pytest.mark.gpu
