@@ -28,6 +28,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <stddef.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <time.h>
@@ -410,3 +411,46 @@ void vmm_finalize() {
 }  // namespace gaamd
 
 extern "C" unsigned long long gaamd_vmm_access_retries() { return gaamd::g_access_retries.load(); }
+
+// CPU self-test of the descriptor exchange (no GPU): every rank of the bootstrap
+// makes a memfd per round holding "rank:round", exchanges the descriptors with every
+// other rank exactly as comex_malloc does, and reads each received one back; the number
+// of wrong or missing descriptors (0 = pass)
+extern "C" int gaamd_vmm_exchange_selftest(int rounds) {
+    using namespace gaamd;
+    Runtime &r = rt();
+    boot_init();
+    vmm_listen();
+    struct Who { int32_t pid, pad; uint64_t gen; };
+    int bad = 0;
+    for (int it = 1; it <= rounds; ++it) {
+        const int fd = (int)memfd_create("gaamd_fdx", MFD_CLOEXEC);
+        if (fd < 0) return -1;
+        char msg[32];
+        const int len = snprintf(msg, sizeof(msg), "%d:%d", r.rank, it);
+        if (write(fd, msg, (size_t)len) != len) return -1;
+        Who me{(int32_t)getpid(), 0, (uint64_t)(1000 + it)};
+        std::vector<Who> all((size_t)r.size);
+        boot_allgather(&me, all.data(), sizeof(Who));
+        std::vector<int> to;
+        std::vector<std::pair<int, uint64_t>> from;
+        for (int q = 0; q < r.size; ++q) {
+            if (q == r.rank) continue;
+            to.push_back(all[(size_t)q].pid);
+            from.push_back({q, all[(size_t)q].gen});
+        }
+        std::vector<int> got(from.size(), -1);
+        vmm_exchange(fd, r.rank, me.gen, to, from, got.data());
+        for (size_t k = 0; k < from.size(); ++k) {
+            char buf[32] = {0};
+            const ssize_t n = pread(got[k], buf, sizeof(buf) - 1, 0);
+            char want[32];
+            snprintf(want, sizeof(want), "%d:%d", from[k].first, it);
+            if (n <= 0 || strcmp(buf, want) != 0) ++bad;
+            close(got[k]);
+        }
+        close(fd);
+        boot_barrier();
+    }
+    return bad;
+}

@@ -124,6 +124,9 @@ unsigned long long gaamd_segment_cache_trims(void);
 int gaamd_segment_kind(const void *p);
 /* vmm segment allocator: hipMemSetAccess refusals retried at a fresh range (diagnostic) */
 unsigned long long gaamd_vmm_access_retries(void);
+/* CPU self-test of the vmm allocator's descriptor exchange over the bootstrap (no GPU):
+   wrong or missing descriptors, 0 = pass */
+int gaamd_vmm_exchange_selftest(int rounds);
 /* same-node peers whose staging buffer this rank could not map by IPC at
  * comex_init (remote accumulates to or from them would abort); -1 before init */
 int gaamd_peers_unmapped(void);

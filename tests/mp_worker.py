@@ -74,6 +74,8 @@ def main():
             assert nd.value == order.index(nodes[rank]), (nd.value, nodes)
             assert nn.value == len(order) and ns.value == nodes.count(nodes[rank])
             assert L.gaamd_wire_selftest(3) == 0
+        if mode == "boot-fdx":
+            assert L.gaamd_vmm_exchange_selftest(5) == 0
         print(f"RANK {rank} OK", flush=True)
         return
     if mode in ("ga", "ga-gloo"):

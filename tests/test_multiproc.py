@@ -104,6 +104,14 @@ def test_bootstrap_env_shm_four_ranks():
     launch("boot-env", n=4)
 
 
+@pytest.mark.parametrize("n", [2, 5])
+def test_vmm_descriptor_exchange_cpu(n):
+    """The vmm allocator's descriptor exchange (vmm.cpp: per-process datagram sockets,
+    SCM_RIGHTS, messages keyed by (rank, allocation number)) on the CPU: every rank
+    passes a memfd per round to every other and reads the ones it received back."""
+    launch("boot-fdx", n=n)
+
+
 @pytest.mark.parametrize("nodes", [[0, 1], [0, 0, 1, 1], [1, 0, 1, 2]])
 def test_bootstrap_several_nodes_and_wire(nodes):
     """Per-node shm + cross-node collectives through the hooks + TCP PING frames."""
