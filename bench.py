@@ -250,6 +250,7 @@ def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True
     if not L.comex_initialized():
         bootstrap(L, dist)
     assert L.GA_Initialize() == 0
+    routes0 = ga_amd.route_counts()     # this measurement's routes (warm-up included), not the process's
     ia = ga_amd.int_array
     dims = [args.ga_dims, args.ga_dims] if args.ga_dims else GA_DIMS
     exchange = (args.exchange if exchange is None else exchange) and dist.size > 1
@@ -315,7 +316,7 @@ def run_ga(args, dist, exchange=None, steps=None, warmup_ms=None, terminate=True
     else:
         region_ms, _ = event_region(L, step, steps, nxt + steps)
         avg_kernel_s = dist.max(region_ms / 1e3 / steps)
-    routes = ga_amd.route_counts()
+    routes = {k: v - routes0[k] for k, v in ga_amd.route_counts().items()}
     topology = ga_amd.device_topology()
     if src is not None:
         src.free()
