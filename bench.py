@@ -527,10 +527,11 @@ def run_gpu(args, dist, finalize=True):
         L.comex_barrier(0)
         dist.barrier()
         ga_amd.sync()
-        ns = L.gaamd_time_blocking_accs(op, sp, srcs, ss, dsts, ds, cnt, levels, target, len(ptrs), args.steps)
+        ncall = max(args.steps, 100)   # at least 100 calls: a 20-call mean is one slow call away from noise
+        ns = L.gaamd_time_blocking_accs(op, sp, srcs, ss, dsts, ds, cnt, levels, target, len(ptrs), ncall)
         if not ns:
             raise RuntimeError("blocking step (C loop) failed")
-        tc = dist.max(ns * 1e-9)
+        tc = dist.max(ns * 1e-9) * args.steps / ncall   # per K steps, as the Python figure
         blocking = {"api": "comex_accs per step (blocking: returns after its kernel)",
                     "value": round(dist.size * alg_bytes * args.steps / tb / 2 ** 30, 2),
                     "hbm_peak_frac": round(alg_bytes * args.steps / tb / (HBM_PEAK_GBS * 1e9), 4),
@@ -539,6 +540,7 @@ def run_gpu(args, dist, finalize=True):
                     "c_caller": {"value": round(dist.size * alg_bytes * args.steps / tc / 2 ** 30, 2),
                                  "hbm_peak_frac": round(alg_bytes * args.steps / tc / (HBM_PEAK_GBS * 1e9), 4),
                                  "ms_per_step": round(tc / args.steps * 1e3, 4),
+                                 "calls": ncall,
                                  "how": "the same calls from a C loop in the library (gaamd_time_blocking_accs)"}}
 
     res = dict(op=op, desc=desc, payload=payload, alg_bytes=alg_bytes, elems=elems, elapsed=elapsed,
