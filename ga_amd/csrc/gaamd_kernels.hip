@@ -629,7 +629,8 @@ __global__ __launch_bounds__(64) void k_ordered_cols(const Desc d, const OP op) 
 // Measured read rate of this access pattern (tools/piece_probe.hip, 256 workgroups
 // each reading 256-byte pieces of 2048 rows with 64 KiB in flight): 5.4 TB/s.
 constexpr int KC_NW = 8;                 // waves per workgroup: 1 applier + 7 loaders
-template <class OP, int W, int LV, int CW, int KC_P = 8>
+constexpr int KC_P = 8;                  // 16-byte loads per loader lane per tile (56 KiB tiles)
+template <class OP, int W, int LV, int CW>
 __global__ __launch_bounds__(KC_NW * 64) void k_ordered_cols_lds(const Desc d, const OP op) {
     typedef typename Vec<W>::T V;
     typedef typename Vec<16>::T V16;
@@ -882,13 +883,6 @@ struct Plan {
 static int cols_per_group(uint32_t nvec, int W) {
     if (W != 4 && W != 8 && W != 16) return 0;
     int cw = W == 4 ? 32 : 16;
-    // 16 slices: half-size tiles (KC_P = 4) when that takes more than 256 workgroups, so
-    // two fit a CU and up to 512 run in one pass (EXPERIMENT, off unless GAAMD_COLS_2PERCU=1)
-    static const bool two = [] {
-        const char *e = getenv("GAAMD_COLS_2PERCU");
-        return e && !strcmp(e, "1");
-    }();
-    if (cw == 16 && two && (nvec + 15u) / 16u <= 512u) return 16;
     while (cw < 64 && (nvec + (uint32_t)cw - 1) / (uint32_t)cw > 256u) cw *= 2;
     return cw;
 }
@@ -902,14 +896,9 @@ static void go_cols_lds(const Desc &d, const OP &op, int cw, uint64_t blocks, hi
         else if (cw == 32)
             hipLaunchKernelGGL((k_ordered_cols_lds<OP, W, LV, 32>), dim3((uint32_t)blocks), dim3(KC_NW * 64), 0, st, d,
                                op);
-        else if constexpr (W >= 8) {
-            if (blocks > 256)   // two workgroups per CU: half-size tiles
-                hipLaunchKernelGGL((k_ordered_cols_lds<OP, W, LV, 16, 4>), dim3((uint32_t)blocks), dim3(KC_NW * 64), 0,
-                                   st, d, op);
-            else
-                hipLaunchKernelGGL((k_ordered_cols_lds<OP, W, LV, 16>), dim3((uint32_t)blocks), dim3(KC_NW * 64), 0, st,
-                                   d, op);
-        }
+        else if constexpr (W >= 8)
+            hipLaunchKernelGGL((k_ordered_cols_lds<OP, W, LV, 16>), dim3((uint32_t)blocks), dim3(KC_NW * 64), 0, st, d,
+                               op);
     }
 }
 
