@@ -54,7 +54,7 @@ int main() {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const uint32_t pieces[] = {256, 512, 1024, 2048, 4096};
+    const uint32_t pieces[] = {64, 128, 256, 512, 1024, 2048, 4096};
     const uint32_t rows_per_wg[] = {2048, 1024, 512, 256, 128, 64, 32};
     for (uint32_t piece : pieces) {
         for (uint32_t R : rows_per_wg) {
