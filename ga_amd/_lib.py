@@ -1,14 +1,17 @@
-"""ctypes binding of libga_amd.so (the C-ABI in include/comex.h, armci.h, ga_amd.h).
+"""ctypes binding of libga_amd.so (the C-ABI in include/comex.h, armci.h, message.h,
+armci_acc.h, ga_amd.h) and of libga_amd_ga.so (include/ga.h, the GA caller layer
+over libga_amd.so's public ABI).
 
-The library is built in-tree (``ga_amd/libga_amd.so``) by ``__graft_entry__.build()``
-or ``make -C ga_amd/csrc``.  There is no fallback: if the library is missing,
-importing this module raises, so a GPU test can never pass on a substitute path.
+Both are built in-tree (``ga_amd/``) by ``__graft_entry__.build()`` or
+``make -C ga_amd/csrc``.  There is no fallback: if a library is missing, loading
+raises, so a GPU test can never pass on a substitute path.
 """
 import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libga_amd.so")
+GA_LIB_PATH = os.path.join(_HERE, "libga_amd_ga.so")
 
 c_int_p = ctypes.POINTER(ctypes.c_int)
 
@@ -313,8 +316,11 @@ SIGNATURES = {
     "gaamd_event_elapsed_ms": (ctypes.c_float, [ctypes.c_void_p, ctypes.c_void_p]),
     "gaamd_version": (ctypes.c_char_p, []),
     "gaamd_hip_runtime": (ctypes.c_char_p, []),
+}
+
+# ga.h: libga_amd_ga.so
+GA_SIGNATURES = {
     "gaamd_ga_proc_grid": (ctypes.c_int, [ctypes.c_int, c_int_p, c_int_p, ctypes.c_int, c_int_p]),
-    # ga.h
     "GA_Initialize": (ctypes.c_int, []),
     "GA_Terminate": (None, []),
     "GA_Nodeid": (ctypes.c_int, []),
@@ -350,6 +356,7 @@ SIGNATURES = {
     "GA_Get_proc_grid": (None, [ctypes.c_int, c_int_p]),
     "GA_Print_stats": (None, []),
 }
+SIGNATURES.update(GA_SIGNATURES)
 
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
 BARRIER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
@@ -357,19 +364,34 @@ BARRIER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
 _lib = None
 
 
+class Libs:
+    """Both libraries under one name space: a ga.h function resolves in
+    libga_amd_ga.so, everything else in libga_amd.so."""
+
+    def __init__(self, core, ga):
+        self.core, self.ga = core, ga
+
+    def __getattr__(self, name):
+        fn = getattr(self.ga if name in GA_SIGNATURES else self.core, name)
+        setattr(self, name, fn)
+        return fn
+
+
 def load():
-    """Load (once) and return the ctypes handle of libga_amd.so; raise if absent."""
+    """Load (once) libga_amd.so and libga_amd_ga.so; raise if either is absent."""
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(
-            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
-            "or `make -C ga_amd/csrc` (there is no CPU fallback)")
-    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for path in (LIB_PATH, GA_LIB_PATH):
+        if not os.path.exists(path):
+            raise ImportError(
+                f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "or `make -C ga_amd/csrc` (there is no CPU fallback)")
+    core = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    ga = ctypes.CDLL(GA_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(ga if name in GA_SIGNATURES else core, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
-    return lib
+    _lib = Libs(core, ga)
+    return _lib

@@ -44,6 +44,17 @@ void fatal(const char *fmt, ...) {
     abort();
 }
 
+void trace(int level, const char *fmt, ...) {
+    if (g_rt.debug < level) return;
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "[ga_amd %d] %s\n", g_rt.rank, buf);
+    fflush(stderr);
+}
+
 size_t node_shm_bytes(int size) {
     return sizeof(NodeShm) + sizeof(Inbox) * (size_t)(size > 1 ? size - 1 : 0) + kBootSlot * (size_t)size +
            sizeof(std::atomic<uint32_t>) * (size_t)kMaxMutexes * (size_t)size;

@@ -25,6 +25,7 @@
 // arithmetic runs on the GPU; there is no CPU compute path.
 #include "comex_impl.hpp"
 #include "../../include/ga_amd.h"
+#include <hip/hip_version.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -34,6 +35,10 @@
 #include <deque>
 #include <memory>
 #include <algorithm>
+
+#ifndef GAAMD_ROCM_PATH
+#define GAAMD_ROCM_PATH "/opt/rocm"
+#endif
 
 namespace gaamd {
 
@@ -579,6 +584,40 @@ static void exit_without_finalize() {
     wire_detach();
 }
 
+// The HIP runtime this library's calls resolve to must be the one it was built
+// against.  A torch wheel bundles its own libamdhip64 with the same SONAME
+// (torch 2.10 + rocm7.0: HIP 7.0.51831); loaded before this library (torch imported
+// first) it serves every HIP call here, and on it the inter-process memory calls of
+// comex_malloc stall: hipIpcOpenMemHandle of a 2 GiB segment while a 1 GiB one of
+// the same peer is mapped (profiles/r02, r03/s21), and the vmm allocator's first
+// 1 GiB segment (profiles/r04/final2; the call is named in profiles/r05/).  The
+// reference aborts with a message on any such condition (COMEX_ASSERT ->
+// comex_error, comex_impl.h:52-76); so does this, before anything can hang.
+// COMEX_AMD_ALLOW_HIP_MISMATCH=1 downgrades it to a warning.
+static void check_hip_runtime() {
+    const char *path = gaamd_hip_runtime();
+    int ver = 0;
+    const bool got = hipRuntimeGetVersion(&ver) == hipSuccess;
+    if (!got) (void)hipGetLastError();
+    const int built = HIP_VERSION;
+    trace(1, "HIP runtime %s, version %d (built against %d)", path, ver, built);
+    if (got && ver / 100000 == built / 100000) return;   // same major.minor
+    const char *allow = getenv("COMEX_AMD_ALLOW_HIP_MISMATCH");
+    char msg[768];
+    snprintf(msg, sizeof(msg),
+             "HIP calls resolve to %s, runtime %d.%d.%d, but libga_amd was built against HIP %d.%d.%d "
+             "(%s/lib); comex_malloc's inter-process mappings stall on that runtime. Load libga_amd "
+             "before the library that brought it (import ga_amd before torch), or set "
+             "COMEX_AMD_ALLOW_HIP_MISMATCH=1 to run on it anyway",
+             path, ver / 10000000, ver / 100000 % 100, ver % 100000, built / 10000000, built / 100000 % 100,
+             built % 100000, GAAMD_ROCM_PATH);
+    if (allow && atoi(allow)) {
+        fprintf(stderr, "ga_amd warning: %s\n", msg);
+        return;
+    }
+    fatal("%s", msg);
+}
+
 int comex_init() {
     Runtime &r = rt();
     if (r.initialized) return COMEX_SUCCESS;
@@ -587,17 +626,10 @@ int comex_init() {
         atexit(exit_without_finalize);
         hook = true;
     }
+    const char *dbg = getenv("COMEX_AMD_DEBUG");
+    r.debug = dbg ? atoi(dbg) : 0;
+    check_hip_runtime();
     boot_init();
-    {
-        // a torch wheel bundles a libamdhip64 with the same SONAME: imported
-        // before this library it serves our HIP calls, and that build hangs in
-        // hipIpcOpenMemHandle of a 2 GiB segment while another is mapped
-        // (profiles/r02/README.md)
-        const char *rt_path = gaamd_hip_runtime();
-        if (strstr(rt_path, "/torch/lib/") && r.rank == 0)
-            fprintf(stderr, "ga_amd: HIP calls resolve to %s (loaded before libga_amd); load libga_amd first "
-                    "(import ga_amd before torch) to use /opt/rocm's runtime\n", rt_path);
-    }
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev <= 0)
@@ -683,8 +715,6 @@ int comex_init() {
         r.put_iov = flag("COMEX_ENABLE_PUT_IOV");
         r.get_iov = flag("COMEX_ENABLE_GET_IOV");
     }
-    const char *dbg = getenv("COMEX_AMD_DEBUG");
-    r.debug = dbg ? atoi(dbg) : 0;
     if (r.size > 1 || !r.acc_self_direct || !r.put_self_direct || !r.get_self_direct) {
         remote_init();   // staging HBM + inbox + progress thread (remote.cpp)
         wire_init();

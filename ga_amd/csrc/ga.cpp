@@ -15,10 +15,21 @@
 //   statistics              GAstat.numacc, GAbytes.acctot/accloc (onesided.c:1372-1419)
 // Each rank's block is column-major with the block's extents as leading
 // dimensions (no ghosts), in one comex_malloc segment per array (HBM).
+//
+// This file is its own library, libga_amd_ga.so, linked against libga_amd.so
+// and calling it only through the public C ABI (comex.h, armci.h, ga_amd.h) --
+// the same position global/src has over libarmci.  libga_amd.so itself exports
+// only comex_*/ARMCI_*/armci_*/gaamd_* names (as libarmci does, capi.c:14-27),
+// so a real GA, which defines NGA_*/GA_* itself (global/src/capi.c:2079-2089),
+// links against it without a second definition of its own entry points.
+// built with -fvisibility=hidden: only the names the headers declare are exported
+#pragma GCC visibility push(default)
 #include "../../include/ga.h"
 #include "../../include/armci.h"
 #include "../../include/comex.h"
-#include "runtime.hpp"
+#include "../../include/ga_amd.h"
+#pragma GCC visibility pop
+#include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -28,7 +39,33 @@
 #include <string>
 #include <vector>
 
-namespace gaamd {
+namespace gaamd_ga {
+
+// GA_Error / pnga_error: message, then abort through the runtime (comex_error ->
+// the reference's MPI_Abort, comex_impl.h:52-76)
+[[noreturn]] static void fatal(const char *fmt, ...) {
+    char buf[768];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    char msg[800];
+    snprintf(msg, sizeof(msg), "ga_amd GA: %s", buf);
+    comex_error(msg, 1);
+    abort();   // comex_error does not return
+}
+
+static int my_rank() {
+    int me = 0;
+    comex_group_rank(COMEX_GROUP_WORLD, &me);
+    return me;
+}
+
+static int world_size() {
+    int n = 1;
+    comex_group_size(COMEX_GROUP_WORLD, &n);
+    return n;
+}
 
 struct GArray {
     bool live = false;
@@ -239,20 +276,20 @@ static long block_elems(const GArray &a, int proc, long *lo, long *hi) {
 // the way pnga_zero does it, memset through the host pointer (global.nalg.c:94-129)
 static void zero_block(void *p, size_t bytes) {
     if (!bytes) return;
-    if (segment_kind(p) == 2) memset(p, 0, bytes);
-    else GA_HIP(hipMemsetAsync(p, 0, bytes, rt().stream));
+    if (gaamd_segment_kind(p) == 2) memset(p, 0, bytes);
+    else if (gaamd_memset(p, 0, bytes) != 0) fatal("zeroing a %zu-byte block failed", bytes);
 }
 
 static int allocate(GArray &a) {
-    Runtime &r = rt();
+    const int me = my_rank(), np = world_size();
     long lo[GA_MAX_DIM], hi[GA_MAX_DIM];
     a.nproc_grid = 1;
     for (int d = 0; d < a.ndim; d++) a.nproc_grid *= a.nblock[d];
-    if (a.nproc_grid > r.size) fatal("distribution needs %d processes, have %d", a.nproc_grid, r.size);
-    const long n = block_elems(a, r.rank, lo, hi);
-    a.ptr.assign(r.size, nullptr);
+    if (a.nproc_grid > np) fatal("distribution needs %d processes, have %d", a.nproc_grid, np);
+    const long n = block_elems(a, me, lo, hi);
+    a.ptr.assign(np, nullptr);
     if (comex_malloc(a.ptr.data(), (size_t)n * a.elemsize, COMEX_GROUP_WORLD) != COMEX_SUCCESS) return 0;
-    zero_block(a.ptr[r.rank], (size_t)n * a.elemsize);
+    zero_block(a.ptr[me], (size_t)n * a.elemsize);
     comex_barrier(COMEX_GROUP_WORLD);
     a.live = true;
     g_arrays.push_back(a);
@@ -269,7 +306,7 @@ enum GaOp { GA_ACC, GA_PUT, GA_GET };
 static void patch_op(GaOp kind, int g_a, const long *lo, const long *hi, void *buf, const long *ld, void *alpha,
                      const long *skip = nullptr, std::vector<armci_hdl_t> *nb = nullptr) {
     GArray &a = arr(g_a);
-    Runtime &r = rt();
+    const int me = my_rank();
     const int nd = a.ndim, size = a.elemsize;
     for (int d = 0; d < nd; d++)
         if (lo[d] < 1 || hi[d] > a.dims[d] || lo[d] > hi[d]) fatal("patch out of range in dim %d", d);
@@ -311,7 +348,7 @@ static void patch_op(GaOp kind, int g_a, const long *lo, const long *hi, void *b
     // remote owners first, then the local one (onesided.c:1387-1400); the
     // strided variants keep the iterator's order (gai_iterator_next)
     if (!skip)
-        std::stable_partition(owners.begin(), owners.end(), [&](const Owner &o) { return o.proc != r.rank; });
+        std::stable_partition(owners.begin(), owners.end(), [&](const Owner &o) { return o.proc != me; });
     std::vector<armci_hdl_t> hdl;
     for (size_t k = 0; k < owners.size(); ++k) {
         Owner &o = owners[k];
@@ -372,7 +409,7 @@ static void patch_op(GaOp kind, int g_a, const long *lo, const long *hi, void *b
                 stride_loc[d + 1] = stride_loc[d];
             }
         }
-        if (kind == GA_ACC && o.proc == r.rank) {
+        if (kind == GA_ACC && o.proc == me) {
             long e = 1;
             for (int d = 0; d < nd; d++) e *= (o.phi[d] - o.plo[d]) / (skip ? skip[d] : 1) + 1;
             g_stat.accloc += (double)size * e;
@@ -469,7 +506,7 @@ static inline void gs_locate(const GsCtx &c, long k, int *pr_out, long *off_out)
 static void gatscat(GatScat op, int g_a, void *v, int *const *csubs, const int *cflat, long nv, void *alpha) {
     if (nv < 1) return;   // pnga_gather / pnga_scatter: nv < 1 returns
     GArray &a = arr(g_a);
-    Runtime &r = rt();
+    const int me = my_rank(), np = world_size();
     const int size = a.elemsize, nd = a.ndim;
     static std::vector<int> s_proc;
     static std::vector<long> s_off;
@@ -487,7 +524,7 @@ static void gatscat(GatScat op, int g_a, void *v, int *const *csubs, const int *
     }
     const GsCtx c{&a, csubs, cflat, blo.data(), ext.data(), (char *)v, size};
     void **loc = grow(s_loc, (size_t)nv), **rem = grow(s_rem, (size_t)nv);
-    const int P = r.size;
+    const int P = np;
     // one thread per 128 Ki elements, at most gs_threads() (COMEX_AMD_GS_THREADS, default 8)
     const int T = (int)std::max(1L, std::min<long>(gs_threads(), nv >> 17));
     std::vector<long> cnt((size_t)T * P, 0);   // cnt[t*P + p]: elements of thread t owned by p
@@ -537,8 +574,8 @@ static void gatscat(GatScat op, int g_a, void *v, int *const *csubs, const int *
     double &lcl = op == GS_GATHER ? g_stat.gatloc : g_stat.scaloc;
     (op == GS_GATHER ? g_stat.numgat : g_stat.numsca)++;
     tot += (double)size * nv;
-    lcl += (double)size * nelem[r.rank];
-    for (int p = 0; p < r.size; p++) {
+    lcl += (double)size * nelem[me];
+    for (int p = 0; p < np; p++) {
         if (!nelem[p]) continue;
         armci_giov_t desc;
         desc.bytes = size;
@@ -562,20 +599,27 @@ static void gatscat(GatScat op, int g_a, void *v, int *const *csubs, const int *
 static void c2f_index(int nd, const int *c, long *f) { for (int i = 0; i < nd; i++) f[nd - i - 1] = (long)c[i] + 1; }
 static void c2f(int nd, const int *c, long *f) { for (int i = 0; i < nd; i++) f[nd - i - 1] = c[i]; }
 
-}  // namespace gaamd
+}  // namespace gaamd_ga
 
-using namespace gaamd;
+using namespace gaamd_ga;
 
 extern "C" {
 
 int GA_Initialize(void) { return ARMCI_Init(); }
+static void destroy(int g_a) {
+    GArray &a = arr(g_a);
+    comex_free(a.ptr[my_rank()], COMEX_GROUP_WORLD);
+    a.live = false;
+    a.ptr.clear();
+}
+
 void GA_Terminate(void) {
     for (size_t i = 0; i < g_arrays.size(); ++i)
-        if (g_arrays[i].live) GA_Destroy((int)i + 1);
+        if (g_arrays[i].live) destroy((int)i + 1);
     ARMCI_Finalize();
 }
-int GA_Nodeid(void) { return rt().rank; }
-int GA_Nnodes(void) { return rt().size; }
+int GA_Nodeid(void) { return my_rank(); }
+int GA_Nnodes(void) { return world_size(); }
 void GA_Sync(void) { comex_barrier(COMEX_GROUP_WORLD); }
 void GA_Error(char *msg, int code) { comex_error(msg, code); }
 
@@ -600,7 +644,7 @@ int NGA_Create(int type, int ndim, int dims[], char *name, int chunk[]) {
     else
         for (int d = 0; d < ndim; d++) blk[d] = -1;
     for (int d = 0; d < ndim; d++) if (fdims[d] == 1) blk[d] = 1;
-    ddb(ndim, fdims, rt().size, blk, pe);
+    ddb(ndim, fdims, world_size(), blk, pe);
     for (int d = 0; d < ndim; d++) {
         long pcut;
         if (fchunk[d] > 1) {
@@ -644,22 +688,17 @@ int NGA_Create_irreg(int type, int ndim, int dims[], char *name, int block[], in
     return allocate(a);
 }
 
-void GA_Destroy(int g_a) {
-    GArray &a = arr(g_a);
-    comex_free(a.ptr[rt().rank], COMEX_GROUP_WORLD);
-    a.live = false;
-    a.ptr.clear();
-}
+void GA_Destroy(int g_a) { destroy(g_a); }
 
 void GA_Zero(int g_a) {
     GArray &a = arr(g_a);
-    Runtime &r = rt();
+    const int me = my_rank();
     long lo[GA_MAX_DIM], hi[GA_MAX_DIM];
-    const long n = block_elems(a, r.rank, lo, hi);
+    const long n = block_elems(a, me, lo, hi);
     // pnga_zero (global.nalg.c:60-90) is collective and syncs first: no rank may
     // zero its block while another still reads or writes it
     comex_barrier(COMEX_GROUP_WORLD);
-    zero_block(a.ptr[r.rank], (size_t)n * a.elemsize);
+    zero_block(a.ptr[me], (size_t)n * a.elemsize);
     comex_barrier(COMEX_GROUP_WORLD);   // fences (syncs every library stream) + barrier
 }
 
@@ -769,9 +808,9 @@ void NGA_Get(int g_a, int lo[], int hi[], void *buf, int ld[]) { c_patch(GA_GET,
 
 void NGA_Access(int g_a, int lo[], int hi[], void *ptr, int ld[]) {
     GArray &a = arr(g_a);
-    Runtime &r = rt();
+    const int me = my_rank();
     long blo[GA_MAX_DIM], bhi[GA_MAX_DIM], flo[GA_MAX_DIM], fhi[GA_MAX_DIM];
-    block_elems(a, r.rank, blo, bhi);
+    block_elems(a, me, blo, bhi);
     c2f_index(a.ndim, lo, flo);
     c2f_index(a.ndim, hi, fhi);
     long off = 0, f = 1;
@@ -781,7 +820,7 @@ void NGA_Access(int g_a, int lo[], int hi[], void *ptr, int ld[]) {
         f *= bhi[d] - blo[d] + 1;
     }
     comex_fence_all(COMEX_GROUP_WORLD);   // pending writes land before the caller reads
-    *(char **)ptr = (char *)a.ptr[r.rank] + off * a.elemsize;
+    *(char **)ptr = (char *)a.ptr[me] + off * a.elemsize;
     for (int i = 0; i < a.ndim - 1; i++) ld[a.ndim - 2 - i] = (int)(bhi[i] - blo[i] + 1);
 }
 
@@ -832,8 +871,8 @@ int gaamd_ga_proc_grid(int ndim, const int *dims, const int *chunk, int npes, in
 
 void GA_Print_stats(void) {
     printf("[%d] GA statistics: acc calls %ld, put calls %ld, get calls %ld, scatter calls %ld, gather calls %ld\n",
-           rt().rank, g_stat.numacc, g_stat.numput, g_stat.numget, g_stat.numsca, g_stat.numgat);
-    printf("[%d] accumulate bytes total %.0f, local %.0f (%.1f%%)\n", rt().rank, g_stat.acctot, g_stat.accloc,
+           my_rank(), g_stat.numacc, g_stat.numput, g_stat.numget, g_stat.numsca, g_stat.numgat);
+    printf("[%d] accumulate bytes total %.0f, local %.0f (%.1f%%)\n", my_rank(), g_stat.acctot, g_stat.accloc,
            g_stat.acctot > 0 ? 100.0 * g_stat.accloc / g_stat.acctot : 0.0);
 }
 

@@ -22,6 +22,8 @@
 namespace gaamd {
 
 [[noreturn]] void fatal(const char *fmt, ...);
+// a line on stderr when COMEX_AMD_DEBUG >= level (phase traces of init / comex_malloc)
+void trace(int level, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 
 #define GA_HIP(call)                                                                  \
     do {                                                                              \

@@ -114,7 +114,9 @@ void ipc_close(void *mapped, int peer) {
 // this diagnosis (remote_view / the progress thread).
 void *ipc_open(hipIpcMemHandle_t h, int q, const char *what) {
     void *p = nullptr;
+    trace(2, "hipIpcOpenMemHandle of rank %d's %s", q, what);
     const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+    trace(2, "hipIpcOpenMemHandle -> %d (%p)", (int)e, p);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         fprintf(stderr, "ga_amd rank %d: cannot map rank %d's %s over IPC (%s); operations that need it will "
@@ -187,6 +189,7 @@ void export_alloc(void **p, size_t bytes, hipIpcMemHandle_t *h, const char *what
         return !e || atoi(e) != 0;
     }();
     std::vector<void *> held;
+    trace(2, "hipIpcGetMemHandle of a %zu-byte %s at %p", bytes, what, *p);
     hipError_t e = hipIpcGetMemHandle(h, *p);
     for (int tries = 0; e != hipSuccess && tries < 4; ++tries) {
         (void)hipGetLastError();
@@ -502,8 +505,8 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
     // collective over the group's members (comex.c comex_malloc): ptr_arr is
     // indexed by group rank; non-members keep no view of the segment
     const std::vector<int> members = group_members(group);
-    const bool trace = r.debug >= 2;
-    if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc(%zu, group %d): enter\n", r.rank, bytes, group);
+    const bool tr = r.debug >= 2;
+    if (tr) fprintf(stderr, "[ga_amd %d] comex_malloc(%zu, group %d): enter\n", r.rank, bytes, group);
     struct Info {
         uint64_t base, bytes;
         hipIpcMemHandle_t h;
@@ -564,14 +567,15 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         mine.device = r.device;
         mine.gen = ++gen;
         if (tagged) {
+            trace(2, "comex_malloc: writing the tags of %p", p);
             const uint64_t t0 = seg_tag(r.rank, mine.gen, 0), t1 = seg_tag(r.rank, mine.gen, 1);
             GA_HIP(hipMemcpy(p, &t0, 8, hipMemcpyHostToDevice));
             GA_HIP(hipMemcpy((char *)p + bytes - 8, &t1, 8, hipMemcpyHostToDevice));
         }
-        if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: allocated %p, allgather\n", r.rank, p);
+        if (tr) fprintf(stderr, "[ga_amd %d] comex_malloc: allocated %p, allgather\n", r.rank, p);
         std::vector<Info> gathered(members.size());
         members_allgather(members, group, &mine, gathered.data(), sizeof(Info));
-        if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: allgather done, opening peers\n", r.rank);
+        if (tr) fprintf(stderr, "[ga_amd %d] comex_malloc: allgather done, opening peers\n", r.rank);
         memset(all.data(), 0, sizeof(Info) * all.size());
         for (size_t k = 0; k < members.size(); ++k) {
             all[members[k]] = gathered[k];
@@ -615,6 +619,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
             }
             if (!mapped[q] || all[q].bytes < 16) continue;
             uint64_t t[2] = {0, 0};
+            trace(2, "comex_malloc: reading rank %d's tags through %p", q, mapped[q]);
             GA_HIP(hipMemcpy(&t[0], mapped[q], 8, hipMemcpyDeviceToHost));
             GA_HIP(hipMemcpy(&t[1], (char *)mapped[q] + all[q].bytes - 8, 8, hipMemcpyDeviceToHost));
             if (attempt == 0 && all[q].gen == test_stale_gen()) {
@@ -703,11 +708,11 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         std::lock_guard<std::mutex> g(r.seg_mu);
         r.segs.push_back(std::move(s));
     }
-    if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: peers mapped, barrier\n", r.rank);
+    if (tr) fprintf(stderr, "[ga_amd %d] comex_malloc: peers mapped, barrier\n", r.rank);
     members_barrier(members, group);
     // every member has mapped the shm object: its name can go (the mappings stay)
     if (!device && bytes) shm_unlink(mine.name);
-    if (trace) fprintf(stderr, "[ga_amd %d] comex_malloc: done\n", r.rank);
+    if (tr) fprintf(stderr, "[ga_amd %d] comex_malloc: done\n", r.rank);
     return COMEX_SUCCESS;
 }
 

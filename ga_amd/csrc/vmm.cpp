@@ -96,6 +96,7 @@ char *va_take(size_t bytes) {
     }
     void *hint = (void *)g_window;
     void *base = nullptr;
+    trace(2, "vmm: hipMemAddressReserve(%zu at %p)", bytes, hint);
     GA_HIP(hipMemAddressReserve(&base, bytes, granularity(), hint, 0));
     // one empty 2 MiB guard after every range, so no range starts where another
     // ends (a precaution: tools/vmm_probe.hip r_adjacent found adjacent ranges fine)
@@ -210,8 +211,11 @@ char *map_fresh(hipMemGenericAllocationHandle_t h, size_t bytes, int q) {
     hipError_t e;
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
+        trace(2, "vmm: hipMemMap(%p, %zu) of %s", (void *)va, bytes, q < 0 ? "a new block" : "an imported block");
         GA_HIP(hipMemMap(va, bytes, 0, h, 0));
+        trace(2, "vmm: hipMemSetAccess");
         e = hipMemSetAccess(va, bytes, &d, 1);
+        trace(2, "vmm: hipMemSetAccess -> %d", (int)e);
         if (e != hipSuccess) {
             (void)hipGetLastError();
             (void)hipMemUnmap(va, bytes);   // may be refused as well: the range is retired either way
@@ -263,6 +267,7 @@ void *vmm_alloc(size_t bytes, VmmBlock *b) {
     // a handle is set aside and another created; its descriptor never leaves.
     for (int attempt = 0;; ++attempt) {
         hipMemGenericAllocationHandle_t h;
+        trace(2, "vmm: hipMemCreate(%zu)", n);
         hipError_t e = hipMemCreate(&h, n, &prop, 0);
         if (e == hipErrorOutOfMemory) {   // the freed-segment cache first (segments.cpp)
             (void)hipGetLastError();
@@ -277,7 +282,9 @@ void *vmm_alloc(size_t bytes, VmmBlock *b) {
             continue;
         }
         int fd = -1;
+        trace(2, "vmm: hipMemExportToShareableHandle");
         GA_HIP(hipMemExportToShareableHandle(&fd, h, hipMemHandleTypePosixFileDescriptor, 0));
+        trace(2, "vmm: exported as descriptor %d", fd);
         b->va = va;
         b->bytes = n;
         b->handle = h;
@@ -359,6 +366,7 @@ void vmm_exchange(int fd, int rank, uint64_t gen, const std::vector<int> &to_pid
 // by b from here on), `bytes` (granularity-rounded)
 void *vmm_import(int myfd, size_t bytes, int q, VmmBlock *b) {
     hipMemGenericAllocationHandle_t h;
+    trace(2, "vmm: hipMemImportFromShareableHandle(descriptor %d) of rank %d", myfd, q);
     // the descriptor is passed by value, as the POSIX-fd handle type is documented
     // for the driver API this one mirrors
     GA_HIP(hipMemImportFromShareableHandle(&h, (void *)(uintptr_t)myfd, hipMemHandleTypePosixFileDescriptor));

@@ -1,6 +1,9 @@
 /*
  * ga.h -- the Global Arrays C API subset on the one-sided accumulate path,
- * exported by libga_amd.so (the caller row a15 of SURVEY.md §8(a)).
+ * exported by libga_amd_ga.so (the caller row a15 of SURVEY.md §8(a)), a
+ * library of its own over libga_amd.so's public ABI.  libga_amd.so -- the
+ * drop-in beneath global/src -- defines none of these names, so a real GA that
+ * defines them itself (global/src/capi.c) links against it unchanged.
  *
  * Same names, argument order and index conventions as the reference C API
  * (global/src/capi.c, global/src/ga.h): C (row-major, 0-based) subscripts at
@@ -82,6 +85,9 @@ void NGA_Release_update(int g_a, int lo[], int hi[]);
 
 /* process grid the REGULAR distribution chose, C order (ga.h GA_Get_proc_grid) */
 void GA_Get_proc_grid(int g_a, int dims[]);
+/* process grid (C order) that NGA_Create picks for npes ranks (restated
+ * ddb/ddb_h2 of global/src/decomp.c); host-only, no GPU */
+int gaamd_ga_proc_grid(int ndim, const int *dims, const int *chunk, int npes, int *grid);
 /* statistics of global/src/onesided.c:1372-1419 (GAstat.numacc, GAbytes.acctot/accloc) */
 void GA_Print_stats(void);
 

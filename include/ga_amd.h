@@ -171,9 +171,6 @@ float gaamd_event_elapsed_ms(void *start, void *stop);
 const char *gaamd_version(void);
 /* path of the HIP runtime (libamdhip64) this library's calls resolve to */
 const char *gaamd_hip_runtime(void);
-/* process grid (C order) that NGA_Create picks for npes ranks (restated
- * ddb/ddb_h2 of global/src/decomp.c); host-only */
-int gaamd_ga_proc_grid(int ndim, const int *dims, const int *chunk, int npes, int *grid);
 
 #if defined(__cplusplus)
 }

@@ -1,11 +1,11 @@
 /* abi_client.c -- a plain C (C99) caller of the drop-in boundary, as GA's
  * global/src would be: includes include/comex.h, armci.h and ga.h, links
- * libga_amd.so, and on a GPU box runs one strided accumulate through each of
+ * libga_amd_ga.so (ga.h) over libga_amd.so, and on a GPU box runs one strided accumulate through each of
  * comex_accs and ARMCI_AccS on a host patch, checked against the reference's
  * loop expression (acc.h:46 IADD_SCALE_REG: dst += src*scale, no FMA), plus an
  * NGA_Acc / NGA_Get round trip on a 1-rank GA.
  * Build (tests/test_abi.py does this): gcc -std=c99 -Wall -Werror -ffp-contract=off
- *   -Iinclude tests/c/abi_client.c -Lga_amd -lga_amd -Wl,-rpath,<repo>/ga_amd
+ *   -Iinclude tests/c/abi_client.c -Lga_amd -lga_amd_ga -lga_amd -Wl,-rpath,<repo>/ga_amd
  * Run: ./abi_client  -> prints "abi_client OK" and exits 0. */
 #include <stdio.h>
 #include <stdlib.h>

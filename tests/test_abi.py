@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import ga_amd
-from ga_amd._lib import LIB_PATH, SIGNATURES
+from ga_amd._lib import GA_LIB_PATH, GA_SIGNATURES, LIB_PATH, SIGNATURES
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADERS = [os.path.join(ROOT, "include", h) for h in ("comex.h", "armci.h", "message.h", "armci_acc.h", "ga_amd.h", "ga.h")]
@@ -30,8 +30,8 @@ def declared_functions(path):
     return names - typedef_fns
 
 
-def exported_symbols():
-    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True, check=True)
+def exported_symbols(path=LIB_PATH):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True)
     syms = {}
     for line in out.stdout.splitlines():
         parts = line.split()
@@ -47,7 +47,8 @@ def test_library_loads():
 
 @pytest.mark.parametrize("header", HEADERS, ids=os.path.basename)
 def test_every_declared_symbol_is_exported(header):
-    syms = exported_symbols()
+    """ga.h is libga_amd_ga.so's; every other header is libga_amd.so's."""
+    syms = exported_symbols(GA_LIB_PATH if header.endswith("ga.h") and "ga_amd" not in header else LIB_PATH)
     decl = declared_functions(header)
     assert decl, header
     missing = sorted(n for n in decl if n not in syms)
@@ -60,6 +61,57 @@ def test_python_binding_covers_headers():
         decl |= declared_functions(h)
     decl -= {n for n in decl if n.startswith("PARMCI_")}
     assert not sorted(decl - set(SIGNATURES)), sorted(decl - set(SIGNATURES))
+
+
+GA_NAME = re.compile(r"^(N?GA_|GA[A-Z]|gaamd_ga_)")
+
+
+def test_core_library_has_no_ga_names():
+    """libga_amd.so sits beneath global/src as libarmci does (capi.c:14-27 exports
+    ARMCI_*/PARMCI_*/armci_* only): it neither defines nor imports a GA name, so a
+    real GA's own NGA_*/GA_* (global/src/capi.c:2079-2089) meet no second
+    definition and are never called back.  Those names live in libga_amd_ga.so."""
+    defined = [n for n in exported_symbols() if GA_NAME.match(n)]
+    assert not defined, defined
+    out = subprocess.run(["nm", "-D", "--undefined-only", LIB_PATH], capture_output=True, text=True, check=True)
+    imported = [ln.split()[-1] for ln in out.stdout.splitlines() if ln.split() and GA_NAME.match(ln.split()[-1])]
+    assert not imported, imported
+    ga = exported_symbols(GA_LIB_PATH)
+    assert all(n in ga for n in GA_SIGNATURES), sorted(n for n in GA_SIGNATURES if n not in ga)
+    # the GA library exports nothing of the runtime's own
+    assert not [n for n in ga if n.startswith(("comex_", "ARMCI_", "PARMCI_", "armci_"))]
+
+
+def _build_ga_coexist(tmp_path):
+    exe = tmp_path / "ga_coexist"
+    cmd = ["gcc", "-std=c99", "-Wall", "-Werror", "-ffp-contract=off", "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "c", "ga_coexist.c"), "-rdynamic", "-L", os.path.join(ROOT, "ga_amd"),
+           "-lga_amd", "-Wl,-rpath," + os.path.join(ROOT, "ga_amd"), "-ldl", "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def test_program_defining_ga_names_links(tmp_path):
+    """A program that defines GA_Initialize, NGA_Acc, GA_Destroy and GA_Terminate
+    itself (as global/src does) links against libga_amd.so alone; the process
+    resolves those names to the program, and libga_amd.so defines none of them
+    (tests/c/ga_coexist.c, no GPU)."""
+    exe = _build_ga_coexist(tmp_path)
+    r = subprocess.run([str(exe), "link"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "ga_coexist OK (link)" in r.stdout, (r.returncode, r.stdout, r.stderr)
+
+
+@pytest.mark.gpu
+def test_program_defining_ga_names_runs(tmp_path):
+    """The same program on the GPU: its own GA_Initialize -> ARMCI_Init, NGA_Acc ->
+    ARMCI_AccS of a 2-D host patch into an ARMCI_Malloc block (exact vs acc.h:46),
+    GA_Destroy -> ARMCI_Free, GA_Terminate -> ARMCI_Finalize; each of its GA names
+    is entered exactly as often as the program called it -- the runtime never
+    calls back into them."""
+    exe = _build_ga_coexist(tmp_path)
+    r = subprocess.run([str(exe), "run"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ga_coexist OK" in r.stdout, (r.returncode, r.stdout, r.stderr[-2000:])
 
 
 def test_armci_names_are_weak_aliases():
@@ -118,6 +170,36 @@ def test_comex_without_gpu_fails_loudly():
     assert "no HIP device" in r.stderr
 
 
+def _torch_first_init():
+    """import torch (whose wheel bundles its own HIP runtime, same SONAME) before
+    libga_amd, then comex_init: must abort at once with the diagnosis, before any
+    device work (comex_impl.h:52-76 convention), not stall later in comex_malloc."""
+    code = ("import time,sys; t=time.time(); import torch; import ga_amd; L=ga_amd.lib(); "
+            "sys.stderr.write('init after %.1f s\\n' % (time.time()-t)); sys.stderr.flush(); "
+            "t=time.time(); rc=L.comex_init(); sys.exit(100 + rc)")
+    env = dict(os.environ)
+    env.pop("COMEX_AMD_ALLOW_HIP_MISMATCH", None)
+    import time
+    t0 = time.time()
+    r = subprocess.run(["python", "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode not in (0, 100), (r.returncode, r.stderr[-2000:])
+    assert "libga_amd was built against HIP" in r.stderr and "/torch/lib/" in r.stderr, r.stderr[-2000:]
+    assert "import ga_amd before torch" in r.stderr
+    return time.time() - t0
+
+
+def test_torch_runtime_first_fails_fast():
+    """CPU: the check runs before the device query, so it fires here too."""
+    _torch_first_init()
+
+
+@pytest.mark.gpu
+def test_torch_runtime_first_fails_fast_gpu():
+    """GPU box: torch first -> non-zero exit with the message, not the stall of
+    profiles/r04/final2/malloc_repro_torch_vmm.log."""
+    _torch_first_init()
+
+
 @pytest.mark.parametrize("npes,grid", [(1, [1, 1]), (2, [1, 2]), (4, [2, 2]), (8, [2, 4])])
 def test_ga_process_grid_matches_reference_survey(npes, grid):
     """NGA_Create's REGULAR grid for 32768^2 (C order).  The survey ran the reference
@@ -148,7 +230,7 @@ def _build_c_client(tmp_path):
     import subprocess
     exe = tmp_path / "abi_client"
     cmd = ["gcc", "-std=c99", "-Wall", "-Werror", "-ffp-contract=off", "-I", os.path.join(ROOT, "include"),
-           os.path.join(ROOT, "tests", "c", "abi_client.c"), "-L", os.path.join(ROOT, "ga_amd"), "-lga_amd",
+           os.path.join(ROOT, "tests", "c", "abi_client.c"), "-L", os.path.join(ROOT, "ga_amd"), "-lga_amd_ga", "-lga_amd",
            "-Wl,-rpath," + os.path.join(ROOT, "ga_amd"), "-o", str(exe)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr

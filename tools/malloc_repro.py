@@ -22,7 +22,7 @@ def main():
                                            MASTER_ADDR="127.0.0.1", MASTER_PORT=port, COMEX_AMD_JOBID="m" + port))
                  for r in range(2)]
         sys.exit(max(p.wait() for p in procs))
-    faulthandler.dump_traceback_later(50, exit=True)
+    faulthandler.dump_traceback_later(int(os.environ.get("REPRO_DUMP_S", "50")), exit=True)
     if os.environ.get("REPRO_TORCH") == "1":   # torch's own HIP runtime loaded first, as in bench.py N>1
         import torch  # noqa: F401
         import torch.distributed  # noqa: F401
