@@ -435,7 +435,7 @@ def run_gpu(args, dist, finalize=True):
     dist.barrier()
     ga_amd.sync()
     # BENCH_STAMPS=1 (diagnostic runs only, never the driver's): the library's host
-    # stamps (gaamd_stamps, CLOCK_BOOTTIME) of the first call and of the closing wait,
+    # stamps (gaamd_diag "stamps", CLOCK_BOOTTIME) of the first call and of the closing wait,
     # read after the region, for tools/region_edges.py to place on a kernel trace
     stamps_on = os.environ.get("BENCH_STAMPS") == "1"
     st_buf = (ctypes.c_ulonglong * 8)()
@@ -443,13 +443,13 @@ def run_gpu(args, dist, finalize=True):
     def value_region(first):
         first_stamps = None
         if stamps_on:
-            L.gaamd_stamps(1, None)
+            L.gaamd_diag(b"stamps", 1, None, 0)
         b0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
         t0 = time.perf_counter()
         step(first)
         t_first = time.perf_counter()
         if stamps_on:
-            L.gaamd_stamps(-1, st_buf)
+            L.gaamd_diag(b"stamps", -1, st_buf, 8)
             first_stamps = list(st_buf[:5])
         for i in range(1, args.steps):
             step(first + i)
@@ -468,7 +468,7 @@ def run_gpu(args, dist, finalize=True):
                 "enqueue_all_us": round((t_enq - t0) * 1e6, 1), "total_us": round((t1 - t0) * 1e6, 1),
                 "boottime_ns": [b0, b1]}
         if stamps_on:
-            L.gaamd_stamps(0, st_buf)
+            L.gaamd_diag(b"stamps", 0, st_buf, 8)
             prof["stamps_ns"] = {"region_start": b0, "first_call": first_stamps, "wait_call_py": bw,
                                  "wait": list(st_buf[5:8]), "region_end": b1}
         return t1 - t0, prof
@@ -541,7 +541,7 @@ def run_gpu(args, dist, finalize=True):
                                  "hbm_peak_frac": round(alg_bytes * args.steps / tc / (HBM_PEAK_GBS * 1e9), 4),
                                  "ms_per_step": round(tc / args.steps * 1e3, 4),
                                  "calls": ncall,
-                                 "how": "the same calls from a C loop in the library (gaamd_time_blocking_accs)"}}
+                                 "how": "the same calls from a C loop (libga_amd_diag.so gaamd_time_blocking_accs, over the public comex_accs)"}}
 
     res = dict(op=op, desc=desc, payload=payload, alg_bytes=alg_bytes, elems=elems, elapsed=elapsed,
                avg_kernel_s=avg_kernel_s, launch=launch, streams=L.gaamd_num_streams(), pipeline=pipeline,

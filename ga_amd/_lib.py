@@ -12,6 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libga_amd.so")
 GA_LIB_PATH = os.path.join(_HERE, "libga_amd_ga.so")
+DIAG_LIB_PATH = os.path.join(_HERE, "libga_amd_diag.so")
 
 c_int_p = ctypes.POINTER(ctypes.c_int)
 
@@ -273,7 +274,6 @@ SIGNATURES = {
     "gaamd_route_counts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     "gaamd_toggle_counts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     "gaamd_iov_path_counts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
-    "gaamd_stamps": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong)]),
     "gaamd_one_pass_count": (ctypes.c_ulonglong, []),
     "gaamd_segment_cache_reuse": (ctypes.c_ulonglong, []),
     "gaamd_segment_remaps": (ctypes.c_ulonglong, []),
@@ -281,9 +281,6 @@ SIGNATURES = {
     "gaamd_segment_kind": (ctypes.c_int, [ctypes.c_void_p]),
     "gaamd_vmm_access_retries": (ctypes.c_ulonglong, []),
     "gaamd_vmm_exchange_selftest": (ctypes.c_int, [ctypes.c_int]),
-    "gaamd_time_blocking_accs": (ctypes.c_ulonglong, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, c_int_p,
-                                                      ctypes.c_void_p, c_int_p, c_int_p, ctypes.c_int, ctypes.c_int,
-                                                      ctypes.c_int, ctypes.c_int]),
     "gaamd_owner_counts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     "gaamd_peers_unmapped": (ctypes.c_int, []),
     "gaamd_plan_strided": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, c_int_p, ctypes.c_void_p, c_int_p, c_int_p,
@@ -316,6 +313,8 @@ SIGNATURES = {
     "gaamd_event_elapsed_ms": (ctypes.c_float, [ctypes.c_void_p, ctypes.c_void_p]),
     "gaamd_version": (ctypes.c_char_p, []),
     "gaamd_hip_runtime": (ctypes.c_char_p, []),
+    "gaamd_diag": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_ulonglong),
+                                  ctypes.c_int]),
 }
 
 # ga.h: libga_amd_ga.so
@@ -358,6 +357,14 @@ GA_SIGNATURES = {
 }
 SIGNATURES.update(GA_SIGNATURES)
 
+# ga_amd_diag.h: libga_amd_diag.so (measurement helpers, not the boundary)
+DIAG_SIGNATURES = {
+    "gaamd_time_blocking_accs": (ctypes.c_ulonglong, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, c_int_p,
+                                                      ctypes.c_void_p, c_int_p, c_int_p, ctypes.c_int, ctypes.c_int,
+                                                      ctypes.c_int, ctypes.c_int]),
+}
+SIGNATURES.update(DIAG_SIGNATURES)
+
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
 BARRIER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
 
@@ -365,33 +372,36 @@ _lib = None
 
 
 class Libs:
-    """Both libraries under one name space: a ga.h function resolves in
-    libga_amd_ga.so, everything else in libga_amd.so."""
+    """The three libraries under one name space: a ga.h function resolves in
+    libga_amd_ga.so, a ga_amd_diag.h one in libga_amd_diag.so, everything else in
+    libga_amd.so."""
 
-    def __init__(self, core, ga):
-        self.core, self.ga = core, ga
+    def __init__(self, core, ga, diag):
+        self.core, self.ga, self.diag = core, ga, diag
+
+    def _of(self, name):
+        return self.ga if name in GA_SIGNATURES else self.diag if name in DIAG_SIGNATURES else self.core
 
     def __getattr__(self, name):
-        fn = getattr(self.ga if name in GA_SIGNATURES else self.core, name)
+        fn = getattr(self._of(name), name)
         setattr(self, name, fn)
         return fn
 
 
 def load():
-    """Load (once) libga_amd.so and libga_amd_ga.so; raise if either is absent."""
+    """Load (once) libga_amd.so, libga_amd_ga.so and libga_amd_diag.so; raise if one is absent."""
     global _lib
     if _lib is not None:
         return _lib
-    for path in (LIB_PATH, GA_LIB_PATH):
+    for path in (LIB_PATH, GA_LIB_PATH, DIAG_LIB_PATH):
         if not os.path.exists(path):
             raise ImportError(
                 f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "or `make -C ga_amd/csrc` (there is no CPU fallback)")
-    core = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-    ga = ctypes.CDLL(GA_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    libs = Libs(*(ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL) for p in (LIB_PATH, GA_LIB_PATH, DIAG_LIB_PATH)))
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(ga if name in GA_SIGNATURES else core, name)
+        fn = getattr(libs._of(name), name)
         fn.restype = res
         fn.argtypes = args
-    _lib = Libs(core, ga)
-    return _lib
+    _lib = libs
+    return libs

@@ -157,7 +157,7 @@ static int get_via_scratch(const char *src, const int *ss, char *dst, const int 
 // ---- host-side stamps (diagnostic) -----------------------------------------
 // CLOCK_BOOTTIME ns (the clock rocprofv3 stamps kernels with) at fixed points of the
 // last strided call and the last comex_wait_all, for placing the bench's value
-// region edges on a kernel trace.  Off unless gaamd_stamps(1).
+// region edges on a kernel trace.  Off unless gaamd_diag("stamps", 1).
 static std::atomic<bool> g_stamp_on{false};
 static uint64_t g_stamp[8];
 static inline void stamp(int i) {
@@ -588,9 +588,10 @@ static void exit_without_finalize() {
 // against.  A torch wheel bundles its own libamdhip64 with the same SONAME
 // (torch 2.10 + rocm7.0: HIP 7.0.51831); loaded before this library (torch imported
 // first) it serves every HIP call here, and on it the inter-process memory calls of
-// comex_malloc stall: hipIpcOpenMemHandle of a 2 GiB segment while a 1 GiB one of
-// the same peer is mapped (profiles/r02, r03/s21), and the vmm allocator's first
-// 1 GiB segment (profiles/r04/final2; the call is named in profiles/r05/).  The
+// comex_malloc fail: hipIpcOpenMemHandle of a 2 GiB segment stalls while a 1 GiB
+// one of the same peer is mapped, and hipMemImportFromShareableHandle of the vmm
+// allocator's first 1 GiB descriptor kills the process with SIGSEGV
+// (profiles/r05/runtime_diag/, phase traces; /opt/rocm 7.2 passes both).  The
 // reference aborts with a message on any such condition (COMEX_ASSERT ->
 // comex_error, comex_impl.h:52-76); so does this, before anything can hang.
 // COMEX_AMD_ALLOW_HIP_MISMATCH=1 downgrades it to a warning.
@@ -606,7 +607,7 @@ static void check_hip_runtime() {
     char msg[768];
     snprintf(msg, sizeof(msg),
              "HIP calls resolve to %s, runtime %d.%d.%d, but libga_amd was built against HIP %d.%d.%d "
-             "(%s/lib); comex_malloc's inter-process mappings stall on that runtime. Load libga_amd "
+             "(%s/lib); comex_malloc's inter-process mappings hang or crash on that runtime. Load libga_amd "
              "before the library that brought it (import ga_amd before torch), or set "
              "COMEX_AMD_ALLOW_HIP_MISMATCH=1 to run on it anyway",
              path, ver / 10000000, ver / 100000 % 100, ver % 100000, built / 10000000, built / 100000 % 100,
@@ -1121,32 +1122,30 @@ int gaamd_peers_unmapped(void) {
     return n;
 }
 
-int gaamd_stamps(int on, unsigned long long out[8]) {
-    if (out)
-        for (int k = 0; k < 8; ++k) out[k] = g_stamp[k];
-    if (on >= 0) {
-        if (on) memset(g_stamp, 0, sizeof(g_stamp));
-        g_stamp_on.store(on != 0, std::memory_order_relaxed);
+// Test and diagnostic hooks: one entry point, not used by GA (include/ga_amd.h
+// section 7).  "stamps": the bench's value-region stamps (value 1: clear and start,
+// 0: stop, -1: leave as is; out[0..7] gets them when nout >= 8).  "stale_gen" /
+// "stale_granule": the segment tests' stale-mapping hooks (segments.cpp).
+int gaamd_diag(const char *key, long long value, unsigned long long *out, int nout) {
+    if (!key) return -1;
+    if (!strcmp(key, "stamps")) {
+        if (out && nout >= 8)
+            for (int k = 0; k < 8; ++k) out[k] = g_stamp[k];
+        if (value >= 0) {
+            if (value) memset(g_stamp, 0, sizeof(g_stamp));
+            g_stamp_on.store(value != 0, std::memory_order_relaxed);
+        }
+        return 0;
     }
-    return 0;
-}
-
-// Diagnostic: `steps` blocking comex_accs calls issued from C, the k-th on pointer
-// set k % nsets (srcs[k], dsts[k]); returns the elapsed wall-clock ns (0 on a failed
-// call).  The bench's blocking_api line times the same calls from Python, whose
-// per-call cost is the interpreter's, not the library's: this is the figure a C or
-// Fortran caller (GA's NGA_Acc -> ARMCI_AccS) sees.
-unsigned long long gaamd_time_blocking_accs(int op, void *scale, void *const *srcs, int *ss, void *const *dsts, int *ds,
-                                            int *count, int levels, int proc, int nsets, int steps) {
-    if (nsets <= 0 || steps <= 0) return 0;
-    timespec t0, t1;
-    clock_gettime(CLOCK_MONOTONIC, &t0);
-    for (int i = 0; i < steps; ++i)
-        if (comex_accs(op, scale, srcs[i % nsets], ss, dsts[i % nsets], ds, count, levels, proc, COMEX_GROUP_WORLD) !=
-            COMEX_SUCCESS)
-            return 0;
-    clock_gettime(CLOCK_MONOTONIC, &t1);
-    return (unsigned long long)(t1.tv_sec - t0.tv_sec) * 1000000000ull + (unsigned long long)(t1.tv_nsec - t0.tv_nsec);
+    if (!strcmp(key, "stale_gen")) {
+        g_diag_stale_gen.store(value);
+        return 0;
+    }
+    if (!strcmp(key, "stale_granule")) {
+        g_diag_stale_granule.store(value);
+        return 0;
+    }
+    return -1;
 }
 
 int gaamd_iov_path_counts(unsigned long long counts[3]) {

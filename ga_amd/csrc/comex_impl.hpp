@@ -91,6 +91,10 @@ void *ipc_open(hipIpcMemHandle_t h, int q, const char *what);
 void ipc_close(void *mapped, int peer);
 // IPC handle of a fresh hipMalloc block *p (another block if the export is refused)
 void export_alloc(void **p, size_t bytes, hipIpcMemHandle_t *h, const char *what);
+// test hooks (gaamd_diag): every peer treats its first mapping of each rank's N-th
+// allocation as stale (stale_gen = N, stale_granule < 0), or the owner writes a
+// foreign tag into granule G of it (stale_granule = G) for the check to find
+extern std::atomic<long long> g_diag_stale_gen, g_diag_stale_granule;
 void segments_finalize();         // every live segment: peer mappings closed, block freed
 void segments_release_blocks();   // the freed-segment cache and the quarantined blocks
 

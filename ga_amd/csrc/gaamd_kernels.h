@@ -112,6 +112,18 @@ int elem_size(int op);            // bytes per element for op; 1 for copy; 0 if 
 int launch_rmw(int swap, void *addr, int bytes, uint64_t val, uint64_t *out_dev, hipStream_t stream);
 // one lane stores v into *flag_dev (pinned host memory) after the stream's earlier work
 int launch_flag(uint64_t *flag_dev, uint64_t v, hipStream_t stream);
+// segment tags (segments.cpp): the tag of granule g (g * kSegGranule bytes into a
+// block) for the block key `key` (granule 0's tag is the key itself)
+constexpr uint64_t kSegGranule = 2ull << 20;
+__host__ __device__ inline uint64_t seg_granule_tag(uint64_t key, uint32_t g) {
+    return key ^ ((uint64_t)g * 0x9E3779B97F4A7C15ull);
+}
+// write every granule's tag and the end tag (key_end, last 8 bytes) of a block
+int launch_seg_tags(void *p, uint64_t bytes, uint64_t key, uint64_t key_end, hipStream_t stream);
+// check them through a mapping (system-scope loads); out_dev[2] (device memory,
+// preset {0, ~0u}): mismatches, and the first bad granule (granule count = the end tag)
+int launch_seg_check(const void *p, uint64_t bytes, uint64_t key, uint64_t key_end, uint32_t *out_dev,
+                     hipStream_t stream);
 LaunchInfo *last_launch_info();   // most recent launch_strided (any caller)
 unsigned long long kernel_count(int kind);   // launch_strided launches so far, by KernelKind (< kKinds)
 

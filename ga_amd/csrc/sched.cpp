@@ -240,7 +240,10 @@ void sched_wait_flag(int s) {
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
         if (!g_flag_host) {
-            GA_HIP(hipHostMalloc((void **)&g_flag_host, 64 * sizeof(uint64_t), hipHostMallocMapped));
+            // coherent (fine-grained) stated, not left to the runtime's default: the GPU's
+            // store must reach the host's polling loads without any cache maintenance
+            GA_HIP(hipHostMalloc((void **)&g_flag_host, 64 * sizeof(uint64_t),
+                                 hipHostMallocMapped | hipHostMallocCoherent));
             GA_HIP(hipHostGetDevicePointer((void **)&g_flag_dev, g_flag_host, 0));
             memset(g_flag_host, 0, 64 * sizeof(uint64_t));
             g_flag_seq.assign(64, 0);
@@ -253,9 +256,12 @@ void sched_wait_flag(int s) {
     }
     for (unsigned long spins = 0; __atomic_load_n(f, __ATOMIC_ACQUIRE) < v; ++spins) {
         if ((spins & 0xfffff) == 0xfffff) {
-            // every ~1M polls: a failed stream reports its error instead of spinning on
+            // every ~1M polls: a failed stream reports its error instead of spinning on,
+            // and an idle stream ends the wait -- the flag kernel behind the call has
+            // finished, so the call has, whether or not its store was seen
             const hipError_t e = hipStreamQuery(r.streams[s]);
-            if (e != hipSuccess && e != hipErrorNotReady) fatal("stream failed: %s", hipGetErrorString(e));
+            if (e == hipSuccess) break;
+            if (e != hipErrorNotReady) fatal("stream failed: %s", hipGetErrorString(e));
         }
         __builtin_ia32_pause();
     }

@@ -16,6 +16,7 @@
 #include <unistd.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <time.h>
 #include <sys/mman.h>
 #include <deque>
 #include <mutex>
@@ -480,23 +481,52 @@ static void shm_unmap_registered(char *p, size_t map_bytes) {
     munmap(p, map_bytes);
 }
 
-// Every segment gets a per-rank, per-allocation tag in its first and last 8 bytes
-// before its handle goes out, and every peer reads both through its fresh mapping.
-// Eight ranks on one GPU (profiles/r03/s32), with freed blocks going back to the
-// runtime: in 2 of 30 runs, after the runtime had refused an export and a new block
-// was exported instead, EVERY peer's mapping of that rank's new block reached other
-// memory -- the block later read only its owner's own contribution, nobody else's,
-// with no error anywhere.  A mapping that does not read the tags is therefore
-// closed, the owner's block set aside (quarantined) and replaced, and the exchange
-// repeated (all ranks, collectively), up to 4 times.
-// COMEX_AMD_TEST_STALE_GEN=N (tests only): every peer treats its first mapping of each
-// rank's N-th allocation as stale
-static uint64_t test_stale_gen() {
-    static const uint64_t v = [] {
-        const char *e = getenv("COMEX_AMD_TEST_STALE_GEN");
-        return e ? (uint64_t)strtoull(e, nullptr, 10) : 0ull;
-    }();
-    return v;
+// Every segment gets a per-rank, per-allocation tag at the start of every 2 MiB
+// granule and in its last 8 bytes (k_seg_tags) before its handle goes out, and every
+// peer checks all of them through its fresh mapping in one kernel (k_seg_check,
+// system-scope loads).  Eight ranks on one GPU (profiles/r03/s32), with freed blocks
+// going back to the runtime: in 2 of 30 runs, after the runtime had refused an export
+// and a new block was exported instead, EVERY peer's mapping of that rank's new block
+// reached other memory -- the block later read only its owner's own contribution,
+// nobody else's, with no error anywhere -- and tools/vmm_probe.hip reproduced such a
+// binding without this library (profiles/r04/s08).  A block is mapped granule by
+// granule, so the tags cover every granule, not only the two ends.
+// A mapping that does not read them all is closed, the owner's block set aside
+// (quarantined) and replaced, and the exchange repeated (all ranks, collectively), up
+// to 4 times.  Test hooks (gaamd_diag "stale_gen" / "stale_granule"): every peer
+// treats its first mapping of each rank's N-th allocation as stale, or the owner
+// writes a foreign tag into granule G of it so that the check must find it.
+std::atomic<long long> g_diag_stale_gen{0}, g_diag_stale_granule{-1};
+
+// the tag key of a rank's allocation (granule 0's tag) and its end tag
+static uint64_t tag_key(int rank, uint64_t gen) { return seg_tag(rank, gen, 0); }
+static uint64_t tag_end(int rank, uint64_t gen) { return seg_tag(rank, gen, 1); }
+
+static double now_us() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return 1e6 * (double)t.tv_sec + 1e-3 * (double)t.tv_nsec;
+}
+
+// the owner: every tag of its new block (null stream, waited for before the descriptor
+// or handle goes out); the test hook's foreign tag on the first exchange
+static void write_tags(void *p, size_t bytes, int rank, uint64_t gen, int attempt) {
+    const double t0 = now_us();
+    int rc = launch_seg_tags(p, bytes, tag_key(rank, gen), tag_end(rank, gen), nullptr);
+    if (rc) fatal("segment tag kernel failed (%d)", rc);
+    const long long sg = g_diag_stale_granule.load(), sn = g_diag_stale_gen.load();
+    if (attempt == 0 && sn > 0 && (uint64_t)sn == gen && sg >= 0) {
+        const uint64_t ngran = (bytes - 8 + kSegGranule - 1) / kSegGranule;
+        const uint64_t g = (uint64_t)sg % ngran;
+        const uint64_t foreign = seg_granule_tag(tag_key(rank, gen + 1000), (uint32_t)g);
+        GA_HIP(hipStreamSynchronize(nullptr));
+        GA_HIP(hipMemcpy((char *)p + g * kSegGranule, &foreign, 8, hipMemcpyHostToDevice));
+        fprintf(stderr, "[ga_amd %d] gaamd_diag stale_granule: allocation %llu's granule %llu carries a foreign tag\n",
+                rt().rank, (unsigned long long)gen, (unsigned long long)g);
+    }
+    GA_HIP(hipStreamSynchronize(nullptr));
+    trace(1, "comex_malloc: tags of %zu bytes (%llu granules) written in %.1f us", bytes,
+          (unsigned long long)((bytes - 8 + kSegGranule - 1) / kSegGranule), now_us() - t0);
 }
 
 static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool device) {
@@ -568,9 +598,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
         mine.gen = ++gen;
         if (tagged) {
             trace(2, "comex_malloc: writing the tags of %p", p);
-            const uint64_t t0 = seg_tag(r.rank, mine.gen, 0), t1 = seg_tag(r.rank, mine.gen, 1);
-            GA_HIP(hipMemcpy(p, &t0, 8, hipMemcpyHostToDevice));
-            GA_HIP(hipMemcpy((char *)p + bytes - 8, &t1, 8, hipMemcpyHostToDevice));
+            write_tags(p, bytes, r.rank, mine.gen, attempt);
         }
         if (tr) fprintf(stderr, "[ga_amd %d] comex_malloc: allocated %p, allgather\n", r.rank, p);
         std::vector<Info> gathered(members.size());
@@ -601,8 +629,9 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
             vmm_exchange(vlocal.fd, r.rank, mine.gen, to, from, got.data());
             for (size_t k = 0; k < from.size(); ++k) vfd[from_rank[k]] = got[k];
         }
-        // open, and check that each IPC mapping reads its owner's tags
+        // open, and check that each mapping reads every one of its owner's tags
         std::vector<uint8_t> stale(r.size, 0);
+        std::vector<int> checked;   // peers whose tags the check kernel reads
         for (int q = 0; q < r.size; ++q) {
             mapped[q] = nullptr;
             if (q == r.rank || !all[q].bytes || !r.same_node(q)) continue;
@@ -614,27 +643,67 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
             if (all[q].vmm) {    // the owner's dmabuf descriptor, mapped at a fresh address here
                 if (vpeer.size() != (size_t)r.size) vpeer.assign(r.size, VmmBlock());
                 mapped[q] = vmm_import(vfd[q], all[q].vmm_bytes, q, &vpeer[q]);
+                if (!mapped[q]) {
+                    // the runtime refused this GPU access to the imported block (vmm.cpp): a
+                    // broken binding like a stale one -- the owner replaces the block and every
+                    // member repeats the exchange, instead of this rank aborting alone
+                    stale[q] = 1;
+                    continue;
+                }
             } else {
                 mapped[q] = ipc_open(all[q].h, q, "segment");
             }
             if (!mapped[q] || all[q].bytes < 16) continue;
-            uint64_t t[2] = {0, 0};
-            trace(2, "comex_malloc: reading rank %d's tags through %p", q, mapped[q]);
-            GA_HIP(hipMemcpy(&t[0], mapped[q], 8, hipMemcpyDeviceToHost));
-            GA_HIP(hipMemcpy(&t[1], (char *)mapped[q] + all[q].bytes - 8, 8, hipMemcpyDeviceToHost));
-            if (attempt == 0 && all[q].gen == test_stale_gen()) {
+            const long long sn = g_diag_stale_gen.load();
+            if (attempt == 0 && sn > 0 && all[q].gen == (uint64_t)sn && g_diag_stale_granule.load() < 0) {
                 // test hook: this round's mappings of allocation N are treated as stale, so the
                 // replacement path (set aside, new block, repeated exchange) runs on demand
-                fprintf(stderr, "[ga_amd %d] COMEX_AMD_TEST_STALE_GEN: treating rank %d's allocation %llu as stale\n",
+                fprintf(stderr, "[ga_amd %d] gaamd_diag stale_gen: treating rank %d's allocation %llu as stale\n",
                         r.rank, q, (unsigned long long)all[q].gen);
                 stale[q] = 1;
-            } else if (t[0] != seg_tag(q, all[q].gen, 0) || t[1] != seg_tag(q, all[q].gen, 1)) {
+                continue;
+            }
+            checked.push_back(q);
+        }
+        if (!checked.empty()) {
+            const double t0 = now_us();
+            uint32_t *dres = nullptr;
+            std::vector<uint32_t> res(2 * checked.size());
+            for (size_t k = 0; k < checked.size(); ++k) {
+                res[2 * k] = 0;
+                res[2 * k + 1] = ~0u;
+            }
+            GA_HIP(hipMalloc((void **)&dres, res.size() * sizeof(uint32_t)));
+            GA_HIP(hipMemcpy(dres, res.data(), res.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            uint64_t gran = 0;
+            for (size_t k = 0; k < checked.size(); ++k) {
+                const int q = checked[k];
+                trace(2, "comex_malloc: checking rank %d's tags through %p", q, mapped[q]);
+                const int rc = launch_seg_check(mapped[q], all[q].bytes, tag_key(q, all[q].gen),
+                                                tag_end(q, all[q].gen), dres + 2 * k, nullptr);
+                if (rc) fatal("segment tag check kernel failed (%d)", rc);
+                gran += (all[q].bytes - 8 + kSegGranule - 1) / kSegGranule;
+            }
+            GA_HIP(hipMemcpy(res.data(), dres, res.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            GA_HIP(hipFree(dres));
+            trace(1, "comex_malloc: %zu peers' tags (%llu granules) checked in %.1f us", checked.size(),
+                  (unsigned long long)gran, now_us() - t0);
+            for (size_t k = 0; k < checked.size(); ++k) {
+                if (!res[2 * k]) continue;
+                const int q = checked[k];
                 stale[q] = 1;
+                const uint64_t ng = (all[q].bytes - 8 + kSegGranule - 1) / kSegGranule, g = res[2 * k + 1];
+                const uint64_t off = g < ng ? g * kSegGranule : all[q].bytes - 8;
+                uint64_t got = 0;
+                GA_HIP(hipMemcpy(&got, (char *)mapped[q] + off, 8, hipMemcpyDeviceToHost));
                 fprintf(stderr, "[ga_amd %d] the %s mapping of rank %d's new %zu-byte segment (%p in its space) "
-                        "reads %#llx / %#llx, not its tags: another allocation's memory\n", r.rank, all[q].vmm ? "vmm" : "IPC", q,
-                        (size_t)all[q].bytes, (void *)(uintptr_t)all[q].base, (unsigned long long)t[0],
-                        (unsigned long long)t[1]);
-                if (!all[q].vmm) report_stale(q, all[q].gen, all[q].base, all[q].bytes, all[q].h, t[0]);
+                        "reads %u of its %llu tags wrong, the first at byte %llu (%s): %#llx, not %#llx -- another "
+                        "allocation's memory\n", r.rank, all[q].vmm ? "vmm" : "IPC", q, (size_t)all[q].bytes,
+                        (void *)(uintptr_t)all[q].base, res[2 * k], (unsigned long long)ng + 1,
+                        (unsigned long long)off, g < ng ? "a granule tag" : "the end tag", (unsigned long long)got,
+                        (unsigned long long)(g < ng ? seg_granule_tag(tag_key(q, all[q].gen), (uint32_t)g)
+                                                    : tag_end(q, all[q].gen)));
+                if (!all[q].vmm && g == 0) report_stale(q, all[q].gen, all[q].base, all[q].bytes, all[q].h, got);
             }
         }
         std::vector<uint8_t> seen(members.size() * (size_t)r.size);
@@ -834,7 +903,10 @@ int comex_free(void *ptr, comex_group_t group) {
     // (hipIpcGetMemHandle: invalid argument in the next comex_malloc)
     members_barrier(members, group);
     if (is_vmm) {
-        if (block_cache_cap()) {   // kept, with its descriptor, for the next comex_malloc
+        if (!vblock.va) {
+            // this rank owns no bytes of the segment: nothing to keep or give back (a
+            // zero-byte entry in the cache would never be taken nor evicted)
+        } else if (block_cache_cap()) {   // kept, with its descriptor, for the next comex_malloc
             CachedBlock b;
             b.p = vblock.va;
             b.bytes = local_bytes;

@@ -63,8 +63,12 @@ size_t granularity() {
 }
 
 // Each mapping gets a virtual range of its own, taken from a window of the address
-// space no runtime allocation uses (COMEX_AMD_VMM_VA_BASE, default 32 TiB, asked for
-// by address hint, bump-allocated, never handed out twice), and a range is not
+// space no runtime allocation uses ([COMEX_AMD_VMM_VA_BASE, COMEX_AMD_VMM_VA_LIMIT),
+// default [32 TiB, 96 TiB): below the runtime's own mappings, which sit near the top
+// of the 128 TiB user space), asked for by address hint, bump-allocated, never handed
+// out twice -- a range the runtime places elsewhere, or a window used up, is an error
+// that names the two variables (a range it picks itself may be one handed back
+// earlier, which is what read stale), and a range is not
 // reserved again after its mapping is gone: it stays reserved (retired) until the
 // retired total passes COMEX_AMD_VMM_RETAIN_GB (default 16384 = 16 TiB), oldest first.
 // Measured (tools/vmm_probe.hip, profiles/r04/s05): two processes exchanging 2 MiB
@@ -76,7 +80,6 @@ std::vector<Retired> g_retired;
 std::atomic<unsigned long long> g_access_retries{0};
 size_t g_retired_bytes = 0;
 uintptr_t g_window = 0;            // next hint in the private window
-bool g_window_warned = false;
 
 size_t retain_cap() {
     static const size_t cap = [] {
@@ -86,6 +89,8 @@ size_t retain_cap() {
     return cap;
 }
 
+uintptr_t g_window_end = 0;
+
 char *va_take(size_t bytes) {
     std::lock_guard<std::mutex> g(g_vmm_mu);
     constexpr uintptr_t kAlign = 2u << 20;
@@ -93,18 +98,28 @@ char *va_take(size_t bytes) {
         const char *e = getenv("COMEX_AMD_VMM_VA_BASE");
         g_window = e ? (uintptr_t)strtoull(e, nullptr, 0) : (uintptr_t)0x200000000000ull;
         g_window = (g_window + kAlign - 1) & ~(kAlign - 1);
+        const char *l = getenv("COMEX_AMD_VMM_VA_LIMIT");
+        g_window_end = l ? (uintptr_t)strtoull(l, nullptr, 0) : (uintptr_t)0x600000000000ull;
     }
+    // one empty 2 MiB guard after every range, so no range starts where another
+    // ends (a precaution: tools/vmm_probe.hip r_adjacent found adjacent ranges fine)
+    const uintptr_t step = ((bytes + kAlign - 1) & ~(kAlign - 1)) + kAlign;
+    if (g_window + step > g_window_end)
+        fatal("vmm: the private address window is used up (%zu more bytes at %p, window end %p): every mapping "
+              "takes a range never used before, and a long job of many array creations needs a larger window -- "
+              "raise COMEX_AMD_VMM_VA_LIMIT (or lower COMEX_AMD_VMM_VA_BASE), or keep freed blocks for reuse "
+              "(COMEX_AMD_SEGMENT_CACHE_MB); COMEX_AMD_VMM_RETAIN_GB bounds the retired ranges still reserved",
+              bytes, (void *)g_window, (void *)g_window_end);
     void *hint = (void *)g_window;
     void *base = nullptr;
     trace(2, "vmm: hipMemAddressReserve(%zu at %p)", bytes, hint);
     GA_HIP(hipMemAddressReserve(&base, bytes, granularity(), hint, 0));
-    // one empty 2 MiB guard after every range, so no range starts where another
-    // ends (a precaution: tools/vmm_probe.hip r_adjacent found adjacent ranges fine)
-    g_window += ((bytes + kAlign - 1) & ~(kAlign - 1)) + kAlign;
-    if (base != hint && !g_window_warned) {
-        g_window_warned = true;
-        fprintf(stderr, "[ga_amd %d] vmm: the runtime placed a range at %p, not at the requested %p\n", rt().rank,
-                base, hint);
+    g_window += step;
+    if (base != hint) {
+        (void)hipMemAddressFree(base, bytes);
+        fatal("vmm: the runtime placed a range at %p, not at the requested %p: the private window "
+              "[COMEX_AMD_VMM_VA_BASE, COMEX_AMD_VMM_VA_LIMIT) meets other mappings, and a range the runtime "
+              "chooses may be one handed back earlier (which read stale data); move the window", base, hint);
     }
     return (char *)base;
 }
@@ -363,7 +378,8 @@ void vmm_exchange(int fd, int rank, uint64_t gen, const std::vector<int> &to_pid
 }
 
 // rank q's block: `myfd` (this process's descriptor of it, from vmm_exchange, owned
-// by b from here on), `bytes` (granularity-rounded)
+// by b from here on), `bytes` (granularity-rounded); nullptr when the runtime refuses
+// this GPU access to it
 void *vmm_import(int myfd, size_t bytes, int q, VmmBlock *b) {
     hipMemGenericAllocationHandle_t h;
     trace(2, "vmm: hipMemImportFromShareableHandle(descriptor %d) of rank %d", myfd, q);
@@ -371,7 +387,16 @@ void *vmm_import(int myfd, size_t bytes, int q, VmmBlock *b) {
     // for the driver API this one mirrors
     GA_HIP(hipMemImportFromShareableHandle(&h, (void *)(uintptr_t)myfd, hipMemHandleTypePosixFileDescriptor));
     char *va = map_fresh(h, bytes, q);
-    if (!va) fatal("access to rank %d's block refused", q);
+    if (!va) {
+        // refused (the runtime defect above, seen from the importer): kept like a broken
+        // handle, the descriptor closed; the caller reports the mapping stale so the owner
+        // replaces the block and every member repeats the exchange together
+        std::lock_guard<std::mutex> g(g_vmm_mu);
+        g_broken.push_back(h);
+        if (myfd >= 0) close(myfd);
+        *b = VmmBlock();
+        return nullptr;
+    }
     b->va = va;
     b->bytes = bytes;
     b->handle = h;

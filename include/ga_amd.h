@@ -101,16 +101,6 @@ int gaamd_toggle_counts(unsigned long long counts[3]);
  * the radix path for the pairs it could not order (more than 8192 such pairs),
  * [2] the radix path (over 2^19 pairs, or COMEX_AMD_IOV_HASH=0). */
 int gaamd_iov_path_counts(unsigned long long counts[3]);
-/* Diagnostic host stamps (CLOCK_BOOTTIME ns) of the last strided call and the last
- * comex_wait_all: [0] call entry, [1] route decided (launch lock held), [2] stream
- * picked, [3] kernel launched, [4] call return, [5] wait entry, [6] streams about
- * to be synchronised, [7] synchronised.  out (may be NULL) receives the current
- * stamps; on = 1 clears them and turns stamping on, 0 off, -1 leaves it. */
-int gaamd_stamps(int on, unsigned long long out[8]);
-/* diagnostic: `steps` blocking comex_accs calls from C over `nsets` (src, dst) pointer
-   sets; elapsed wall-clock ns, 0 if a call failed (the bench's C-caller blocking rate) */
-unsigned long long gaamd_time_blocking_accs(int op, void *scale, void *const *srcs, int *ss, void *const *dsts,
-                                            int *ds, int *count, int levels, int proc, int nsets, int steps);
 /* one-pass accumulates this rank applied into the segment of a rank on the same GPU */
 unsigned long long gaamd_one_pass_count(void);
 /* comex_malloc calls served by a freed segment block kept for reuse (with its IPC export) */
@@ -171,6 +161,24 @@ float gaamd_event_elapsed_ms(void *start, void *stop);
 const char *gaamd_version(void);
 /* path of the HIP runtime (libamdhip64) this library's calls resolve to */
 const char *gaamd_hip_runtime(void);
+
+/* ---- test and diagnostic hooks (not used by GA) ------------
+ * One entry point; returns 0, or -1 for an unknown key.
+ *   "stamps"        host stamps (CLOCK_BOOTTIME ns) of the last strided call and
+ *                   the last comex_wait_all: [0] call entry, [1] route decided
+ *                   (launch lock held), [2] stream picked, [3] kernel launched,
+ *                   [4] call return, [5] wait entry, [6] streams about to be
+ *                   synchronised, [7] synchronised.  out (nout >= 8, may be NULL)
+ *                   receives them; value 1 clears them and starts stamping, 0
+ *                   stops, -1 leaves it.
+ *   "stale_gen"     N > 0: every peer treats its first mapping of each rank's N-th
+ *                   allocation as stale, so the replace-and-repeat path of
+ *                   comex_malloc runs on demand (0: off).
+ *   "stale_granule" G >= 0 (with stale_gen): instead, each owner writes a foreign
+ *                   tag into granule G (G * 2 MiB bytes in) of its N-th allocation
+ *                   on the first exchange, and the peers' check must find it
+ *                   (-1: off). */
+int gaamd_diag(const char *key, long long value, unsigned long long *out, int nout);
 
 #if defined(__cplusplus)
 }

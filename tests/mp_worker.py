@@ -762,16 +762,21 @@ def self_order_test(L, rank, size):
 
 
 def stale_fix_test(L, rank, size):
-    """Run with COMEX_AMD_TEST_STALE_GEN=2: every peer treats its first mapping of each
-    rank's second segment as stale (the runtime binding a new block to other memory,
-    DESIGN.md section 6), so every owner sets that block aside, allocates another and the
-    exchange repeats.  Three segments, each accumulated into by its owner and the
-    previous rank, checked exactly; the remap counter must show the replacement."""
+    """TEST_STALE_GEN=2 (gaamd_diag "stale_gen"): every peer treats its first mapping of
+    each rank's second segment as stale (the runtime binding a new block to other
+    memory); or, with TEST_STALE_GRANULE=G too ("stale_granule"),
+    every owner writes a foreign tag into granule G of that segment, an interior 2 MiB
+    granule, so the peers' whole-block tag check has to find the mismatch itself.
+    Either way every owner sets that block aside, allocates another and the exchange
+    repeats.  Three segments (TEST_STALE_N f64 each), each accumulated into by its owner
+    and the previous rank, checked exactly; the remap counter must show the replacement."""
     import ga_amd
+    assert L.gaamd_diag(b"stale_gen", int(os.environ.get("TEST_STALE_GEN", "2")), None, 0) == 0
+    assert L.gaamd_diag(b"stale_granule", int(os.environ.get("TEST_STALE_GRANULE", "-1")), None, 0) == 0
     assert ga_amd.comex_init() == 0
     r0 = L.gaamd_segment_remaps()
     one = ctypes.c_double(1.0)
-    n = 1 << 18
+    n = int(os.environ.get("TEST_STALE_N", str(1 << 18)))
     segs = []
     for it in range(3):
         seg = ga_amd.comex_malloc(n * 8, size)

@@ -9,10 +9,11 @@ import numpy as np
 import pytest
 
 import ga_amd
-from ga_amd._lib import GA_LIB_PATH, GA_SIGNATURES, LIB_PATH, SIGNATURES
+from ga_amd._lib import DIAG_LIB_PATH, GA_LIB_PATH, GA_SIGNATURES, LIB_PATH, SIGNATURES
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("comex.h", "armci.h", "message.h", "armci_acc.h", "ga_amd.h", "ga.h")]
+HEADERS = [os.path.join(ROOT, "include", h)
+           for h in ("comex.h", "armci.h", "message.h", "armci_acc.h", "ga_amd.h", "ga.h", "ga_amd_diag.h")]
 
 
 def declared_functions(path):
@@ -47,8 +48,10 @@ def test_library_loads():
 
 @pytest.mark.parametrize("header", HEADERS, ids=os.path.basename)
 def test_every_declared_symbol_is_exported(header):
-    """ga.h is libga_amd_ga.so's; every other header is libga_amd.so's."""
-    syms = exported_symbols(GA_LIB_PATH if header.endswith("ga.h") and "ga_amd" not in header else LIB_PATH)
+    """ga.h is libga_amd_ga.so's, ga_amd_diag.h libga_amd_diag.so's; every other
+    header is libga_amd.so's."""
+    name = os.path.basename(header)
+    syms = exported_symbols({"ga.h": GA_LIB_PATH, "ga_amd_diag.h": DIAG_LIB_PATH}.get(name, LIB_PATH))
     decl = declared_functions(header)
     assert decl, header
     missing = sorted(n for n in decl if n not in syms)
@@ -112,6 +115,15 @@ def test_program_defining_ga_names_runs(tmp_path):
     exe = _build_ga_coexist(tmp_path)
     r = subprocess.run([str(exe), "run"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ga_coexist OK" in r.stdout, (r.returncode, r.stdout, r.stderr[-2000:])
+
+
+def test_product_library_has_no_bench_helpers():
+    """The bench's C-loop timer lives in libga_amd_diag.so, over the public ABI;
+    the product library keeps one test/diagnostic entry point (gaamd_diag)."""
+    syms = exported_symbols()
+    assert "gaamd_time_blocking_accs" not in syms and "gaamd_stamps" not in syms
+    assert "gaamd_diag" in syms
+    assert "gaamd_time_blocking_accs" in exported_symbols(DIAG_LIB_PATH)
 
 
 def test_armci_names_are_weak_aliases():

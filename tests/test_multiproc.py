@@ -374,17 +374,23 @@ def test_vmm_segments(mode, n, extra):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("alloc,finalize", [("ipc", True), ("vmm", True), ("ipc", False), ("vmm", False)])
-def test_stale_segment_replaced(alloc, finalize):
+@pytest.mark.parametrize("alloc,finalize,granule", [("ipc", True, None), ("vmm", True, None), ("ipc", False, None),
+                                                    ("vmm", False, None), ("ipc", True, 17), ("vmm", True, 17)])
+def test_stale_segment_replaced(alloc, finalize, granule):
     """The replacement path for a new segment whose peer mappings read other memory
     (the runtime defect of DESIGN.md section 6), forced on demand
-    (COMEX_AMD_TEST_STALE_GEN=2): the owner sets the block aside, allocates another, the
+    (gaamd_diag "stale_gen" = 2): the owner sets the block aside, allocates another, the
     exchange repeats, and every accumulate into the segments is exact, on both segment
     allocators; with comex_finalize and without (the exit hook then joins the idle
-    progress thread: a process exiting with set-aside blocks once crashed there)."""
-    launch("stalefix", n=3, timeout=120,
-           extra_env={"COMEX_AMD_TEST_STALE_GEN": "2", "COMEX_AMD_SEGMENT_ALLOC": alloc,
-                      "STALEFIX_NO_FINALIZE": "0" if finalize else "1"})
+    progress thread: a process exiting with set-aside blocks once crashed there).
+    granule: 64 MiB segments whose owners write a foreign tag into interior granule 17
+    (34 MiB in) of the second one -- the whole-block check (k_seg_check, VERDICT r4
+    item 4) must find it, not only a mismatch at the block's ends."""
+    env = {"TEST_STALE_GEN": "2", "COMEX_AMD_SEGMENT_ALLOC": alloc,
+           "STALEFIX_NO_FINALIZE": "0" if finalize else "1"}
+    if granule is not None:
+        env.update(TEST_STALE_GRANULE=str(granule), TEST_STALE_N=str(1 << 23))
+    launch("stalefix", n=3, timeout=120, extra_env=env)
 
 
 @pytest.mark.gpu
@@ -511,3 +517,26 @@ def test_segment_cache_reuse(n, cache):
     their size; remote accumulates into reused segments stay exact (and with the cache
     off, every segment is a fresh block)."""
     launch("segcache", n=n, timeout=120, extra_env={"COMEX_AMD_SEGMENT_CACHE_MB": cache})
+
+
+@pytest.mark.gpu
+def test_vmm_window_used_up_is_a_clear_error():
+    """ADVICE r4: the vmm allocator maps every block at a range never used before;
+    when its private window [COMEX_AMD_VMM_VA_BASE, COMEX_AMD_VMM_VA_LIMIT) is used up
+    the next comex_malloc aborts with a message naming the variables -- not a
+    runtime-chosen range that may be one handed back earlier.  A 1 GiB window and
+    64 MiB segments with the freed-block cache off: the first ~15 cycles run, then
+    the error, well within the timeout."""
+    code = ("import ctypes, ga_amd\n"
+            "assert ga_amd.comex_init() == 0\n"
+            "for i in range(64):\n"
+            "    seg = ga_amd.comex_malloc(64 << 20, 1)\n"
+            "    assert ga_amd.comex_free(seg[0]) == 0\n"
+            "print('no error after 64 cycles', flush=True)\n")
+    env = dict(os.environ, COMEX_AMD_SEGMENT_ALLOC="vmm", COMEX_AMD_SEGMENT_CACHE_MB="0",
+               COMEX_AMD_VMM_VA_BASE=hex(0x200000000000), COMEX_AMD_VMM_VA_LIMIT=hex(0x200000000000 + (1 << 30)))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0, r.stdout
+    assert "private address window is used up" in r.stderr and "COMEX_AMD_VMM_VA_LIMIT" in r.stderr, r.stderr[-2000:]

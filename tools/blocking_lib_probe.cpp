@@ -40,11 +40,11 @@ int main(int argc, char **argv) {
         std::vector<double> t, d01, d12, d23, d34, tail;
         unsigned long long st[8];
         for (int i = 0; i < calls; ++i) {
-            gaamd_stamps(1, nullptr);
+            gaamd_diag("stamps", 1, nullptr, 0);
             const double t0 = now_us();
             comex_accs(COMEX_ACC_DBL, &alpha, src[i % 3], stride, dst[i % 3], stride, count, 1, 0, 0);
             const double t1 = now_us();
-            gaamd_stamps(0, st);
+            gaamd_diag("stamps", 0, st, 8);
             t.push_back(t1 - t0);
             d01.push_back((st[1] - st[0]) * 1e-3);
             d12.push_back((st[2] - st[1]) * 1e-3);
@@ -61,7 +61,7 @@ int main(int argc, char **argv) {
                rep, m, alg / (m * 1e-6) / 8e12, med(d01), med(d12), med(d23), med(d34));
         fflush(stdout);
     }
-    gaamd_stamps(0, nullptr);
+    gaamd_diag("stamps", 0, nullptr, 0);
     comex_finalize();
     return 0;
 }
