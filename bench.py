@@ -49,7 +49,9 @@ the max-over-ranks reduction.  At N > 1 the line also carries C5 (GA_Acc into a
 block-distributed 32768^2 f64 GA): M1 (every rank its own
 block) and M2 (every rank the whole array: (p-1)/p of it through the remote
 path over xGMI), with per-GPU HBM fraction and per-GPU xGMI bytes/s, and an
-exactness check of the exchange on both remote routes (c5.exchange_check).
+exactness check of the exchange on both remote routes: on a 4096^2 GA before any
+timed C5 step (c5.exchange_precheck) and at the configured size after them
+(c5.exchange_check).
 """
 import argparse
 import ctypes
@@ -373,6 +375,9 @@ def run_gpu(args, dist, finalize=True):
             s = None
             src_segs.append(sseg)
             sptr = sseg[dist.rank]
+        elif args.host_src:                # pinned host memory: GA's local (MA) buffer
+            s = ga_amd.DeviceBuffer(sbytes, host=True)
+            sptr = s.ptr
         else:
             s = ga_amd.DeviceBuffer(sbytes)
             sptr = s.ptr
@@ -549,8 +554,9 @@ def run_gpu(args, dist, finalize=True):
                blocking=blocking)
     for b in packed:
         b.free()
-    if args.host_rates and dist.rank == 0:
-        res["host"] = host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_bytes)
+    if (dist.size == 1 and not args.no_host and xfer == "acc" and not pipeline and not self_packed
+            and args.api == "nb"):
+        res["host"] = host_inclusive(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, payload, alg_bytes)
     routes = ga_amd.route_counts()
     for s, d, _ in sets:
         if s is not None:
@@ -577,6 +583,14 @@ def c5_extras(args, dist, wd=None):
     the owner's unpack-acc reading it over xGMI).  Few steps: these are reported
     beside the headline, not as `value`."""
     out = {}
+    # the exchange's exactness FIRST, on a small GA (4096^2, both routes) before any
+    # timed C5 step (VERDICT r4 item 5): on the first run over separate GPUs a
+    # visibility bug reads as exchange_precheck MISMATCH, not as a plausible rate
+    if wd is not None:
+        wd.phase = "exchange_precheck"
+    assert ga_amd_lib().GA_Initialize() == 0
+    out["exchange_precheck"] = {route: c5_exchange_check(dist, src_seg, n=4096) for route, src_seg in
+                                (("buffer_src", False), ("segment_src", True))}
     saved = args.src_seg
     m2 = max(1, args.c5_steps // 2)
     for mode, exchange, steps, src_seg in (("M1", False, args.c5_steps, False), ("M2", True, m2, False),
@@ -714,48 +728,99 @@ def c5_exchange_check(dist, src_seg, n=4096):
     return res
 
 
-def host_rates(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, alg_bytes, iters=5):
-    """Host-inclusive rates (recorded in DESIGN.md, never `value`): the patch starts
-    and ends in host memory (MA segments).  (a) explicit hipMemcpy H2D of the src and
-    dst spans + device kernel + D2H of the dst span, pinned and pageable; (b)
-    comex_accs directly on host pointers (per-call pinning, zero-copy kernel)."""
-    out = {}
+PCIE_GBS = 63.0   # PCIe Gen5 x16 per direction (MI355X_MICROARCH.md host link, spec)
+
+
+def host_inclusive(L, ga_amd, op, count, sstr, dstr, levels, sbytes, dbytes, payload, alg_bytes, iters=5):
+    """The path as north_star states it: it starts and ends in host memory (MA
+    segments that feed MPI/OFI).  Reported beside `value`, never as it.  Each case
+    one untimed call, then `iters` timed ones (median and best):
+      staged_*     : hipMemcpy2D of the src and the dst PATCH host -> HBM (the rows of
+                     the patch only, not the whole leading-dimension span), the same
+                     strided accumulate kernel as the headline, hipMemcpy2D of the dst
+                     patch HBM -> host: 3 x payload over PCIe, one direction at a time
+      ga_host_src_*: comex_accs with src in host memory and dst in HBM -- GA's NGA_Acc
+                     from a local (MA) buffer into a block the GPU owns (onesided.c:
+                     1403-1438): the kernel reads the src patch over PCIe (pinned:
+                     directly; pageable: the library registers its pages per call),
+                     1 x payload over PCIe
+      both_host_pinned: comex_accs with both sides in pinned host memory (zero-copy):
+                     2 x payload read + 1 x payload written over PCIe
+    rate = algorithmic bytes (3 x payload, as `value`) / time; roofline = the
+    PCIe-bound time (PCIE_GBS per direction: H2D + D2H bytes when the copies take
+    turns, the busier direction when a kernel moves both at once) / time."""
+    out = {"unit": "GiB/s", "note": "host-inclusive rates beside value (never value); rate = 3 x payload / time",
+           "pcie_peak_GBps_per_direction": PCIE_GBS,
+           "pcie_peak_basis": "PCIe Gen5 x16, 63 GB/s per direction (MI355X_MICROARCH.md)"}
     keep, sp = ga_amd.scale_buffer(op, SCALE[op])
     ss, ds, cnt = ga_amd.int_array(sstr), ga_amd.int_array(dstr), ga_amd.int_array(count)
     dsrc, ddst = ga_amd.DeviceBuffer(sbytes), ga_amd.DeviceBuffer(dbytes)
+    rows = payload // count[0]
+    # a 2-D view of the patch for hipMemcpy2D: rows of count[0] bytes; 1-D patches one
+    # row, 3-D ones (C4) need a contiguous outer level -- only 1/2-level patches here
+    two_d = levels <= 1 or all(sstr[j] == sstr[j - 1] * count[j] and dstr[j] == dstr[j - 1] * count[j]
+                               for j in range(1, levels))
+    spitch = sstr[0] if levels else count[0]
+    dpitch = dstr[0] if levels else count[0]
+
+    def timed(fn):
+        fn()
+        ts = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return ts[len(ts) // 2], ts[0]
+
+    def entry(t_med, t_best, h2d, d2h, overlapped, how):
+        # the PCIe-bound time: one direction after the other for the staged copies,
+        # both directions at once for a kernel reading and writing host memory
+        peak_t = (max(h2d, d2h) if overlapped else h2d + d2h) / (PCIE_GBS * 1e9)
+        return {"value": round(alg_bytes / t_med / 2 ** 30, 2), "best": round(alg_bytes / t_best / 2 ** 30, 2),
+                "ms": round(t_med * 1e3, 3), "pcie_h2d_bytes": h2d, "pcie_d2h_bytes": d2h,
+                "roofline": {"bound": "pcie", "achieved": round((h2d + d2h) / t_med / 1e9, 2),
+                             "peak": PCIE_GBS * (2 if overlapped and h2d and d2h else 1), "unit": "GB/s",
+                             "frac": round(peak_t / t_med, 4),
+                             "basis": ("H2D and D2H concurrently, bound by the busier direction" if overlapped
+                                       else "one direction at a time")},
+                "how": how}
+
     for kind in ("pinned", "pageable"):
         if kind == "pinned":
             hs, hd = ga_amd.DeviceBuffer(sbytes, host=True), ga_amd.DeviceBuffer(dbytes, host=True)
             hsp, hdp = hs.ptr, hd.ptr
+            L.gaamd_memset(ctypes.c_void_p(hsp), 1, sbytes)
+            L.gaamd_memset(ctypes.c_void_p(hdp), 0, dbytes)
         else:
             hs_a, hd_a = np.ones(sbytes, np.uint8), np.zeros(dbytes, np.uint8)
             hsp, hdp = hs_a.ctypes.data, hd_a.ctypes.data
-        ts = []
-        for _ in range(iters):
-            t0 = time.perf_counter()
-            L.gaamd_memcpy(ctypes.c_void_p(dsrc.ptr), ctypes.c_void_p(hsp), sbytes)
-            L.gaamd_memcpy(ctypes.c_void_p(ddst.ptr), ctypes.c_void_p(hdp), dbytes)
-            L.comex_accs(op, sp, ctypes.c_void_p(dsrc.ptr), ss, ctypes.c_void_p(ddst.ptr), ds, cnt, levels, 0, 0)
-            L.gaamd_memcpy(ctypes.c_void_p(hdp), ctypes.c_void_p(ddst.ptr), dbytes)
-            ts.append(time.perf_counter() - t0)
-        out[f"staged_{kind}_GiBps"] = alg_bytes / min(ts) / 2 ** 30
-        ts = []
-        for _ in range(iters):
-            t0 = time.perf_counter()
-            L.comex_accs(op, sp, ctypes.c_void_p(hsp), ss, ctypes.c_void_p(hdp), ds, cnt, levels, 0, 0)
+        if two_d:
+            def staged():
+                L.gaamd_memcpy2d(ctypes.c_void_p(dsrc.ptr), spitch, ctypes.c_void_p(hsp), spitch, count[0], rows)
+                L.gaamd_memcpy2d(ctypes.c_void_p(ddst.ptr), dpitch, ctypes.c_void_p(hdp), dpitch, count[0], rows)
+                if L.comex_accs(op, sp, ctypes.c_void_p(dsrc.ptr), ss, ctypes.c_void_p(ddst.ptr), ds, cnt, levels,
+                                0, 0):
+                    raise RuntimeError("staged accumulate failed")
+                L.gaamd_memcpy2d(ctypes.c_void_p(hdp), dpitch, ctypes.c_void_p(ddst.ptr), dpitch, count[0], rows)
+            out[f"staged_{kind}"] = entry(*timed(staged), 2 * payload, payload, False,
+                                          f"hipMemcpy2D src+dst patch H2D ({kind}), strided accumulate kernel, "
+                                          "hipMemcpy2D dst patch D2H")
+
+        def host_src():
+            if L.comex_accs(op, sp, ctypes.c_void_p(hsp), ss, ctypes.c_void_p(ddst.ptr), ds, cnt, levels, 0, 0):
+                raise RuntimeError("host-source accumulate failed")
             L.comex_fence_all(0)
-            ts.append(time.perf_counter() - t0)
-        out[f"zerocopy_{kind}_GiBps"] = alg_bytes / min(ts) / 2 ** 30
-        # the GA-typical case: the patch comes from host memory (MA), the array
-        # block (dst) lives in HBM -- only src crosses PCIe
-        ts = []
-        for _ in range(iters):
-            t0 = time.perf_counter()
-            L.comex_accs(op, sp, ctypes.c_void_p(hsp), ss, ctypes.c_void_p(ddst.ptr), ds, cnt, levels, 0, 0)
-            L.comex_fence_all(0)
-            ts.append(time.perf_counter() - t0)
-        out[f"host_src_{kind}_hbm_dst_GiBps"] = alg_bytes / min(ts) / 2 ** 30
+        out[f"ga_host_src_{kind}"] = entry(*timed(host_src), payload, 0, True,
+                                           f"comex_accs, src patch in {kind} host memory, dst in HBM "
+                                           "(GA's NGA_Acc from a local buffer, onesided.c:1403-1438)")
         if kind == "pinned":
+            def both_host():
+                if L.comex_accs(op, sp, ctypes.c_void_p(hsp), ss, ctypes.c_void_p(hdp), ds, cnt, levels, 0, 0):
+                    raise RuntimeError("host accumulate failed")
+                L.comex_fence_all(0)
+            out["both_host_pinned"] = entry(*timed(both_host), 2 * payload, payload, True,
+                                            "comex_accs, src and dst patch in pinned host memory (zero-copy kernel)")
             hs.free()
             hd.free()
     dsrc.free()
@@ -900,7 +965,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host workers of the CPU baseline (the GPU box's CPU share is 16 per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--host-rates", action="store_true", help="also measure host-inclusive rates")
+    ap.add_argument("--no-host", action="store_true",
+                    help="N=1: skip the host-inclusive block (patch H2D/D2H and host-source rates)")
     ap.add_argument("--exchange", action="store_true",
                     help="N>1: rank r accumulates into rank r+1's partition (remote path, SURVEY 8(d) M2)")
     ap.add_argument("--streams", type=int, default=0,
@@ -909,6 +975,9 @@ def main():
                     help="N=1: force the packed route for accumulates to self (COMEX_ENABLE_ACC_SELF/SMP=0)")
     ap.add_argument("--src-seg", action="store_true",
                     help="sources in this rank's comex_malloc segment (the direct-source route for --exchange)")
+    ap.add_argument("--host-src", action="store_true",
+                    help="sources in pinned host memory (GA's local MA buffer); with --exchange: remote "
+                         "accumulates from a host source")
     ap.add_argument("--pipeline", action="store_true",
                     help="step = pack + unpack-acc (the remote path's two kernels) instead of the fused acc")
     ap.add_argument("--xfer", default="acc", choices=["acc", "put", "get"],
@@ -1036,7 +1105,9 @@ def make_line(args, dist, r, ga_amd):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64" if r["op"] == DBL else "c128",
-        "data": "synthetic (splitmix64, SURVEY.md 8(d)); device-resident src+dst, %d rotating buffer sets" % args.sets,
+        "data": ("synthetic (splitmix64, SURVEY.md 8(d)); %s, %d rotating buffer sets"
+                 % ("src in pinned host memory, dst in HBM" if args.host_src else "device-resident src+dst",
+                    args.sets)),
         "config": {"workload": args.workload, "patch": r["desc"], "payload_bytes": r["payload"],
                    "algorithmic_bytes_per_step": alg,
                    "parallelism": (("GA_Acc of the whole array by every rank: remote owners apply the "
@@ -1108,7 +1179,7 @@ def make_line(args, dist, r, ga_amd):
         line["roofline"] = None
         line["exchange_achieved_GBps_per_rank"] = round(achieved, 1)
     if "host" in r:
-        line["host_inclusive_GiB_per_s"] = {k: round(v, 2) for k, v in r["host"].items()}
+        line["host_inclusive"] = r["host"]
     return line
 
 

@@ -297,6 +297,8 @@ SIGNATURES = {
     "gaamd_host_malloc": (ctypes.c_void_p, [ctypes.c_size_t]),
     "gaamd_host_free": (ctypes.c_int, [ctypes.c_void_p]),
     "gaamd_memcpy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "gaamd_memcpy2d": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                      ctypes.c_size_t, ctypes.c_size_t]),
     "gaamd_memset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]),
     "gaamd_sync": (ctypes.c_int, [ctypes.c_void_p]),
     "gaamd_join": (ctypes.c_int, []),

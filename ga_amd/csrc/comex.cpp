@@ -353,9 +353,10 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
             drain_target(world);   // earlier packed chunks to world are posted first (inbox order)
             {
                 // the owner's kernel must see every write of ours to the source
-                // (and our IPC puts into world's memory): our streams drain first
+                // (and our IPC puts into world's memory): our streams drain first,
+                // behind a system-scope release each (the owner may sit on another GPU)
                 std::lock_guard<std::mutex> g(r.launch_mu);
-                sched_sync_all();
+                sched_publish_all();
             }
             int cnt[8];
             for (int k = 0; k <= levels; ++k) cnt[k] = count[k];

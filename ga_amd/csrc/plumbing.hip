@@ -208,6 +208,11 @@ int gaamd_host_free(void *p) { return hipHostFree(p) == hipSuccess ? 0 : -1; }
 int gaamd_memcpy(void *dst, const void *src, size_t bytes) {
     return hipMemcpy(dst, src, bytes, hipMemcpyDefault) == hipSuccess ? 0 : -1;
 }
+// a 2-D patch: `height` rows of `width` bytes, rows `spitch` / `dpitch` bytes
+// apart (hipMemcpy2D; host or device on either side; returns when done)
+int gaamd_memcpy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height) {
+    return hipMemcpy2D(dst, dpitch, src, spitch, width, height, hipMemcpyDefault) == hipSuccess ? 0 : -1;
+}
 int gaamd_memset(void *dst, int value, size_t bytes) {
     return hipMemset(dst, value, bytes) == hipSuccess ? 0 : -1;
 }

@@ -638,7 +638,14 @@ bool progress_jobs() {
             r.stage_head[j.t] = off + ring_len(len);
             char *stage = r.staging + (size_t)j.t * sub + off;
             hipEvent_t ev;
-            if (g_chunk_ev.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            // the chunk's publication: the owner (possibly on another GPU) reads this
+            // slice of our staging with system-scope loads once the request is posted,
+            // and the request is posted only after this event completed -- recorded
+            // with a system-scope release (hipEventReleaseToSystem, stated rather than
+            // left to the default), so the pack kernel's stores are written back past
+            // every cache of this GPU before the post
+            if (g_chunk_ev.empty())
+                GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToSystem));
             else { ev = g_chunk_ev.back(); g_chunk_ev.pop_back(); }
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);

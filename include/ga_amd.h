@@ -139,6 +139,9 @@ int gaamd_dev_free(void *p);
 void *gaamd_host_malloc(size_t bytes);   /* pinned, device-mapped */
 int gaamd_host_free(void *p);
 int gaamd_memcpy(void *dst, const void *src, size_t bytes);   /* any direction, synchronous */
+/* a 2-D patch, any direction, synchronous: `height` rows of `width` bytes, rows
+ * `spitch` / `dpitch` bytes apart (hipMemcpy2D) */
+int gaamd_memcpy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height);
 int gaamd_memset(void *dst, int value, size_t bytes);
 int gaamd_sync(void *stream);          /* NULL: all library streams */
 /* order the primary stream (gaamd_stream()) after everything enqueued on the
