@@ -1,0 +1,604 @@
+// gaamd_iov.hip -- gfx950 io-vector kernels (comex_accv / putv / getv,
+// comex/src-mpi-pr/comex.c:7327-7400; the owner side _acc_iov_handler 4284-4397)
+// and their ordering machinery for repeated destinations: the hashed LDS path
+// and the library's own stable LSD radix sort.
+#include "gaamd_device.hpp"
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <vector>
+
+namespace gaamd {
+
+// ---------------------------------------------------------------------------
+// I/O-vector kernels: n (src[i], dst[i]) pairs of `bytes` each -- comex_accv /
+// putv / getv (comex/src-mpi-pr/comex.c:7327-7400; the server side
+// _acc_iov_handler 4284-4397).  A side is either a device array of n 64-bit
+// addresses or one packed buffer (address = base + i*bytes).  Vectors of all
+// pairs are flattened so short pairs (GA scatter-acc: one element each) still
+// fill every lane.
+// SYS: the sources lie in a peer GPU's memory (getv from another device):
+// system-scope source loads, as the strided kernels' vload_sys
+template <int W, bool SYS>
+__device__ __forceinline__ typename Vec<W>::T src_load(const char *p) {
+    if constexpr (SYS) return vload_sys<W>(p);
+    else return vload<W, false>(p);
+}
+
+template <class OP, int W, int U, bool SYS = false>
+__global__ __launch_bounds__(256) void k_iov(const IovDesc d, const OP op) {
+    typedef typename Vec<W>::T V;
+    const uint32_t span = 256u * U;
+    for (uint32_t base = blockIdx.x * span; base < d.items; base += gridDim.x * span) {
+        V a[U], b[U];
+        char *dps[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint32_t g = base + threadIdx.x + (uint32_t)(k * 256);
+            dps[k] = nullptr;
+            if (g < d.items) {
+                const uint32_t i = d.nvec_div.div(g);
+                const uint32_t v = g - i * d.nvec;
+                const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
+                char *dp = d.dst_list ? (char *)d.dst_list[i] : d.dst_base + (size_t)i * d.bytes;
+                dps[k] = dp + (size_t)v * W;
+                a[k] = src_load<W, SYS>(sp + (size_t)v * W);
+                if constexpr (OP::kReadsDst) b[k] = vload<W, false>(dps[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (dps[k]) vstore<W, false>(dps[k], op.template apply<W>(b[k], a[k]));
+    }
+}
+
+// pairs in reference order when destinations overlap (duplicates in a scatter-acc)
+template <class OP, int W, bool SYS = false>
+__global__ __launch_bounds__(64) void k_iov_serial(const IovDesc d, const OP op) {
+    if (threadIdx.x != 0) return;
+    for (uint32_t i = 0; i < d.n; ++i) {
+        const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
+        char *dp = d.dst_list ? (char *)d.dst_list[i] : d.dst_base + (size_t)i * d.bytes;
+        for (uint32_t v = 0; v < d.nvec; ++v) {
+            typename Vec<W>::T x = src_load<W, SYS>(sp + (size_t)v * W), y = x;
+            if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
+            vstore<W, false>(dp + (size_t)v * W, op.template apply<W>(y, x));
+        }
+    }
+}
+
+constexpr uint32_t kIovRunSkip = 0xffffffffu;   // k_iov_runs: a run of this key was applied already
+
+// the hashed path's state for one launch (see k_iovh_insert below)
+struct IovHashArgs {
+    uint64_t dlo;
+    uint32_t shift;
+    bool pow2;
+    const uint64_t *first, *last;
+    const uint32_t *slot;
+    uint64_t *conf;
+    uint32_t *count, *overflow;
+};
+
+// launch_iov_runs: sort keys = destination index relative to dlo, values = pair index
+__global__ __launch_bounds__(256) void k_iov_keys(const uint64_t *dst_list, uint64_t dlo, uint32_t bytes, uint32_t n,
+                                                  uint32_t *keys, uint32_t *vals) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = (uint32_t)((dst_list[i] - dlo) / bytes);
+    vals[i] = i;
+}
+
+// one lane per distinct destination (the first sorted position of its run)
+// applies the run's pairs in input order
+template <class OP, int W, bool SYS = false>
+__global__ __launch_bounds__(256) void k_iov_runs(const IovDesc d, const OP op) {
+    const uint32_t j0 = blockIdx.x * 256u + threadIdx.x;
+    if (j0 >= d.n) return;
+    const uint32_t key = d.run_key[j0];
+    if (key == kIovRunSkip || (j0 > 0 && d.run_key[j0 - 1] == key)) return;
+    for (uint32_t j = j0; j < d.n && d.run_key[j] == key; ++j) {
+        const uint32_t i = d.run_perm[j];
+        const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
+        char *dp = (char *)d.dst_list[i];
+        for (uint32_t v = 0; v < d.nvec; ++v) {
+            typename Vec<W>::T x = src_load<W, SYS>(sp + (size_t)v * W), y = x;
+            if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
+            vstore<W, false>(dp + (size_t)v * W, op.template apply<W>(y, x));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Hashed io-vector path (the radix sort is 8 launches,
+// ~40 us at 64 Ki pairs).  Only repeated destinations need ordering, and in a
+// scatter they are rare, so:
+//   k_iovh_insert : every pair's unit key = (dst - dlo) / bytes goes into an
+//                   open-addressing table (tag = epoch:key, no clearing between
+//                   calls); per slot the first and the last pair index
+//                   (atomicMin / atomicMax of epoch-tagged indices)
+//   k_iovh_apply  : a pair whose slot has first == last is its destination's
+//                   only pair: applied at once; the others are appended to a
+//                   conflict list as key:index
+//   k_iovh_conf   : one workgroup sorts the conflict list in LDS (bitonic, by
+//                   key then index) and one lane per distinct key applies its
+//                   pairs in index order -- the reference's order
+// More conflicts than the LDS holds (heavy repeats, a histogram-like scatter):
+// k_iovh_conf applies nothing and raises a flag; the caller, after the stream
+// completed, runs launch_iov_runs with the table as a mask (pairs already
+// applied get the sentinel key and are skipped).
+constexpr uint32_t kIovhCap = 8192;          // conflict entries sorted in LDS (64 KiB)
+constexpr uint32_t kIovhMaxPairs = 1u << 19;  // above: the radix path (1 Mi random pairs overflow the LDS list)
+
+struct IovHash {
+    char *mem = nullptr;          // keys | first | last (P each), slot (n), conflicts (cap), count
+    size_t bytes = 0;
+    uint32_t P = 0;               // table slots (power of two >= 2n)
+    uint32_t npairs = 0;          // capacity of the slot array
+    uint32_t epoch = 0;
+    uint32_t *flag_host = nullptr, *flag_dev = nullptr;   // overflow flag (mapped pinned)
+    uint64_t dlo = 0;
+    uint32_t n = 0, shift = 0;    // the last hashed launch (for the masked fallback)
+    bool pow2 = false;
+};
+
+IovHash *iov_hash_create() { return new IovHash(); }
+
+static __device__ __forceinline__ uint32_t iovh_slot0(uint32_t key, uint32_t mask) {
+    return (key * 0x9E3779B1u) & mask;
+}
+
+__global__ __launch_bounds__(256) void k_iovh_insert(const uint64_t *dst_list, uint64_t dlo, uint32_t bytes,
+                                                     uint32_t shift, bool pow2, uint32_t n, uint64_t *keys,
+                                                     uint64_t *first, uint64_t *last, uint32_t mask, uint32_t epoch,
+                                                     uint32_t *slot, uint32_t *count) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i == 0) *count = 0;   // the conflict list of this call (k_iovh_apply runs after this kernel)
+    if (i >= n) return;
+    const uint64_t off = dst_list[i] - dlo;
+    const uint32_t key = (uint32_t)(pow2 ? (off >> shift) : off / bytes);
+    const uint64_t tag = ((uint64_t)epoch << 32) | key;
+    uint32_t h = iovh_slot0(key, mask);
+    for (;;) {
+        const uint64_t cur = __hip_atomic_load(keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == tag) break;
+        if ((uint32_t)(cur >> 32) != epoch) {   // empty this call (an earlier call's tag): claim it
+            const uint64_t old = atomicCAS((unsigned long long *)(keys + h), cur, tag);
+            if (old == cur || old == tag) break;
+            if ((uint32_t)(old >> 32) != epoch) continue;   // another stale value: try again here
+        }
+        h = (h + 1) & mask;                      // a different key of this call: probe on
+    }
+    slot[i] = h;
+    // first: min over (~epoch : i) -- this call's entries sort below every older one
+    atomicMin((unsigned long long *)(first + h), ((uint64_t)(~epoch) << 32) | i);
+    atomicMax((unsigned long long *)(last + h), ((uint64_t)epoch << 32) | i);
+}
+
+template <class OP, int W, bool SYS>
+__device__ __forceinline__ void iov_apply_pair(const IovDesc &d, const OP &op, uint32_t i) {
+    const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
+    char *dp = (char *)d.dst_list[i];
+    for (uint32_t v = 0; v < d.nvec; ++v) {
+        typename Vec<W>::T x = src_load<W, SYS>(sp + (size_t)v * W), y = x;
+        if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
+        vstore<W, false>(dp + (size_t)v * W, op.template apply<W>(y, x));
+    }
+}
+
+template <class OP, int W, bool SYS>
+__global__ __launch_bounds__(256) void k_iovh_apply(const IovDesc d, const OP op, uint64_t dlo, uint32_t shift,
+                                                    bool pow2, const uint64_t *first, const uint64_t *last,
+                                                    const uint32_t *slot, uint64_t *conf, uint32_t *count) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= d.n) return;
+    const uint32_t h = slot[i];
+    if ((uint32_t)first[h] == (uint32_t)last[h]) {
+        iov_apply_pair<OP, W, SYS>(d, op, i);
+        return;
+    }
+    const uint64_t off = d.dst_list[i] - dlo;
+    const uint32_t key = (uint32_t)(pow2 ? (off >> shift) : off / (uint64_t)d.bytes);
+    const uint32_t pos = atomicAdd(count, 1u);
+    if (pos < kIovhCap) conf[pos] = ((uint64_t)key << 32) | i;
+}
+
+template <class OP, int W, bool SYS>
+__global__ __launch_bounds__(1024) void k_iovh_conf(const IovDesc d, const OP op, const uint64_t *conf,
+                                                    const uint32_t *count, uint32_t *overflow) {
+    __shared__ uint64_t s[kIovhCap];
+    const uint32_t m = *count;
+    if (m == 0) return;
+    if (m > kIovhCap) {
+        if (threadIdx.x == 0) *overflow = 1;
+        return;
+    }
+    uint32_t P = 1;
+    while (P < m) P <<= 1;
+    for (uint32_t t = threadIdx.x; t < P; t += 1024) s[t] = t < m ? conf[t] : ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < P; t += 1024) {
+                const uint32_t l = t ^ j;
+                if (l > t) {
+                    const uint64_t a = s[t], b = s[l];
+                    const bool up = (t & k) == 0;
+                    if ((a > b) == up) {
+                        s[t] = b;
+                        s[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t t = threadIdx.x; t < m; t += 1024) {
+        const uint32_t key = (uint32_t)(s[t] >> 32);
+        if (t > 0 && (uint32_t)(s[t - 1] >> 32) == key) continue;
+        for (uint32_t u = t; u < m && (uint32_t)(s[u] >> 32) == key; ++u) iov_apply_pair<OP, W, SYS>(d, op, (uint32_t)s[u]);
+    }
+}
+
+// the fallback's keys: pairs k_iovh_apply already applied (their slot's first ==
+// last) get the sentinel key, sorted last and skipped by k_iov_runs
+__global__ __launch_bounds__(256) void k_iov_keys_masked(const uint64_t *dst_list, uint64_t dlo, uint32_t bytes,
+                                                         uint32_t n, const uint64_t *first, const uint64_t *last,
+                                                         const uint32_t *slot, uint32_t *keys, uint32_t *vals) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t h = slot[i];
+    keys[i] = ((uint32_t)first[h] == (uint32_t)last[h]) ? kIovRunSkip : (uint32_t)((dst_list[i] - dlo) / bytes);
+    vals[i] = i;
+}
+
+template <class OP, int W, bool SYS>
+static hipError_t iov_ws(const IovDesc &d, const OP &op, bool serial, hipStream_t st, const IovHashArgs *ha) {
+    if (ha) {
+        hipLaunchKernelGGL((k_iovh_apply<OP, W, SYS>), dim3((d.n + 255u) / 256u), dim3(256), 0, st, d, op, ha->dlo,
+                           ha->shift, ha->pow2, ha->first, ha->last, ha->slot, ha->conf, ha->count);
+        hipLaunchKernelGGL((k_iovh_conf<OP, W, SYS>), dim3(1), dim3(1024), 0, st, d, op, ha->conf, ha->count,
+                           ha->overflow);
+    } else if (d.run_key) {
+        hipLaunchKernelGGL((k_iov_runs<OP, W, SYS>), dim3((d.n + 255u) / 256u), dim3(256), 0, st, d, op);
+    } else if (serial) {
+        hipLaunchKernelGGL((k_iov_serial<OP, W, SYS>), dim3(1), dim3(64), 0, st, d, op);
+    } else {
+        constexpr int U = 2;
+        uint64_t blocks = ((uint64_t)d.items + 256u * U - 1) / (256u * U);
+        if (blocks > 65536) blocks = 65536;
+        hipLaunchKernelGGL((k_iov<OP, W, U, SYS>), dim3((uint32_t)blocks), dim3(256), 0, st, d, op);
+    }
+    return hipGetLastError();
+}
+
+// sys: sources in a peer GPU's memory -- built for the byte copy only (getv from
+// another device; every other cross-device io-vector is applied by the owner)
+template <class OP, int W>
+static hipError_t iov_w(const IovDesc &d, const OP &op, bool serial, bool sys, hipStream_t st,
+                        const IovHashArgs *ha) {
+    if constexpr (W < OP::kElem) {
+        return hipErrorInvalidValue;
+    } else {
+        if (sys) {
+            if constexpr (std::is_same<OP, CopyOp>::value) return iov_ws<OP, W, true>(d, op, serial, st, ha);
+            else return hipErrorInvalidValue;
+        }
+        return iov_ws<OP, W, false>(d, op, serial, st, ha);
+    }
+}
+
+template <class OP>
+static hipError_t iov_op(int W, const IovDesc &d, const OP &op, bool serial, bool sys, hipStream_t st,
+                         const IovHashArgs *ha) {
+    switch (W) {
+    case 16: return iov_w<OP, 16>(d, op, serial, sys, st, ha);
+    case 8: return iov_w<OP, 8>(d, op, serial, sys, st, ha);
+    case 4: return iov_w<OP, 4>(d, op, serial, sys, st, ha);
+    case 2: return iov_w<OP, 2>(d, op, serial, sys, st, ha);
+    case 1: return iov_w<OP, 1>(d, op, serial, sys, st, ha);
+    }
+    return hipErrorInvalidValue;
+}
+
+static int iov_dispatch(int op, const void *scale, int W, const IovDesc &d, bool serial, bool sys,
+                        hipStream_t stream, const IovHashArgs *ha = nullptr);
+
+int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool serial, hipStream_t stream,
+               bool src_peer) {
+    const int esz = elem_size(op);
+    if (!esz || d.bytes <= 0) return -4;
+    if (op != kOpCopy && !scale) return -5;
+    const int64_t row = (op == kOpCopy) ? d.bytes : (int64_t)(d.bytes / esz) * esz;   // acc.h:122
+    if (d.n == 0 || row == 0) return 0;
+    uint64_t a = align_or | (uint64_t)row | 16;
+    if (!d.src_list) a |= (uint64_t)(uintptr_t)d.src_base | (uint64_t)d.bytes;
+    if (!d.dst_list) a |= (uint64_t)(uintptr_t)d.dst_base | (uint64_t)d.bytes;
+    int W = (int)lowbit(a);
+    if (W > 16) W = 16;
+    if (W < esz) {   // sub-natural element alignment: see launch_strided
+        if (W < 4) return -8;
+        W = esz;
+    }
+    if (serial) W = esz;
+    d.nvec = (uint32_t)(row / W);
+    d.nvec_div = make_fastdiv(d.nvec);
+    if ((uint64_t)d.n * d.nvec >= (1ull << 31)) return -7;
+    d.items = d.n * d.nvec;
+    return iov_dispatch(op, scale, W, d, serial, src_peer, stream);
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// ---------------------------------------------------------------------------
+// stable LSD radix sort of (key, value) u32 pairs for the io-vector run path,
+// 8-bit digits over bits [0, end_bit).  Per pass three launches:
+//   k_rs_hist    one workgroup per tile of 4096 keys: digit counts in LDS,
+//                stored digit-major (counts[digit * ntiles + tile])
+//   k_rs_scan    one workgroup per digit: exclusive prefix of its row of tile
+//                counts, the digit's total to totals[digit]
+//   k_rs_scatter one workgroup per tile: the 256 digit bases (exclusive scan of
+//                the totals) + the tile's offsets; the tile's keys in 16 rounds
+//                of 256 (input order), each key's rank among equal digits of
+//                its round from wave ballots (8 of them: the lanes whose digit
+//                matches) and per-wave counts in LDS -- equal keys keep their
+//                input order, which the run kernel's order relies on.
+// A hand-written sort rather than a library one: one instantiation, three
+// kernels, no per-architecture dispatch code in the shipped object.
+constexpr int kRsThreads = 256, kRsRounds = 16, kRsTile = kRsThreads * kRsRounds;
+
+__global__ __launch_bounds__(256) void k_rs_hist(const uint32_t *keys, uint32_t n, uint32_t shift, uint32_t ntiles,
+                                                 uint32_t *counts) {
+    __shared__ uint32_t h[256];
+    const uint32_t t = threadIdx.x, tile = blockIdx.x;
+    h[t] = 0;
+    __syncthreads();
+    const uint32_t base = tile * (uint32_t)kRsTile;
+#pragma unroll 4
+    for (int j = 0; j < kRsRounds; ++j) {
+        const uint32_t i = base + (uint32_t)j * kRsThreads + t;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    counts[(size_t)t * ntiles + tile] = h[t];
+}
+
+// exclusive scan of one digit's tile counts (in place); its total to totals[digit]
+__global__ __launch_bounds__(256) void k_rs_scan(uint32_t *counts, uint32_t ntiles, uint32_t *totals) {
+    __shared__ uint32_t part[256];
+    const uint32_t t = threadIdx.x;
+    uint32_t *row = counts + (size_t)blockIdx.x * ntiles;
+    const uint32_t per = (ntiles + 255u) / 256u, lo = min(ntiles, t * per), hi = min(ntiles, lo + per);
+    uint32_t sum = 0;
+    for (uint32_t k = lo; k < hi; ++k) sum += row[k];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {   // inclusive Hillis-Steele scan of the partial sums
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    for (uint32_t k = lo; k < hi; ++k) {
+        const uint32_t c = row[k];
+        row[k] = run;
+        run += c;
+    }
+    if (t == 255) totals[blockIdx.x] = part[255];
+}
+
+__global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t *kin, const uint32_t *vin, uint32_t *kout,
+                                                    uint32_t *vout, uint32_t n, uint32_t shift, uint32_t ntiles,
+                                                    const uint32_t *counts, const uint32_t *totals) {
+    __shared__ uint32_t base[256];
+    __shared__ uint32_t wcnt[4][256];
+    const uint32_t t = threadIdx.x, tile = blockIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t tot = totals[t];
+    base[t] = tot;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {
+        const uint32_t v = t >= off ? base[t - off] : 0u;
+        __syncthreads();
+        base[t] += v;
+        __syncthreads();
+    }
+    const uint32_t mine = base[t] - tot + counts[(size_t)t * ntiles + tile];   // exclusive + the tile's offset
+    __syncthreads();
+    base[t] = mine;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int j = 0; j < kRsRounds; ++j) {
+        wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
+        __syncthreads();
+        const uint32_t i = tile * (uint32_t)kRsTile + (uint32_t)j * kRsThreads + t;
+        const bool valid = i < n;
+        const uint32_t key = valid ? kin[i] : 0u;
+        const uint32_t dg = (key >> shift) & 255u;
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (dg >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(m & lt);
+        if (valid && rank == 0) wcnt[w][dg] = (uint32_t)__popcll(m);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = base[dg] + rank;
+            for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][dg];
+            kout[pos] = key;
+            vout[pos] = vin[i];
+        }
+        __syncthreads();
+        base[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+    }
+}
+
+static size_t iov_sort_temp_bytes(uint32_t n) {
+    const size_t ntiles = ((size_t)n + kRsTile - 1) / kRsTile;
+    return (256 * ntiles + 256) * 4;
+}
+
+// sorts (k[0], v[0]), (k[1], v[1]) the other half of the ping-pong; returns the index
+// of the pair of buffers that holds the result
+static int radix_sort_pairs(uint32_t *const k[2], uint32_t *const v[2], uint32_t n, int end_bit, void *temp,
+                            hipStream_t stream) {
+    const uint32_t ntiles = (n + kRsTile - 1) / kRsTile;
+    uint32_t *counts = (uint32_t *)temp, *totals = counts + (size_t)256 * ntiles;
+    int cur = 0;
+    for (int shift = 0; shift < end_bit; shift += 8, cur ^= 1) {
+        hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(256), 0, stream, k[cur], n, (uint32_t)shift, ntiles, counts);
+        hipLaunchKernelGGL(k_rs_scan, dim3(256), dim3(256), 0, stream, counts, ntiles, totals);
+        hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(256), 0, stream, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], n,
+                           (uint32_t)shift, ntiles, counts, totals);
+    }
+    return cur;
+}
+
+size_t iov_runs_work_bytes(uint32_t n) { return 4 * align256((size_t)n * 4) + align256(iov_sort_temp_bytes(n)); }
+
+int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
+                    void *work, size_t work_bytes, hipStream_t stream, bool src_peer, const IovHash *mask) {
+    const int esz = elem_size(op);
+    if (!esz || d.bytes <= 0 || d.bytes > kIovRunsMaxBytes || !d.dst_list) return -4;
+    if (op != kOpCopy && !scale) return -5;
+    if (units > (1ull << 32)) return -7;
+    const int64_t row = (op == kOpCopy) ? d.bytes : (int64_t)(d.bytes / esz) * esz;   // acc.h:122
+    if (d.n == 0 || row == 0) return 0;
+    if (work_bytes < iov_runs_work_bytes(d.n)) return -6;
+    uint64_t a = align_or | (uint64_t)row | 16;
+    if (!d.src_list) a |= (uint64_t)(uintptr_t)d.src_base | (uint64_t)d.bytes;
+    int W = (int)lowbit(a);
+    if (W > 16) W = 16;
+    if (W < esz) {
+        if (W < 4) return -8;
+        W = esz;
+    }
+    d.nvec = (uint32_t)(row / W);
+    d.nvec_div = make_fastdiv(d.nvec);
+    d.items = d.n * d.nvec;
+    char *w = (char *)work;
+    const size_t q = align256((size_t)d.n * 4);
+    uint32_t *kin = (uint32_t *)w, *kout = (uint32_t *)(w + q), *vin = (uint32_t *)(w + 2 * q),
+             *vout = (uint32_t *)(w + 3 * q);
+    void *temp = w + 4 * q;
+    int end_bit = 1;
+    while (end_bit < 32 && (1ull << end_bit) < units) ++end_bit;
+    if (mask) {
+        // the pairs the hashed launch applied already sort last (sentinel key)
+        if (mask->n != d.n || mask->dlo != dlo || units >= (uint64_t)kIovRunSkip) return -9;
+        const uint64_t P = mask->P;
+        const uint64_t *first = (const uint64_t *)(mask->mem + P * 8), *last = (const uint64_t *)(mask->mem + 2 * P * 8);
+        const uint32_t *slot = (const uint32_t *)(mask->mem + 3 * P * 8);
+        hipLaunchKernelGGL(k_iov_keys_masked, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, d.dst_list, dlo,
+                           (uint32_t)d.bytes, d.n, first, last, slot, kin, vin);
+        end_bit = 32;
+    } else {
+        hipLaunchKernelGGL(k_iov_keys, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, d.dst_list, dlo,
+                           (uint32_t)d.bytes, d.n, kin, vin);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return -100 - (int)e;
+    uint32_t *const kb[2] = {kin, kout}, *const vb[2] = {vin, vout};
+    const int r = radix_sort_pairs(kb, vb, d.n, end_bit, temp, stream);
+    e = hipGetLastError();
+    if (e != hipSuccess) return -100 - (int)e;
+    d.run_key = kb[r];
+    d.run_perm = vb[r];
+    return iov_dispatch(op, scale, W, d, false, src_peer, stream);
+}
+
+int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo,
+                      uint64_t units, hipStream_t stream, bool src_peer) {
+    const int esz = elem_size(op);
+    if (!esz || d.bytes <= 0 || d.bytes > kIovRunsMaxBytes || !d.dst_list) return -4;
+    if (op != kOpCopy && !scale) return -5;
+    if (d.n > kIovhMaxPairs || units >= (uint64_t)kIovRunSkip) return 1;   // the radix path
+    const int64_t row = (op == kOpCopy) ? d.bytes : (int64_t)(d.bytes / esz) * esz;   // acc.h:122
+    if (d.n == 0 || row == 0) return 0;
+    uint64_t a = align_or | (uint64_t)row | 16;
+    if (!d.src_list) a |= (uint64_t)(uintptr_t)d.src_base | (uint64_t)d.bytes;
+    int W = (int)lowbit(a);
+    if (W > 16) W = 16;
+    if (W < esz) {
+        if (W < 4) return -8;
+        W = esz;
+    }
+    d.nvec = (uint32_t)(row / W);
+    d.nvec_div = make_fastdiv(d.nvec);
+    d.items = d.n * d.nvec;
+    // table of P >= 2n slots, kept across calls (epoch tags: no clearing); grown
+    // (and re-initialised) when a larger n arrives -- the caller has drained every
+    // earlier launch that used it
+    uint32_t P = 1024;
+    while (P < 2 * d.n) P <<= 1;
+    auto off_slot = [](uint32_t P_) { return (size_t)P_ * 24; };
+    auto off_conf = [&](uint32_t P_, uint32_t np) { return align256(off_slot(P_) + (size_t)np * 4); };
+    if (P > h->P || d.n > h->npairs) {
+        const uint32_t nP = std::max(P, h->P), np = std::max(d.n, h->npairs);
+        if (h->mem) {
+            hipError_t e = hipFree(h->mem);
+            if (e != hipSuccess) return -100 - (int)e;
+        }
+        h->bytes = off_conf(nP, np) + (size_t)kIovhCap * 8 + 256;
+        hipError_t e = hipMalloc((void **)&h->mem, h->bytes);
+        if (e != hipSuccess) return -100 - (int)e;
+        e = hipMemsetAsync(h->mem, 0, (size_t)nP * 8, stream);                       // keys: epoch 0
+        if (e == hipSuccess) e = hipMemsetAsync(h->mem + (size_t)nP * 8, 0xff, (size_t)nP * 8, stream);   // first
+        if (e == hipSuccess) e = hipMemsetAsync(h->mem + (size_t)nP * 16, 0, (size_t)nP * 8, stream);     // last
+        if (e != hipSuccess) return -100 - (int)e;
+        h->P = nP;
+        h->npairs = np;
+        h->epoch = 0;
+    }
+    if (!h->flag_host) {
+        hipError_t e = hipHostMalloc((void **)&h->flag_host, 64, hipHostMallocMapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&h->flag_dev, h->flag_host, 0);
+        if (e != hipSuccess) return -100 - (int)e;
+    }
+    if (++h->epoch == 0) {   // 2^32 calls: start the tags over
+        hipError_t e = hipMemsetAsync(h->mem, 0, (size_t)h->P * 8, stream);
+        if (e == hipSuccess) e = hipMemsetAsync(h->mem + (size_t)h->P * 8, 0xff, (size_t)h->P * 8, stream);
+        if (e == hipSuccess) e = hipMemsetAsync(h->mem + (size_t)h->P * 16, 0, (size_t)h->P * 8, stream);
+        if (e != hipSuccess) return -100 - (int)e;
+        h->epoch = 1;
+    }
+    *(volatile uint32_t *)h->flag_host = 0;
+    const bool pow2 = (d.bytes & (d.bytes - 1)) == 0;
+    const uint32_t shift = pow2 ? (uint32_t)__builtin_ctz((unsigned)d.bytes) : 0;
+    uint64_t *keys = (uint64_t *)h->mem, *first = keys + h->P, *last = first + h->P;
+    uint32_t *slot = (uint32_t *)(h->mem + off_slot(h->P));
+    uint64_t *conf = (uint64_t *)(h->mem + off_conf(h->P, h->npairs));
+    uint32_t *count = (uint32_t *)(conf + kIovhCap);
+    hipLaunchKernelGGL(k_iovh_insert, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, d.dst_list, dlo,
+                       (uint32_t)d.bytes, shift, pow2, d.n, keys, first, last, h->P - 1, h->epoch, slot, count);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return -100 - (int)e;
+    IovHashArgs ha{dlo, shift, pow2, first, last, slot, conf, count, h->flag_dev};
+    h->dlo = dlo;
+    h->n = d.n;
+    h->shift = shift;
+    h->pow2 = pow2;
+    return iov_dispatch(op, scale, W, d, false, src_peer, stream, &ha);
+}
+
+bool iov_hash_overflowed(const IovHash *h) { return h->flag_host && *(volatile uint32_t *)h->flag_host != 0; }
+
+static int iov_dispatch(int op, const void *scale, int W, const IovDesc &d, bool serial, bool sys,
+                        hipStream_t stream, const IovHashArgs *ha) {
+    hipError_t e;
+    switch (op) {
+    case kOpCopy: e = iov_op(W, d, CopyOp{}, serial, sys, stream, ha); break;
+    case 37: { AccInt o; int32_t s; memcpy(&s, scale, 4); o.s = (uint32_t)s; e = iov_op(W, d, o, serial, sys, stream, ha); break; }
+    case 42: { AccLng o; int64_t s; memcpy(&s, scale, 8); o.s = (uint64_t)s; e = iov_op(W, d, o, serial, sys, stream, ha); break; }
+    case 39: { AccFlt o; memcpy(&o.s, scale, 4); e = iov_op(W, d, o, serial, sys, stream, ha); break; }
+    case 38: { AccDbl o; memcpy(&o.s, scale, 8); e = iov_op(W, d, o, serial, sys, stream, ha); break; }
+    case 40: { AccCpl o; float s[2]; memcpy(s, scale, 8); o.sr = s[0]; o.si = s[1]; e = iov_op(W, d, o, serial, sys, stream, ha); break; }
+    case 41: { AccDcp o; double s[2]; memcpy(s, scale, 16); o.sr = s[0]; o.si = s[1]; e = iov_op(W, d, o, serial, sys, stream, ha); break; }
+    default: return -4;
+    }
+    return e == hipSuccess ? 0 : -100 - (int)e;
+}
+
+}  // namespace gaamd

@@ -370,14 +370,10 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     ds.lo = dst_listed ? (int64_t)dlo : (int64_t)(uintptr_t)(dev + o_res);
     ds.hi = dst_listed ? (int64_t)dhi : ds.lo + (int64_t)pk;
     const int si = sched_pick(ss, ds);
-    // the upload: the copy kernel reading the mapped pinned buffer (no DMA engine
-    // round trip before the first io-vector kernel), or the runtime's copy
-    static const bool kernel_upload = [] {
-        const char *e = getenv("COMEX_AMD_IOV_KERNEL_UPLOAD");
-        return !e || atoi(e) != 0;
-    }();
-    if (kernel_upload) upload_pinned(dev, up, o_res, r.streams[si]);
-    else GA_HIP(hipMemcpyAsync(dev, up, o_res, hipMemcpyHostToDevice, r.streams[si]));
+    // the upload: the copy kernel reading the mapped pinned buffer -- no DMA engine
+    // round trip before the first io-vector kernel (64 Ki pairs 0.111-0.120 ms against
+    // 0.122-0.130 with the runtime's copy, profiles/r03/s08)
+    upload_pinned(dev, up, o_res, r.streams[si]);
     const uint64_t units = runs ? (dhi - dlo) / (uint64_t)bytes + 1 : 0;
     int rc;
     if (runs) {

@@ -764,20 +764,11 @@ int remote_acc_start(int t, int op, const void *scale, void *src, const int *ss,
     }
     const uint64_t sub = sub_ring_bytes();
     if ((uint64_t)row_bytes > sub) fatal("row of %ld bytes exceeds staging ring", (long)row_bytes);
-    // An owner on another GPU pulls a chunk over one xGMI link (~64 GB/s per direction,
-    // half a millisecond for a 32 MiB sub-ring) while the next chunk could already be
-    // packed: COMEX_AMD_PEER_CHUNKS cuts the ring into that many slices for such targets,
-    // so packing and posting chunk k+1 overlap the pull of chunk k.  Default 1, the only
-    // setting measured: the one-GPU proxy (every peer treated as another GPU, 2-rank
-    // exchange of C3, profiles/r03/s38) reads 2950-3140 GiB/s with 1, 2922-2941 with 2,
-    // 2607-2637 with 4 -- there is no link to hide there, only per-chunk overhead.
-    static const uint64_t peer_chunks = [] {
-        const char *e = getenv("COMEX_AMD_PEER_CHUNKS");
-        const long v = e ? atol(e) : 1;
-        return (uint64_t)(v < 1 ? 1 : v);
-    }();
-    const uint64_t slices = (t != r.rank && r.peer_src(t)) ? peer_chunks : 1;
-    j.per_req = std::max<uint64_t>(1, sub / slices / (uint64_t)row_bytes);
+    // One chunk per sub-ring for every target.  Cutting the ring into slices for an
+    // owner on another GPU (packing chunk k+1 while it pulls chunk k) measured only
+    // slower on the one-GPU proxy (2-rank C3 exchange, profiles/r03/s38: 2950-3140
+    // GiB/s with one slice, 2922-2941 with 2, 2607-2637 with 4), so it went.
+    j.per_req = std::max<uint64_t>(1, sub / (uint64_t)row_bytes);
     j.rows = rows;
     int64_t acc = row_bytes;
     for (int k = 0; k < levels; ++k) { j.pstride[k] = (int)acc; acc *= count[k + 1]; }
