@@ -489,7 +489,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         // HBM operands only: a completion flag behind the kernel (sched_wait_flag,
         // ~4 us sooner than the runtime's signal); otherwise the runtime's sync, whose
         // system-scope release makes a host-memory destination's bytes visible
-        if (sv.hbm && dv.hbm && sched_flag_wait_enabled()) sched_wait_flag(si);
+        if (sv.hbm && dv.hbm) sched_wait_flag(si);
         else GA_HIP(hipStreamSynchronize(st));
     }
     if (world != r.rank && !synced && !r.direct_pending.empty()) r.direct_pending[world] = 1;
@@ -728,15 +728,14 @@ int comex_init() {
     if (vb && atoi(vb) && r.rank == 0) {
         hipDeviceProp_t prop;
         const bool okp = hipGetDeviceProperties(&prop, r.device) == hipSuccess;
-        const char *async = getenv("COMEX_AMD_ASYNC_ACC");
         const char *seg = getenv("COMEX_AMD_SEGMENT");
         fprintf(stderr,
                 "%s: ranks %d on %d node(s), device %d (%s, %d CUs), library streams %d, "
-                "staging %zu MiB/rank, remote acc %s, segments in %s, blocking sync %d, "
+                "staging %zu MiB/rank, segments in %s, blocking sync %d, "
                 "acc to self %s, put to self %s, same-node put %s\n",
                 gaamd_version(), r.size, r.nnodes, r.device, okp ? prop.gcnArchName : "?",
                 okp ? prop.multiProcessorCount : 0, (int)r.streams.size(), r.staging_bytes >> 20,
-                (async && !atoi(async)) ? "synchronous" : "asynchronous jobs", (seg && !strcmp(seg, "host")) ? "host" : "HBM",
+                (seg && !strcmp(seg, "host")) ? "host" : "HBM",
                 r.blocking_sync ? 1 : 0, r.acc_self_direct ? "direct" : "packed",
                 r.put_self_direct ? "direct" : "packed", r.put_smp_direct ? "IPC" : "packed");
     }

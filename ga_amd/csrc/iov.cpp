@@ -167,13 +167,9 @@ template <class F> static void par_for(long n, int T, F fn) {
 // device allocations are either PROT_NONE reservations or /dev/dri mappings, so
 // a side that passes is safe to gather/scatter on the host.  Any address not
 // covered (or a line that does not parse) answers false and the per-pair
-// classification decides as before.  COMEX_AMD_IOV_MAPS=0 disables it.
+// classification decides as before.
 static bool host_cpu_range(uint64_t lo, uint64_t hi, bool write) {
-    static const bool on = [] {
-        const char *e = getenv("COMEX_AMD_IOV_MAPS");
-        return !(e && atoi(e) == 0);
-    }();
-    if (!on || hi <= lo) return false;
+    if (hi <= lo) return false;
     FILE *f = fopen("/proc/self/maps", "r");
     if (!f) return false;
     char line[512];
@@ -378,14 +374,10 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     int rc;
     if (runs) {
         // repeated destinations: the hashed path (sorts only the pairs that share a
-        // destination), or the radix path above 2^19 pairs / with COMEX_AMD_IOV_HASH=0
-        static const bool hash_on = [] {
-            const char *e = getenv("COMEX_AMD_IOV_HASH");
-            return !e || atoi(e) != 0;
-        }();
+        // destination), or the radix path above 2^19 pairs
         static IovHash *g_hash = nullptr;
         rc = 1;
-        if (hash_on) {
+        {
             if (!g_hash) g_hash = iov_hash_create();
             rc = launch_iov_hashed(g_hash, cop, scale, d, align_or, dlo, units, r.streams[si], src_peer);
             if (rc == 0) {

@@ -124,20 +124,14 @@ struct OnePassHold {
     std::vector<hipEvent_t> evs;
 };
 // A holder with launches in flight keeps a wanted lock for up to this long after it
-// took it (COMEX_AMD_ONE_PASS_LEASE_US): requesters streaming accumulates into one
+// took it (400 us): requesters streaming accumulates into one
 // owner then hand the lock over once per lease instead of once per call, each
 // hand-over costing a completion wait and a dispatch (tens of us against a few us
 // of enqueue per call); the wait a requester sees stays bounded by the lease.
 // Every rank but one accumulating into that one (tools/remote_sweep.py --all-to-one,
 // profiles/r03/s26): 3 ranks 37 us per call per requester without a lease, 17.5-19.7
 // with 100 us, 16.2-17.6 with 400 us; 5 ranks 77-82 / 36-58 / 36-40.
-static double one_pass_lease_s() {
-    static const double v = [] {
-        const char *e = getenv("COMEX_AMD_ONE_PASS_LEASE_US");
-        return (e ? atof(e) : 400.0) * 1e-6;
-    }();
-    return v;
-}
+static double one_pass_lease_s() { return 400e-6; }
 static double steady_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }

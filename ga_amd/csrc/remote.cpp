@@ -215,12 +215,10 @@ static void progress_loop() {
     // idle policy: the reference's progress rank polls without sleeping
     // (comex.c:3379-3565); here the thread keeps polling (yielding the core)
     // while kernels it launched are in flight -- their completion releases the
-    // requesters' staging and fences -- and for COMEX_AMD_PROGRESS_SPIN_US after
-    // the last request (default 2000), then backs off to short sleeps
-    static const double spin_s = [] {
-        const char *e = getenv("COMEX_AMD_PROGRESS_SPIN_US");
-        return (e ? atof(e) : 2000.0) * 1e-6;
-    }();
+    // requesters' staging and fences -- and for 2 ms after the last request, then
+    // backs off to short sleeps (+6.5 % on the packed route to self, +20 % on the
+    // 2-rank exchange against sleeping once idle, profiles/r02/session_l)
+    constexpr double spin_s = 2000e-6;
     auto now_s = [] {
         timespec ts;
         clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -781,11 +779,7 @@ int remote_acc_start(int t, int op, const void *scale, void *src, const int *ss,
     if (j.nchunks > 1 && t != r.rank && dst_rows_disjoint(ds, count, levels, row_bytes))
         j.first = (uint64_t)r.rank * j.nchunks / (uint64_t)r.size;
     if (g_out.size() != (size_t)r.size) g_out.resize(r.size);
-    static const bool async_ok = [] {
-        const char *e = getenv("COMEX_AMD_ASYNC_ACC");   // 0: every remote accumulate completes in its call
-        return !e || atoi(e) != 0;
-    }();
-    const bool host_src = j.sv.registered || j.sv.staged || !async_ok;
+    const bool host_src = j.sv.registered || j.sv.staged;
     g_jobs.push_back(j);
     const int id = j.id;
     progress_jobs();

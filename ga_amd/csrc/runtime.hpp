@@ -259,10 +259,8 @@ void own_write_guard(const Span &dst);
 // op with no dependency (owner pulls from a peer GPU: one stream per source rank)
 int sched_pick(const Span &src, const Span &dst, uint64_t payload = 0, int prefer = -1);
 void sched_join();
-// blocking-call completion: whether the flag wait is on (COMEX_AMD_BLOCKING_WAIT), and
-// the wait itself -- a flag kernel behind stream s's work, the host spinning on it
-// (caller does NOT hold launch_mu); sched_flag_fini at finalize
-bool sched_flag_wait_enabled();
+// blocking-call completion with HBM operands: a flag kernel behind stream s's work,
+// the host spinning on it (caller does NOT hold launch_mu); sched_flag_fini at finalize
 void sched_wait_flag(int s);
 void sched_flag_fini();
 // sched_join before a launch that writes `dst` (own_write_guard first); a span of

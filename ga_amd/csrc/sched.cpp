@@ -238,19 +238,10 @@ void sched_publish_all() {
 // spins on, is seen that much sooner.  Only for HBM operands: the CPU never reads
 // them, so nothing but the ORDER of the GPU's work matters; a host-memory
 // destination keeps hipStreamSynchronize (the runtime's system-scope release at
-// the stream's end makes its bytes visible to the CPU).  COMEX_AMD_BLOCKING_WAIT=
-// sync restores hipStreamSynchronize everywhere.
+// the stream's end makes its bytes visible to the CPU).
 namespace {
 uint64_t *g_flag_host = nullptr, *g_flag_dev = nullptr;
 std::vector<uint64_t> g_flag_seq;
-}
-
-bool sched_flag_wait_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("COMEX_AMD_BLOCKING_WAIT");
-        return !(e && !strcmp(e, "sync"));
-    }();
-    return on;
 }
 
 void sched_wait_flag(int s) {

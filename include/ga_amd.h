@@ -99,7 +99,7 @@ int gaamd_toggle_counts(unsigned long long counts[3]);
 /* Local io-vector launches whose destinations may repeat (>= 4096 pairs), by path:
  * [0] hashed (only pairs sharing a destination sorted, in LDS), [1] hashed, then
  * the radix path for the pairs it could not order (more than 8192 such pairs),
- * [2] the radix path (over 2^19 pairs, or COMEX_AMD_IOV_HASH=0). */
+ * [2] the radix path (over 2^19 pairs). */
 int gaamd_iov_path_counts(unsigned long long counts[3]);
 /* one-pass accumulates this rank applied into the segment of a rank on the same GPU */
 unsigned long long gaamd_one_pass_count(void);

@@ -341,3 +341,15 @@ def test_armci_init_over_a_sub_communicator_gpu(tmp_path):
     assert r.returncode == 0, (r.stdout, r.stderr[-3000:])
     for w, part in enumerate(["0/2", "1/2", "0/1"]):
         assert f"world {w} part {part}: exact" in r.stdout, r.stdout
+
+
+def test_every_runtime_knob_is_documented():
+    """INTEGRATION.md section 3 lists exactly the COMEX_AMD_* variables the library
+    reads (every knob with its default, none stale)."""
+    csrc = os.path.join(ROOT, "ga_amd", "csrc")
+    code = set()
+    for name in os.listdir(csrc):
+        if name.endswith((".cpp", ".hip", ".hpp", ".h")):
+            code |= set(re.findall(r'getenv\("(COMEX_AMD_[A-Z0-9_]+)"\)', open(os.path.join(csrc, name)).read()))
+    doc = set(re.findall(r"^\| `(COMEX_AMD_[A-Z0-9_]+)`", open(os.path.join(ROOT, "INTEGRATION.md")).read(), re.M))
+    assert code == doc, {"undocumented": sorted(code - doc), "stale": sorted(doc - code)}
