@@ -205,6 +205,19 @@ def test_torch_runtime_first_fails_fast():
     _torch_first_init()
 
 
+def test_torch_runtime_mismatch_opt_out():
+    """COMEX_AMD_ALLOW_HIP_MISMATCH=1: the mismatch is a warning and comex_init goes
+    on (here, without a GPU, to the no-device abort -- past the runtime check)."""
+    code = ("import torch, ga_amd, sys; L=ga_amd.lib(); "
+            "sys.exit(0 if L.gaamd_device_count()>0 else (L.comex_init() or 3))")
+    env = dict(os.environ, COMEX_AMD_ALLOW_HIP_MISMATCH="1")
+    r = subprocess.run(["python", "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    if r.returncode == 0:
+        pytest.skip("a GPU is visible here")
+    assert "ga_amd warning: HIP calls resolve to" in r.stderr, r.stderr[-2000:]
+    assert "no HIP device" in r.stderr, r.stderr[-2000:]
+
+
 @pytest.mark.gpu
 def test_torch_runtime_first_fails_fast_gpu():
     """GPU box: torch first -> non-zero exit with the message, not the stall of
