@@ -819,8 +819,10 @@ int comex_fence_proc(int proc, comex_group_t group) {
     ensure_init();
     fence_target(translate_world(group, proc));
     {
+        // behind a system-scope release: what our kernels wrote is visible to a
+        // rank on another GPU that reads it after this fence
         std::lock_guard<std::mutex> g(rt().launch_mu);
-        sched_sync_all();
+        sched_publish_all();
     }
     one_pass_reap(true);   // our one-pass kernels are done: hand the owners' locks back
     return COMEX_SUCCESS;
@@ -834,7 +836,7 @@ int comex_fence_all(comex_group_t group) {
     for (int t = 0; t < r.size; ++t) fence_target(t);
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
-        sched_sync_all();
+        sched_publish_all();   // as comex_fence_proc (and so comex_barrier)
     }
     one_pass_reap(true);
     return COMEX_SUCCESS;

@@ -23,6 +23,12 @@
 
 namespace gaamd {
 
+// Events the owner's progress thread records behind the kernels it applies (their
+// completion bumps done[src][owner], or frees a staging slice): a system-scope
+// release, stated rather than left to HIP's default, so what the owner wrote is
+// visible to a requester on another GPU that reads it after its fence (§6)
+constexpr unsigned kOwnerEventFlags = hipEventDisableTiming | hipEventReleaseToSystem;
+
 static const char *peer_staging_or_die(int src) {
     const char *p = rt().peer_staging[src];
     if (!p) fatal("rank %d's staging buffer is not mapped here (IPC open failed at comex_init)", src);
@@ -252,7 +258,7 @@ static void progress_loop() {
             x.bytes = std::max<size_t>(need, 1 << 20);
             GA_HIP(hipMalloc((void **)&x.p, x.bytes));
         }
-        if (!x.ev) GA_HIP(hipEventCreateWithFlags(&x.ev, hipEventDisableTiming));
+        if (!x.ev) GA_HIP(hipEventCreateWithFlags(&x.ev, kOwnerEventFlags));
         return x.p;
     };
     // contiguous bytes of a peer GPU into local memory (system-scope loads)
@@ -281,7 +287,7 @@ static void progress_loop() {
             const bool peer = r.peer_src(src);
             const char *packed = peer_staging_or_die(src) + q.staging_off;
             hipEvent_t ev;
-            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, kOwnerEventFlags));
             else { ev = pool.back(); pool.pop_back(); }
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
@@ -313,7 +319,7 @@ static void progress_loop() {
                         prog_work_bytes = std::max<size_t>(need, 1 << 20);
                         GA_HIP(hipMalloc((void **)&prog_work, prog_work_bytes));
                     }
-                    if (!prog_work_ev) GA_HIP(hipEventCreateWithFlags(&prog_work_ev, hipEventDisableTiming));
+                    if (!prog_work_ev) GA_HIP(hipEventCreateWithFlags(&prog_work_ev, kOwnerEventFlags));
                     rc = launch_iov_runs(q.op, q.scale, d, q.iov_align, q.dst_addr,
                                          (q.dst_hi - q.dst_addr) / (uint64_t)d.bytes + 1, prog_work, prog_work_bytes,
                                          r.streams[si]);
@@ -341,7 +347,7 @@ static void progress_loop() {
             uint64_t val = 0;
             memcpy(&val, q.scale, 8);
             hipEvent_t ev;
-            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, kOwnerEventFlags));
             else { ev = pool.back(); pool.pop_back(); }
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
@@ -364,7 +370,7 @@ static void progress_loop() {
             side_span_host(q.dst_stride, q.count, q.levels, q.count[0], &dlo, &dhi);
             const char *sp = remote_view(src, (const void *)q.src_addr, slo, shi);
             hipEvent_t ev;
-            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, kOwnerEventFlags));
             else { ev = pool.back(); pool.pop_back(); }
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
@@ -420,7 +426,7 @@ static void progress_loop() {
             int64_t slo = 0, shi = 0;
             side_span_host(q.src_stride, q.count, q.levels, q.count[0], &slo, &shi);
             hipEvent_t ev;
-            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, kOwnerEventFlags));
             else { ev = pool.back(); pool.pop_back(); }
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
@@ -447,7 +453,7 @@ static void progress_loop() {
             // packed rows rb..re start at staging_off; rebase the packed side
             const char *packed0 = packed - (int64_t)rb * q.count[0];
             hipEvent_t ev;
-            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, kOwnerEventFlags));
             else { ev = pool.back(); pool.pop_back(); }
             {
                 std::lock_guard<std::mutex> g(r.launch_mu);
