@@ -353,10 +353,12 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
             drain_target(world);   // earlier packed chunks to world are posted first (inbox order)
             {
                 // the owner's kernel must see every write of ours to the source
-                // (and our IPC puts into world's memory): our streams drain first,
-                // behind a system-scope release each (the owner may sit on another GPU)
+                // (and our IPC puts into world's memory): our streams drain first --
+                // every kernel's end-of-kernel release (agent scope at least: the XCD
+                // L2s written back) has then put its bytes where another GPU's
+                // system-scope loads read them
                 std::lock_guard<std::mutex> g(r.launch_mu);
-                sched_publish_all();
+                sched_sync_all();
             }
             int cnt[8];
             for (int k = 0; k <= levels; ++k) cnt[k] = count[k];
@@ -819,10 +821,8 @@ int comex_fence_proc(int proc, comex_group_t group) {
     ensure_init();
     fence_target(translate_world(group, proc));
     {
-        // behind a system-scope release: what our kernels wrote is visible to a
-        // rank on another GPU that reads it after this fence
         std::lock_guard<std::mutex> g(rt().launch_mu);
-        sched_publish_all();
+        sched_sync_all();
     }
     one_pass_reap(true);   // our one-pass kernels are done: hand the owners' locks back
     return COMEX_SUCCESS;
@@ -836,7 +836,7 @@ int comex_fence_all(comex_group_t group) {
     for (int t = 0; t < r.size; ++t) fence_target(t);
     {
         std::lock_guard<std::mutex> g(r.launch_mu);
-        sched_publish_all();   // as comex_fence_proc (and so comex_barrier)
+        sched_sync_all();
     }
     one_pass_reap(true);
     return COMEX_SUCCESS;

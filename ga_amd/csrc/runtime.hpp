@@ -267,9 +267,6 @@ void sched_flag_fini();
 // unknown extent is Span{0, INT64_MAX}
 void sched_join_write(const Span &dst);
 void sched_sync_all();
-// sched_sync_all behind a system-scope release on every library stream: before a
-// request whose data another GPU reads in place (direct-source route)
-void sched_publish_all();
 // completion marks (user thread): sequence number of an op just enqueued on
 // stream s; whether op `seq` of stream s has completed (waiting for it if `wait`)
 uint64_t sched_track(int s);

@@ -156,12 +156,8 @@ void sched_resize(int n) {
     sched_init(n, pull);
 }
 
-static std::vector<hipEvent_t> g_pub_ev;   // sched_publish_all
-
 void sched_fini() {
     Runtime &r = rt();
-    for (hipEvent_t e : g_pub_ev) (void)hipEventDestroy(e);
-    g_pub_ev.clear();
     for (size_t i = 1; i < r.streams.size(); ++i) (void)hipStreamDestroy(r.streams[i]);
     for (hipEvent_t e : g_ev) (void)hipEventDestroy(e);
     g_ev.clear();
@@ -212,22 +208,6 @@ void sched_sync_all() {
     }
     g_hist.clear();
     g_base = -1;
-}
-
-// Before a request whose data another GPU's kernel reads in place (the direct-source
-// route: the owner reads our segment with system-scope loads): every library
-// stream's earlier writes released at system scope -- an event recorded with
-// hipEventReleaseToSystem on each stream -- and waited for.
-
-void sched_publish_all() {
-    Runtime &r = rt();
-    while (g_pub_ev.size() < r.streams.size()) {
-        hipEvent_t e;
-        GA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToSystem));
-        g_pub_ev.push_back(e);
-    }
-    for (size_t i = 0; i < r.streams.size(); ++i) GA_HIP(hipEventRecord(g_pub_ev[i], r.streams[i]));
-    sched_sync_all();
 }
 
 // ---- blocking-call completion through a flag -----------------
