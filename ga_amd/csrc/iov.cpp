@@ -221,15 +221,21 @@ static void scatter_runs(void *const *p, const char *in, int n, int bytes) {
 // Host-bound at GA scatter sizes (64 Ki pairs: ~85 us per list on one core with
 // baseline x86-64 code), so it is built for AVX-512 and AVX2 as well and the
 // loader picks the best the host has (GCC function multiversioning).
+// Also whether the range continues the progression a0 + i * step from global index
+// i0 (*seq_out, 0 or 1): a side that is one contiguous vector of runs in pair order
+// (GA's `v` of a scatter from one owner) needs no uploaded list at all.
 __attribute__((optimize("O3"), target_clones("avx512f", "avx2", "default")))
-static void translate_range(const uint64_t *in, int64_t delta, uint64_t *u, long n, uint64_t a0, uint64_t *or_out,
-                            uint64_t *xor_out, uint64_t *lo_out, uint64_t *hi_out) {
-    uint64_t ot = 0, lt = ~0ull, ht = 0, xt = 0;
+static void translate_range(const uint64_t *in, int64_t delta, uint64_t *u, long n, uint64_t a0, long i0,
+                            uint64_t step, uint64_t *or_out, uint64_t *xor_out, uint64_t *lo_out, uint64_t *hi_out,
+                            uint64_t *seq_out) {
+    uint64_t ot = 0, lt = ~0ull, ht = 0, xt = 0, off = 0;
+    const uint64_t e0 = a0 + (uint64_t)i0 * step;
     for (long i = 0; i < n; ++i) {
         const uint64_t a = in[i] + (uint64_t)delta;
         u[i] = a;
         ot |= a;
         xt |= a ^ a0;
+        off |= a ^ (e0 + (uint64_t)i * step);
         lt = a < lt ? a : lt;
         ht = a > ht ? a : ht;
     }
@@ -237,6 +243,7 @@ static void translate_range(const uint64_t *in, int64_t delta, uint64_t *u, long
     *xor_out = xt;
     *lo_out = lt;
     *hi_out = ht;
+    *seq_out = off == 0;
 }
 
 // io-vector pairs from this many up use the GPU-sorted run kernel (launch_iov_runs)
@@ -275,24 +282,28 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     // translate a list into the staging, taking its OR / min / max and the OR of every
     // address XOR the first one (per range, then combined)
     auto translate = [&](const uint64_t *in, int64_t delta, uint64_t *u, uint64_t *lo_out, uint64_t *hi_out,
-                         uint64_t *xor_out) {
+                         uint64_t *xor_out, bool *seq) {
         const int T = par_threads(n);
-        uint64_t o[8] = {0}, lo[8], hi[8] = {0}, xo[8] = {0};
+        uint64_t o[8] = {0}, lo[8], hi[8] = {0}, xo[8] = {0}, sq[8] = {0};
         for (int t = 0; t < 8; ++t) lo[t] = ~0ull;
         const uint64_t a0 = in[0] + (uint64_t)delta;
         par_for(n, T, [&](int t, long i0, long i1) {
-            translate_range(in + i0, delta, u + i0, i1 - i0, a0, &o[t], &xo[t], &lo[t], &hi[t]);
+            translate_range(in + i0, delta, u + i0, i1 - i0, a0, i0, (uint64_t)bytes, &o[t], &xo[t], &lo[t], &hi[t],
+                            &sq[t]);
         });
+        *seq = true;
         for (int t = 0; t < T; ++t) {
             align_or |= o[t];
             *xor_out |= xo[t];
             *lo_out = std::min(*lo_out, lo[t]);
             *hi_out = std::max(*hi_out, hi[t]);
+            *seq = *seq && sq[t];
         }
     };
     uint64_t sxor = 0;
+    bool src_seq = false, dst_seq = false;   // a side that is one contiguous vector in pair order
     if (src_listed) {
-        translate(src, sdelta, (uint64_t *)(up + o_src), &slo, &shi, &sxor);
+        translate(src, sdelta, (uint64_t *)(up + o_src), &slo, &shi, &sxor, &src_seq);
         shi += (uint64_t)bytes;
     } else if (gather_src) {
         // pageable sources gathered straight into the pinned staging, in pair order, on
@@ -303,7 +314,7 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         memcpy(up + o_src, host_src, (size_t)n * (size_t)bytes);
     }
     if (dst_listed) {
-        translate(dst, ddelta, (uint64_t *)(up + o_dst), &dlo, &dhi, &dxor);
+        translate(dst, ddelta, (uint64_t *)(up + o_dst), &dlo, &dhi, &dxor, &dst_seq);
         dhi += (uint64_t)bytes;
     }
     if (bounds && src_listed && dst_listed &&
@@ -341,6 +352,8 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         const uint64_t units = (dhi - dlo) / (uint64_t)bytes + 1;
         if (cross) {
             serial = true;
+        } else if (dst_seq) {
+            // one contiguous vector of destinations in pair order: none repeats or overlaps
         } else if (n >= kIovRunsMin && congruent && bytes <= kIovRunsMaxBytes && units <= (1ull << 32)) {
             runs = true;   // repeated destinations are ordered on the GPU
         } else {
@@ -354,9 +367,14 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     char *dev = iov_scratch(o_work + work);
     IovDesc d;
     memset(&d, 0, sizeof(d));
-    if (src_listed) d.src_list = (const uint64_t *)(dev + o_src);
+    // sources in one contiguous vector, pair i at src[0] + i * bytes: the kernels read
+    // them as a packed side at that device address and the list is not uploaded (half the
+    // upload of a scatter-accumulate of GA's `v` into one owner)
+    if (src_listed && src_seq) d.src_base = (const char *)(uintptr_t)src[0];
+    else if (src_listed) d.src_list = (const uint64_t *)(dev + o_src);
     else d.src_base = dev + o_src;
-    if (dst_listed) d.dst_list = (const uint64_t *)(dev + o_dst);
+    if (dst_listed && dst_seq) d.dst_base = (char *)(uintptr_t)dst[0];   // likewise, no list uploaded
+    else if (dst_listed) d.dst_list = (const uint64_t *)(dev + o_dst);
     else d.dst_base = dev + o_res;
     d.bytes = bytes;
     d.n = (uint32_t)n;
@@ -369,7 +387,9 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     // the upload: the copy kernel reading the mapped pinned buffer -- no DMA engine
     // round trip before the first io-vector kernel (64 Ki pairs 0.111-0.120 ms against
     // 0.122-0.130 with the runtime's copy, profiles/r03/s08)
-    upload_pinned(dev, up, o_res, r.streams[si]);
+    // the upload: [dst list | src list | packed sources], less a list not needed
+    const size_t up_lo = (dst_listed && dst_seq) ? o_src : 0, up_hi = (src_listed && src_seq) ? o_src : o_res;
+    if (up_hi > up_lo) upload_pinned(dev + up_lo, up + up_lo, up_hi - up_lo, r.streams[si]);
     const uint64_t units = runs ? (dhi - dlo) / (uint64_t)bytes + 1 : 0;
     int rc;
     if (runs) {

@@ -462,6 +462,43 @@ def test_accv_local(gpu_lib, oracle, op, nbytes, dups):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("layout,n", [("src_seq", 6000), ("src_seq", 700), ("dst_seq", 6000), ("both_seq", 6000),
+                                      ("chain", 3000), ("both_seq", 1)])
+def test_accv_contiguous_sides(gpu_lib, oracle, layout, n):
+    """A side that is one contiguous vector in pair order (pair i at base + i*bytes:
+    GA's `v` of a scatter into one owner) is read as a packed side and its list is
+    not uploaded; a contiguous destination side needs no repeat ordering. Same bits
+    as the reference's per-pair loop (comex.c:7327-7400): src_seq with random,
+    repeating destinations (6000 pairs: the GPU-ordered path), dst_seq with random
+    sources, both, and a chain inside one buffer (pair i's source is pair i-1's
+    destination: the in-order kernel must see each update)."""
+    op, nbytes, nslots = C.DBL, 16, 8000
+    rng = np.random.default_rng(31 + n + len(layout))
+    src = C.fill_bytes(op, nslots * nbytes, 41)
+    dst = C.fill_bytes(op, nslots * nbytes, 42)
+    sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
+    sb.upload(src)
+    db.upload(dst)
+    if layout == "chain":
+        so = [i * nbytes for i in range(n)]
+        do = [(i + 1) * nbytes for i in range(n)]
+        descs = [([db.ptr + a for a in so], [db.ptr + b for b in do], nbytes)]
+    else:
+        so = ([int(x) * nbytes for x in rng.integers(0, nslots, n)] if layout == "dst_seq" else
+              [(i + 7) * nbytes for i in range(n)])
+        do = ([int(x) * nbytes for x in rng.integers(0, 60, n)] if layout == "src_seq" else
+              [(i + 3) * nbytes for i in range(n)])
+        descs = [([sb.ptr + a for a in so], [db.ptr + b for b in do], nbytes)]
+    assert ga_amd.comex_accv(op, C.SCALE[op], descs, 0) == 0
+    ga_amd.comex_fence_all()
+    want = dst.copy()
+    if layout == "chain":
+        _oracle_acc_pairs(oracle, op, C.SCALE[op], want, want, list(zip(so, do)), nbytes)
+    else:
+        _oracle_acc_pairs(oracle, op, C.SCALE[op], src, want, list(zip(so, do)), nbytes)
+    assert np.array_equal(db.download(np.uint8, dst.size), want)
+
+
 @pytest.mark.parametrize("split", ["src", "dst", "both"])
 def test_accv_sides_in_two_allocations(gpu_lib, oracle, split):
     """A descriptor of >= 1024 pairs whose sources (or destinations) lie in two
