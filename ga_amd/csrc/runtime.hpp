@@ -262,6 +262,7 @@ void sched_join();
 // blocking-call completion with HBM operands: a flag kernel behind stream s's work,
 // the host spinning on it (caller does NOT hold launch_mu); sched_flag_fini at finalize
 void sched_wait_flag(int s);
+void sched_flag_init();   // the flag page (sched_init)
 void sched_flag_fini();
 // sched_join before a launch that writes `dst` (own_write_guard first); a span of
 // unknown extent is Span{0, INT64_MAX}
