@@ -74,7 +74,8 @@ struct IovHashArgs {
     uint64_t dlo;
     uint32_t shift;
     bool pow2;
-    const uint64_t *first, *last;
+    uint32_t epoch;
+    const uint32_t *dup;
     const uint32_t *slot;
     uint64_t *conf;
     uint32_t *count, *overflow;
@@ -115,9 +116,13 @@ __global__ __launch_bounds__(256) void k_iov_runs(const IovDesc d, const OP op) 
 // scatter they are rare, so:
 //   k_iovh_insert : every pair's unit key = (dst - dlo) / bytes goes into an
 //                   open-addressing table (tag = epoch:key, no clearing between
-//                   calls); per slot the first and the last pair index
-//                   (atomicMin / atomicMax of epoch-tagged indices)
-//   k_iovh_apply  : a pair whose slot has first == last is its destination's
+//                   calls); the lane whose compare-and-swap claims a slot is its
+//                   key's first pair, any other lane that finds the key there marks
+//                   the slot repeated (dup[slot] = epoch) -- one load and one CAS for
+//                   a destination that does not repeat (round 5; an atomicMin and an
+//                   atomicMax of epoch-tagged pair indices on every pair before: the
+//                   insert of 16 Ki pairs took 13.7 us, profiles/r05/ivt)
+//   k_iovh_apply  : a pair whose slot is not marked repeated is its destination's
 //                   only pair: applied at once; the others are appended to a
 //                   conflict list as key:index
 //   k_iovh_conf   : one workgroup sorts the conflict list in LDS (bitonic, by
@@ -131,7 +136,7 @@ constexpr uint32_t kIovhCap = 8192;          // conflict entries sorted in LDS (
 constexpr uint32_t kIovhMaxPairs = 1u << 19;  // above: the radix path (1 Mi random pairs overflow the LDS list)
 
 struct IovHash {
-    char *mem = nullptr;          // keys | first | last (P each), slot (n), conflicts (cap), count
+    char *mem = nullptr;          // keys (8 B x P) | dup (4 B x P) | slot (n) | conflicts (cap) | count
     size_t bytes = 0;
     uint32_t P = 0;               // table slots (power of two >= 2n)
     uint32_t npairs = 0;          // capacity of the slot array
@@ -144,14 +149,17 @@ struct IovHash {
 
 IovHash *iov_hash_create() { return new IovHash(); }
 
+// where the slot array starts in IovHash::mem (after the keys and the dup marks)
+static size_t iovh_off_slot(uint32_t P) { return ((size_t)P * 12 + 255) & ~(size_t)255; }
+
 static __device__ __forceinline__ uint32_t iovh_slot0(uint32_t key, uint32_t mask) {
     return (key * 0x9E3779B1u) & mask;
 }
 
 __global__ __launch_bounds__(256) void k_iovh_insert(const uint64_t *dst_list, uint64_t dlo, uint32_t bytes,
                                                      uint32_t shift, bool pow2, uint32_t n, uint64_t *keys,
-                                                     uint64_t *first, uint64_t *last, uint32_t mask, uint32_t epoch,
-                                                     uint32_t *slot, uint32_t *count) {
+                                                     uint32_t *dup, uint32_t mask, uint32_t epoch, uint32_t *slot,
+                                                     uint32_t *count) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i == 0) *count = 0;   // the conflict list of this call (k_iovh_apply runs after this kernel)
     if (i >= n) return;
@@ -159,20 +167,26 @@ __global__ __launch_bounds__(256) void k_iovh_insert(const uint64_t *dst_list, u
     const uint32_t key = (uint32_t)(pow2 ? (off >> shift) : off / bytes);
     const uint64_t tag = ((uint64_t)epoch << 32) | key;
     uint32_t h = iovh_slot0(key, mask);
+    bool repeated = false;
     for (;;) {
         const uint64_t cur = __hip_atomic_load(keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == tag) break;
+        if (cur == tag) {                        // another pair of this call holds the key
+            repeated = true;
+            break;
+        }
         if ((uint32_t)(cur >> 32) != epoch) {   // empty this call (an earlier call's tag): claim it
             const uint64_t old = atomicCAS((unsigned long long *)(keys + h), cur, tag);
-            if (old == cur || old == tag) break;
+            if (old == cur) break;               // claimed: the first pair of this key
+            if (old == tag) {                    // claimed by another pair of the same key meanwhile
+                repeated = true;
+                break;
+            }
             if ((uint32_t)(old >> 32) != epoch) continue;   // another stale value: try again here
         }
         h = (h + 1) & mask;                      // a different key of this call: probe on
     }
     slot[i] = h;
-    // first: min over (~epoch : i) -- this call's entries sort below every older one
-    atomicMin((unsigned long long *)(first + h), ((uint64_t)(~epoch) << 32) | i);
-    atomicMax((unsigned long long *)(last + h), ((uint64_t)epoch << 32) | i);
+    if (repeated) __hip_atomic_store(dup + h, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <class OP, int W, bool SYS>
@@ -188,12 +202,12 @@ __device__ __forceinline__ void iov_apply_pair(const IovDesc &d, const OP &op, u
 
 template <class OP, int W, bool SYS>
 __global__ __launch_bounds__(256) void k_iovh_apply(const IovDesc d, const OP op, uint64_t dlo, uint32_t shift,
-                                                    bool pow2, const uint64_t *first, const uint64_t *last,
+                                                    bool pow2, uint32_t epoch, const uint32_t *dup,
                                                     const uint32_t *slot, uint64_t *conf, uint32_t *count) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= d.n) return;
     const uint32_t h = slot[i];
-    if ((uint32_t)first[h] == (uint32_t)last[h]) {
+    if (dup[h] != epoch) {
         iov_apply_pair<OP, W, SYS>(d, op, i);
         return;
     }
@@ -240,15 +254,15 @@ __global__ __launch_bounds__(1024) void k_iovh_conf(const IovDesc d, const OP op
     }
 }
 
-// the fallback's keys: pairs k_iovh_apply already applied (their slot's first ==
-// last) get the sentinel key, sorted last and skipped by k_iov_runs
+// the fallback's keys: pairs k_iovh_apply already applied (their slot not marked
+// repeated) get the sentinel key, sorted last and skipped by k_iov_runs
 __global__ __launch_bounds__(256) void k_iov_keys_masked(const uint64_t *dst_list, uint64_t dlo, uint32_t bytes,
-                                                         uint32_t n, const uint64_t *first, const uint64_t *last,
+                                                         uint32_t n, uint32_t epoch, const uint32_t *dup,
                                                          const uint32_t *slot, uint32_t *keys, uint32_t *vals) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
     const uint32_t h = slot[i];
-    keys[i] = ((uint32_t)first[h] == (uint32_t)last[h]) ? kIovRunSkip : (uint32_t)((dst_list[i] - dlo) / bytes);
+    keys[i] = (dup[h] != epoch) ? kIovRunSkip : (uint32_t)((dst_list[i] - dlo) / bytes);
     vals[i] = i;
 }
 
@@ -256,7 +270,7 @@ template <class OP, int W, bool SYS>
 static hipError_t iov_ws(const IovDesc &d, const OP &op, bool serial, hipStream_t st, const IovHashArgs *ha) {
     if (ha) {
         hipLaunchKernelGGL((k_iovh_apply<OP, W, SYS>), dim3((d.n + 255u) / 256u), dim3(256), 0, st, d, op, ha->dlo,
-                           ha->shift, ha->pow2, ha->first, ha->last, ha->slot, ha->conf, ha->count);
+                           ha->shift, ha->pow2, ha->epoch, ha->dup, ha->slot, ha->conf, ha->count);
         hipLaunchKernelGGL((k_iovh_conf<OP, W, SYS>), dim3(1), dim3(1024), 0, st, d, op, ha->conf, ha->count,
                            ha->overflow);
     } else if (d.run_key) {
@@ -489,10 +503,10 @@ int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uin
         // the pairs the hashed launch applied already sort last (sentinel key)
         if (mask->n != d.n || mask->dlo != dlo || units >= (uint64_t)kIovRunSkip) return -9;
         const uint64_t P = mask->P;
-        const uint64_t *first = (const uint64_t *)(mask->mem + P * 8), *last = (const uint64_t *)(mask->mem + 2 * P * 8);
-        const uint32_t *slot = (const uint32_t *)(mask->mem + 3 * P * 8);
+        const uint32_t *dup = (const uint32_t *)(mask->mem + P * 8);
+        const uint32_t *slot = (const uint32_t *)(mask->mem + iovh_off_slot((uint32_t)P));
         hipLaunchKernelGGL(k_iov_keys_masked, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, d.dst_list, dlo,
-                           (uint32_t)d.bytes, d.n, first, last, slot, kin, vin);
+                           (uint32_t)d.bytes, d.n, mask->epoch, dup, slot, kin, vin);
         end_bit = 32;
     } else {
         hipLaunchKernelGGL(k_iov_keys, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, d.dst_list, dlo,
@@ -533,8 +547,7 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
     // earlier launch that used it
     uint32_t P = 1024;
     while (P < 2 * d.n) P <<= 1;
-    auto off_slot = [](uint32_t P_) { return (size_t)P_ * 24; };
-    auto off_conf = [&](uint32_t P_, uint32_t np) { return align256(off_slot(P_) + (size_t)np * 4); };
+    auto off_conf = [&](uint32_t P_, uint32_t np) { return align256(iovh_off_slot(P_) + (size_t)np * 4); };
     if (P > h->P || d.n > h->npairs) {
         const uint32_t nP = std::max(P, h->P), np = std::max(d.n, h->npairs);
         if (h->mem) {
@@ -544,9 +557,7 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
         h->bytes = off_conf(nP, np) + (size_t)kIovhCap * 8 + 256;
         hipError_t e = hipMalloc((void **)&h->mem, h->bytes);
         if (e != hipSuccess) return -100 - (int)e;
-        e = hipMemsetAsync(h->mem, 0, (size_t)nP * 8, stream);                       // keys: epoch 0
-        if (e == hipSuccess) e = hipMemsetAsync(h->mem + (size_t)nP * 8, 0xff, (size_t)nP * 8, stream);   // first
-        if (e == hipSuccess) e = hipMemsetAsync(h->mem + (size_t)nP * 16, 0, (size_t)nP * 8, stream);     // last
+        e = hipMemsetAsync(h->mem, 0, (size_t)nP * 12, stream);   // keys and dup marks: epoch 0
         if (e != hipSuccess) return -100 - (int)e;
         h->P = nP;
         h->npairs = np;
@@ -558,24 +569,23 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
         if (e != hipSuccess) return -100 - (int)e;
     }
     if (++h->epoch == 0) {   // 2^32 calls: start the tags over
-        hipError_t e = hipMemsetAsync(h->mem, 0, (size_t)h->P * 8, stream);
-        if (e == hipSuccess) e = hipMemsetAsync(h->mem + (size_t)h->P * 8, 0xff, (size_t)h->P * 8, stream);
-        if (e == hipSuccess) e = hipMemsetAsync(h->mem + (size_t)h->P * 16, 0, (size_t)h->P * 8, stream);
+        hipError_t e = hipMemsetAsync(h->mem, 0, (size_t)h->P * 12, stream);
         if (e != hipSuccess) return -100 - (int)e;
         h->epoch = 1;
     }
     *(volatile uint32_t *)h->flag_host = 0;
     const bool pow2 = (d.bytes & (d.bytes - 1)) == 0;
     const uint32_t shift = pow2 ? (uint32_t)__builtin_ctz((unsigned)d.bytes) : 0;
-    uint64_t *keys = (uint64_t *)h->mem, *first = keys + h->P, *last = first + h->P;
-    uint32_t *slot = (uint32_t *)(h->mem + off_slot(h->P));
+    uint64_t *keys = (uint64_t *)h->mem;
+    uint32_t *dup = (uint32_t *)(keys + h->P);
+    uint32_t *slot = (uint32_t *)(h->mem + iovh_off_slot(h->P));
     uint64_t *conf = (uint64_t *)(h->mem + off_conf(h->P, h->npairs));
     uint32_t *count = (uint32_t *)(conf + kIovhCap);
     hipLaunchKernelGGL(k_iovh_insert, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, d.dst_list, dlo,
-                       (uint32_t)d.bytes, shift, pow2, d.n, keys, first, last, h->P - 1, h->epoch, slot, count);
+                       (uint32_t)d.bytes, shift, pow2, d.n, keys, dup, h->P - 1, h->epoch, slot, count);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return -100 - (int)e;
-    IovHashArgs ha{dlo, shift, pow2, first, last, slot, conf, count, h->flag_dev};
+    IovHashArgs ha{dlo, shift, pow2, h->epoch, dup, slot, conf, count, h->flag_dev};
     h->dlo = dlo;
     h->n = d.n;
     h->shift = shift;
