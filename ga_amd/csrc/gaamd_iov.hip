@@ -156,14 +156,26 @@ static __device__ __forceinline__ uint32_t iovh_slot0(uint32_t key, uint32_t mas
     return (key * 0x9E3779B1u) & mask;
 }
 
-__global__ __launch_bounds__(256) void k_iovh_insert(const uint64_t *dst_list, uint64_t dlo, uint32_t bytes,
+// dst_in / src_in (optional): the address lists still in the caller's mapped pinned
+// buffer -- read here over PCIe and written to dst_list / src_out in HBM for the kernels
+// after this one, which saves the separate upload launch (7-16 us, profiles/r05/ivt)
+__global__ __launch_bounds__(256) void k_iovh_insert(uint64_t *dst_list, uint64_t dlo, uint32_t bytes,
                                                      uint32_t shift, bool pow2, uint32_t n, uint64_t *keys,
                                                      uint32_t *dup, uint32_t mask, uint32_t epoch, uint32_t *slot,
-                                                     uint32_t *count) {
+                                                     uint32_t *count, const uint64_t *dst_in, const uint64_t *src_in,
+                                                     uint64_t *src_out) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i == 0) *count = 0;   // the conflict list of this call (k_iovh_apply runs after this kernel)
     if (i >= n) return;
-    const uint64_t off = dst_list[i] - dlo;
+    if (src_in) src_out[i] = src_in[i];
+    uint64_t a;
+    if (dst_in) {
+        a = dst_in[i];
+        dst_list[i] = a;
+    } else {
+        a = dst_list[i];
+    }
+    const uint64_t off = a - dlo;
     const uint32_t key = (uint32_t)(pow2 ? (off >> shift) : off / bytes);
     const uint64_t tag = ((uint64_t)epoch << 32) | key;
     uint32_t h = iovh_slot0(key, mask);
@@ -524,7 +536,8 @@ int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uin
 }
 
 int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo,
-                      uint64_t units, hipStream_t stream, bool src_peer) {
+                      uint64_t units, hipStream_t stream, bool src_peer, const uint64_t *dst_in,
+                      const uint64_t *src_in) {
     const int esz = elem_size(op);
     if (!esz || d.bytes <= 0 || d.bytes > kIovRunsMaxBytes || !d.dst_list) return -4;
     if (op != kOpCopy && !scale) return -5;
@@ -581,8 +594,10 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
     uint32_t *slot = (uint32_t *)(h->mem + iovh_off_slot(h->P));
     uint64_t *conf = (uint64_t *)(h->mem + off_conf(h->P, h->npairs));
     uint32_t *count = (uint32_t *)(conf + kIovhCap);
-    hipLaunchKernelGGL(k_iovh_insert, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, d.dst_list, dlo,
-                       (uint32_t)d.bytes, shift, pow2, d.n, keys, dup, h->P - 1, h->epoch, slot, count);
+    if (src_in && !d.src_list) return -4;
+    hipLaunchKernelGGL(k_iovh_insert, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, (uint64_t *)d.dst_list, dlo,
+                       (uint32_t)d.bytes, shift, pow2, d.n, keys, dup, h->P - 1, h->epoch, slot, count, dst_in, src_in,
+                       (uint64_t *)d.src_list);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return -100 - (int)e;
     IovHashArgs ha{dlo, shift, pow2, h->epoch, dup, slot, conf, count, h->flag_dev};

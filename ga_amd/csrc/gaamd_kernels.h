@@ -169,9 +169,13 @@ int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uin
 // launch, iov_hash_overflowed(h) true means more conflicting pairs than the LDS
 // holds: none of those was applied -- run launch_iov_runs(..., mask = h) next.
 // The caller serialises its launches on one IovHash (the table is reused).
+// dst_in / src_in (optional, device-mapped pinned memory): the lists not yet in HBM --
+// the first kernel copies them to d.dst_list / d.src_list on its way (no upload launch);
+// when this returns 1 nothing was launched and the caller uploads them itself.
 IovHash *iov_hash_create();
 int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo,
-                      uint64_t units, hipStream_t stream, bool src_peer = false);
+                      uint64_t units, hipStream_t stream, bool src_peer = false, const uint64_t *dst_in = nullptr,
+                      const uint64_t *src_in = nullptr);
 bool iov_hash_overflowed(const IovHash *h);
 
 }  // namespace gaamd

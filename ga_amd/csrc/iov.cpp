@@ -387,9 +387,15 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     // the upload: the copy kernel reading the mapped pinned buffer -- no DMA engine
     // round trip before the first io-vector kernel (64 Ki pairs 0.111-0.120 ms against
     // 0.122-0.130 with the runtime's copy, profiles/r03/s08)
-    // the upload: [dst list | src list | packed sources], less a list not needed
+    // the upload: [dst list | src list | packed sources], less a list not needed; on the
+    // GPU-ordered path the hashed insert copies the lists itself (one launch less), so only
+    // packed sources go up here -- and everything, should that path decline (rc 1 below)
     const size_t up_lo = (dst_listed && dst_seq) ? o_src : 0, up_hi = (src_listed && src_seq) ? o_src : o_res;
-    if (up_hi > up_lo) upload_pinned(dev + up_lo, up + up_lo, up_hi - up_lo, r.streams[si]);
+    if (runs) {
+        if (!src_listed && o_res > o_src) upload_pinned(dev + o_src, up + o_src, o_res - o_src, r.streams[si]);
+    } else if (up_hi > up_lo) {
+        upload_pinned(dev + up_lo, up + up_lo, up_hi - up_lo, r.streams[si]);
+    }
     const uint64_t units = runs ? (dhi - dlo) / (uint64_t)bytes + 1 : 0;
     int rc;
     if (runs) {
@@ -399,7 +405,11 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         rc = 1;
         {
             if (!g_hash) g_hash = iov_hash_create();
-            rc = launch_iov_hashed(g_hash, cop, scale, d, align_or, dlo, units, r.streams[si], src_peer);
+            char *up_dev = nullptr;   // the device view of the pinned upload buffer
+            GA_HIP(hipHostGetDevicePointer((void **)&up_dev, up, 0));
+            rc = launch_iov_hashed(g_hash, cop, scale, d, align_or, dlo, units, r.streams[si], src_peer,
+                                   (const uint64_t *)(up_dev + o_dst),
+                                   d.src_list ? (const uint64_t *)(up_dev + o_src) : nullptr);
             if (rc == 0) {
                 // more repeated destinations than the hashed launch orders in LDS: after
                 // it completed, the radix path applies the pairs it left (the rest masked)
@@ -412,6 +422,7 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
             }
         }
         if (rc == 1) {
+            if (up_hi > up_lo) upload_pinned(dev + up_lo, up + up_lo, up_hi - up_lo, r.streams[si]);
             g_iov_path[2].fetch_add(1, std::memory_order_relaxed);
             rc = launch_iov_runs(cop, scale, d, align_or, dlo, units, dev + o_work, work, r.streams[si], src_peer);
         }

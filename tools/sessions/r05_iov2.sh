@@ -1,7 +1,7 @@
 # round-5: hashed io-vector insert with claim + dup mark -- io-vector tests, kernel trace
 # of 16 Ki / 64 Ki calls, whole-call rates
 set -o pipefail
-out=gpurun_out/r05iov2
+out=gpurun_out/${R05_TAG:-r05iov2}
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_semantics.py -m gpu -v --timeout 170 --timeout-method thread -p no:cacheprovider -k "accv or putv or getv or vector or iov" > $out/tests_local.log 2>&1 || { tail -30 $out/tests_local.log; exit 11; }
