@@ -15,5 +15,7 @@ for i in 1 2 3; do
 done
 bash tools/evidence.sh r05
 cp -r gpurun_out/evidence $out/
+timeout -k 10 300 python3 bench.py --workload C5 --no-cpu > $out/bench_C5_n1.json 2> $out/bench_C5_n1.err
+python3 -c "import json;d=json.load(open('$out/bench_C5_n1.json'));print('C5 N=1', d['value'], d['hbm_peak_frac'], d['roofline']['frac'])"
 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29543 bench.py --gpus 2 --steps 20 --warmup 5 > $out/bench_n2.json 2> $out/bench_n2.err
 python3 -c "import json;d=json.load(open('$out/bench_n2.json'));c=d['c5'];print('N2', d['value'], {k:v['result'] for k,v in c['exchange_precheck'].items()}, {k:v['result'] for k,v in c['exchange_check'].items()})"
