@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <chrono>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -30,6 +31,16 @@ std::atomic<unsigned long long> g_iov_path[3];
 
 static char *g_iov_host = nullptr;
 static size_t g_iov_host_bytes = 0;
+
+// COMEX_AMD_DEBUG >= 3: the host phases of each io-vector call on stderr (time since
+// the previous phase mark; "start" resets)
+static void phase(const char *what) {
+    if (rt().debug < 3) return;
+    static thread_local double last = 0;
+    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    if (strcmp(what, "start")) trace(3, "iov %-12s %8.1f us", what, (t - last) * 1e6);
+    last = t;
+}
 
 static char *iov_host_scratch(size_t bytes) {   // pinned upload staging; caller holds launch_mu
     if (bytes <= g_iov_host_bytes) return g_iov_host;
@@ -278,6 +289,7 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     std::unique_lock<std::mutex> g(r.launch_mu);
     sched_sync_all();   // the previous io-vector kernel and its upload are done with both scratches
     char *up = iov_host_scratch(o_res);
+    phase("drain");
     uint64_t align_or = 0, slo = ~0ull, shi = 0, dlo = ~0ull, dhi = 0, dxor = 0;
     // translate a list into the staging, taking its OR / min / max and the OR of every
     // address XOR the first one (per range, then combined)
@@ -313,10 +325,12 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     } else {
         memcpy(up + o_src, host_src, (size_t)n * (size_t)bytes);
     }
+    phase("src side");
     if (dst_listed) {
         translate(dst, ddelta, (uint64_t *)(up + o_dst), &dlo, &dhi, &dxor, &dst_seq);
         dhi += (uint64_t)bytes;
     }
+    phase("dst side");
     if (bounds && src_listed && dst_listed &&
         (slo - (uint64_t)sdelta < bounds[0] || shi - (uint64_t)sdelta > bounds[1] ||
          dlo - (uint64_t)ddelta < bounds[2] || dhi - (uint64_t)ddelta > bounds[3]))
@@ -362,6 +376,7 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
             serial = ranges_overlap(dr);
         }
     }
+    phase("classify");
     const size_t o_work = (o_res + (dst_listed ? 0 : pk) + 255) & ~(size_t)255;   // sort work: 256-aligned
     const size_t work = runs ? iov_runs_work_bytes((uint32_t)n) : 0;
     char *dev = iov_scratch(o_work + work);
@@ -430,9 +445,12 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         rc = launch_iov(cop, scale, d, align_or, serial, r.streams[si], src_peer);
     }
     if (rc) fatal("io-vector launch failed (%d): misaligned elements?", rc);
+    phase("launch");
     if (!dst_listed) {
         GA_HIP(hipStreamSynchronize(r.streams[si]));
+        phase("kernels");
         GA_HIP(hipMemcpy(host_dst, dev + o_res, (size_t)n * (size_t)bytes, hipMemcpyDeviceToHost));
+        phase("results down");
     }
     // completion (blocking call) or the handle (non-blocking) is taken by xfer_vec
     return true;
@@ -441,6 +459,7 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
 int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int proc, int group,
              comex_request_t *hdl) {
     ensure_init();
+    phase("start");
     Runtime &r = rt();
     const int world = translate_world(group, proc);
     const int cop = (kind == X_ACC) ? op : kOpCopy;
@@ -542,6 +561,7 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
             int64_t sdel = 0, ddel = 0;
             const bool sdev = vc.span(smin, smax + (uint64_t)bytes, &sdel);
             const bool ddev = vc.span(dmin, dmax + (uint64_t)bytes, &ddel);
+            phase("spans");
             if (sdev && ddev) {
                 iov_local(cop, scale, rs, rd, bytes, n, nullptr, nullptr, sdel, ddel);
                 continue;
@@ -558,6 +578,7 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
                 if (g_hpack.size() < (size_t)n * (size_t)bytes) g_hpack.resize((size_t)n * (size_t)bytes);
                 iov_local(cop, scale, rs, nullptr, bytes, n, nullptr, g_hpack.data(), sdel, 0);
                 scatter_runs(darr[k].dst, g_hpack.data(), n, bytes);
+                phase("host scatter");
                 continue;
             }
         }
@@ -722,6 +743,7 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
         if (hdl) sched_join();
         else if (blocking) sched_sync_all();
     }
+    phase("complete");
     if (world != r.rank && r.same_node(world) && kind != X_ACC && !blocking && !r.direct_pending.empty())
         r.direct_pending[world] = 1;
     if (hdl) nb_complete_now(hdl, 0, true);
