@@ -1147,6 +1147,10 @@ int gaamd_diag(const char *key, long long value, unsigned long long *out, int no
         g_diag_stale_granule.store(value);
         return 0;
     }
+    if (!strcmp(key, "iov_host_sides")) {   // io-vector sides found wholly in pageable host memory
+        if (out && nout >= 1) out[0] = g_iov_host_sides.load(std::memory_order_relaxed);
+        return 0;
+    }
     return -1;
 }
 

@@ -160,6 +160,7 @@ extern std::atomic<unsigned long long> g_one_pass;
 int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int proc, int group, comex_request_t *hdl);
 void iov_finalize();
 extern std::atomic<unsigned long long> g_iov_path[3];   // gaamd_iov_path_counts
+extern std::atomic<unsigned long long> g_iov_host_sides;   // gaamd_diag("iov_host_sides")
 
 // ---- comex.cpp ----------------------------------------------------------------
 // handle of an op just enqueued on library stream `stream_idx` (`on_stream`), or of

@@ -171,34 +171,47 @@ template <class F> static void par_for(long n, int T, F fn) {
     for (std::thread &x : th) x.join();
 }
 
-// Is every byte of [lo, hi) ordinary CPU memory of this process (one readable,
-// and if `write` writable, mapping that is not a device file)?  One lookup in
+// Is every byte of [lo, hi) ordinary CPU memory of this process (readable, and if
+// `write` writable, mappings that are not device files)?  One pass over
 // /proc/self/maps replaces a device-view query per page when a whole io-vector
 // side lies in pageable host memory (GA's MA buffer `v` of a scatter/gather):
 // device allocations are either PROT_NONE reservations or /dev/dri mappings, so
-// a side that passes is safe to gather/scatter on the host.  Any address not
-// covered (or a line that does not parse) answers false and the per-pair
-// classification decides as before.
+// a side that passes is safe to gather/scatter on the host.  The range may run
+// over several adjacent mappings: one buffer is often split into a few VMAs with
+// different flags (numpy advises transparent huge pages on the 2 MiB-aligned part
+// of an array from 4 MiB up), and a 1 Mi-element scatter whose `v` failed this test
+// fell back to the per-page query, 10 ms instead of 1.5 (profiles/r05/scatter).
+// Any gap, any address not covered (or a line that does not parse) answers false
+// and the per-pair classification decides as before.
+std::atomic<unsigned long long> g_iov_host_sides{0};
 static bool host_cpu_range(uint64_t lo, uint64_t hi, bool write) {
     if (hi <= lo) return false;
     FILE *f = fopen("/proc/self/maps", "r");
     if (!f) return false;
     char line[512];
     bool ok = false;
+    uint64_t need = lo;   // the first byte not yet covered
     while (fgets(line, sizeof(line), f)) {
         const bool whole = strchr(line, '\n') != nullptr;
         unsigned long long a = 0, b = 0;
         char perms[8] = {0};
         int path_at = 0;
         if (sscanf(line, "%llx-%llx %7s %*s %*s %*s %n", &a, &b, perms, &path_at) < 3) break;
-        if (lo >= a && lo < b) {
+        if (need >= a && need < b) {
             const char *path = path_at > 0 ? line + path_at : "";
-            ok = hi <= b && perms[0] == 'r' && (!write || perms[1] == 'w') && strncmp(path, "/dev/", 5) != 0;
-            break;
+            if (perms[0] != 'r' || (write && perms[1] != 'w') || strncmp(path, "/dev/", 5) == 0) break;
+            if (hi <= b) {
+                ok = true;
+                break;
+            }
+            need = b;   // the rest must start exactly where this mapping ends
+        } else if (need != lo && a > need) {
+            break;      // a hole after the first part
         }
         while (!whole && fgets(line, sizeof(line), f) && !strchr(line, '\n')) {}   // rest of a long line
     }
     fclose(f);
+    if (ok) g_iov_host_sides.fetch_add(1, std::memory_order_relaxed);
     return ok;
 }
 
@@ -569,11 +582,13 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
             // one side wholly in pageable host memory (GA's `v`): packed on the host in
             // pair order, as the per-pair classification below would, without it
             if (n >= kIovMapsMin && ddev && !sdev && host_cpu_range(smin, smax + (uint64_t)bytes, false)) {
+                phase("host side");
                 iov_local(cop, scale, nullptr, rd, bytes, n, nullptr, nullptr, 0, ddel, darr[k].src);
                 continue;
             }
             if (n >= kIovMapsMin && sdev && !ddev && cop == kOpCopy &&
                 host_cpu_range(dmin, dmax + (uint64_t)bytes, true)) {
+                phase("host side");
                 static std::vector<char> g_hpack;
                 if (g_hpack.size() < (size_t)n * (size_t)bytes) g_hpack.resize((size_t)n * (size_t)bytes);
                 iov_local(cop, scale, rs, nullptr, bytes, n, nullptr, g_hpack.data(), sdel, 0);
@@ -594,10 +609,12 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
                 smax = rs[i] > smax ? rs[i] : smax;
             }
             if (host_cpu_range(smin, smax + (uint64_t)bytes, false)) {
+                phase("host side");
                 src_host = classified = true;
                 memcpy(dv, darr[k].dst, (size_t)n * 8);   // owner addresses, checked per chunk below
             }
         }
+        phase("fast paths");
         for (int i = 0; i < n && !host_bounce && !classified; ++i) {
             void *sp = darr[k].src[i], *dp = darr[k].dst[i];
             uint64_t v = 0;
@@ -623,6 +640,7 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
                 host_bounce = true;
             }
         }
+        phase("per pair");
         // packed host side: sources of an accumulate/put (local or same-node put), or the
         // results of a copy (get/put into host memory); an accumulate into host memory
         // needs the old values and stays per pair

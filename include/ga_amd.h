@@ -180,7 +180,9 @@ const char *gaamd_hip_runtime(void);
  *   "stale_granule" G >= 0 (with stale_gen): instead, each owner writes a foreign
  *                   tag into granule G (G * 2 MiB bytes in) of its N-th allocation
  *                   on the first exchange, and the peers' check must find it
- *                   (-1: off). */
+ *                   (-1: off).
+ *   "iov_host_sides" out[0] (nout >= 1): io-vector sides found wholly in pageable
+ *                   host memory by one /proc/self/maps pass (value ignored). */
 int gaamd_diag(const char *key, long long value, unsigned long long *out, int nout);
 
 #if defined(__cplusplus)
