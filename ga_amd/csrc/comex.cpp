@@ -1147,6 +1147,11 @@ int gaamd_diag(const char *key, long long value, unsigned long long *out, int no
         g_diag_stale_granule.store(value);
         return 0;
     }
+    if (!strcmp(key, "host_range")) {   // out[0], out[1] in: [lo, hi); value: 1 = writable; out[0] out: 1/0
+        if (!out || nout < 2) return -1;
+        out[0] = host_cpu_range_probe(out[0], out[1], value != 0) ? 1 : 0;
+        return 0;
+    }
     if (!strcmp(key, "iov_host_sides")) {   // io-vector sides found wholly in pageable host memory
         if (out && nout >= 1) out[0] = g_iov_host_sides.load(std::memory_order_relaxed);
         return 0;

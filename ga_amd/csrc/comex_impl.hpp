@@ -161,6 +161,7 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
 void iov_finalize();
 extern std::atomic<unsigned long long> g_iov_path[3];   // gaamd_iov_path_counts
 extern std::atomic<unsigned long long> g_iov_host_sides;   // gaamd_diag("iov_host_sides")
+bool host_cpu_range_probe(uint64_t lo, uint64_t hi, bool write);   // gaamd_diag("host_range")
 
 // ---- comex.cpp ----------------------------------------------------------------
 // handle of an op just enqueued on library stream `stream_idx` (`on_stream`), or of

@@ -184,6 +184,7 @@ template <class F> static void par_for(long n, int T, F fn) {
 // Any gap, any address not covered (or a line that does not parse) answers false
 // and the per-pair classification decides as before.
 std::atomic<unsigned long long> g_iov_host_sides{0};
+
 static bool host_cpu_range(uint64_t lo, uint64_t hi, bool write) {
     if (hi <= lo) return false;
     FILE *f = fopen("/proc/self/maps", "r");
@@ -205,8 +206,8 @@ static bool host_cpu_range(uint64_t lo, uint64_t hi, bool write) {
                 break;
             }
             need = b;   // the rest must start exactly where this mapping ends
-        } else if (need != lo && a > need) {
-            break;      // a hole after the first part
+        } else if (a > need) {
+            break;      // a hole: lo not mapped, or a gap after the first part
         }
         while (!whole && fgets(line, sizeof(line), f) && !strchr(line, '\n')) {}   // rest of a long line
     }
@@ -214,6 +215,9 @@ static bool host_cpu_range(uint64_t lo, uint64_t hi, bool write) {
     if (ok) g_iov_host_sides.fetch_add(1, std::memory_order_relaxed);
     return ok;
 }
+
+// gaamd_diag("host_range"): the test hook of host_cpu_range
+bool host_cpu_range_probe(uint64_t lo, uint64_t hi, bool write) { return host_cpu_range(lo, hi, write); }
 
 // host-side packing of pageable io-vector runs, in pair order (fixed-size copies
 // for the element sizes GA scatters, so the compiler emits plain loads/stores)

@@ -182,7 +182,11 @@ const char *gaamd_hip_runtime(void);
  *                   on the first exchange, and the peers' check must find it
  *                   (-1: off).
  *   "iov_host_sides" out[0] (nout >= 1): io-vector sides found wholly in pageable
- *                   host memory by one /proc/self/maps pass (value ignored). */
+ *                   host memory by one /proc/self/maps pass (value ignored).
+ *   "host_range"    that pass on its own: out[0], out[1] (nout >= 2) hold [lo, hi) on
+ *                   entry, value 1 asks for writable memory; out[0] is 1 when every
+ *                   byte lies in readable (writable) mappings that are not device
+ *                   files, else 0.  Needs no GPU. */
 int gaamd_diag(const char *key, long long value, unsigned long long *out, int nout);
 
 #if defined(__cplusplus)

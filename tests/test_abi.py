@@ -163,6 +163,87 @@ def test_library_check_contiguous_matches_oracle(oracle):
         assert got == oracle.check_contiguous(ss, ds, count, n), (ss, ds, count)
 
 
+def _maps():
+    """/proc/self/maps as (lo, hi, perms, path) tuples"""
+    out = []
+    with open("/proc/self/maps") as f:
+        for line in f:
+            parts = line.split(None, 5)
+            lo, hi = (int(x, 16) for x in parts[0].split("-"))
+            out.append((lo, hi, parts[1], parts[5].strip() if len(parts) > 5 else ""))
+    return out
+
+
+def _host_range_want(lo, hi, write):
+    """every byte of [lo, hi) in readable (writable) mappings that are not device files"""
+    if hi <= lo:
+        return False
+    need = lo
+    for a, b, perms, path in _maps():
+        if a <= need < b:
+            if perms[0] != "r" or (write and perms[1] != "w") or path.startswith("/dev/"):
+                return False
+            if hi <= b:
+                return True
+            need = b
+        elif a > need:
+            return False
+    return False
+
+
+def test_host_range_check_over_mappings():
+    """The io-vector path's one-pass test of a pageable host side (iov.cpp
+    host_cpu_range, through gaamd_diag("host_range"); host code, no GPU): a range over
+    several adjacent mappings passes, any hole, device-file mapping, PROT_NONE or
+    read-only range (when writing) fails -- checked against a parse of /proc/self/maps."""
+    L = ga_amd.lib()
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    libc.madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    libc.mprotect.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    pg, MB = 4096, 1 << 20
+    anon = lambda n, prot=3: libc.mmap(None, n, prot, 0x22, -1, 0)   # MAP_PRIVATE | MAP_ANONYMOUS
+
+    def check(lo, hi, write, want):
+        io = (ctypes.c_ulonglong * 2)(lo, hi)
+        assert L.gaamd_diag(b"host_range", int(write), io, 2) == 0
+        assert bool(io[0]) == want == _host_range_want(lo, hi, write), (hex(lo), hex(hi), write, io[0], want)
+
+    split = anon(4 * MB + pg)
+    assert libc.munmap(ctypes.c_void_p(split + 4 * MB), pg) == 0    # a hole right after it
+    assert libc.madvise(ctypes.c_void_p(split + MB), MB, 10) == 0   # MADV_DONTFORK: three mappings
+    holed = anon(3 * pg)
+    assert libc.munmap(ctypes.c_void_p(holed + pg), pg) == 0
+    ro = anon(2 * pg)
+    assert libc.mprotect(ctypes.c_void_p(ro + pg), pg, 1) == 0     # second page read-only
+    none = anon(pg, 0)
+    import mmap
+    shared = mmap.mmap(-1, 2 * pg)                                  # /dev/zero (deleted): a device path
+    sh = ctypes.addressof(ctypes.c_char.from_buffer(shared))
+    arr = np.ones(3 * MB // 8)
+    try:
+        check(split, split + 4 * MB, True, True)
+        check(split + 100, split + 3 * MB + 5, False, True)
+        check(split + MB - 8, split + MB + 8, True, True)
+        check(split, split + 4 * MB + pg, False, False)             # runs past the end
+        check(holed, holed + 3 * pg, False, False)                  # a hole in the middle
+        check(holed, holed + pg, True, True)
+        check(holed + pg, holed + pg + 8, False, False)             # inside the hole
+        check(ro, ro + 2 * pg, False, True)
+        check(ro, ro + 2 * pg, True, False)
+        check(none, none + 8, False, False)
+        check(sh, sh + 8, False, False)
+        check(arr.ctypes.data, arr.ctypes.data + arr.nbytes, True, True)
+        check(16, 32, False, False)                                 # nothing mapped there
+        check(split + 8, split + 8, False, False)                   # empty range
+    finally:
+        del sh
+        for base, n in ((split, 4 * MB), (holed, pg), (holed + 2 * pg, pg), (ro, 2 * pg), (none, pg)):
+            libc.munmap(ctypes.c_void_p(base), n)
+
+
 def test_no_oracle_in_product_library():
     """The product .so must not link or embed the CPU checker."""
     out = subprocess.run(["nm", "-D", LIB_PATH], capture_output=True, text=True, check=True).stdout
