@@ -719,9 +719,21 @@ static void go_cols_lds(const Desc &d, const OP &op, int cw, uint64_t blocks, hi
 static int flat_block_threads(int W) { return W == 16 ? 64 : 256; }
 static uint64_t flat_block_items(int W) { return W == 16 ? 64 : 256ull * 4; }
 
-// vectors per thread: 16 B per thread per stream
+// vectors per thread: 16 B per thread per stream (8 B for 1- and 2-byte vectors).
+// unroll_for is the same table at run time: the launcher sizes its chunks with it,
+// so it must agree with what the kernels are instantiated with (it once said 16
+// for W = 1, and byte-wide rows kernels skipped half of every chunk: a put of odd-
+// length rows longer than the flat kernel's limit; tests/test_gpu_fuzz.py).
 template <int W> struct DefaultU { static constexpr int value = W == 16 ? 1 : (W == 8 ? 2 : (W == 4 ? 4 : 8)); };
-static int unroll_for(int W) { return W >= 16 ? 1 : 16 / W; }
+static int unroll_for(int W) {
+    switch (W) {
+    case 16: return DefaultU<16>::value;
+    case 8: return DefaultU<8>::value;
+    case 4: return DefaultU<4>::value;
+    case 2: return DefaultU<2>::value;
+    default: return DefaultU<1>::value;
+    }
+}
 constexpr int kSysBS = 256;   // peer-source rows kernel block
 
 template <class OP, int W, int BS, bool SYS = false>
