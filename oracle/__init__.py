@@ -54,6 +54,8 @@ class Oracle:
             "ora_unpack": (ctypes.c_long, [_vp, _vp, _ip, _ip, ctypes.c_int]),
             "ora_unpack_acc": (ctypes.c_long, [ctypes.c_int, _vp, _vp, _vp, _ip, _ip, ctypes.c_int]),
             "ora_accs": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
+            "ora_accv": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, ctypes.c_long, ctypes.c_int]),
+            "ora_copyv": (None, [_vp, _vp, ctypes.c_long, ctypes.c_int]),
             "ora_accs_mt": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int, ctypes.c_int]),
             "ora_accs_packed": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
             "ora_puts": (ctypes.c_int, [_vp, _ip, _vp, _ip, _ip, ctypes.c_int]),
@@ -93,6 +95,16 @@ class Oracle:
         rc = self.L.ora_accs_packed(op, _ptr(s), _vp(src.ctypes.data + src_off), _ints(src_stride),
                                     _vp(dst.ctypes.data + dst_off), _ints(dst_stride), _ints(count), levels)
         assert rc == 0
+
+    def accv(self, op, scale, src_addrs, dst_addrs, nbytes):
+        """one _acc per (src, dst) pair in order; uint64 arrays of host addresses"""
+        s = np.array([scale], dtype=_scale_dtype(op))
+        assert self.L.ora_accv(op, _ptr(s), _vp(src_addrs.ctypes.data), _vp(dst_addrs.ctypes.data),
+                               len(src_addrs), nbytes) == 0
+
+    def copyv(self, src_addrs, dst_addrs, nbytes):
+        """one memcpy per (src, dst) pair in order (putv / getv)"""
+        self.L.ora_copyv(_vp(src_addrs.ctypes.data), _vp(dst_addrs.ctypes.data), len(src_addrs), nbytes)
 
     def puts(self, src, src_off, src_stride, dst, dst_off, dst_stride, count, levels):
         self.L.ora_puts(_vp(src.ctypes.data + src_off), _ints(src_stride), _vp(dst.ctypes.data + dst_off),

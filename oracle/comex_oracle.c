@@ -109,6 +109,23 @@ int ora_elem_size(int op)
 }
 
 /* comex.c:1237-1264 */
+/* io-vector accumulate / copy to a self/SMP target: one _acc (or one memcpy) per
+ * (src[i], dst[i]) pair, in pair order -- nb_accv / nb_putv / nb_getv for such
+ * targets (comex.c:7327-7400 -> nb_acc 6228-6260, nb_put / nb_get) */
+int ora_accv(int op, const void *scale, void *const *src, void *const *dst, long n, int bytes)
+{
+    long i;
+    for (i = 0; i < n; i++)
+        if (ora_acc(op, bytes, dst[i], src[i], scale)) return -1;
+    return 0;
+}
+
+void ora_copyv(void *const *src, void *const *dst, long n, int bytes)
+{
+    long i;
+    for (i = 0; i < n; i++) memcpy(dst[i], src[i], (size_t)bytes);
+}
+
 long ora_packed_size(const int *count, int stride_levels)
 {
     long n1dim = 1;

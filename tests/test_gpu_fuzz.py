@@ -224,3 +224,96 @@ def test_random_pack_unpack_acc_and_puts(gpu_lib, oracle, seed):
         finally:
             sb.free()
             db.free()
+
+
+def _giov(src_addrs, dst_addrs, nbytes):
+    src_addrs = np.ascontiguousarray(src_addrs, dtype=np.uint64)
+    dst_addrs = np.ascontiguousarray(dst_addrs, dtype=np.uint64)
+    g = ga_amd.GIOV()
+    g._keep = (src_addrs, dst_addrs)
+    g.src = ctypes.cast(ctypes.c_void_p(src_addrs.ctypes.data), ctypes.POINTER(ctypes.c_void_p))
+    g.dst = ctypes.cast(ctypes.c_void_p(dst_addrs.ctypes.data), ctypes.POINTER(ctypes.c_void_p))
+    g.count, g.bytes = len(src_addrs), nbytes
+    return g
+
+
+def random_pairs(rng, n, nbytes, esz):
+    """(src offsets, dst offsets, dst region bytes): sources one vector in pair order
+    (GA's `v`), a permutation or random repeats; destinations one vector (cannot
+    repeat), sparse random (a few repeats, the hashed path), dense random (many repeats,
+    conflicts beyond the LDS list: the radix fallback) or a small hot set"""
+    k = int(rng.integers(0, 3))
+    if k == 0:
+        so = np.arange(n, dtype=np.uint64) * np.uint64(nbytes)
+    elif k == 1:
+        so = rng.permutation(n).astype(np.uint64) * np.uint64(nbytes)
+    else:
+        so = rng.integers(0, n, n).astype(np.uint64) * np.uint64(nbytes)
+    mode = int(rng.integers(0, 4))
+    if mode == 0:
+        do, slots = np.arange(n, dtype=np.uint64) * np.uint64(nbytes), n
+        return so, do, n * nbytes
+    slots = {1: 8 * n + 16, 2: max(1, n // 4), 3: int(rng.integers(1, 64))}[mode]
+    # destinations on a grid of whole pairs, or (when a pair holds several elements)
+    # of single elements, so that pairs overlap partially
+    step = nbytes if rng.random() < 0.7 else esz
+    do = rng.integers(0, slots, n).astype(np.uint64) * np.uint64(step)
+    return so, do, slots * step + nbytes
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_io_vectors(gpu_lib, oracle, seed):
+    """comex_accv / comex_putv / comex_getv (comex.c:7327-7400) on random pair lists
+    through every ordering path the io-vector code has (contiguous sides, hashed
+    repeats, radix fallback, per-pair serial), sources in HBM or pageable host memory,
+    1 to 150 000 pairs: bit-exact against the oracle's pair-by-pair loop (ora_accv /
+    ora_copyv, pinned against the reference's _acc per pair)."""
+    rng = np.random.default_rng(6000 + seed)
+    for k in range(12):
+        kind = ("acc", "acc", "put", "get")[k % 4]
+        op = OPS[int(rng.integers(0, len(OPS)))] if kind == "acc" else C.DBL
+        esz = C.ESZ[op]
+        nel = int(rng.choice([1, 1, 1, 2, 3, 8]))
+        nbytes = esz * nel if kind == "acc" else int(rng.choice([esz * nel, 1 + int(rng.integers(0, 40))]))
+        n = max(1, int(np.exp(rng.uniform(0, np.log(150000)))))
+        so, do, d_bytes = random_pairs(rng, n, nbytes, esz if kind == "acc" else 1)
+        s_bytes = int(so.max()) + nbytes
+        src_h = C.fill_bytes(op, s_bytes, 50 + k)
+        dst_h = C.fill_bytes(op, d_bytes, 60 + k)
+        host_src = kind != "get" and rng.random() < 0.3
+        host_dst = kind == "get" and rng.random() < 0.5
+        sb = None if host_src else ga_amd.DeviceBuffer(s_bytes)
+        db = None if host_dst else ga_amd.DeviceBuffer(d_bytes)
+        src_g = src_h.copy()                      # what the library reads when host_src
+        dst_g = dst_h.copy()                      # what the library writes when host_dst
+        try:
+            if sb:
+                sb.upload(src_h)
+            if db:
+                db.upload(dst_h)
+            s_base = src_g.ctypes.data if host_src else sb.ptr
+            d_base = dst_g.ctypes.data if host_dst else db.ptr
+            g = _giov(so + np.uint64(s_base), do + np.uint64(d_base), nbytes)
+            if kind == "acc":
+                alpha = random_alpha(rng, op)
+                keep, sp = ga_amd.scale_buffer(op, alpha)
+                assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
+            elif kind == "put":
+                assert gpu_lib.comex_putv(ctypes.byref(g), 1, 0, 0) == 0
+            else:
+                assert gpu_lib.comex_getv(ctypes.byref(g), 1, 0, 0) == 0
+            ga_amd.comex_fence_all()
+            got = dst_g if host_dst else db.download(np.uint8, d_bytes)
+            want = dst_h.copy()
+            sa, da = so + np.uint64(src_h.ctypes.data), do + np.uint64(want.ctypes.data)
+            if kind == "acc":
+                oracle.accv(op, alpha, sa, da, nbytes)
+            else:
+                oracle.copyv(sa, da, nbytes)
+            what = dict(kind=kind, op=C.NAMES[op], n=n, nbytes=nbytes, host_src=host_src, host_dst=host_dst)
+            assert same_bits_nan_aware(got, want, op), (what, first_mismatch(got, want, op))
+        finally:
+            if sb:
+                sb.free()
+            if db:
+                db.free()

@@ -152,6 +152,27 @@ def test_restatement_vs_reference_random(oracle):
         assert np.array_equal(d1, d2), (op, levels)
 
 
+@pytest.mark.skipif(not ref_available(), reason="oracle/_ref not built (no reference tree)")
+def test_accv_restatement_vs_reference(oracle):
+    """io-vector accumulate: the restated per-pair loop (ora_accv) == the reference's
+    _acc per pair (ref_accv over acc.h), with repeated and overlapping destinations,
+    every op, 1..5 elements per pair."""
+    ref = Ref()
+    rng = np.random.default_rng(12)
+    for op in (C.INT, C.DBL, C.FLT, C.CPL, C.DCP, C.LNG):
+        esz = C.ESZ[op]
+        for nel in (1, 2, 5):
+            nbytes, n = esz * nel, 3000
+            src = C.fill_bytes(op, n * nbytes, 31)
+            dst = C.fill_bytes(op, 200 * esz + nbytes, 32)
+            so = (rng.integers(0, n, n) * nbytes).astype(np.uint64)
+            do = (rng.integers(0, 200, n) * esz).astype(np.uint64)   # repeats, and overlaps when nel > 1
+            d1, d2 = dst.copy(), dst.copy()
+            oracle.accv(op, C.SCALE[op], so + np.uint64(src.ctypes.data), do + np.uint64(d1.ctypes.data), nbytes)
+            ref.accv(op, C.SCALE[op], so + np.uint64(src.ctypes.data), do + np.uint64(d2.ctypes.data), nbytes)
+            assert np.array_equal(d1, d2), (op, nel)
+
+
 @pytest.mark.parametrize("nthreads", [1, 3, 8])
 def test_multi_worker_baseline_matches_single(oracle, manifest, golden, nthreads):
     """The P-worker CPU baseline (mt_split.h) splits a patch into disjoint slabs:
