@@ -58,7 +58,7 @@ def main():
     import ga_amd
     L = ga_amd.lib()
     if mode in ("boot-gloo", "remote-gloo", "boot-nodes", "ga-gloo", "stress-gloo", "scatremote-gloo",
-                "armcimisc-gloo"):
+                "armcimisc-gloo", "rdesc-gloo"):
         ag, bar = torch_hooks(rank, size)
         keep = (ag, bar)  # noqa: F841
         assert L.gaamd_set_bootstrap(rank, size, rank, ctypes.cast(ag, ctypes.c_void_p),
@@ -118,6 +118,8 @@ def main():
         stale_fix_test(L, rank, size)
     elif mode in ("armcimisc", "armcimisc-gloo"):
         armci_misc_test(L, rank, size)
+    elif mode in ("rdesc", "rdesc-gloo"):
+        random_remote_descriptors_test(L, rank, size)
     else:
         remote_test(L, rank, size)
     print(f"RANK {rank} OK", flush=True)
@@ -2362,6 +2364,141 @@ def ngatest_gs(L, rank, size):
     L.GA_Terminate()
 
 
+def random_remote_descriptors_test(L, rank, size):
+    """Seeded random strided descriptors (tests/test_gpu_fuzz.py's generator: every op,
+    0..7 stride levels, rows of 1..8 Ki elements, padded / overlapping / zero strides,
+    offsets below the natural alignment) from rank 0 into rank 1's segment: accumulates
+    and puts, blocking and non-blocking, from a plain device buffer, from rank 0's own
+    segment (the direct-source route when the owner is another GPU), from pageable and
+    from pinned host memory; and gets back from a region nobody writes.  One writer, so
+    program order decides every byte: rank 1 replays the same sequence with the oracle
+    and compares its segment exactly; rank 0 checks each get."""
+    import ga_amd
+    import cases as C
+    from oracle import Oracle
+    from test_gpu_fuzz import OPS, phased_fill, random_alpha, random_case
+    from helpers import same_bits_nan_aware, first_mismatch
+    ora = Oracle()
+    assert ga_amd.comex_init() == 0
+    owner = 1 % size
+    REG = 4 << 20
+    nreg = len(OPS) + 2                    # one region per op, one for puts, one for gets
+    PUT, GET = len(OPS), len(OPS) + 1
+    seg = ga_amd.comex_malloc(REG * nreg, size)
+    srcseg = ga_amd.comex_malloc(REG, size)
+    init = [phased_fill(op, REG, 0, 900 + i) for i, op in enumerate(OPS)]
+    init += [np.random.default_rng(77).integers(0, 256, REG, dtype=np.uint8) for _ in range(2)]
+    if rank == owner:
+        for i, a in enumerate(init):
+            assert L.gaamd_memcpy(ctypes.c_void_p(seg[owner] + i * REG), a.ctypes.data_as(ctypes.c_void_p), REG) == 0
+    ga_amd.comex_barrier()
+    rng = np.random.default_rng(int(os.environ.get("RDESC_SEED", "3")))
+    ncase = int(os.environ.get("RDESC_CASES", "150"))
+
+    def fits(c):
+        s_hi = c["so"] + C.span(c["ss"], c["count"], c["levels"])[1]
+        d_hi = c["do"] + C.span(c["ds"], c["count"], c["levels"])[1]
+        return s_hi <= REG and d_hi <= REG
+
+    def draw(op):
+        while True:
+            c = random_case(rng, op)
+            c["alias"] = False
+            if fits(c):
+                return c
+
+    plan = []
+    for k in range(ncase):
+        op = OPS[k % len(OPS)]
+        c = draw(op)
+        c["kind"] = ("acc", "acc", "put", "get")[int(rng.integers(0, 4))]
+        c["src_kind"] = ("dev", "seg", "host", "pinned")[k % 4]
+        c["nb"] = bool(rng.random() < 0.4)
+        if c["kind"] != "acc":   # byte copies: whole rows of any length
+            c["count"] = [c["count"][0] + int(rng.integers(0, 8))] + c["count"][1:]
+            if not fits(c):
+                c["kind"] = "acc"
+                c["count"][0] = c["count"][0] // C.ESZ[op] * C.ESZ[op]
+        plan.append(c)
+    if rank == 0:
+        handles, keep = [], []
+        dev = ga_amd.DeviceBuffer(REG)
+        pin = ga_amd.DeviceBuffer(REG, host=True)
+        for k, c in enumerate(plan):
+            op, count, levels = c["op"], c["count"], c["levels"]
+            s_hi = c["so"] + C.span(c["ss"], count, levels)[1]
+            if c["kind"] == "get":
+                # owner's GET region (src side, strides ds) into a local buffer (strides ss)
+                d_hi = c["do"] + C.span(c["ds"], count, levels)[1]
+                local = np.random.default_rng(k).integers(0, 256, max(16, s_hi), dtype=np.uint8)
+                lb = ga_amd.DeviceBuffer(local.size)
+                lb.upload(local)
+                assert ga_amd.comex_gets(seg[owner] + GET * REG + c["do"], c["ds"], lb.ptr + c["so"], c["ss"], count,
+                                         levels, owner) == 0
+                assert ga_amd.comex_fence_all() == 0
+                want = local.copy()
+                ora.puts(init[GET], c["do"], c["ds"], want, c["so"], c["ss"], count, levels)
+                got = lb.download(np.uint8, local.size)
+                assert np.array_equal(got, want), ("get", k, c)
+                lb.free()
+                continue
+            src = phased_fill(op, max(16, s_hi), c["so"], 3000 + k)
+            if c["src_kind"] == "dev":
+                assert L.gaamd_memcpy(ctypes.c_void_p(dev.ptr), src.ctypes.data_as(ctypes.c_void_p), src.size) == 0
+                sp = dev.ptr
+            elif c["src_kind"] == "seg":
+                assert L.gaamd_memcpy(ctypes.c_void_p(srcseg[rank]), src.ctypes.data_as(ctypes.c_void_p),
+                                      src.size) == 0
+                sp = srcseg[rank]
+            elif c["src_kind"] == "pinned":
+                ctypes.memmove(pin.ptr, src.ctypes.data, src.size)
+                sp = pin.ptr
+            else:
+                sp = src.ctypes.data
+            if c["kind"] == "acc":
+                alpha = c["alpha"]
+                dst = seg[owner] + OPS.index(op) * REG + c["do"]
+                if c["nb"]:
+                    rc, h = ga_amd.comex_nbaccs(op, alpha, sp + c["so"], c["ss"], dst, c["ds"], count, levels, owner)
+                    assert rc == 0
+                    assert ga_amd.comex_wait(h) == 0   # the source buffer is reused by the next case
+                else:
+                    assert ga_amd.comex_accs(op, alpha, sp + c["so"], c["ss"], dst, c["ds"], count, levels,
+                                             owner) == 0
+            else:
+                assert ga_amd.comex_puts(sp + c["so"], c["ss"], seg[owner] + PUT * REG + c["do"], c["ds"], count,
+                                         levels, owner) == 0
+            keep.append(src)
+        assert ga_amd.comex_fence_all() == 0
+        dev.free()
+        pin.free()
+        say(rank, f"{ncase} random descriptors issued")
+    ga_amd.comex_barrier()
+    if rank == owner:
+        want = [a.copy() for a in init]
+        for k, c in enumerate(plan):
+            if c["kind"] == "get":
+                continue
+            op, count, levels = c["op"], c["count"], c["levels"]
+            s_hi = c["so"] + C.span(c["ss"], count, levels)[1]
+            src = phased_fill(op, max(16, s_hi), c["so"], 3000 + k)
+            if c["kind"] == "acc":
+                ora.accs(op, c["alpha"], src, c["so"], c["ss"], want[OPS.index(op)], c["do"], c["ds"], count, levels)
+            else:
+                ora.puts(src, c["so"], c["ss"], want[PUT], c["do"], c["ds"], count, levels)
+        for i in range(nreg):
+            got = np.empty(REG, dtype=np.uint8)
+            assert L.gaamd_memcpy(got.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(seg[owner] + i * REG), REG) == 0
+            op = OPS[i] if i < len(OPS) else 0
+            if i < len(OPS):
+                assert same_bits_nan_aware(got, want[i], op), (C.NAMES[op], first_mismatch(got, want[i], op))
+            else:
+                assert np.array_equal(got, want[i]), ("put" if i == PUT else "get", i)
+        say(rank, "segment equals the replayed sequence")
+    ga_amd.comex_barrier()
+    ga_amd.comex_free(srcseg[rank])
+    ga_amd.comex_free(seg[rank])
+
+
 if __name__ == "__main__":
     main()
-

@@ -214,6 +214,27 @@ def test_stress_random_programs(mode, n, nodes, staging):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["same-gpu", "cross-device", "cross-device-1MiB-staging", "packed", "wire"])
+def test_random_remote_descriptors(variant):
+    """Seeded random strided descriptors (every op, 0..7 levels, overlapping and zero
+    strides, offsets below the natural alignment) accumulated, put and got between
+    two ranks on every route: the one-pass route (same GPU), the packed and direct-
+    source routes with every peer treated as another GPU (also with a 1 MiB staging
+    ring, so rows travel as row ranges), the packed route forced by the reference's
+    SMP toggles, and the wire protocol between simulated nodes.  One writer: the
+    owner's segment must equal the oracle replaying the sequence, byte for byte."""
+    env = {"same-gpu": {}, "cross-device": {"COMEX_AMD_PEER_LOADS": "all"},
+           "cross-device-1MiB-staging": {"COMEX_AMD_PEER_LOADS": "all", "COMEX_AMD_STAGING_MB": "1",
+                                         "RDESC_SEED": "4"},
+           "packed": {"COMEX_ENABLE_ACC_SMP": "0", "COMEX_ENABLE_PUT_SMP": "0", "RDESC_SEED": "5"},
+           "wire": {"RDESC_SEED": "6"}}[variant]
+    if variant == "wire":
+        launch("rdesc-gloo", n=2, timeout=170, nodes=[0, 1], extra_env=env)
+    else:
+        launch("rdesc", n=2, timeout=170, extra_env=env)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,seed", [(3, "0"), (4, "5"), (4, "11"), (3, "17")])
 def test_stress_random_programs_one_pass_everywhere(n, seed):
     """The same random programs with the one-pass route taken by every device-source
