@@ -1448,9 +1448,107 @@ def ga_test(L, rank, size):
     L.GA_Sync()
     say(rank, "ga sync 13")
     L.GA_Destroy(g3)
+    ga_irregular_test(L, rank, size)
     if rank == 0:
         L.GA_Print_stats()
     L.GA_Terminate()
+
+
+def ga_irregular_test(L, rank, size):
+    """NGA_Create_irreg (capi.c:244-265 + copy_map): random block boundaries per
+    dimension, blocks owned in GA's order (the Fortran-first dimension, i.e. the last C
+    dimension, fastest: ga_ComputeIndexM), possibly fewer blocks than ranks (those own
+    nothing).  Every rank accumulates a random patch (integer-valued: exact in any order),
+    rank 0 puts one, all get them back, and a scatter-accumulate with repeats lands on
+    the right owners."""
+    import ga_amd
+    ia = ga_amd.int_array
+    C_DBL = 1004
+    rng = np.random.default_rng(41)                      # the same on every rank
+    dims = [97, 61, 13]
+    # 3 ranks: two blocks, so rank 2 owns nothing
+    nblk = {1: [1, 1, 1], 2: [1, 2, 1], 3: [2, 1, 1], 4: [2, 1, 2]}.get(size, [2, 2, 2] if size >= 8 else [2, 2, 1])
+    maps = []
+    for d, b in enumerate(nblk):
+        starts = np.sort(rng.choice(np.arange(1, dims[d]), b - 1, replace=False)) if b > 1 else np.array([], int)
+        maps.append([0] + [int(x) for x in starts])
+    flat = [x for m in maps for x in m]
+    g = L.NGA_Create_irreg(C_DBL, 3, ia(dims), b"irr", ia(nblk), ia(flat))
+    assert g > 0
+    # ownership: block (i0, i1, i2) in C order belongs to rank i2 + nb2 * (i1 + nb1 * i0)
+    bounds = [m + [dims[d]] for d, m in enumerate(maps)]
+    for p in range(size):
+        lo, hi = (ctypes.c_int * 3)(), (ctypes.c_int * 3)()
+        L.NGA_Distribution(g, p, lo, hi)
+        nb = nblk[0] * nblk[1] * nblk[2]
+        if p >= nb:
+            assert any(hi[d] < lo[d] for d in range(3)), (p, list(lo), list(hi))
+            continue
+        i2, r = p % nblk[2], p // nblk[2]
+        i1, i0 = r % nblk[1], r // nblk[1]
+        want_lo = [bounds[0][i0], bounds[1][i1], bounds[2][i2]]
+        want_hi = [bounds[0][i0 + 1] - 1, bounds[1][i1 + 1] - 1, bounds[2][i2 + 1] - 1]
+        assert list(lo) == want_lo and list(hi) == want_hi, (p, list(lo), list(hi), want_lo, want_hi)
+    L.GA_Zero(g)
+
+    def patch(r):
+        pr = np.random.default_rng(300 + r)
+        lo = [int(pr.integers(0, dims[d])) for d in range(3)]
+        hi = [int(pr.integers(lo[d], dims[d])) for d in range(3)]
+        shape = [hi[d] - lo[d] + 1 for d in range(3)]
+        ld = [shape[1] + 2, shape[2] + 1]
+        buf = pr.integers(-40, 40, shape[0] * ld[0] * ld[1]).astype(np.float64).reshape(shape[0], ld[0], ld[1])
+        return lo, hi, shape, ld, buf
+
+    lo, hi, shape, ld, buf = patch(rank)
+    alpha = ctypes.c_double(rank + 1)
+    L.NGA_Acc(g, ia(lo), ia(hi), buf.ctypes.data_as(ctypes.c_void_p), ia(ld), ctypes.byref(alpha))
+    L.GA_Sync()
+    full = np.zeros(dims)
+    L.NGA_Get(g, ia([0, 0, 0]), ia([dims[0] - 1, dims[1] - 1, dims[2] - 1]), full.ctypes.data_as(ctypes.c_void_p),
+              ia([dims[1], dims[2]]))
+    want = np.zeros(dims)
+    for r in range(size):
+        lo_r, hi_r, sh, _, b = patch(r)
+        want[lo_r[0]:hi_r[0] + 1, lo_r[1]:hi_r[1] + 1, lo_r[2]:hi_r[2] + 1] += (r + 1) * b[:, :sh[1], :sh[2]]
+    assert np.array_equal(full, want), "irregular NGA_Acc"
+    L.GA_Sync()
+    say(rank, "irregular acc checked")
+    # rank 0 puts a patch over every block; every rank gets it back
+    plo, phi = [5, 3, 1], [90, 57, 11]
+    pv = np.arange(86 * 55 * 11, dtype=np.float64).reshape(86, 55, 11) + 0.25
+    if rank == 0:
+        L.NGA_Put(g, ia(plo), ia(phi), pv.ctypes.data_as(ctypes.c_void_p), ia([55, 11]))
+    L.GA_Sync()
+    gv = np.zeros_like(pv)
+    L.NGA_Get(g, ia(plo), ia(phi), gv.ctypes.data_as(ctypes.c_void_p), ia([55, 11]))
+    assert np.array_equal(gv, pv), "irregular NGA_Put/NGA_Get"
+    L.GA_Sync()
+    # scatter-accumulate with repeated subscripts over every owner
+    L.GA_Zero(g)
+    sr = np.random.default_rng(60 + rank)
+    nv = 3000
+    subs = np.stack([sr.integers(0, dims[d], nv) for d in range(3)], axis=1).astype(np.int32)
+    subs[nv // 2:nv // 2 + 100] = subs[:100]
+    vals = sr.integers(-20, 20, nv).astype(np.float64)
+    three = ctypes.c_double(3.0)
+    L.NGA_Scatter_acc_flat(g, vals.ctypes.data_as(ctypes.c_void_p),
+                           np.ascontiguousarray(subs).ravel().ctypes.data_as(ctypes.POINTER(ctypes.c_int)), nv,
+                           ctypes.byref(three))
+    L.GA_Sync()
+    L.NGA_Get(g, ia([0, 0, 0]), ia([dims[0] - 1, dims[1] - 1, dims[2] - 1]), full.ctypes.data_as(ctypes.c_void_p),
+              ia([dims[1], dims[2]]))
+    want = np.zeros(dims)
+    for r in range(size):
+        rr = np.random.default_rng(60 + r)
+        sb = np.stack([rr.integers(0, dims[d], nv) for d in range(3)], axis=1)
+        sb[nv // 2:nv // 2 + 100] = sb[:100]
+        vv = rr.integers(-20, 20, nv).astype(np.float64)
+        np.add.at(want, (sb[:, 0], sb[:, 1], sb[:, 2]), 3.0 * vv)
+    assert np.array_equal(full, want), "irregular NGA_Scatter_acc"
+    L.GA_Sync()
+    say(rank, "irregular scatter-acc checked")
+    L.GA_Destroy(g)
 
 
 # ---------------------------------------------------------------------------
