@@ -716,19 +716,18 @@ void NGA_Distribution(int g_a, int iproc, int lo[], int hi[]) {
     }
 }
 
+// pnga_locate_num_blocks (base.c:5591-5627): the region is bounds-checked, and the
+// count is only defined for block-cyclic distributions; an array with a map
+// (NGA_Create's regular blocks or NGA_Create_irreg's) is GA's REGULAR type, for which
+// the reference returns -1 -- so does this.
 int NGA_Locate_num_blocks(int g_a, int lo[], int hi[]) {
     GArray &a = arr(g_a);
     long flo[GA_MAX_DIM], fhi[GA_MAX_DIM];
     c2f_index(a.ndim, lo, flo);
     c2f_index(a.ndim, hi, fhi);
-    int n = 1;
-    for (int d = 0; d < a.ndim; d++) {
-        const std::vector<long> &m = a.map[d];
-        const int b0 = (int)(std::upper_bound(m.begin(), m.end(), flo[d]) - m.begin()) - 1;
-        const int b1 = (int)(std::upper_bound(m.begin(), m.end(), fhi[d]) - m.begin()) - 1;
-        n *= b1 - b0 + 1;
-    }
-    return n;
+    for (int d = 0; d < a.ndim; d++)
+        if (flo[d] < 1 || fhi[d] > a.dims[d] || flo[d] > fhi[d]) fatal("Requested region out of bounds");
+    return -1;
 }
 
 static void c_patch(GaOp kind, int g_a, int lo[], int hi[], void *buf, int ld[], void *alpha) {

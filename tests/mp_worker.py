@@ -1162,6 +1162,125 @@ def armci_misc_test(L, rank, size):
     assert np.array_equal(back, packed)
     say(rank, "memget/strided")
 
+    ARMCI_ACC_DBL, ARMCI_LONG, ARMCI_DOUBLE, SCOPE_ALL = 38, -101, -307, 333   # armci.h, message.h
+    # the rest of the one-sided surface GA links against: contiguous non-blocking put/get,
+    # WaitProc, non-blocking single values, the contiguous flagged put, PutS_flag_dir,
+    # non-blocking io-vectors, aggregate-handle no-ops, ARMCI_Test (armci.c / capi.c)
+    base = 1 << 19
+    pv = np.arange(512, dtype=np.float64) + 100.0 * rank
+    h1, h2 = c_int(-1), c_int(-1)
+    L.ARMCI_SET_AGGREGATE_HANDLE(byref(h1))
+    assert L.ARMCI_NbPut(pv.ctypes.data_as(vp), vp(seg[nxt] + base), 4096, nxt, byref(h1)) == 0
+    L.ARMCI_UNSET_AGGREGATE_HANDLE(byref(h1))
+    assert L.ARMCI_Wait(byref(h1)) == 0
+    hv = [c_int(-1) for _ in range(3)]
+    assert L.ARMCI_NbPutValueLong(ctypes.c_long(-(3 << 33) - rank), vp(seg[nxt] + base + 4096), nxt, byref(hv[0])) == 0
+    assert L.ARMCI_NbPutValueFloat(ctypes.c_float(1.5 + rank), vp(seg[nxt] + base + 4104), nxt, byref(hv[1])) == 0
+    assert L.ARMCI_NbPutValueDouble(ctypes.c_double(2.25e-300 * (rank + 1)), vp(seg[nxt] + base + 4112), nxt,
+                                    byref(hv[2])) == 0
+    assert L.ARMCI_WaitProc(nxt) == 0
+    for x in hv:
+        assert L.ARMCI_Test(byref(x)) == 0   # complete: status 0
+    L.ARMCI_Barrier()
+    g1 = np.zeros(512)
+    assert L.ARMCI_NbGet(vp(seg[rank] + base), g1.ctypes.data_as(vp), 4096, rank, byref(h2)) == 0
+    assert L.ARMCI_Wait(byref(h2)) == 0
+    assert np.array_equal(g1, np.arange(512) + 100.0 * prv)
+    assert L.ARMCI_GetValueLong(vp(seg[rank] + base + 4096), rank) == -(3 << 33) - prv
+    assert L.ARMCI_GetValueFloat(vp(seg[rank] + base + 4104), rank) == 1.5 + prv
+    assert L.ARMCI_GetValueDouble(vp(seg[rank] + base + 4112), rank) == 2.25e-300 * (prv + 1)
+    L.ARMCI_Barrier()
+    # contiguous flagged put, then the strided one with the _dir form
+    fl_off, d_off = base + 8192, base + 12288
+    blob = np.arange(300, dtype=np.int32) * (rank + 3)
+    assert L.ARMCI_Put_flag(blob.ctypes.data_as(vp), vp(seg[nxt] + d_off), blob.nbytes,
+                            ctypes.cast(vp(seg[nxt] + fl_off), ctypes.POINTER(c_int)), 10 + rank, nxt) == 0
+    while L.ARMCI_GetValueInt(vp(seg[rank] + fl_off), rank) != 10 + prv:
+        pass
+    rb = np.zeros(300, dtype=np.int32)
+    assert L.ARMCI_Get(vp(seg[rank] + d_off), rb.ctypes.data_as(vp), rb.nbytes, rank) == 0
+    assert np.array_equal(rb, np.arange(300, dtype=np.int32) * (prv + 3))
+    L.ARMCI_Barrier()
+    pat2 = np.arange(16 * 20, dtype=np.float64).reshape(16, 20) - rank
+    assert L.ARMCI_PutS_flag_dir(pat2.ctypes.data_as(vp), ga_amd.int_array([160]), vp(seg[nxt] + d_off),
+                                 ga_amd.int_array([320]), ga_amd.int_array([160, 16]), 1,
+                                 ctypes.cast(vp(seg[nxt] + fl_off + 4), ctypes.POINTER(c_int)), 20 + rank, nxt) == 0
+    while L.ARMCI_GetValueInt(vp(seg[rank] + fl_off + 4), rank) != 20 + prv:
+        pass
+    rb2 = np.zeros(16 * 40, dtype=np.float64)
+    assert L.ARMCI_Get(vp(seg[rank] + d_off), rb2.ctypes.data_as(vp), rb2.nbytes, rank) == 0
+    assert np.array_equal(rb2.reshape(16, 40)[:, :20], np.arange(16 * 20, dtype=np.float64).reshape(16, 20) - prv)
+    L.ARMCI_Barrier()
+    # non-blocking io-vectors: put 64 scattered doubles into nxt, accumulate them twice
+    # more (alpha 2), get them back with NbGetV
+    v_off = base + 65536
+    nv = 64
+    src = np.arange(nv, dtype=np.float64) + 10.0 * rank
+    idx = (np.arange(nv) * 7) % 97
+    s_arr = (vp * nv)(*[src.ctypes.data + 8 * i for i in range(nv)])
+    d_arr = (vp * nv)(*[seg[nxt] + v_off + 8 * int(j) for j in idx])
+    iov = ga_amd.GIOV()
+    iov.src = ctypes.cast(s_arr, ctypes.POINTER(vp))
+    iov.dst = ctypes.cast(d_arr, ctypes.POINTER(vp))
+    iov.count, iov.bytes = nv, 8
+    h3, h4, h5 = c_int(-1), c_int(-1), c_int(-1)
+    assert L.ARMCI_NbPutV(byref(iov), 1, nxt, byref(h3)) == 0
+    assert L.ARMCI_Wait(byref(h3)) == 0
+    two = ctypes.c_double(2.0)
+    assert L.ARMCI_NbAccV(ARMCI_ACC_DBL, byref(two), byref(iov), 1, nxt, byref(h4)) == 0
+    assert L.ARMCI_Wait(byref(h4)) == 0
+    L.ARMCI_AllFence()
+    L.ARMCI_Barrier()
+    out = np.zeros(nv)
+    g_src = (vp * nv)(*[seg[rank] + v_off + 8 * int(j) for j in idx])
+    g_dst = (vp * nv)(*[out.ctypes.data + 8 * i for i in range(nv)])
+    giov = ga_amd.GIOV()
+    giov.src = ctypes.cast(g_src, ctypes.POINTER(vp))
+    giov.dst = ctypes.cast(g_dst, ctypes.POINTER(vp))
+    giov.count, giov.bytes = nv, 8
+    assert L.ARMCI_NbGetV(byref(giov), 1, rank, byref(h5)) == 0
+    assert L.ARMCI_Wait(byref(h5)) == 0
+    assert np.array_equal(out, 3.0 * (np.arange(nv) + 10.0 * prv)), out[:4]
+    L.ARMCI_Barrier()
+    say(rank, "nb put/get, values, flags, io-vectors")
+
+    # processor groups through the ARMCI default / child forms and comex's own group API
+    dflt, child = c_int(-1), c_int(-1)
+    L.ARMCI_Group_get_default(byref(dflt))
+    members = list(range(size - 1, -1, -1))            # every rank, in reverse order
+    L.ARMCI_Group_create_child(size, ga_amd.int_array(members), byref(child), byref(dflt))
+    cr, cs = c_int(), c_int()
+    L.ARMCI_Group_rank(byref(child), byref(cr))
+    L.ARMCI_Group_size(byref(child), byref(cs))
+    assert (cr.value, cs.value) == (size - 1 - rank, size)
+    L.ARMCI_Group_free(byref(child))
+    cg = c_int(-1)
+    assert L.comex_group_create(size, ga_amd.int_array(members), 0, byref(cg)) == 0
+    gsz, wr = c_int(), c_int()
+    assert L.comex_group_size(cg, byref(gsz)) == 0 and gsz.value == size
+    assert L.comex_group_translate_world(cg, 0, byref(wr)) == 0 and wr.value == size - 1
+    tr = (c_int * size)()
+    assert L.comex_group_translate_ranks(size, cg, ga_amd.int_array(list(range(size))), 0, tr) == 0
+    assert list(tr) == members
+    assert L.comex_group_free(cg) == 0
+    say(rank, "groups (default, child, comex)")
+
+    # message layer: brdcst, reduce (+ scope), timer
+    bb = (c_int * 4)(*([rank] * 4))
+    L.armci_msg_brdcst(bb, 16, size - 1)
+    assert list(bb) == [size - 1] * 4
+    rx = (ctypes.c_long * 2)(rank, -rank)
+    L.armci_msg_reduce(rx, 2, b"+", ARMCI_LONG)
+    assert list(rx) == [sum(range(size)), -sum(range(size))]
+    ry = (ctypes.c_double * 1)(float(rank))
+    L.armci_msg_reduce_scope(SCOPE_ALL, ry, 1, b"max", ARMCI_DOUBLE)
+    assert ry[0] == float(size - 1)
+    t0 = L.armci_timer()
+    t1 = L.armci_timer()
+    assert t1 >= t0 > 0
+    L.ARMCI_Barrier()
+    say(rank, "brdcst/reduce/timer")
+
     L.ARMCI_Barrier()
     assert L.ARMCI_Free(vp(seg[rank])) == 0
     L.ARMCI_Finalize()
@@ -1501,6 +1620,9 @@ def ga_irregular_test(L, rank, size):
         return lo, hi, shape, ld, buf
 
     lo, hi, shape, ld, buf = patch(rank)
+    # NGA_Locate_num_blocks (base.c:5591-5627) counts blocks only for block-cyclic
+    # distributions; for an array with a map (regular or irregular) the reference returns -1
+    assert L.NGA_Locate_num_blocks(g, ia(lo), ia(hi)) == -1
     alpha = ctypes.c_double(rank + 1)
     L.NGA_Acc(g, ia(lo), ia(hi), buf.ctypes.data_as(ctypes.c_void_p), ia(ld), ctypes.byref(alpha))
     L.GA_Sync()
