@@ -1600,8 +1600,8 @@ def ga_irregular_test(L, rank, size):
         lo, hi = (ctypes.c_int * 3)(), (ctypes.c_int * 3)()
         L.NGA_Distribution(g, p, lo, hi)
         nb = nblk[0] * nblk[1] * nblk[2]
-        if p >= nb:
-            assert any(hi[d] < lo[d] for d in range(3)), (p, list(lo), list(hi))
+        if p >= nb:   # ga_ownsM_no_handle (base.h:157-161): lo 0, hi -1 in Fortran, C lo -1, hi -2
+            assert list(lo) == [-1] * 3 and list(hi) == [-2] * 3, (p, list(lo), list(hi))
             continue
         i2, r = p % nblk[2], p // nblk[2]
         i1, i0 = r % nblk[1], r // nblk[1]
