@@ -135,7 +135,8 @@ def test_remote_across_devices():
     """One rank per MI355X of the box (2..8): each opens the others' segments and
     staging by IPC on other devices; remote acc/put/get/accv/getv/putv over xGMI
     (peer memory read with system-scope loads, puts applied by the owner), the
-    put/acc ordering case, and the full-size C5 exchange check (32768^2 f64 GA,
+    put/acc ordering case, random strided descriptors between two GPUs (every op,
+    overlapping and sub-aligned rows, all source kinds), and the full-size C5 exchange check (32768^2 f64 GA,
     M1 + M2 on both routes, exact).  Needs a multi-GPU box (skipped on one)."""
     import ga_amd
     ndev = ga_amd.lib().gaamd_device_count()
@@ -144,6 +145,7 @@ def test_remote_across_devices():
     n = min(ndev, 8)
     launch("remote", n=n, timeout=180, extra_env={"TEST_DISTINCT_DEVICES": "1"})
     launch("order", n=n, timeout=180)
+    launch("rdesc", n=2, timeout=170)   # random descriptors from GPU 0 into GPU 1's segment
     launch("c5full", n=n, timeout=420, extra_env={"COMEX_AMD_STAGING_MB": "256", "TEST_DISTINCT_DEVICES": "1"})
 
 
