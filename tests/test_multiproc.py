@@ -225,11 +225,13 @@ def test_random_remote_descriptors(variant):
     ring, so rows travel as row ranges), the packed route forced by the reference's
     SMP toggles, and the wire protocol between simulated nodes.  One writer: the
     owner's segment must equal the oracle replaying the sequence, byte for byte."""
-    env = {"same-gpu": {}, "cross-device": {"COMEX_AMD_PEER_LOADS": "all"},
+    base = int(os.environ.get("RDESC_SEED", "3"))   # soak runs set another base
+    env = {"same-gpu": {"RDESC_SEED": str(base)},
+           "cross-device": {"COMEX_AMD_PEER_LOADS": "all", "RDESC_SEED": str(base)},
            "cross-device-1MiB-staging": {"COMEX_AMD_PEER_LOADS": "all", "COMEX_AMD_STAGING_MB": "1",
-                                         "RDESC_SEED": "4"},
-           "packed": {"COMEX_ENABLE_ACC_SMP": "0", "COMEX_ENABLE_PUT_SMP": "0", "RDESC_SEED": "5"},
-           "wire": {"RDESC_SEED": "6"}}[variant]
+                                         "RDESC_SEED": str(base + 1)},
+           "packed": {"COMEX_ENABLE_ACC_SMP": "0", "COMEX_ENABLE_PUT_SMP": "0", "RDESC_SEED": str(base + 2)},
+           "wire": {"RDESC_SEED": str(base + 3)}}[variant]
     if variant == "wire":
         launch("rdesc-gloo", n=2, timeout=170, nodes=[0, 1], extra_env=env)
     else:
