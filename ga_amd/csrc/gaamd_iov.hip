@@ -133,6 +133,7 @@ __global__ __launch_bounds__(256) void k_iov_runs(const IovDesc d, const OP op) 
 // completed, runs launch_iov_runs with the table as a mask (pairs already
 // applied get the sentinel key and are skipped).
 constexpr uint32_t kIovhCap = 8192;          // conflict entries sorted in LDS (64 KiB)
+constexpr uint32_t kIovhBS = 64;             // insert / apply block: one wave, spread over more CUs
 constexpr uint32_t kIovhMaxPairs = 1u << 19;  // above: the radix path (1 Mi random pairs overflow the LDS list)
 
 struct IovHash {
@@ -159,12 +160,12 @@ static __device__ __forceinline__ uint32_t iovh_slot0(uint32_t key, uint32_t mas
 // dst_in / src_in (optional): the address lists still in the caller's mapped pinned
 // buffer -- read here over PCIe and written to dst_list / src_out in HBM for the kernels
 // after this one, which saves the separate upload launch (7-16 us, profiles/r05/ivt)
-__global__ __launch_bounds__(256) void k_iovh_insert(uint64_t *dst_list, uint64_t dlo, uint32_t bytes,
+__global__ __launch_bounds__(kIovhBS) void k_iovh_insert(uint64_t *dst_list, uint64_t dlo, uint32_t bytes,
                                                      uint32_t shift, bool pow2, uint32_t n, uint64_t *keys,
                                                      uint32_t *dup, uint32_t mask, uint32_t epoch, uint32_t *slot,
                                                      uint32_t *count, const uint64_t *dst_in, const uint64_t *src_in,
                                                      uint64_t *src_out) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t i = blockIdx.x * kIovhBS + threadIdx.x;
     if (i == 0) *count = 0;   // the conflict list of this call (k_iovh_apply runs after this kernel)
     if (i >= n) return;
     if (src_in) src_out[i] = src_in[i];
@@ -213,10 +214,10 @@ __device__ __forceinline__ void iov_apply_pair(const IovDesc &d, const OP &op, u
 }
 
 template <class OP, int W, bool SYS>
-__global__ __launch_bounds__(256) void k_iovh_apply(const IovDesc d, const OP op, uint64_t dlo, uint32_t shift,
+__global__ __launch_bounds__(kIovhBS) void k_iovh_apply(const IovDesc d, const OP op, uint64_t dlo, uint32_t shift,
                                                     bool pow2, uint32_t epoch, const uint32_t *dup,
                                                     const uint32_t *slot, uint64_t *conf, uint32_t *count) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t i = blockIdx.x * kIovhBS + threadIdx.x;
     if (i >= d.n) return;
     const uint32_t h = slot[i];
     if (dup[h] != epoch) {
@@ -281,7 +282,8 @@ __global__ __launch_bounds__(256) void k_iov_keys_masked(const uint64_t *dst_lis
 template <class OP, int W, bool SYS>
 static hipError_t iov_ws(const IovDesc &d, const OP &op, bool serial, hipStream_t st, const IovHashArgs *ha) {
     if (ha) {
-        hipLaunchKernelGGL((k_iovh_apply<OP, W, SYS>), dim3((d.n + 255u) / 256u), dim3(256), 0, st, d, op, ha->dlo,
+        hipLaunchKernelGGL((k_iovh_apply<OP, W, SYS>), dim3((d.n + kIovhBS - 1) / kIovhBS), dim3(kIovhBS), 0, st, d, op,
+                           ha->dlo,
                            ha->shift, ha->pow2, ha->epoch, ha->dup, ha->slot, ha->conf, ha->count);
         hipLaunchKernelGGL((k_iovh_conf<OP, W, SYS>), dim3(1), dim3(1024), 0, st, d, op, ha->conf, ha->count,
                            ha->overflow);
@@ -595,7 +597,8 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
     uint64_t *conf = (uint64_t *)(h->mem + off_conf(h->P, h->npairs));
     uint32_t *count = (uint32_t *)(conf + kIovhCap);
     if (src_in && !d.src_list) return -4;
-    hipLaunchKernelGGL(k_iovh_insert, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, (uint64_t *)d.dst_list, dlo,
+    hipLaunchKernelGGL(k_iovh_insert, dim3((d.n + kIovhBS - 1) / kIovhBS), dim3(kIovhBS), 0, stream,
+                       (uint64_t *)d.dst_list, dlo,
                        (uint32_t)d.bytes, shift, pow2, d.n, keys, dup, h->P - 1, h->epoch, slot, count, dst_in, src_in,
                        (uint64_t *)d.src_list);
     hipError_t e = hipGetLastError();
