@@ -246,7 +246,8 @@ static void get_via_owner(int t, char *src, const int *ss, char *dst, const int 
     side_span_host(ds, count, levels, (int64_t)row, &dlo, &dhi);
     check_remote(t, src, slo, shi);
     drain_target(t);   // our earlier chunks to t are posted first: its done counter stays in order
-    View dv = local_view(dst, dlo, dhi, true);
+    View dv = local_view(dst, dlo, dhi, true, true);
+    if (dv.bounce) view_rows(dv, ds, count, levels, (int64_t)row);
     const bool host_side = needs_sync(dv);
     int pstride[8];
     {
@@ -315,14 +316,15 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
             side_span_host(ss, count, levels, count[0], &slo, &shi);
             side_span_host(ds, count, levels, count[0], &dlo, &dhi);
             check_remote(world, src, slo, shi);
-            View dv = local_view(dst, dlo, dhi, true);
+            View dv = local_view(dst, dlo, dhi, true, true);
+            if (dv.bounce) view_rows(dv, ds, count, levels, count[0]);
             wire_get_strided((uint64_t)(uintptr_t)src, ss, dv.dev, ds, count, levels, world);
             release_view(dv);
         } else {
             side_span_host(ss, count, levels, count[0], &slo, &shi);
             side_span_host(ds, count, levels, rb, &dlo, &dhi);
             check_remote(world, dst, dlo, dhi);
-            View sv = local_view(src, slo, shi);
+            View sv = local_view(src, slo, shi, false, true);
             wire_send_strided(cop, scale, sv.dev, ss, (uint64_t)(uintptr_t)dst, ds, count, levels, world);
             release_view(sv);
         }
@@ -451,18 +453,25 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         // put: remote dst / get: remote src, through the owner's IPC mapping
         fence_target(world);   // order after our own pending accumulates to it
         if (kind == X_PUT) {
-            sv = local_view(src, slo, shi);
+            sv = local_view(src, slo, shi, false, true);
             dv.dev = remote_view(world, dst, dlo, dhi);
             dv.hbm = segment_kind_of(world, (const char *)dst + dlo) == 1;
         } else {
             sv.dev = remote_view(world, src, slo, shi);
             sv.hbm = segment_kind_of(world, (const char *)src + slo) == 1;
-            dv = local_view(dst, dlo, dhi, true);
+            dv = local_view(dst, dlo, dhi, true, true);
         }
     } else {
         local_views(src, slo, shi, dst, dlo, dhi, sv, dv);
     }
-    const bool host_side = needs_sync(sv) || needs_sync(dv);
+    if (dv.bounce) view_rows(dv, ds, count, levels, kind == X_ACC ? rb : count[0]);
+    // a pageable side in this thread's pinned bounce buffer, or pinned for this call, is
+    // private to the call: the operation is scheduled as any other and completes on its
+    // own stream before the views are released (small calls 37 -> 15 us,
+    // profiles/r05/lat/); a staged copy (hipMemcpyAsync on stream 0) keeps the ordered
+    // path below (stream 0, every stream synced)
+    const bool bounce_only = (needs_sync(sv) || needs_sync(dv)) && !sv.staged && !dv.staged;
+    const bool host_side = (needs_sync(sv) || needs_sync(dv)) && !bounce_only;
     // a get from another GPU's memory reads it with system-scope loads
     const bool peer = kind == X_GET && world != r.rank && r.peer_src(world);
     int si = 0;
@@ -486,12 +495,13 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     }
     // blocking call: local completion before returning (src reusable, a get's
     // dst filled) -- the stream the op went to holds it and its dependencies
-    const bool synced = host_side || (!hdl && r.blocking_sync);
+    const bool synced = host_side || bounce_only || (!hdl && r.blocking_sync);
     if (!host_side && synced) {
-        // HBM operands only: a completion flag behind the kernel (sched_wait_flag,
-        // ~4 us sooner than the runtime's signal); otherwise the runtime's sync, whose
-        // system-scope release makes a host-memory destination's bytes visible
-        if (sv.hbm && dv.hbm) sched_wait_flag(si);
+        // HBM destination: a completion flag behind the kernel (sched_wait_flag, ~4 us
+        // sooner than the runtime's signal; for a bounced source it also says the kernel
+        // has read the bounce buffer); otherwise the runtime's sync, whose system-scope
+        // release makes a host-memory destination's bytes visible
+        if (dv.hbm && (sv.hbm || sv.bounce || sv.registered)) sched_wait_flag(si);
         else GA_HIP(hipStreamSynchronize(st));
     }
     if (world != r.rank && !synced && !r.direct_pending.empty()) r.direct_pending[world] = 1;
@@ -500,7 +510,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
                 kind == X_ACC ? "acc" : (kind == X_PUT ? "put" : "get"), world, levels, count[0],
                 levels ? count[levels] : 1, sv.registered ? "registered" : (sv.staged ? "staged" : "device"),
                 dv.registered ? "registered" : (dv.staged ? "staged" : "device"), si);
-    if (host_side) {
+    if (host_side || bounce_only) {
         release_view(sv);
         release_view(dv);
     }

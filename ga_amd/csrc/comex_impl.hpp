@@ -36,6 +36,13 @@ struct View {
     char *dev = nullptr;          // device-accessible address of the user pointer
     void *registered = nullptr;   // page base we registered for this call
     char *staged = nullptr;       // fallback: device copy of [host+lo, host+hi)
+    char *bounce = nullptr;       // small pageable span: pinned copy of [host+lo, host+hi)
+    // a bounced destination is written back row by row (only the bytes the kernel wrote):
+    // wb_host is the user's dst pointer, wb_bounce the matching address in the bounce copy
+    char *wb_host = nullptr, *wb_bounce = nullptr;
+    const int *wb_stride = nullptr, *wb_count = nullptr;
+    int wb_levels = -1;
+    int64_t wb_row = 0;
     char *host = nullptr;
     int64_t lo = 0, hi = 0;
     bool copy_back = false;
@@ -46,9 +53,16 @@ struct View {
 bool direct_view(void *p, char **dev, bool *hbm = nullptr);
 // src and dst of one local transfer; a pageable pair whose page ranges overlap is
 // registered once as a union
+// (small pageable spans through a pinned bounce buffer: synchronous callers only)
 void local_views(void *src, int64_t slo, int64_t shi, void *dst, int64_t dlo, int64_t dhi, View &sv, View &dv);
-View local_view(void *p, int64_t lo, int64_t hi, bool is_dst = false);
-inline bool needs_sync(const View &v) { return v.registered || v.staged; }
+// bounce_ok: the caller completes the transfer before release_view and before its next
+// transfer (a small pageable span may then use the thread's pinned bounce buffer)
+View local_view(void *p, int64_t lo, int64_t hi, bool is_dst = false, bool bounce_ok = false);
+inline bool needs_sync(const View &v) { return v.registered || v.staged || v.bounce; }
+// the rows a bounced destination view's kernel writes (dst strides, count, levels, row
+// bytes): release_view copies back those rows only; without it, nothing but the view's
+// own span [lo, hi)
+void view_rows(View &v, const int *stride, const int *count, int levels, int64_t row_bytes);
 // after the kernel: copy a staged dst back, then unpin / free (stream synced by caller)
 void release_view(View &v);
 

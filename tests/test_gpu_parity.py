@@ -192,6 +192,42 @@ def test_host_memory_operands(gpu_lib, manifest, golden):
         assert same_bits_nan_aware(got, want, op), ("pinned dst", n)
 
 
+@pytest.mark.parametrize("rows,row_el", [(7, 5), (40, 33), (300, 100)])
+def test_pageable_sides_on_shared_pages(gpu_lib, oracle, rows, row_el):
+    """Source and destination patches interleaved in ONE pageable buffer (their pages
+    overlap): small spans go through the thread's pinned bounce buffer as one union, and
+    only the destination's rows are written back -- every byte outside them, including
+    the source rows and the gaps, is left as it was; above the bounce limit (the 300-row
+    case, 240 KiB) the union is registered instead.  Also a put and a get between the
+    two patches.  Exact against the oracle."""
+    op, esz = C.DBL, 8
+    row = row_el * esz
+    ld = 2 * row + 24                      # src row, gap, dst row, gap
+    buf = C.fill_bytes(op, rows * ld + 64, 77)
+    so, do = 0, row + 8                    # dst rows start 8 bytes after each src row ends
+    keep, sp = ga_amd.scale_buffer(op, C.SCALE[op])
+    want = buf.copy()
+    oracle.accs(op, C.SCALE[op], want, so, [ld], want, do, [ld], [row, rows], 1)
+    got = buf.copy()
+    assert gpu_lib.comex_accs(op, sp, ctypes.c_void_p(got.ctypes.data + so), ga_amd.int_array([ld]),
+                              ctypes.c_void_p(got.ctypes.data + do), ga_amd.int_array([ld]),
+                              ga_amd.int_array([row, rows]), 1, 0, 0) == 0
+    ga_amd.comex_fence_all()
+    assert np.array_equal(got, want), first_mismatch(got, want, op)
+    # put: src rows -> dst rows (byte copy), then get them back into the src rows' place
+    got2 = buf.copy()
+    want2 = buf.copy()
+    oracle.puts(want2, so, [ld], want2, do, [ld], [row - 3, rows], 1)
+    assert ga_amd.comex_puts(got2.ctypes.data + so, [ld], got2.ctypes.data + do, [ld], [row - 3, rows], 1, 0) == 0
+    ga_amd.comex_fence_all()
+    assert np.array_equal(got2, want2)
+    oracle.puts(want2, do + 5, [ld], want2, so + 1, [ld], [row - 9, rows], 1)
+    assert ga_amd.comex_gets(got2.ctypes.data + do + 5, [ld], got2.ctypes.data + so + 1, [ld], [row - 9, rows], 1,
+                             0) == 0
+    ga_amd.comex_fence_all()
+    assert np.array_equal(got2, want2)
+
+
 @pytest.mark.parametrize("type_code,dtype", [(0, np.float64), (1, np.float32), (2, np.int32), (3, np.int64)])
 def test_device_generator_matches_host(gpu_lib, type_code, dtype):
     n = 100003

@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Small-call latency on one rank: blocking comex_accs / puts / gets of 64 B .. 1 MiB
+(device and pinned-host sources), the non-blocking form + wait, GA's NGA_Acc / NGA_Get of
+small patches and GA_Sync.  Median of 200 calls after 20 untimed.  Looks for host-side
+costs that do not belong to the operation (as the io-vector host sort did).
+Diagnostic evidence, not the bench."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import ga_amd  # noqa: E402
+
+L = ga_amd.lib()
+
+
+def med(fn, n=200, w=20):
+    for _ in range(w):
+        fn()
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return round(ts[len(ts) // 2] * 1e6, 1)
+
+
+assert L.GA_Initialize() == 0
+dev = ga_amd.DeviceBuffer(4 << 20)
+dst = ga_amd.DeviceBuffer(4 << 20)
+pin = ga_amd.DeviceBuffer(4 << 20, host=True)
+host = np.zeros(1 << 19)
+L.gaamd_memset(ctypes.c_void_p(dev.ptr), 0, 4 << 20)
+L.gaamd_memset(ctypes.c_void_p(dst.ptr), 0, 4 << 20)
+out = {}
+for nb in (64, 4096, 65536, 1 << 20):
+    rows = max(1, nb // 4096)
+    row = nb // rows
+    cnt = [row, rows]
+    st = [row * 2]
+    out[f"accs_dev_{nb}"] = med(lambda: ga_amd.comex_accs(38, 0.5, dev.ptr, st, dst.ptr, st, cnt, 1, 0))
+    out[f"accs_pinned_{nb}"] = med(lambda: ga_amd.comex_accs(38, 0.5, pin.ptr, st, dst.ptr, st, cnt, 1, 0))
+    out[f"accs_pageable_{nb}"] = med(lambda: ga_amd.comex_accs(38, 0.5, host.ctypes.data, st, dst.ptr, st, cnt, 1, 0))
+
+    def nbw():
+        rc, h = ga_amd.comex_nbaccs(38, 0.5, dev.ptr, st, dst.ptr, st, cnt, 1, 0)
+        ga_amd.comex_wait(h)
+    out[f"nbaccs_wait_dev_{nb}"] = med(nbw)
+    out[f"puts_pageable_{nb}"] = med(lambda: ga_amd.comex_puts(host.ctypes.data, st, dst.ptr, st, cnt, 1, 0))
+    out[f"gets_pageable_{nb}"] = med(lambda: ga_amd.comex_gets(dst.ptr, st, host.ctypes.data, st, cnt, 1, 0))
+ia = ga_amd.int_array
+g = L.NGA_Create(1004, 2, ia([1024, 1024]), b"lat", None)
+buf = np.ones(64 * 64)
+one = ctypes.c_double(1.0)
+for side in (4, 16, 64):
+    out[f"NGA_Acc_{side}x{side}"] = med(lambda: L.NGA_Acc(g, ia([10, 10]), ia([9 + side, 9 + side]),
+                                                          buf.ctypes.data_as(ctypes.c_void_p), ia([side]),
+                                                          ctypes.byref(one)))
+    out[f"NGA_Get_{side}x{side}"] = med(lambda: L.NGA_Get(g, ia([10, 10]), ia([9 + side, 9 + side]),
+                                                          buf.ctypes.data_as(ctypes.c_void_p), ia([side])))
+out["GA_Sync"] = med(lambda: L.GA_Sync())
+for k, v in out.items():
+    print(json.dumps({"call": k, "median_us": v}))
+L.GA_Destroy(g)
+L.GA_Terminate()
