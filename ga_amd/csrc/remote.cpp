@@ -760,7 +760,9 @@ int remote_acc_start(int t, int op, const void *scale, void *src, const int *ss,
     int64_t dlo = 0, dhi = 0;
     side_span_host(ds, count, levels, count[0], &dlo, &dhi);
     (void)remote_view(t, dst, dlo, dhi);
-    j.sv = local_view(src, j.slo, j.shi);
+    // a small pageable source goes through the thread's pinned bounce buffer: such a job
+    // completes before the call returns (host_src below), so the buffer is free again
+    j.sv = local_view(src, j.slo, j.shi, false, true);
     j.staged_src = j.sv.staged != nullptr;
     if (j.staged_src) {
         std::lock_guard<std::mutex> g(r.launch_mu);
@@ -785,7 +787,7 @@ int remote_acc_start(int t, int op, const void *scale, void *src, const int *ss,
     if (j.nchunks > 1 && t != r.rank && dst_rows_disjoint(ds, count, levels, row_bytes))
         j.first = (uint64_t)r.rank * j.nchunks / (uint64_t)r.size;
     if (g_out.size() != (size_t)r.size) g_out.resize(r.size);
-    const bool host_src = j.sv.registered || j.sv.staged;
+    const bool host_src = j.sv.registered || j.sv.staged || j.sv.bounce;
     g_jobs.push_back(j);
     const int id = j.id;
     progress_jobs();

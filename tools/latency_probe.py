@@ -32,6 +32,7 @@ def med(fn, n=200, w=20):
 
 
 assert L.GA_Initialize() == 0
+ME = L.GA_Nodeid()   # the local calls target this rank
 dev = ga_amd.DeviceBuffer(4 << 20)
 dst = ga_amd.DeviceBuffer(4 << 20)
 pin = ga_amd.DeviceBuffer(4 << 20, host=True)
@@ -44,16 +45,16 @@ for nb in (64, 4096, 65536, 1 << 20):
     row = nb // rows
     cnt = [row, rows]
     st = [row * 2]
-    out[f"accs_dev_{nb}"] = med(lambda: ga_amd.comex_accs(38, 0.5, dev.ptr, st, dst.ptr, st, cnt, 1, 0))
-    out[f"accs_pinned_{nb}"] = med(lambda: ga_amd.comex_accs(38, 0.5, pin.ptr, st, dst.ptr, st, cnt, 1, 0))
-    out[f"accs_pageable_{nb}"] = med(lambda: ga_amd.comex_accs(38, 0.5, host.ctypes.data, st, dst.ptr, st, cnt, 1, 0))
+    out[f"accs_dev_{nb}"] = med(lambda: ga_amd.comex_accs(38, 0.5, dev.ptr, st, dst.ptr, st, cnt, 1, ME))
+    out[f"accs_pinned_{nb}"] = med(lambda: ga_amd.comex_accs(38, 0.5, pin.ptr, st, dst.ptr, st, cnt, 1, ME))
+    out[f"accs_pageable_{nb}"] = med(lambda: ga_amd.comex_accs(38, 0.5, host.ctypes.data, st, dst.ptr, st, cnt, 1, ME))
 
     def nbw():
-        rc, h = ga_amd.comex_nbaccs(38, 0.5, dev.ptr, st, dst.ptr, st, cnt, 1, 0)
+        rc, h = ga_amd.comex_nbaccs(38, 0.5, dev.ptr, st, dst.ptr, st, cnt, 1, ME)
         ga_amd.comex_wait(h)
     out[f"nbaccs_wait_dev_{nb}"] = med(nbw)
-    out[f"puts_pageable_{nb}"] = med(lambda: ga_amd.comex_puts(host.ctypes.data, st, dst.ptr, st, cnt, 1, 0))
-    out[f"gets_pageable_{nb}"] = med(lambda: ga_amd.comex_gets(dst.ptr, st, host.ctypes.data, st, cnt, 1, 0))
+    out[f"puts_pageable_{nb}"] = med(lambda: ga_amd.comex_puts(host.ctypes.data, st, dst.ptr, st, cnt, 1, ME))
+    out[f"gets_pageable_{nb}"] = med(lambda: ga_amd.comex_gets(dst.ptr, st, host.ctypes.data, st, cnt, 1, ME))
 ia = ga_amd.int_array
 g = L.NGA_Create(1004, 2, ia([1024, 1024]), b"lat", None)
 buf = np.ones(64 * 64)
@@ -65,6 +66,22 @@ for side in (4, 16, 64):
     out[f"NGA_Get_{side}x{side}"] = med(lambda: L.NGA_Get(g, ia([10, 10]), ia([9 + side, 9 + side]),
                                                           buf.ctypes.data_as(ctypes.c_void_p), ia([side])))
 out["GA_Sync"] = med(lambda: L.GA_Sync())
+if L.GA_Nnodes() > 1:
+    # remote owner: rank 0 accumulates into / gets from a patch at the corner of the last
+    # rank's block; the others wait at the sync
+    me, last = L.GA_Nodeid(), L.GA_Nnodes() - 1
+    blo, bhi = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
+    L.NGA_Distribution(g, last, blo, bhi)            # the last rank's block
+    for side in (4, 16, 64):
+        lo, hi = ia([blo[0], blo[1]]), ia([blo[0] + side - 1, blo[1] + side - 1])
+        if me == 0:
+            out[f"remote_NGA_Acc_{side}x{side}"] = med(lambda: L.NGA_Acc(g, lo, hi, buf.ctypes.data_as(ctypes.c_void_p),
+                                                                         ia([side]), ctypes.byref(one)))
+            out[f"remote_NGA_Get_{side}x{side}"] = med(lambda: L.NGA_Get(g, lo, hi, buf.ctypes.data_as(ctypes.c_void_p),
+                                                                         ia([side])))
+        L.GA_Sync()
+if L.GA_Nodeid() != 0:
+    out = {}
 for k, v in out.items():
     print(json.dumps({"call": k, "median_us": v}))
 L.GA_Destroy(g)
