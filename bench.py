@@ -974,7 +974,7 @@ def main():
     ap.add_argument("--exchange", action="store_true",
                     help="N>1: rank r accumulates into rank r+1's partition (remote path, SURVEY 8(d) M2)")
     ap.add_argument("--streams", type=int, default=0,
-                    help="library HIP streams (COMEX_AMD_STREAMS; 0 = the library default, 2)")
+                    help="library HIP streams (COMEX_AMD_STREAMS; 0 = the library default: 2, or 1 when ranks share the GPU)")
     ap.add_argument("--self-packed", action="store_true",
                     help="N=1: force the packed route for accumulates to self (COMEX_ENABLE_ACC_SELF/SMP=0)")
     ap.add_argument("--src-seg", action="store_true",

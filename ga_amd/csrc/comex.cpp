@@ -698,8 +698,18 @@ int comex_init() {
         // different peers (different xGMI links) are applied side by side
         const char *ps = getenv("COMEX_AMD_PULL_STREAMS");
         const int pull = std::min(peers, ps ? atoi(ps) : 6);
+        // 2 library streams: independent ops overlap kernel edges; 1 when
+        // other ranks of the job share this GPU: their processes fill it anyway, and two
+        // streams per process made a small blocking call wait 55-80 us for its kernel
+        // instead of 13-15 and lowered the aggregate rate by 2-8 % (2 and 4 ranks on one
+        // GPU, profiles/r05/lat7/)
+        // (ranks read as another GPU's, COMEX_AMD_PEER_LOADS=all, are counted as such: the
+        // one-GPU proxy of a multi-GPU node keeps that node's two streams)
+        int sharing = 0;
+        for (int q = 0; q < r.size; ++q)
+            if (q != r.rank && r.same_dev[q] && !r.peer_src(q)) ++sharing;
         const char *ns = getenv("COMEX_AMD_STREAMS");
-        sched_init(ns ? atoi(ns) : 2, pull);   // 2: independent ops overlap kernel edges
+        sched_init(ns ? atoi(ns) : (sharing ? 1 : 2), pull);
         const char *op1 = getenv("COMEX_AMD_ONE_PASS");
         r.one_pass = false;
         if (!op1 || atoi(op1) != 0)

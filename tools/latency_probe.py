@@ -40,7 +40,18 @@ host = np.zeros(1 << 19)
 L.gaamd_memset(ctypes.c_void_p(dev.ptr), 0, 4 << 20)
 L.gaamd_memset(ctypes.c_void_p(dst.ptr), 0, 4 << 20)
 out = {}
-for nb in (64, 4096, 65536, 1 << 20):
+BUSY = ME == 0 or not os.environ.get("LAT_ONLY_RANK0")   # LAT_ONLY_RANK0: the other ranks idle
+if os.environ.get("LAT_STAMPS") and BUSY:
+    # where one small blocking call's time goes: gaamd_diag("stamps") of the last call
+    # ([0] entry, [1] route decided, [2] stream picked, [3] kernel launched, [4] return)
+    L.gaamd_diag(b"stamps", 1, None, 0)
+    for _ in range(50):
+        ga_amd.comex_accs(38, 0.5, dev.ptr, [128], dst.ptr, [128], [64, 1], 1, ME)
+    st8 = (ctypes.c_ulonglong * 8)()
+    L.gaamd_diag(b"stamps", -1, st8, 8)
+    out["stamps_us"] = [round((st8[i] - st8[0]) / 1e3, 1) for i in range(5)]
+    L.gaamd_diag(b"stamps", 0, None, 0)
+for nb in ((64, 4096, 65536, 1 << 20) if BUSY else ()):
     rows = max(1, nb // 4096)
     row = nb // rows
     cnt = [row, rows]
@@ -59,7 +70,7 @@ ia = ga_amd.int_array
 g = L.NGA_Create(1004, 2, ia([1024, 1024]), b"lat", None)
 buf = np.ones(64 * 64)
 one = ctypes.c_double(1.0)
-for side in (4, 16, 64):
+for side in ((4, 16, 64) if BUSY else ()):
     out[f"NGA_Acc_{side}x{side}"] = med(lambda: L.NGA_Acc(g, ia([10, 10]), ia([9 + side, 9 + side]),
                                                           buf.ctypes.data_as(ctypes.c_void_p), ia([side]),
                                                           ctypes.byref(one)))
