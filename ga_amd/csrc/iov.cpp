@@ -86,6 +86,30 @@ static bool ranges_overlap(std::vector<std::pair<uint64_t, uint64_t>> v) {
     return false;
 }
 
+// Does any destination repeat?  The destinations are congruent (whole pairs from dlo)
+// and fewer than kIovRunsMin: an open-addressing set of their unit indices in a
+// thread-local table, a few ns per pair where sorting the pairs took 20-100 us at
+// 1-2 Ki pairs.
+static bool has_repeat(const uint64_t *dst, int n, uint64_t dlo, int bytes) {
+    static thread_local std::vector<uint64_t> tab;
+    uint32_t P = 64;
+    while (P < 2u * (uint32_t)n) P <<= 1;
+    tab.assign(P, 0u);   // 0: empty; unit index + 1 stored
+    const bool pow2 = (bytes & (bytes - 1)) == 0;
+    const int shift = pow2 ? __builtin_ctz((unsigned)bytes) : 0;
+    for (int i = 0; i < n; ++i) {
+        const uint64_t off = dst[i] - dlo;
+        const uint64_t key = (pow2 ? off >> shift : off / (uint64_t)bytes) + 1u;
+        uint32_t h = ((uint32_t)key * 0x9E3779B1u) & (P - 1);
+        while (tab[h] != 0) {
+            if (tab[h] == key) return true;
+            h = (h + 1) & (P - 1);
+        }
+        tab[h] = key;
+    }
+    return false;
+}
+
 static bool any_cross_overlap(std::vector<std::pair<uint64_t, uint64_t>> a, std::vector<std::pair<uint64_t, uint64_t>> b) {
     std::sort(a.begin(), a.end());
     std::sort(b.begin(), b.end());
@@ -279,6 +303,8 @@ static void translate_range(const uint64_t *in, int64_t delta, uint64_t *u, long
 // pairs): whole calls of 4095 pairs took 0.107 ms through the host check against 0.031
 // for 4096 on the GPU path, 2048 pairs 0.032 (profiles/r05/iovmid/)
 constexpr int kIovRunsMin = 2048;
+// io-vectors with at most this many bytes of lists and packed sources skip the upload
+constexpr size_t kIovZeroCopyMax = 64 << 10;
 // io-vectors from this many pairs try the whole-side host test (host_cpu_range)
 constexpr int kIovMapsMin = 65536;
 
@@ -387,8 +413,12 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
             serial = true;
         } else if (dst_seq) {
             // one contiguous vector of destinations in pair order: none repeats or overlaps
-        } else if (n >= kIovRunsMin && congruent && bytes <= kIovRunsMaxBytes && units <= (1ull << 32)) {
-            runs = true;   // repeated destinations are ordered on the GPU
+        } else if (congruent && bytes <= kIovRunsMaxBytes && units <= (1ull << 32)) {
+            // destinations on a grid of whole pairs overlap only by repeating: from
+            // kIovRunsMin pairs, or when a host hash check finds a repeat among fewer, the
+            // GPU orders them (before, a small scatter with one repeated destination went
+            // to the one-lane serial kernel)
+            runs = n >= kIovRunsMin || has_repeat(dst, n, dlo, bytes);
         } else {
             std::vector<std::pair<uint64_t, uint64_t>> dr((size_t)n);
             for (int i = 0; i < n; ++i) dr[i] = {dst[i], dst[i] + (uint64_t)bytes};
@@ -425,7 +455,17 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     // GPU-ordered path the hashed insert copies the lists itself (one launch less), so only
     // packed sources go up here -- and everything, should that path decline (rc 1 below)
     const size_t up_lo = (dst_listed && dst_seq) ? o_src : 0, up_hi = (src_listed && src_seq) ? o_src : o_res;
-    if (runs) {
+    // a small io-vector (at most 64 KiB of lists and packed sources, pairs of at most two
+    // 16-byte vectors, no one-lane serial order) is read by its kernel straight from the
+    // pinned staging through its device mapping: one launch instead of upload + apply
+    const bool zero_copy = !runs && !serial && up_hi - up_lo <= kIovZeroCopyMax && bytes <= 32;
+    if (zero_copy) {
+        char *up_dev = nullptr;
+        GA_HIP(hipHostGetDevicePointer((void **)&up_dev, up, 0));
+        if (d.src_list) d.src_list = (const uint64_t *)(up_dev + o_src);
+        else if (!src_listed) d.src_base = up_dev + o_src;
+        if (d.dst_list) d.dst_list = (const uint64_t *)(up_dev + o_dst);
+    } else if (runs) {
         if (!src_listed && o_res > o_src) upload_pinned(dev + o_src, up + o_src, o_res - o_src, r.streams[si]);
     } else if (up_hi > up_lo) {
         upload_pinned(dev + up_lo, up + up_lo, up_hi - up_lo, r.streams[si]);
@@ -706,11 +746,11 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
             // repeated destinations: the owner orders them on its GPU when every destination
             // is a whole number of pairs from dlo, else a host check picks the serial kernel
             int mode = 0;
-            bool congruent = m >= kIovRunsMin && bytes <= kIovRunsMaxBytes &&
-                             (dhi - dlo) / (uint64_t)bytes < (1ull << 32);
+            bool congruent = bytes <= kIovRunsMaxBytes && (dhi - dlo) / (uint64_t)bytes < (1ull << 32);
             for (int i = 0; i < m && congruent; ++i) congruent = (dv[(size_t)i0 + i] - dlo) % (uint64_t)bytes == 0;
             if (congruent) {
-                mode = 2;
+                // the owner orders repeats on its GPU; fewer pairs with none go plain
+                mode = (m >= kIovRunsMin || has_repeat(dv + i0, m, dlo, bytes)) ? 2 : 0;
             } else {
                 std::vector<std::pair<uint64_t, uint64_t>> dr((size_t)m);
                 for (int i = 0; i < m; ++i) dr[i] = {dv[(size_t)i0 + i], dv[(size_t)i0 + i] + (uint64_t)bytes};

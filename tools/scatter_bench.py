@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--src", default="dev", choices=["dev", "host"])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--slots", type=int, default=0,
+                    help="destinations drawn from this many f64 slots (repeats) instead of the whole 1 GiB")
     ap.add_argument("--ga", action="store_true",
                     help="NGA_Scatter_acc_flat / NGA_Gather_flat of n elements of a 16384^2 f64 GA (host v)")
     args = ap.parse_args()
@@ -48,7 +50,7 @@ def main():
     rng = np.random.default_rng(7)
     keep_s, sp = ga_amd.scale_buffer(DBL, ALPHA)
     for n in [int(x) for x in args.pairs.split(",")]:
-        idx = rng.integers(0, region // 8, n).astype(np.uint64)
+        idx = rng.integers(0, args.slots or region // 8, n).astype(np.uint64)
         dups = n - len(np.unique(idx))
         v = rng.random(n)
         if args.src == "dev":

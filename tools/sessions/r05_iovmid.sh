@@ -3,7 +3,7 @@
 set -o pipefail
 out=gpurun_out/r05iovmid
 mkdir -p $out
-timeout -k 10 200 python3 tools/scatter_bench.py --pairs 256,512,1024,2047,2048,3000,4095,4096,8192 --steps 50 > $out/accv_$TAG.jsonl 2> $out/accv_$TAG.err || { tail -5 $out/accv_$TAG.err; exit 11; }
+timeout -k 10 200 python3 tools/scatter_bench.py --pairs 16,64,256,512,1024,2047,2048,4096,8192 --steps 50 > $out/accv_$TAG.jsonl 2> $out/accv_$TAG.err || { tail -5 $out/accv_$TAG.err; exit 11; }
 python3 -c "
 import json
 for l in open('$out/accv_$TAG.jsonl'):
