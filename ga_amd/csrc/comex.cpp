@@ -453,7 +453,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         // put: remote dst / get: remote src, through the owner's IPC mapping
         fence_target(world);   // order after our own pending accumulates to it
         if (kind == X_PUT) {
-            sv = local_view(src, slo, shi, false, true);
+            sv = local_view(src, slo, shi, false, true, hdl != nullptr);
             dv.dev = remote_view(world, dst, dlo, dhi);
             dv.hbm = segment_kind_of(world, (const char *)dst + dlo) == 1;
         } else {
@@ -462,7 +462,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
             dv = local_view(dst, dlo, dhi, true, true);
         }
     } else {
-        local_views(src, slo, shi, dst, dlo, dhi, sv, dv);
+        local_views(src, slo, shi, dst, dlo, dhi, sv, dv, hdl != nullptr);
     }
     if (dv.bounce) view_rows(dv, ds, count, levels, kind == X_ACC ? rb : count[0]);
     // a pageable side in this thread's pinned bounce buffer, or pinned for this call, is
@@ -501,7 +501,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         // sooner than the runtime's signal; for a bounced source it also says the kernel
         // has read the bounce buffer); otherwise the runtime's sync, whose system-scope
         // release makes a host-memory destination's bytes visible
-        if (dv.hbm && (sv.hbm || sv.bounce || sv.registered)) sched_wait_flag(si);
+        if (dv.hbm) sched_wait_flag(si);
         else GA_HIP(hipStreamSynchronize(st));
     }
     if (world != r.rank && !synced && !r.direct_pending.empty()) r.direct_pending[world] = 1;
@@ -514,7 +514,10 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
         release_view(sv);
         release_view(dv);
     }
-    if (hdl) nb_complete_now(hdl, si, true);
+    if (hdl) {
+        nb_complete_now(hdl, si, true);
+        if (sv.ring) ring_commit(si, r.nb_seq[*hdl]);
+    }
     stamp(4);
     return COMEX_SUCCESS;
 }

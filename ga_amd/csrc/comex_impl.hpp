@@ -47,6 +47,7 @@ struct View {
     int64_t lo = 0, hi = 0;
     bool copy_back = false;
     bool hbm = false;             // device memory the CPU never touches (HBM segment or hipMalloc)
+    bool ring = false;            // a pageable source copied into the thread's nb ring (ring_view)
 };
 // device-visible without help (our segments, HBM, managed, pinned/registered host);
 // *hbm (optional): the memory is HBM (not managed, not host)
@@ -54,10 +55,18 @@ bool direct_view(void *p, char **dev, bool *hbm = nullptr);
 // src and dst of one local transfer; a pageable pair whose page ranges overlap is
 // registered once as a union
 // (small pageable spans through a pinned bounce buffer: synchronous callers only)
-void local_views(void *src, int64_t slo, int64_t shi, void *dst, int64_t dlo, int64_t dhi, View &sv, View &dv);
+// ring_src: a non-blocking call -- a small pageable source with a direct destination goes
+// through the thread's ring (ring_view), and the call need not wait for its kernel
+void local_views(void *src, int64_t slo, int64_t shi, void *dst, int64_t dlo, int64_t dhi, View &sv, View &dv,
+                 bool ring_src = false);
 // bounce_ok: the caller completes the transfer before release_view and before its next
 // transfer (a small pageable span may then use the thread's pinned bounce buffer)
-View local_view(void *p, int64_t lo, int64_t hi, bool is_dst = false, bool bounce_ok = false);
+// ring_ok: a non-blocking call's source (ring_view)
+View local_view(void *p, int64_t lo, int64_t hi, bool is_dst = false, bool bounce_ok = false, bool ring_ok = false);
+// a small pageable source [p + lo, p + hi) copied into this thread's pinned ring (false: too
+// large); ring_commit then names the operation that reads it (stream, sched_track sequence)
+bool ring_view(View &v, void *p, int64_t lo, int64_t hi);
+void ring_commit(int stream, uint64_t seq);
 inline bool needs_sync(const View &v) { return v.registered || v.staged || v.bounce; }
 // the rows a bounced destination view's kernel writes (dst strides, count, levels, row
 // bytes): release_view copies back those rows only; without it, nothing but the view's

@@ -272,6 +272,8 @@ void sched_sync_all();
 // stream s; whether op `seq` of stream s has completed (waiting for it if `wait`)
 uint64_t sched_track(int s);
 bool sched_complete(int s, uint64_t seq, bool wait);
+// bumped by sched_init: sequence numbers of an earlier epoch were drained (finalize, resize)
+uint64_t sched_epoch();
 
 // wire.cpp: the host fallback between nodes (MPI-PR message protocol over TCP)
 void wire_init();                                   // collective; no-op on one node

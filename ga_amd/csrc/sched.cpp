@@ -25,6 +25,7 @@
 // Callers hold Runtime::launch_mu around pick + launch.  The completion marks
 // have their own lock (g_marks_mu): sched_track / sched_complete run outside
 // launch_mu, and a wait on an event is done with the lock released.
+#include <atomic>
 #include "runtime.hpp"
 #include "gaamd_kernels.h"
 #include <string.h>
@@ -123,8 +124,12 @@ bool sched_complete(int s, uint64_t seq, bool wait) {
     return m.done >= seq;
 }
 
+static std::atomic<uint64_t> g_epoch{0};
+uint64_t sched_epoch() { return g_epoch.load(std::memory_order_relaxed); }
+
 void sched_init(int n, int pull) {
     Runtime &r = rt();
+    g_epoch.fetch_add(1, std::memory_order_relaxed);
     if (n < 1) n = 1;
     if (n > 8) n = 8;
     if (pull < 0) pull = 0;

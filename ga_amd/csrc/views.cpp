@@ -9,6 +9,7 @@
 #include "comex_impl.hpp"
 #include <string.h>
 #include <algorithm>
+#include <deque>
 
 namespace gaamd {
 
@@ -128,6 +129,78 @@ static void write_back_rows(const View &v) {
     }
 }
 
+// Non-blocking calls from small pageable sources: the bytes are copied into a per-thread
+// pinned ring and the call returns with its kernel queued, as for a device source (ComEx
+// lets the caller reuse the source only after the wait; here it may at once).  Before a
+// ring range is written again, the operations that read it have completed.  Through the
+// one-call bounce buffer above, such a call waited for its kernel: 11 us per
+// comex_nbaccs of 64 B-4 KiB against 4 from HBM (profiles/r05/small/).
+constexpr int64_t kRingBytes = 4 << 20, kRingMax = 64 << 10, kRingAlign = 256;
+namespace {
+struct RingUse {
+    int64_t off, end;   // [off, end) of the ring
+    int stream;
+    uint64_t seq, epoch;
+};
+struct NbRing {
+    char *host = nullptr, *dev = nullptr;
+    int64_t head = 0;          // next free byte
+    int64_t pend_off = -1, pend_end = 0;   // taken by ring_view, not yet committed
+    std::deque<RingUse> q;     // oldest first
+};
+thread_local NbRing t_ring;
+
+void ring_retire(NbRing &g) {
+    const RingUse u = g.q.front();
+    g.q.pop_front();
+    if (u.epoch == sched_epoch()) (void)sched_complete(u.stream, u.seq, true);   // else drained at finalize
+}
+
+// does [a, b) meet the ring bytes still in use ([front.off, head), circularly)?
+bool ring_busy(const NbRing &g, int64_t a, int64_t b) {
+    if (g.q.empty()) return false;
+    const int64_t t = g.q.front().off, h = g.head;
+    if (t < h) return a < h && t < b;
+    return a < h || t < b;   // wrapped (or full): [t, end of ring) and [0, h)
+}
+}  // namespace
+
+bool ring_view(View &v, void *p, int64_t lo, int64_t hi) {
+    const int64_t n = hi - lo;
+    if (n <= 0 || n > kRingMax) return false;
+    NbRing &g = t_ring;
+    if (!g.host) {
+        GA_HIP(hipHostMalloc((void **)&g.host, kRingBytes, hipHostMallocMapped));
+        GA_HIP(hipHostGetDevicePointer((void **)&g.dev, g.host, 0));
+    }
+    if (g.q.empty()) g.head = 0;
+    // the copy keeps the source's offset within kRingAlign (the kernel's vector width
+    // follows the src/dst alignment)
+    const int64_t mis = (int64_t)(((uintptr_t)p + lo) % kRingAlign);
+    const int64_t need = (mis + n + kRingAlign - 1) / kRingAlign * kRingAlign;
+    int64_t off = g.head;
+    if (off + need > kRingBytes) off = 0;
+    while (ring_busy(g, off, off + need)) ring_retire(g);
+    if (g.q.empty()) g.head = off;   // everything retired: the live region restarts here
+    g.pend_off = off;
+    g.pend_end = off + need;
+    g.head = off + need;
+    memcpy(g.host + off + mis, (char *)p + lo, (size_t)n);
+    v.host = (char *)p;
+    v.lo = lo;
+    v.hi = hi;
+    v.ring = true;
+    v.dev = g.dev + off + mis - lo;
+    return true;
+}
+
+void ring_commit(int stream, uint64_t seq) {
+    NbRing &g = t_ring;
+    if (g.pend_off < 0) return;
+    g.q.push_back({g.pend_off, g.pend_end, stream, seq, sched_epoch()});
+    g.pend_off = -1;
+}
+
 static void stage_view(View &v, void *p, int64_t lo, int64_t hi, bool is_dst) {
     Runtime &r = rt();
     v.host = (char *)p;
@@ -142,7 +215,7 @@ static void stage_view(View &v, void *p, int64_t lo, int64_t hi, bool is_dst) {
 // resolve src and dst of one local transfer; a pageable pair whose page
 // ranges overlap is registered once as a union
 void local_views(void *src, int64_t slo, int64_t shi, void *dst, int64_t dlo, int64_t dhi,
-                        View &sv, View &dv) {
+                        View &sv, View &dv, bool ring_src) {
     char *d = nullptr;
     const bool sd = direct_view(src, &d, &sv.hbm);
     if (sd) sv.dev = d;
@@ -183,7 +256,8 @@ void local_views(void *src, int64_t slo, int64_t shi, void *dst, int64_t dlo, in
     }
     char *base = nullptr;
     if (!sd) {
-        if (shi - slo <= kBounceMax) bounce_view(sv, src, slo, shi, false, 0);
+        if (ring_src && dd && ring_view(sv, src, slo, shi)) {}   // the destination needs no sync either
+        else if (shi - slo <= kBounceMax) bounce_view(sv, src, slo, shi, false, 0);
         else if (register_range(s0, s1, &base)) { sv.registered = (void *)s0; sv.dev = base + ((uintptr_t)src - s0); }
         else stage_view(sv, src, slo, shi, false);
     }
@@ -194,10 +268,11 @@ void local_views(void *src, int64_t slo, int64_t shi, void *dst, int64_t dlo, in
     }
 }
 
-View local_view(void *p, int64_t lo, int64_t hi, bool is_dst, bool bounce_ok) {
+View local_view(void *p, int64_t lo, int64_t hi, bool is_dst, bool bounce_ok, bool ring_ok) {
     View v;
     char *d = nullptr;
     if (direct_view(p, &d, &v.hbm)) { v.dev = d; return v; }
+    if (ring_ok && !is_dst && ring_view(v, p, lo, hi)) return v;
     if (bounce_ok && hi - lo <= kBounceMax) {
         bounce_view(v, p, lo, hi, is_dst, is_dst ? 1 : 0);
         return v;

@@ -228,6 +228,63 @@ def test_pageable_sides_on_shared_pages(gpu_lib, oracle, rows, row_el):
     assert np.array_equal(got2, want2)
 
 
+def test_nb_pageable_sources_through_ring(gpu_lib, oracle):
+    """Non-blocking accumulates and puts from ONE pageable buffer, refilled right after
+    every call: a small source is copied into the thread's pinned ring and the call
+    returns with its kernel queued (views.cpp ring_view), so each kernel must read the
+    bytes of its own call.  About 10 MiB of sources in 4 MiB of ring (several laps and
+    wrap gaps), destinations overlapping earlier calls (issue order), handles waited at
+    random, sources above the ring's 64 KiB limit on the synchronous route.  Exact
+    against the oracle applied in issue order."""
+    op, esz = C.DBL, 8
+    rng = np.random.default_rng(C.SEED + 901)
+    D = 6 << 20
+    dst0 = C.fill_bytes(op, D, 91)
+    db = ga_amd.DeviceBuffer(D)
+    db.upload(dst0)
+    want = dst0.copy()
+    src = np.zeros(200 << 10, dtype=np.uint8)          # pageable, reused by every call
+    handles = []
+    for k in range(320):
+        big = k % 37 == 5
+        row = int(rng.integers(1, 40 if not big else 200)) * esz
+        rows = int(rng.integers(1, 24))
+        ld = row + int(rng.integers(0, 6)) * esz
+        span = (rows - 1) * ld + row
+        if not big:
+            while span > (64 << 10) - 512:
+                rows = max(1, rows // 2)
+                span = (rows - 1) * ld + row
+        so = int(rng.integers(0, 32)) * esz
+        src[:] = 0
+        src[so:so + span] = C.fill_bytes(op, span, 1000 + k)
+        dld = row + int(rng.integers(0, 9)) * esz
+        dspan = (rows - 1) * dld + row
+        do = int(rng.integers(0, (D - dspan) // esz)) * esz
+        if k % 5 == 4:
+            do = int(rng.integers(0, 4096)) * esz                        # a region many calls hit
+        put = k % 7 == 3
+        if put:
+            oracle.puts(src, so, [ld], want, do, [dld], [row, rows], 1)
+            h = ctypes.c_int(-1)
+            rc = gpu_lib.comex_nbputs(ctypes.c_void_p(src.ctypes.data + so), ga_amd.int_array([ld]),
+                                      ctypes.c_void_p(db.ptr + do), ga_amd.int_array([dld]),
+                                      ga_amd.int_array([row, rows]), 1, 0, 0, ctypes.byref(h))
+        else:
+            oracle.accs(op, C.SCALE[op], src, so, [ld], want, do, [dld], [row, rows], 1)
+            rc, h = ga_amd.comex_nbaccs(op, C.SCALE[op], src.ctypes.data + so, [ld], db.ptr + do, [dld],
+                                        [row, rows], 1, 0)
+        assert rc == 0
+        src[:] = 0xAB                                     # the call's bytes are gone from the source
+        handles.append(h)
+        if rng.random() < 0.1 and handles:
+            assert ga_amd.comex_wait(handles.pop(int(rng.integers(0, len(handles))))) == 0
+    assert gpu_lib.comex_wait_all(0) == 0
+    got = db.download(np.uint8, D)
+    db.free()
+    assert np.array_equal(got, want), first_mismatch(got, want, op)
+
+
 @pytest.mark.parametrize("type_code,dtype", [(0, np.float64), (1, np.float32), (2, np.int32), (3, np.int64)])
 def test_device_generator_matches_host(gpu_lib, type_code, dtype):
     n = 100003

@@ -1,0 +1,75 @@
+// small_call_probe.cpp -- small ComEx calls from C (no Python in the timing): the blocking
+// comex_accs / comex_acc per call, and the issue rate of many non-blocking comex_nbaccs
+// (K calls to distinct destinations, then comex_wait_all), from HBM, pinned and pageable
+// sources.  GA codes that accumulate many small patches (NGA_NbAcc, task-parallel Fock
+// builds) pay the per-call issue cost, not the blocking latency.  Diagnostic evidence.
+// Build: g++ -O2 -std=c++17 tools/small_call_probe.cpp -Iinclude -Lga_amd -lga_amd
+//          -Wl,-rpath,'$ORIGIN/../ga_amd' -o tools/small_call_probe
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <algorithm>
+#include <chrono>
+#include <vector>
+#include "comex.h"
+#include "ga_amd.h"
+
+static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static double median(std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+}
+
+int main(int argc, char **argv) {
+    const int K = argc > 1 ? atoi(argv[1]) : 1024;   // non-blocking calls per batch
+    if (comex_init() != COMEX_SUCCESS) return 1;
+    const size_t span = (size_t)64 << 20;
+    char *dev = (char *)gaamd_dev_malloc(span), *dst = (char *)gaamd_dev_malloc(span);
+    char *pin = (char *)gaamd_host_malloc(1 << 20);
+    std::vector<double> host_vec(1 << 17, 1.0);
+    char *host = (char *)host_vec.data();
+    if (!dev || !dst || !pin) return 2;
+    gaamd_memset(dev, 0, span);
+    gaamd_memset(dst, 0, span);
+    memset(pin, 0, 1 << 20);
+    double alpha = 0.5;
+    struct Src { const char *name; char *p; } srcs[3] = {{"dev", dev}, {"pinned", pin}, {"pageable", host}};
+    for (int bytes : {64, 512, 4096}) {
+        int count[1] = {bytes}, stride[1] = {bytes};
+        for (const Src &s : srcs) {
+            // blocking, one destination
+            std::vector<double> t;
+            for (int i = 0; i < 220; ++i) {
+                const double t0 = now_us();
+                comex_accs(COMEX_ACC_DBL, &alpha, s.p, stride, dst, stride, count, 0, 0, COMEX_GROUP_WORLD);
+                if (i >= 20) t.push_back(now_us() - t0);
+            }
+            printf("{\"call\": \"accs_blocking\", \"src\": \"%s\", \"bytes\": %d, \"median_us\": %.2f}\n",
+                   s.name, bytes, median(t));
+            // non-blocking: K calls to distinct destinations (a 4 KiB pitch), then wait_all
+            std::vector<double> issue, total;
+            for (int rep = 0; rep < 12; ++rep) {
+                const double t0 = now_us();
+                for (int k = 0; k < K; ++k) {
+                    comex_request_t h;
+                    comex_nbaccs(COMEX_ACC_DBL, &alpha, s.p, stride, dst + (size_t)k * 4096, stride, count, 0, 0,
+                                 COMEX_GROUP_WORLD, &h);
+                }
+                const double t1 = now_us();
+                comex_wait_all(COMEX_GROUP_WORLD);
+                const double t2 = now_us();
+                if (rep >= 2) {
+                    issue.push_back((t1 - t0) / K);
+                    total.push_back((t2 - t0) / K);
+                }
+            }
+            printf("{\"call\": \"nbaccs_x%d_wait_all\", \"src\": \"%s\", \"bytes\": %d, \"issue_us_per_call\": %.2f, "
+                   "\"total_us_per_call\": %.2f}\n", K, s.name, bytes, median(issue), median(total));
+        }
+    }
+    comex_finalize();
+    return 0;
+}
