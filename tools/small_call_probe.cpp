@@ -70,6 +70,27 @@ int main(int argc, char **argv) {
                    "\"total_us_per_call\": %.2f}\n", K, s.name, bytes, median(issue), median(total));
         }
     }
+    // where one non-blocking call's host time goes: the library's stamps of each call
+    // (0 entry, 1 launch lock taken, 2 stream picked, 3 kernel launched, 4 return)
+    for (const Src &s : srcs) {
+        int count[1] = {64}, stride[1] = {64};
+        unsigned long long st[8];
+        std::vector<double> d[4];
+        gaamd_diag("stamps", 1, nullptr, 0);
+        for (int i = 0; i < 600; ++i) {
+            comex_request_t h;
+            comex_nbaccs(COMEX_ACC_DBL, &alpha, s.p, stride, dst + (size_t)(i % 200) * 4096, stride, count, 0, 0,
+                         COMEX_GROUP_WORLD, &h);
+            gaamd_diag("stamps", -1, st, 8);
+            if (i >= 100)
+                for (int k = 0; k < 4; ++k) d[k].push_back((double)(st[k + 1] - st[k]) / 1e3);
+            if (i % 200 == 199) comex_wait_all(COMEX_GROUP_WORLD);
+        }
+        gaamd_diag("stamps", 0, nullptr, 0);
+        printf("{\"call\": \"nbaccs_stamps\", \"src\": \"%s\", \"bytes\": 64, \"entry_to_lock_us\": %.2f, "
+               "\"lock_to_pick_us\": %.2f, \"pick_to_launched_us\": %.2f, \"launched_to_return_us\": %.2f}\n",
+               s.name, median(d[0]), median(d[1]), median(d[2]), median(d[3]));
+    }
     comex_finalize();
     return 0;
 }
