@@ -24,7 +24,9 @@ static double median(std::vector<double> v) {
 }
 
 int main(int argc, char **argv) {
-    const int K = argc > 1 ? atoi(argv[1]) : 1024;   // non-blocking calls per batch
+    // non-blocking calls per batch: 48 leaves the queue unfilled (the host's issue cost),
+    // 1024 fills it (the rate the GPU retires them)
+    const int K = argc > 1 ? atoi(argv[1]) : 48;
     if (comex_init() != COMEX_SUCCESS) return 1;
     const size_t span = (size_t)64 << 20;
     char *dev = (char *)gaamd_dev_malloc(span), *dst = (char *)gaamd_dev_malloc(span);
@@ -51,7 +53,7 @@ int main(int argc, char **argv) {
                    s.name, bytes, median(t));
             // non-blocking: K calls to distinct destinations (a 4 KiB pitch), then wait_all
             std::vector<double> issue, total;
-            for (int rep = 0; rep < 12; ++rep) {
+            for (int rep = 0; rep < (K < 100 ? 100 : 12); ++rep) {
                 const double t0 = now_us();
                 for (int k = 0; k < K; ++k) {
                     comex_request_t h;
