@@ -42,6 +42,22 @@ def lib():
     return load()
 
 
+def build_id():
+    """sha256 of the sources libga_amd.so was compiled from (gaamd_build_id)."""
+    return lib().gaamd_build_id().decode()
+
+
+def check_build():
+    """Raise when libga_amd.so was not built from the sources beside it (a stale
+    prebuilt library shipped with a newer tree); returns the build id."""
+    from .provenance import tree_hash
+    built, tree = build_id(), tree_hash()
+    if built != tree:
+        raise RuntimeError(f"libga_amd.so is stale: built from sources {built[:16]}..., the tree here is "
+                           f"{tree[:16]}... -- rebuild it (make -C ga_amd/csrc)")
+    return built
+
+
 def int_array(vals):
     vals = list(vals) if vals is not None else []
     arr = (ctypes.c_int * max(1, len(vals)))(*vals)

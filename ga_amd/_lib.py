@@ -315,6 +315,7 @@ SIGNATURES = {
     "gaamd_event_elapsed_ms": (ctypes.c_float, [ctypes.c_void_p, ctypes.c_void_p]),
     "gaamd_version": (ctypes.c_char_p, []),
     "gaamd_hip_runtime": (ctypes.c_char_p, []),
+    "gaamd_build_id": (ctypes.c_char_p, []),
     "gaamd_diag": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_ulonglong),
                                   ctypes.c_int]),
 }

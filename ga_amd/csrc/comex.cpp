@@ -609,9 +609,11 @@ static void exit_without_finalize() {
 // allocator's first 1 GiB descriptor kills the process with SIGSEGV
 // (profiles/r05/runtime_diag/, phase traces; /opt/rocm 7.2 passes both).  The
 // reference aborts with a message on any such condition (COMEX_ASSERT ->
-// comex_error, comex_impl.h:52-76); so does this, before anything can hang.
-// COMEX_AMD_ALLOW_HIP_MISMATCH=1 downgrades it to a warning.
-static void check_hip_runtime() {
+// comex_error, comex_impl.h:52-76); so does this, before any device work, when other
+// ranks share this node (their segments will be mapped here, and ours there).  A
+// rank alone on its node never opens an inter-process mapping: for it the mismatch
+// is a warning.  COMEX_AMD_ALLOW_HIP_MISMATCH=1 makes it a warning always.
+static void check_hip_runtime(bool peers_map) {
     const char *path = gaamd_hip_runtime();
     int ver = 0;
     const bool got = hipRuntimeGetVersion(&ver) == hipSuccess;
@@ -628,8 +630,9 @@ static void check_hip_runtime() {
              "COMEX_AMD_ALLOW_HIP_MISMATCH=1 to run on it anyway",
              path, ver / 10000000, ver / 100000 % 100, ver % 100000, built / 10000000, built / 100000 % 100,
              built % 100000, GAAMD_ROCM_PATH);
-    if (allow && atoi(allow)) {
-        fprintf(stderr, "ga_amd warning: %s\n", msg);
+    if ((allow && atoi(allow)) || !peers_map) {
+        fprintf(stderr, "ga_amd warning: %s%s\n", msg,
+                peers_map ? "" : " (no other rank on this node: no inter-process mapping, going on)");
         return;
     }
     fatal("%s", msg);
@@ -645,8 +648,8 @@ int comex_init() {
     }
     const char *dbg = getenv("COMEX_AMD_DEBUG");
     r.debug = dbg ? atoi(dbg) : 0;
-    check_hip_runtime();
-    boot_init();
+    boot_init();   // host shm rendezvous only, no HIP call
+    check_hip_runtime(r.node_size > 1);
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev <= 0)
@@ -798,6 +801,7 @@ int comex_finalize() {
     if (g_get_scratch_ev) (void)hipEventDestroy(g_get_scratch_ev);
     g_get_scratch_ev = nullptr;
     iov_finalize();
+    views_finalize();
     (void)hipStreamDestroy(r.stream);
     r.stream = nullptr;
     r.initialized = false;
@@ -1173,6 +1177,15 @@ int gaamd_diag(const char *key, long long value, unsigned long long *out, int no
     if (!strcmp(key, "host_range")) {   // out[0], out[1] in: [lo, hi); value: 1 = writable; out[0] out: 1/0
         if (!out || nout < 2) return -1;
         out[0] = host_cpu_range_probe(out[0], out[1], value != 0) ? 1 : 0;
+        return 0;
+    }
+    if (!strcmp(key, "vmm_window")) {   // out[0] bytes of the vmm private window taken, out[1] left
+        if (!out || nout < 2) return -1;
+        vmm_window_usage(&out[0], &out[1]);
+        return 0;
+    }
+    if (!strcmp(key, "pinned_threads")) {   // threads holding pinned bounce buffers or an nb ring
+        if (out && nout >= 1) out[0] = views_pinned_threads();
         return 0;
     }
     if (!strcmp(key, "iov_host_sides")) {   // io-vector sides found wholly in pageable host memory

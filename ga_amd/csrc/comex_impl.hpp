@@ -67,6 +67,8 @@ View local_view(void *p, int64_t lo, int64_t hi, bool is_dst = false, bool bounc
 // large); ring_commit then names the operation that reads it (stream, sched_track sequence)
 bool ring_view(View &v, void *p, int64_t lo, int64_t hi);
 void ring_commit(int stream, uint64_t seq);
+size_t views_pinned_threads();   // threads holding pinned bounce/ring buffers now
+void views_finalize();    // every thread's pinned bounce buffers and ring (comex_finalize)
 inline bool needs_sync(const View &v) { return v.registered || v.staged || v.bounce; }
 // the rows a bounced destination view's kernel writes (dst strides, count, levels, row
 // bytes): release_view copies back those rows only; without it, nothing but the view's
@@ -123,6 +125,7 @@ void segments_release_blocks();   // the freed-segment cache and the quarantined
 
 // ---- HBM segments through the virtual-memory API (vmm.cpp) ---------------------
 bool vmm_enabled();                       // COMEX_AMD_SEGMENT_ALLOC=vmm
+void vmm_window_usage(unsigned long long *used, unsigned long long *left);   // private window bytes
 size_t vmm_round(size_t bytes);           // to the allocation granularity
 void *vmm_alloc(size_t bytes, VmmBlock *b);                  // this GPU's HBM, exported (b->fd)
 void vmm_listen();                        // this process's descriptor socket (before the allgather)

@@ -118,7 +118,16 @@ constexpr uint64_t kSegGranule = 2ull << 20;
 __host__ __device__ inline uint64_t seg_granule_tag(uint64_t key, uint32_t g) {
     return key ^ ((uint64_t)g * 0x9E3779B97F4A7C15ull);
 }
-// write every granule's tag and the end tag (key_end, last 8 bytes) of a block
+// where a block's end tag lies: the last 8-byte-aligned word (an aligned 64-bit
+// access even when bytes % 8 != 0, e.g. a float block of an odd count)
+__host__ __device__ inline uint64_t seg_end_tag_off(uint64_t bytes) { return (bytes - 8) & ~7ull; }
+// granule tags of a block of `bytes` (>= 16): every granule whose 8-byte tag ends at
+// or before the end tag, so no two tags share a byte (a block of 2 MiB + 12 bytes has
+// one granule tag, at 0, and its end tag at 2 MiB)
+__host__ __device__ inline uint32_t seg_granule_count(uint64_t bytes) {
+    return (uint32_t)((seg_end_tag_off(bytes) - 8) / kSegGranule + 1);
+}
+// write every granule's tag and the end tag (key_end, at seg_end_tag_off) of a block
 int launch_seg_tags(void *p, uint64_t bytes, uint64_t key, uint64_t key_end, hipStream_t stream);
 // check them through a mapping (system-scope loads); out_dev[2] (device memory,
 // preset {0, ~0u}): mismatches, and the first bad granule (granule count = the end tag)

@@ -47,7 +47,8 @@ int launch_flag(uint64_t *flag_dev, uint64_t v, hipStream_t stream) {
 
 // ---------------------------------------------------------------------------
 // Segment tags (segments.cpp do_malloc): one 8-byte tag at the start of every
-// kSegGranule bytes of a new block and one in its last 8 bytes, so a peer's
+// kSegGranule bytes of a new block and one in its last aligned 8 bytes
+// (seg_end_tag_off; seg_granule_count keeps the granule tags clear of it), so a peer's
 // mapping is checked over the whole block, not only at its ends (VERDICT r4 item
 // 4: a multi-GiB block with one interior granule bound to other memory).  The
 // owner's stores are system-scope (`global_store_dwordx2 ... sc0 sc1`: they go
@@ -60,7 +61,7 @@ __global__ __launch_bounds__(256) void k_seg_tags(char *p, uint64_t bytes, uint6
         __hip_atomic_store(reinterpret_cast<uint64_t *>(p + (uint64_t)g * kSegGranule), seg_granule_tag(key, g),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     else if (g == ngran)
-        __hip_atomic_store(reinterpret_cast<uint64_t *>(p + bytes - 8), key_end, __ATOMIC_RELAXED,
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(p + seg_end_tag_off(bytes)), key_end, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(256) void k_seg_check(const char *p, uint64_t bytes
                                                    uint32_t ngran, uint32_t *out) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g > ngran) return;
-    const char *at = g < ngran ? p + (uint64_t)g * kSegGranule : p + bytes - 8;
+    const char *at = g < ngran ? p + (uint64_t)g * kSegGranule : p + seg_end_tag_off(bytes);
     const uint64_t want = g < ngran ? seg_granule_tag(key, g) : key_end;
     const uint64_t got = __hip_atomic_load(reinterpret_cast<const uint64_t *>(at), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_SYSTEM);
@@ -79,11 +80,9 @@ __global__ __launch_bounds__(256) void k_seg_check(const char *p, uint64_t bytes
     }
 }
 
-static uint32_t seg_granules(uint64_t bytes) { return (uint32_t)((bytes - 8 + kSegGranule - 1) / kSegGranule); }
-
 int launch_seg_tags(void *p, uint64_t bytes, uint64_t key, uint64_t key_end, hipStream_t stream) {
-    if (bytes < 16) return -1;
-    const uint32_t n = seg_granules(bytes) + 1;
+    if (bytes < 16 || ((uintptr_t)p & 7)) return -1;
+    const uint32_t n = seg_granule_count(bytes) + 1;
     hipLaunchKernelGGL(k_seg_tags, dim3((n + 255) / 256), dim3(256), 0, stream, (char *)p, bytes, key, key_end,
                        n - 1);
     const hipError_t e = hipGetLastError();
@@ -92,8 +91,8 @@ int launch_seg_tags(void *p, uint64_t bytes, uint64_t key, uint64_t key_end, hip
 
 int launch_seg_check(const void *p, uint64_t bytes, uint64_t key, uint64_t key_end, uint32_t *out_dev,
                      hipStream_t stream) {
-    if (bytes < 16) return -1;
-    const uint32_t n = seg_granules(bytes) + 1;
+    if (bytes < 16 || ((uintptr_t)p & 7)) return -1;
+    const uint32_t n = seg_granule_count(bytes) + 1;
     hipLaunchKernelGGL(k_seg_check, dim3((n + 255) / 256), dim3(256), 0, stream, (const char *)p, bytes, key,
                        key_end, n - 1, out_dev);
     const hipError_t e = hipGetLastError();

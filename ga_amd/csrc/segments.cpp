@@ -516,7 +516,7 @@ static void write_tags(void *p, size_t bytes, int rank, uint64_t gen, int attemp
     if (rc) fatal("segment tag kernel failed (%d)", rc);
     const long long sg = g_diag_stale_granule.load(), sn = g_diag_stale_gen.load();
     if (attempt == 0 && sn > 0 && (uint64_t)sn == gen && sg >= 0) {
-        const uint64_t ngran = (bytes - 8 + kSegGranule - 1) / kSegGranule;
+        const uint64_t ngran = seg_granule_count(bytes);
         const uint64_t g = (uint64_t)sg % ngran;
         const uint64_t foreign = seg_granule_tag(tag_key(rank, gen + 1000), (uint32_t)g);
         GA_HIP(hipStreamSynchronize(nullptr));
@@ -526,7 +526,7 @@ static void write_tags(void *p, size_t bytes, int rank, uint64_t gen, int attemp
     }
     GA_HIP(hipStreamSynchronize(nullptr));
     trace(1, "comex_malloc: tags of %zu bytes (%llu granules) written in %.1f us", bytes,
-          (unsigned long long)((bytes - 8 + kSegGranule - 1) / kSegGranule), now_us() - t0);
+          (unsigned long long)seg_granule_count(bytes), now_us() - t0);
 }
 
 static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool device) {
@@ -682,7 +682,7 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
                 const int rc = launch_seg_check(mapped[q], all[q].bytes, tag_key(q, all[q].gen),
                                                 tag_end(q, all[q].gen), dres + 2 * k, nullptr);
                 if (rc) fatal("segment tag check kernel failed (%d)", rc);
-                gran += (all[q].bytes - 8 + kSegGranule - 1) / kSegGranule;
+                gran += seg_granule_count(all[q].bytes);
             }
             GA_HIP(hipMemcpy(res.data(), dres, res.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
             GA_HIP(hipFree(dres));
@@ -692,8 +692,8 @@ static int do_malloc(void **ptr_arr, size_t bytes, comex_group_t group, bool dev
                 if (!res[2 * k]) continue;
                 const int q = checked[k];
                 stale[q] = 1;
-                const uint64_t ng = (all[q].bytes - 8 + kSegGranule - 1) / kSegGranule, g = res[2 * k + 1];
-                const uint64_t off = g < ng ? g * kSegGranule : all[q].bytes - 8;
+                const uint64_t ng = seg_granule_count(all[q].bytes), g = res[2 * k + 1];
+                const uint64_t off = g < ng ? g * kSegGranule : seg_end_tag_off(all[q].bytes);
                 uint64_t got = 0;
                 GA_HIP(hipMemcpy(&got, (char *)mapped[q] + off, 8, hipMemcpyDeviceToHost));
                 fprintf(stderr, "[ga_amd %d] the %s mapping of rank %d's new %zu-byte segment (%p in its space) "

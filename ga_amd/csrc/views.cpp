@@ -8,8 +8,12 @@
 // already registered elsewhere, staged through a device copy.
 #include "comex_impl.hpp"
 #include <string.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <algorithm>
 #include <deque>
+#include <mutex>
+#include <vector>
 
 namespace gaamd {
 
@@ -68,21 +72,98 @@ static bool register_range(uintptr_t a0, uintptr_t a1, char **dbase) {
 // complete the transfer before their next one (the buffer is reused by the thread's next
 // call); the asynchronous remote jobs keep registering.
 constexpr int64_t kBounceMax = 128 << 10;
+// The non-blocking ring (ring_view, below): 4 MiB per thread, spans up to 64 KiB.
+constexpr int64_t kRingBytes = 4 << 20, kRingMax = 64 << 10, kRingAlign = 256;
 namespace {
 struct BounceBuf {
     char *host = nullptr, *dev = nullptr;
     size_t bytes = 0;
 };
-thread_local BounceBuf t_bounce[2];   // [0] a source, [1] a destination (or both sides' union)
+struct RingUse {
+    int64_t off, end;   // [off, end) of the ring
+    int stream;
+    uint64_t seq, epoch;
+};
+struct NbRing {
+    char *host = nullptr, *dev = nullptr;
+    int64_t head = 0;          // next free byte
+    int64_t pend_off = -1, pend_end = 0;   // taken by ring_view, not yet committed
+    std::deque<RingUse> q;     // oldest first
+};
+
+void ring_retire(NbRing &g) {
+    const RingUse u = g.q.front();
+    g.q.pop_front();
+    if (u.epoch == sched_epoch()) (void)sched_complete(u.stream, u.seq, true);   // else drained at finalize
+}
+
+// A thread's pinned buffers: both bounce buffers and its ring (a thread-pool
+// caller -- OpenMP workers issuing nb calls -- must not leak pinned memory per thread).
+// Every thread that allocated one is listed; a thread that ends frees its own, after the
+// operations still reading its ring have completed; comex_finalize frees those of every
+// thread still alive, when nothing is in flight any more (views_finalize).
+struct ThreadPins;
+std::mutex g_pins_mu;
+std::vector<ThreadPins *> g_pins;
+struct ThreadPins {
+    BounceBuf bounce[2];
+    NbRing ring;
+    bool listed = false;
+    void list() {
+        if (listed) return;
+        std::lock_guard<std::mutex> lk(g_pins_mu);
+        g_pins.push_back(this);
+        listed = true;
+    }
+    // no operation reads these buffers any more
+    void free_all() {
+        for (BounceBuf &b : bounce) {
+            if (b.host) (void)hipHostFree(b.host);
+            b = BounceBuf();
+        }
+        if (ring.host) (void)hipHostFree(ring.host);
+        ring = NbRing();
+    }
+    ~ThreadPins() {
+        if (!listed) return;
+        {
+            std::lock_guard<std::mutex> lk(g_pins_mu);
+            g_pins.erase(std::remove(g_pins.begin(), g_pins.end(), this), g_pins.end());
+        }
+        // the main thread ends with the process, which returns everything (and the HIP
+        // runtime may be going away by then)
+        if ((pid_t)syscall(SYS_gettid) == getpid()) return;
+        while (!ring.q.empty()) ring_retire(ring);
+        free_all();
+    }
+};
+thread_local ThreadPins t_pins;
 }  // namespace
+static ThreadPins &pins() { return t_pins; }
+
+size_t views_pinned_threads() {
+    std::lock_guard<std::mutex> lk(g_pins_mu);
+    return g_pins.size();
+}
+
+void views_finalize() {
+    std::lock_guard<std::mutex> lk(g_pins_mu);
+    for (ThreadPins *t : g_pins) {
+        t->free_all();
+        t->listed = false;
+    }
+    g_pins.clear();
+}
 
 static char *bounce_buffer(int which, size_t bytes, char **dev) {
-    BounceBuf &b = t_bounce[which];
+    ThreadPins &t = pins();   // [0] a source, [1] a destination (or both sides' union)
+    BounceBuf &b = t.bounce[which];
     if (b.bytes < bytes) {
         if (b.host) GA_HIP(hipHostFree(b.host));   // this thread's previous transfer has completed
         b.bytes = std::max<size_t>(bytes, (size_t)64 << 10);
         GA_HIP(hipHostMalloc((void **)&b.host, b.bytes, hipHostMallocMapped));
         GA_HIP(hipHostGetDevicePointer((void **)&b.dev, b.host, 0));
+        t.list();
     }
     *dev = b.dev;
     return b.host;
@@ -135,27 +216,7 @@ static void write_back_rows(const View &v) {
 // ring range is written again, the operations that read it have completed.  Through the
 // one-call bounce buffer above, such a call waited for its kernel: 11 us per
 // comex_nbaccs of 64 B-4 KiB against 4 from HBM (profiles/r05/small/).
-constexpr int64_t kRingBytes = 4 << 20, kRingMax = 64 << 10, kRingAlign = 256;
 namespace {
-struct RingUse {
-    int64_t off, end;   // [off, end) of the ring
-    int stream;
-    uint64_t seq, epoch;
-};
-struct NbRing {
-    char *host = nullptr, *dev = nullptr;
-    int64_t head = 0;          // next free byte
-    int64_t pend_off = -1, pend_end = 0;   // taken by ring_view, not yet committed
-    std::deque<RingUse> q;     // oldest first
-};
-thread_local NbRing t_ring;
-
-void ring_retire(NbRing &g) {
-    const RingUse u = g.q.front();
-    g.q.pop_front();
-    if (u.epoch == sched_epoch()) (void)sched_complete(u.stream, u.seq, true);   // else drained at finalize
-}
-
 // does [a, b) meet the ring bytes still in use ([front.off, head), circularly)?
 bool ring_busy(const NbRing &g, int64_t a, int64_t b) {
     if (g.q.empty()) return false;
@@ -168,10 +229,12 @@ bool ring_busy(const NbRing &g, int64_t a, int64_t b) {
 bool ring_view(View &v, void *p, int64_t lo, int64_t hi) {
     const int64_t n = hi - lo;
     if (n <= 0 || n > kRingMax) return false;
-    NbRing &g = t_ring;
+    ThreadPins &t = pins();
+    NbRing &g = t.ring;
     if (!g.host) {
         GA_HIP(hipHostMalloc((void **)&g.host, kRingBytes, hipHostMallocMapped));
         GA_HIP(hipHostGetDevicePointer((void **)&g.dev, g.host, 0));
+        t.list();
     }
     if (g.q.empty()) g.head = 0;
     // the copy keeps the source's offset within kRingAlign (the kernel's vector width
@@ -195,7 +258,7 @@ bool ring_view(View &v, void *p, int64_t lo, int64_t hi) {
 }
 
 void ring_commit(int stream, uint64_t seq) {
-    NbRing &g = t_ring;
+    NbRing &g = pins().ring;
     if (g.pend_off < 0) return;
     g.q.push_back({g.pend_off, g.pend_end, stream, seq, sched_epoch()});
     g.pend_off = -1;

@@ -89,7 +89,7 @@ size_t retain_cap() {
     return cap;
 }
 
-uintptr_t g_window_end = 0;
+uintptr_t g_window_end = 0, g_window_start = 0;
 
 char *va_take(size_t bytes) {
     std::lock_guard<std::mutex> g(g_vmm_mu);
@@ -98,6 +98,7 @@ char *va_take(size_t bytes) {
         const char *e = getenv("COMEX_AMD_VMM_VA_BASE");
         g_window = e ? (uintptr_t)strtoull(e, nullptr, 0) : (uintptr_t)0x200000000000ull;
         g_window = (g_window + kAlign - 1) & ~(kAlign - 1);
+        g_window_start = g_window;
         const char *l = getenv("COMEX_AMD_VMM_VA_LIMIT");
         g_window_end = l ? (uintptr_t)strtoull(l, nullptr, 0) : (uintptr_t)0x600000000000ull;
     }
@@ -251,6 +252,14 @@ char *map_fresh(hipMemGenericAllocationHandle_t h, size_t bytes, int q) {
 std::vector<hipMemGenericAllocationHandle_t> g_broken;
 std::vector<VmmBlock> g_quarantined;
 }  // namespace
+
+// the private window's use: bytes taken so far (ranges + guards) and bytes left; a
+// mapping of B bytes takes round_up(B, 2 MiB) + 2 MiB, never returned
+void vmm_window_usage(unsigned long long *used, unsigned long long *left) {
+    std::lock_guard<std::mutex> g(g_vmm_mu);
+    *used = g_window ? (unsigned long long)(g_window - g_window_start) : 0;
+    *left = g_window ? (unsigned long long)(g_window_end > g_window ? g_window_end - g_window : 0) : 0;
+}
 
 bool vmm_enabled() {
     static const bool on = [] {

@@ -164,6 +164,10 @@ float gaamd_event_elapsed_ms(void *start, void *stop);
 const char *gaamd_version(void);
 /* path of the HIP runtime (libamdhip64) this library's calls resolve to */
 const char *gaamd_hip_runtime(void);
+/* build provenance: sha256 (hex) of the sources this library was compiled from --
+ * ga_amd/csrc/ and include/ (ga_amd/provenance.py) -- so a stale prebuilt library is
+ * detectable against the tree beside it */
+const char *gaamd_build_id(void);
 
 /* ---- test and diagnostic hooks (not used by GA) ------------
  * One entry point; returns 0, or -1 for an unknown key.
@@ -186,7 +190,15 @@ const char *gaamd_hip_runtime(void);
  *   "host_range"    that pass on its own: out[0], out[1] (nout >= 2) hold [lo, hi) on
  *                   entry, value 1 asks for writable memory; out[0] is 1 when every
  *                   byte lies in readable (writable) mappings that are not device
- *                   files, else 0.  Needs no GPU. */
+ *                   files, else 0.  Needs no GPU.
+ *   "pinned_threads" out[0] (nout >= 1): threads that hold pinned bounce buffers or
+ *                   a non-blocking ring now (a thread's are freed when it ends, every
+ *                   thread's at comex_finalize).
+ *   "vmm_window"    out[0], out[1] (nout >= 2): bytes of the vmm allocator's private
+ *                   address window taken so far and bytes left.  Every mapping (this
+ *                   rank's blocks and its imports of peers' blocks) takes
+ *                   round_up(bytes, 2 MiB) + 2 MiB of it, never handed out again;
+ *                   comex_malloc aborts with a message once it is used up. */
 int gaamd_diag(const char *key, long long value, unsigned long long *out, int nout);
 
 #if defined(__cplusplus)

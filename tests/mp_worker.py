@@ -116,6 +116,8 @@ def main():
         segment_cache_test(L, rank, size)
     elif mode == "stalefix":
         stale_fix_test(L, rank, size)
+    elif mode == "oddseg":
+        odd_segment_test(L, rank, size)
     elif mode in ("armcimisc", "armcimisc-gloo"):
         armci_misc_test(L, rank, size)
     elif mode in ("rdesc", "rdesc-gloo"):
@@ -810,6 +812,36 @@ def stale_fix_test(L, rank, size):
     # process leaves through the exit hook (STALEFIX_NO_FINALIZE=1)
     if os.environ.get("STALEFIX_NO_FINALIZE") != "1":
         assert ga_amd.comex_finalize() == 0
+
+
+def odd_segment_test(L, rank, size):
+    """segments whose size is not a multiple of 8, just past a 2 MiB
+    granule (2 MiB + 9..15 bytes put a granule tag and the end tag on shared bytes before
+    the fix, so every peer found its mapping "stale" and comex_malloc aborted after four
+    replacements), and small ones.  Each size: no block replaced, then every rank puts
+    `bytes` bytes of its own pattern into the next rank's segment and reads its own back
+    exactly, so the peers' mappings reach the owner's block end to end."""
+    import ga_amd
+    assert ga_amd.comex_init() == 0
+    r0 = L.gaamd_segment_remaps()
+    mib2 = 2 << 20
+    for nbytes in (mib2 + 12, mib2 + 9, mib2 + 15, mib2 + 8, mib2 + 16, 2 * mib2 + 4, 16, 17, 23, 3):
+        seg = ga_amd.comex_malloc(nbytes, size)
+        assert L.gaamd_segment_remaps() == r0, f"rank {rank}: a {nbytes}-byte segment was replaced"
+        nxt, prv = (rank + 1) % size, (rank - 1) % size
+        pat = ((np.arange(nbytes, dtype=np.int64) * 7 + 13 * rank + nbytes) % 251).astype(np.uint8)
+        assert L.comex_put(pat.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(seg[nxt]), nbytes, nxt, 0) == 0
+        ga_amd.comex_fence_all()
+        ga_amd.comex_barrier()
+        got = np.zeros(nbytes, dtype=np.uint8)
+        assert L.comex_get(ctypes.c_void_p(seg[rank]), got.ctypes.data_as(ctypes.c_void_p), nbytes, rank, 0) == 0
+        want = ((np.arange(nbytes, dtype=np.int64) * 7 + 13 * prv + nbytes) % 251).astype(np.uint8)
+        bad = int(np.count_nonzero(got != want))
+        assert bad == 0, f"rank {rank}: {nbytes}-byte segment, {bad} bytes wrong"
+        ga_amd.comex_barrier()
+        assert ga_amd.comex_free(seg[rank]) == 0
+    say(rank, "odd-size segments mapped without replacement, exact")
+    assert ga_amd.comex_finalize() == 0
 
 
 def segment_cache_test(L, rank, size):

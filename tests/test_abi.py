@@ -263,27 +263,56 @@ def test_comex_without_gpu_fails_loudly():
     assert "no HIP device" in r.stderr
 
 
+_TORCH_FIRST = ("import time,sys; t=time.time(); import torch; import ga_amd; L=ga_amd.lib(); "
+                "sys.stderr.write('init after %.1f s\\n' % (time.time()-t)); sys.stderr.flush(); "
+                "t=time.time(); rc=L.comex_init(); sys.exit(100 + rc)")
+
+
 def _torch_first_init():
     """import torch (whose wheel bundles its own HIP runtime, same SONAME) before
-    libga_amd, then comex_init: must abort at once with the diagnosis, before any
-    device work (comex_impl.h:52-76 convention), not stall later in comex_malloc."""
-    code = ("import time,sys; t=time.time(); import torch; import ga_amd; L=ga_amd.lib(); "
-            "sys.stderr.write('init after %.1f s\\n' % (time.time()-t)); sys.stderr.flush(); "
-            "t=time.time(); rc=L.comex_init(); sys.exit(100 + rc)")
-    env = dict(os.environ)
+    libga_amd, then comex_init on two ranks of one node: both must abort at once with
+    the diagnosis, before any device work (comex_impl.h:52-76 convention), not stall
+    later in comex_malloc's inter-process mappings."""
+    env = dict(os.environ, WORLD_SIZE="2", COMEX_AMD_JOBID=f"tf{os.getpid()}")
     env.pop("COMEX_AMD_ALLOW_HIP_MISMATCH", None)
-    import time
-    t0 = time.time()
-    r = subprocess.run(["python", "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
-    assert r.returncode not in (0, 100), (r.returncode, r.stderr[-2000:])
-    assert "libga_amd was built against HIP" in r.stderr and "/torch/lib/" in r.stderr, r.stderr[-2000:]
-    assert "import ga_amd before torch" in r.stderr
-    return time.time() - t0
+    procs = [subprocess.Popen(["python", "-c", _TORCH_FIRST], cwd=ROOT, stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True, env=dict(env, RANK=str(r), LOCAL_RANK=str(r)))
+             for r in range(2)]
+    for p in procs:
+        _, err = p.communicate(timeout=300)
+        assert p.returncode not in (0, 100), (p.returncode, err[-2000:])
+        assert "libga_amd was built against HIP" in err and "/torch/lib/" in err, err[-2000:]
+        assert "import ga_amd before torch" in err and "ga_amd warning" not in err, err[-2000:]
+
+
+def _torch_first_alone():
+    """a rank alone on its node opens no inter-process mapping, so the same
+    mismatch is a warning there and comex_init goes on (on a CPU host to the no-device
+    abort, on a GPU box to success)."""
+    env = dict(os.environ)
+    for k in ("COMEX_AMD_ALLOW_HIP_MISMATCH", "RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run(["python", "-c", _TORCH_FIRST], cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert "ga_amd warning: HIP calls resolve to" in r.stderr and "no other rank on this node" in r.stderr, \
+        r.stderr[-2000:]
+    return r
 
 
 def test_torch_runtime_first_fails_fast():
     """CPU: the check runs before the device query, so it fires here too."""
     _torch_first_init()
+
+
+def test_torch_runtime_first_single_rank_warns():
+    r = _torch_first_alone()
+    if "no HIP device" not in r.stderr:
+        pytest.skip("a GPU is visible here")
+
+
+@pytest.mark.gpu
+def test_torch_runtime_first_single_rank_warns_gpu():
+    r = _torch_first_alone()
+    assert r.returncode == 100, (r.returncode, r.stderr[-2000:])
 
 
 def test_torch_runtime_mismatch_opt_out():
@@ -447,3 +476,31 @@ def test_every_runtime_knob_is_documented():
             code |= set(re.findall(r'getenv\("(COMEX_AMD_[A-Z0-9_]+)"\)', open(os.path.join(csrc, name)).read()))
     doc = set(re.findall(r"^\| `(COMEX_AMD_[A-Z0-9_]+)`", open(os.path.join(ROOT, "INTEGRATION.md")).read(), re.M))
     assert code == doc, {"undocumented": sorted(code - doc), "stale": sorted(doc - code)}
+
+
+def test_build_id_is_the_tree_hash():
+    """libga_amd.so carries the sha256 of the sources it was built
+    from; here (where build() just ran) it equals the tree's."""
+    assert ga_amd.check_build() == ga_amd.build_id()
+    assert len(ga_amd.build_id()) == 64
+
+
+@pytest.mark.gpu
+def test_build_id_is_the_tree_hash_gpu():
+    """On the GPU box: the prebuilt library that travelled with the snapshot was built
+    from exactly the sources in it -- a stale .so fails here, loudly."""
+    ga_amd.check_build()
+
+
+def test_stale_build_id_is_detected(tmp_path):
+    """A changed source changes the tree hash, so check_build() would refuse the
+    library: the hash of a copy of the sources with one byte appended differs."""
+    import shutil
+    from ga_amd.provenance import source_files, tree_hash
+    for rel in source_files():
+        os.makedirs(tmp_path / os.path.dirname(rel), exist_ok=True)
+        shutil.copy(os.path.join(ROOT, rel), tmp_path / rel)
+    assert tree_hash(str(tmp_path)) == tree_hash()
+    with open(tmp_path / "ga_amd" / "csrc" / "comex.cpp", "ab") as f:
+        f.write(b"\n")
+    assert tree_hash(str(tmp_path)) != tree_hash()

@@ -448,3 +448,59 @@ def test_pageable_sources_sharing_pages_back_to_back(gpu_lib, oracle):
     assert np.array_equal(d2.download(np.uint8, dh2.size), dh2)
     d1.free()
     d2.free()
+
+
+def test_pinned_buffers_of_ended_threads_are_freed(gpu_lib, oracle):
+    """every thread that issues small calls from pageable memory gets pinned
+    buffers (a 4 MiB non-blocking ring, bounce buffers); a thread that ends frees its
+    own after the operations reading them completed.  Eight threads, each a non-blocking
+    accumulate from a pageable 1 KiB source (through its ring) and a blocking one
+    (through its bounce buffer), some never waited for before the thread ends; after
+    the joins no ended thread holds pinned buffers and every result is exact."""
+    import threading
+    L = gpu_lib
+    n = 128                                            # f64 per call: 1 KiB
+    cnt = (ctypes.c_int * 1)(n * 8)
+    ss = (ctypes.c_int * 1)(0)
+    keep, sp = ga_amd.scale_buffer(C.DBL, C.SCALE[C.DBL])
+    out = np.zeros(1, dtype=np.uint64)
+
+    def pinned_threads():
+        assert L.gaamd_diag(b"pinned_threads", 0, out.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), 1) == 0
+        return int(out[0])
+
+    before = pinned_threads()
+    nthr = 8
+    dst = [ga_amd.DeviceBuffer(2 * n * 8) for _ in range(nthr)]
+    base = [C.fill_bytes(C.DBL, 2 * n * 8, 40 + t) for t in range(nthr)]
+    srcs = [C.fill_bytes(C.DBL, n * 8, 60 + t) for t in range(nthr)]
+    for d, b in zip(dst, base):
+        d.upload(b)
+    errs = []
+
+    def work(t):
+        try:
+            h = ctypes.c_int(-1)
+            assert L.comex_nbaccs(C.DBL, sp, ctypes.c_void_p(srcs[t].ctypes.data), ss, ctypes.c_void_p(dst[t].ptr),
+                                  ss, cnt, 0, 0, 0, ctypes.byref(h)) == 0
+            if t % 2:
+                assert L.comex_wait(ctypes.byref(h)) == 0
+            assert L.comex_accs(C.DBL, sp, ctypes.c_void_p(srcs[t].ctypes.data), ss,
+                                ctypes.c_void_p(dst[t].ptr + n * 8), ss, cnt, 0, 0, 0) == 0
+        except AssertionError as e:   # pragma: no cover - reported below
+            errs.append((t, e))
+
+    threads = [threading.Thread(target=work, args=(t,)) for t in range(nthr)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errs, errs
+    assert pinned_threads() == before, (before, pinned_threads())
+    ga_amd.sync()
+    for t in range(nthr):
+        want = base[t].copy()
+        oracle.accs(C.DBL, C.SCALE[C.DBL], srcs[t], 0, [0], want, 0, [0], [n * 8], 0)
+        oracle.accs(C.DBL, C.SCALE[C.DBL], srcs[t], 0, [0], want, n * 8, [0], [n * 8], 0)
+        assert np.array_equal(dst[t].download(np.uint8, want.size), want), t
+        dst[t].free()

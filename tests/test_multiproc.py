@@ -545,6 +545,15 @@ def test_segment_cache_reuse(n, cache):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("alloc", ["ipc", "vmm"])
+def test_odd_size_segments(alloc):
+    """segments of 2 MiB + 9..15 bytes and sizes that are not multiples of 8
+    map on every peer without a replacement (granule tags kept clear of the end tag, the
+    end tag on an aligned word), on both allocators."""
+    launch("oddseg", n=2, timeout=120, extra_env={"COMEX_AMD_SEGMENT_ALLOC": alloc})
+
+
+@pytest.mark.gpu
 def test_vmm_window_used_up_is_a_clear_error():
     """ADVICE r4: the vmm allocator maps every block at a range never used before;
     when its private window [COMEX_AMD_VMM_VA_BASE, COMEX_AMD_VMM_VA_LIMIT) is used up
@@ -553,10 +562,16 @@ def test_vmm_window_used_up_is_a_clear_error():
     64 MiB segments with the freed-block cache off: the first ~15 cycles run, then
     the error, well within the timeout."""
     code = ("import ctypes, ga_amd\n"
+            "L = ga_amd.lib()\n"
+            "out = (ctypes.c_ulonglong * 2)()\n"
             "assert ga_amd.comex_init() == 0\n"
             "for i in range(64):\n"
             "    seg = ga_amd.comex_malloc(64 << 20, 1)\n"
             "    assert ga_amd.comex_free(seg[0]) == 0\n"
+            "    assert L.gaamd_diag(b'vmm_window', 0, out, 2) == 0\n"
+            "    assert out[0] == (i + 1) * (66 << 20), (i, out[0])   # 64 MiB + the 2 MiB guard each\n"
+            "    assert out[0] + out[1] == 1 << 30, (out[0], out[1])\n"
+            "    print('cycle', i, 'window used', out[0], 'left', out[1], flush=True)\n"
             "print('no error after 64 cycles', flush=True)\n")
     env = dict(os.environ, COMEX_AMD_SEGMENT_ALLOC="vmm", COMEX_AMD_SEGMENT_CACHE_MB="0",
                COMEX_AMD_VMM_VA_BASE=hex(0x200000000000), COMEX_AMD_VMM_VA_LIMIT=hex(0x200000000000 + (1 << 30)))
@@ -565,3 +580,6 @@ def test_vmm_window_used_up_is_a_clear_error():
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0, r.stdout
     assert "private address window is used up" in r.stderr and "COMEX_AMD_VMM_VA_LIMIT" in r.stderr, r.stderr[-2000:]
+    # the counter: 1 GiB // 66 MiB = 15 cycles ran, the 16th found the window used up
+    cycles = [l for l in r.stdout.splitlines() if l.startswith("cycle ")]
+    assert len(cycles) == (1 << 30) // (66 << 20), r.stdout[-2000:]
