@@ -159,6 +159,7 @@ static int get_via_scratch(const char *src, const int *ss, char *dst, const int 
 // last strided call and the last comex_wait_all, for placing the bench's value
 // region edges on a kernel trace.  Off unless gaamd_diag("stamps", 1).
 static std::atomic<bool> g_stamp_on{false};
+std::atomic<unsigned long long> g_peer_gets{0};   // strided gets read from another GPU (system-scope loads)
 static uint64_t g_stamp[8];
 static inline void stamp(int i) {
     if (!g_stamp_on.load(std::memory_order_relaxed)) return;
@@ -360,7 +361,8 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
                 // L2s written back) has then put its bytes where another GPU's
                 // system-scope loads read them
                 std::lock_guard<std::mutex> g(r.launch_mu);
-                sched_sync_all();
+                if (g_publish_conservative.load(std::memory_order_relaxed)) sched_publish_all();
+                else sched_sync_all();
             }
             int cnt[8];
             for (int k = 0; k <= levels; ++k) cnt[k] = count[k];
@@ -474,6 +476,7 @@ static int xfer(Xfer kind, int op, void *scale, void *src, int *ss, void *dst, i
     const bool host_side = (needs_sync(sv) || needs_sync(dv)) && !bounce_only;
     // a get from another GPU's memory reads it with system-scope loads
     const bool peer = kind == X_GET && world != r.rank && r.peer_src(world);
+    if (peer) g_peer_gets.fetch_add(1, std::memory_order_relaxed);
     int si = 0;
     hipStream_t st;
     {
@@ -849,7 +852,8 @@ int comex_fence_proc(int proc, comex_group_t group) {
     fence_target(translate_world(group, proc));
     {
         std::lock_guard<std::mutex> g(rt().launch_mu);
-        sched_sync_all();
+        if (g_publish_conservative.load(std::memory_order_relaxed)) sched_publish_all();
+        else sched_sync_all();
     }
     one_pass_reap(true);   // our one-pass kernels are done: hand the owners' locks back
     return COMEX_SUCCESS;
@@ -1177,6 +1181,19 @@ int gaamd_diag(const char *key, long long value, unsigned long long *out, int no
     if (!strcmp(key, "host_range")) {   // out[0], out[1] in: [lo, hi); value: 1 = writable; out[0] out: 1/0
         if (!out || nout < 2) return -1;
         out[0] = host_cpu_range_probe(out[0], out[1], value != 0) ? 1 : 0;
+        return 0;
+    }
+    if (!strcmp(key, "publish")) {   // 1: the conservative publication mode, 0: the default; out[0] = old
+        if (out && nout >= 1) out[0] = g_publish_conservative.load() ? 1 : 0;
+        if (value >= 0) g_publish_conservative.store(value != 0);
+        return 0;
+    }
+    if (!strcmp(key, "drop_chunk")) {   // N > 0: the owner drops every N-th packed chunk (test hook), 0: off
+        g_diag_drop_chunk.store(value);
+        return 0;
+    }
+    if (!strcmp(key, "peer_gets")) {   // strided gets this rank read from another GPU's memory
+        if (out && nout >= 1) out[0] = g_peer_gets.load(std::memory_order_relaxed);
         return 0;
     }
     if (!strcmp(key, "vmm_window")) {   // out[0] bytes of the vmm private window taken, out[1] left

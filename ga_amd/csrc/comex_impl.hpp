@@ -120,6 +120,8 @@ void export_alloc(void **p, size_t bytes, hipIpcMemHandle_t *h, const char *what
 // allocation as stale (stale_gen = N, stale_granule < 0), or the owner writes a
 // foreign tag into granule G of it (stale_granule = G) for the check to find
 extern std::atomic<long long> g_diag_stale_gen, g_diag_stale_granule;
+extern std::atomic<long long> g_diag_drop_chunk;   // gaamd_diag("drop_chunk"): remote.cpp
+extern std::atomic<unsigned long long> g_peer_gets;   // gaamd_diag("peer_gets"): comex.cpp
 void segments_finalize();         // every live segment: peer mappings closed, block freed
 void segments_release_blocks();   // the freed-segment cache and the quarantined blocks
 

@@ -204,6 +204,8 @@ void post_request_rmw(int t, int swap, uint64_t addr, int bytes, uint64_t val) {
 
 // owner side: drain the inbox in ticket order
 static std::atomic<bool> g_progress_exited{false};
+std::atomic<long long> g_diag_drop_chunk{0};
+static std::atomic<unsigned long long> g_drop_seen{0};
 
 static void progress_loop() {
     Runtime &r = rt();
@@ -452,6 +454,13 @@ static void progress_loop() {
             }
             // packed rows rb..re start at staging_off; rebase the packed side
             const char *packed0 = packed - (int64_t)rb * q.count[0];
+            // test hook (gaamd_diag "drop_chunk" N): every N-th packed chunk is counted
+            // applied without its kernel -- a logic fault no publication mode can mend
+            const long long dn = g_diag_drop_chunk.load(std::memory_order_relaxed);
+            const bool drop = dn > 0 && (g_drop_seen.fetch_add(1, std::memory_order_relaxed) + 1) % dn == 0;
+            if (drop)
+                fprintf(stderr, "[ga_amd %d] gaamd_diag drop_chunk: rows %llu..%llu of a chunk from rank %d dropped\n",
+                        r.rank, (unsigned long long)rb, (unsigned long long)re, src);
             hipEvent_t ev;
             if (pool.empty()) GA_HIP(hipEventCreateWithFlags(&ev, kOwnerEventFlags));
             else { ev = pool.back(); pool.pop_back(); }
@@ -462,8 +471,8 @@ static void progress_loop() {
                 side_span_host(q.dst_stride, q.count, q.levels, q.count[0], &dlo, &dhi);
                 const int si = sched_pick(span_of(packed, 0, (int64_t)q.bytes), span_of((void *)q.dst_addr, dlo, dhi),
                                           0, peer ? pull_stream(src) : -1);
-                int rc = launch_strided(q.op, q.scale, packed0, pstride, (void *)q.dst_addr, q.dst_stride, q.count,
-                                        q.levels, r.streams[si], nullptr, rb, re, false, peer);
+                int rc = drop ? 0 : launch_strided(q.op, q.scale, packed0, pstride, (void *)q.dst_addr, q.dst_stride,
+                                                   q.count, q.levels, r.streams[si], nullptr, rb, re, false, peer);
                 if (rc == kErrPeerOrdered) {
                     // the chunk's rows must apply in order: pull the packed chunk into local
                     // scratch first, then the ordinary unpack-acc from there
@@ -613,6 +622,7 @@ bool progress_jobs() {
     const uint64_t sub = sub_ring_bytes();
     bool any = false;
     // post chunks whose pack finished, per target in allocation order
+    bool published = false;
     for (int t = 0; t < (int)g_out.size(); ++t) {
         std::deque<Chunk> &o = g_out[t];
         while (!o.empty()) {
@@ -620,6 +630,13 @@ bool progress_jobs() {
             const hipError_t e = hipEventQuery(c.ev);
             if (e == hipErrorNotReady) break;
             if (e != hipSuccess) fatal("pack kernel failed: %s", hipGetErrorString(e));
+            if (!published && g_publish_conservative.load(std::memory_order_relaxed)) {
+                // the conservative publication mode: a system-scope release on every
+                // library stream, drained, before the first post of this pass
+                std::lock_guard<std::mutex> g(r.launch_mu);
+                sched_publish_all();
+                published = true;
+            }
             RJob *j = find_job(c.job);
             post_request(t, j->op, j->scale, (uint64_t)(uintptr_t)j->dst, j->ds, j->count, j->levels,
                          (uint64_t)t * sub + c.off, c.len, c.rb, c.re);

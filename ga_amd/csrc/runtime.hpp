@@ -268,6 +268,10 @@ void sched_flag_fini();
 // unknown extent is Span{0, INT64_MAX}
 void sched_join_write(const Span &dst);
 void sched_sync_all();
+// sched_sync_all behind a system-scope release on every library stream (the
+// conservative publication mode, g_publish_conservative)
+void sched_publish_all();
+extern std::atomic<bool> g_publish_conservative;   // gaamd_diag("publish")
 // completion marks (user thread): sequence number of an op just enqueued on
 // stream s; whether op `seq` of stream s has completed (waiting for it if `wait`)
 uint64_t sched_track(int s);

@@ -162,8 +162,13 @@ void sched_resize(int n) {
     sched_init(n, pull);
 }
 
+static std::vector<hipEvent_t> g_pub_ev;   // sched_publish_all
+std::atomic<bool> g_publish_conservative{false};
+
 void sched_fini() {
     Runtime &r = rt();
+    for (hipEvent_t e : g_pub_ev) (void)hipEventDestroy(e);
+    g_pub_ev.clear();
     for (size_t i = 1; i < r.streams.size(); ++i) (void)hipStreamDestroy(r.streams[i]);
     for (hipEvent_t e : g_ev) (void)hipEventDestroy(e);
     g_ev.clear();
@@ -214,6 +219,23 @@ void sched_sync_all() {
     }
     g_hist.clear();
     g_base = -1;
+}
+
+// The conservative publication mode (gaamd_diag "publish" 1):
+// sched_sync_all behind an event recorded with hipEventReleaseToSystem on every
+// library stream -- a system-scope release stated on each stream, then waited for.
+// Round 5 measured it on every direct-source post and fence (-33 % on that route,
+// profiles/r05/ab/) and took it out of the default path; a cross-GPU check that reads
+// MISMATCH runs once more under it, to tell a visibility fault from a logic one.
+void sched_publish_all() {
+    Runtime &r = rt();
+    while (g_pub_ev.size() < r.streams.size()) {
+        hipEvent_t e;
+        GA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToSystem));
+        g_pub_ev.push_back(e);
+    }
+    for (size_t i = 0; i < r.streams.size(); ++i) GA_HIP(hipEventRecord(g_pub_ev[i], r.streams[i]));
+    sched_sync_all();
 }
 
 // ---- blocking-call completion through a flag -----------------

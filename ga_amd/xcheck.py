@@ -1,0 +1,475 @@
+"""Cross-GPU exactness self-check of every remote operation.
+
+Runs inside a job whose ranks have all called comex_init (bench.py's N > 1 extras,
+before any timed C5 step; the multi-rank GPU tests).  Between rank pairs (r -> r + s
+for a few shifts s) it issues, through the public C ABI:
+
+  * seeded random strided accumulates of every type (comex_accs / comex_nbaccs,
+    nb_accs comex.c:6890-6962) and strided puts (comex_puts / comex_nbputs,
+    comex.c:6342-6427): 0..7 stride levels, padded strides, rows starting below the
+    element's natural alignment (4 bytes for 8/16-byte types, any byte for puts),
+    sources in a plain device buffer (the packed route to another GPU), in the
+    caller's own segment with >= 1 MiB payloads (the direct-source route) and in
+    pageable host memory;
+  * strided gets of every such patch back from the owner (comex_gets / comex_nbgets,
+    comex.c:6617-6696: another GPU's memory read with system-scope loads);
+  * io-vector accumulates with repeated destinations, puts and gets (comex_accv /
+    putv / getv, comex.c:7327-7400; test.c test_vector);
+  * fetch-and-add (int and long) and swap (comex_rmw, comex.c OP_FETCH_AND_ADD /
+    OP_SWAP).
+
+No oracle is involved: every input is integer-valued (|v| <= 64, alpha a small
+integer or Gaussian integer), so every product and sum is exact in every type and
+the expected bytes follow in closed form (dst[i] + alpha * src[i], or the copied
+bytes, or the arithmetic series of the rmw results).  Each owner checks its own
+segment after a barrier, each source checks what its gets read back, and bytes
+outside the patches must not change.  The report carries, summed over ranks, what
+each route carried (packed chunks, direct-source requests, io-vector and rmw
+requests, one-pass accumulates, the owners' applied requests by kind, gets read from
+another GPU), so a line says which routes this run exercised.
+
+xdev_check_diagnosed() reruns a check that read MISMATCH once more in the same
+process under the conservative publication mode (gaamd_diag "publish": a
+system-scope release on every library stream before every post and fence) and
+classifies the fault: "clears: visibility" or "persists: logic".
+"""
+import ctypes
+import time
+
+import numpy as np
+
+INT, DBL, FLT, CPL, DCP, LNG = 37, 38, 39, 40, 41, 42
+PUT = 0                       # a strided put (bytes, GAAMD_OP_COPY)
+ACC_OPS = (INT, DBL, FLT, CPL, DCP, LNG)
+OP_NAME = {INT: "int", DBL: "dbl", FLT: "flt", CPL: "cpl", DCP: "dcp", LNG: "lng", PUT: "put"}
+DTYPE = {INT: np.int32, DBL: np.float64, FLT: np.float32, CPL: np.complex64, DCP: np.complex128,
+         LNG: np.int64, PUT: np.uint8}
+ALPHA = {INT: 3, LNG: -2, DBL: 2.0, FLT: -3.0, CPL: 1 - 2j, DCP: 2 + 1j}
+SEG_BYTES = 48 << 20          # per rank: the patches other ranks write into it
+SRC_SEG_BYTES = 8 << 20       # per rank: sources of the direct-source descriptors
+ALIGN = 256
+
+
+def _lib():
+    from . import lib
+    return lib()
+
+
+def _esz(op):
+    return np.dtype(DTYPE[op]).itemsize
+
+
+def _values(rng, op, n):
+    """n integer-valued elements of op's type (|v| <= 64); for a put, random bytes"""
+    if op == PUT:
+        return rng.integers(0, 256, n, dtype=np.uint8)
+    v = rng.integers(-64, 65, n)
+    if op in (CPL, DCP):
+        return (v + 1j * rng.integers(-64, 65, n)).astype(DTYPE[op])
+    return v.astype(DTYPE[op])
+
+
+class Desc:
+    """One strided transfer: count[0] bytes per row, `levels` stride levels, padded
+    strides (every level's stride at least the span of the level below: the rows share
+    no byte), each side starting `phase` bytes past an element boundary."""
+
+    def __init__(self, rng, op, big=False):
+        self.op = op
+        esz = _esz(op)
+        if big:   # >= 1 MiB payload, source in the caller's segment: the direct-source route
+            self.levels, n0, counts = 1, 4096 // esz * 8, [int(1.25 * (1 << 20)) // (4096 * 8)]
+        else:
+            self.levels = int(rng.choice([0, 1, 1, 2, 2, 3, 4, 5, 6, 7]))
+            counts = [int(rng.integers(1, 4 if self.levels >= 3 else 40)) for _ in range(self.levels)]
+            n0 = max(1, int(np.exp(rng.uniform(0, np.log(2048)))))
+            while n0 * int(np.prod(counts)) * esz > (384 << 10) and n0 > 1:
+                n0 //= 2
+        self.n0, self.esz = n0, esz
+        self.count = [n0 * esz] + counts
+
+        def strides():
+            s, out = n0 * esz, []
+            for j in range(self.levels):
+                s = s + esz * int(rng.integers(0, 4))
+                out.append(s)
+                s *= counts[j]
+            return out
+
+        self.dstr, self.sstr = strides(), strides()
+        sub = 4 if esz >= 8 else (1 if op == PUT else 0)
+        self.dphase = int(rng.integers(0, 8)) if op == PUT else (sub if rng.random() < 0.3 else 0)
+        self.sphase = int(rng.integers(0, 8)) if op == PUT else (sub if rng.random() < 0.3 else 0)
+        self.dspan = self.dphase + self._last(self.dstr) + n0 * esz
+        self.sspan = self.sphase + self._last(self.sstr) + n0 * esz
+        self.nb = bool(rng.random() < 0.4)
+        self.src_kind = "seg" if big else str(rng.choice(["buf", "buf", "buf", "host"]))
+        nel = n0 * int(np.prod(counts))
+        self.src = _values(rng, op, nel)                  # in odometer order
+        self.init = rng.integers(0, 256, self.dspan, dtype=np.uint8)   # dst bytes before the call
+        tv = self._typed(self.init, self.dphase)
+        tv[:] = _values(rng, op, tv.size)                 # integer-valued elements at the dst phase
+        self.off = 0            # byte offset of the dst region in the owner's segment
+        self.soff = 0           # byte offset of the source region (buffer, segment or host array)
+
+    def _last(self, strides):
+        return sum(s * (c - 1) for s, c in zip(strides, self.count[1:]))
+
+    def _typed(self, buf, phase):
+        n = (len(buf) - phase) // self.esz
+        return buf[phase:phase + n * self.esz].view(DTYPE[self.op])
+
+    def elems(self, strides, phase):
+        """element indices of the patch, in odometer order, in the typed view at `phase`"""
+        off = np.zeros(1, dtype=np.int64)
+        for j in range(self.levels):
+            off = (off[None, :] + np.arange(self.count[j + 1], dtype=np.int64)[:, None] * strides[j]).ravel()
+        el = (off[:, None] + np.arange(self.n0, dtype=np.int64) * self.esz).ravel()
+        return el // self.esz
+
+    def src_bytes(self):
+        buf = np.random.default_rng(len(self.src)).integers(0, 256, self.sspan, dtype=np.uint8)
+        self._typed(buf, self.sphase)[self.elems(self.sstr, 0)] = self.src
+        return buf
+
+    def expected(self):
+        """the owner's dst region after the call"""
+        out = self.init.copy()
+        tv = self._typed(out, self.dphase)
+        idx = self.elems(self.dstr, 0)
+        if self.op == PUT:
+            tv[idx] = self.src
+        else:
+            tv[idx] = tv[idx] + np.asarray(ALPHA[self.op], dtype=DTYPE[self.op]) * self.src
+        return out
+
+
+def _layout(descs, start=0):
+    off = start
+    for d in descs:
+        d.off = off
+        off += (d.dspan + ALIGN - 1) // ALIGN * ALIGN
+    return off
+
+
+def _shifts(size):
+    if size < 2:
+        return []
+    return sorted({1, size // 2, size - 1})[:3]
+
+
+def _program(seed, rnd, src_rank):
+    """the descriptors source `src_rank` sends in round `rnd` (owner and source both
+    regenerate them from the seed)"""
+    rng = np.random.default_rng([seed, rnd, src_rank])
+    descs = []
+    for op in ACC_OPS + (PUT,):
+        for _ in range(3):
+            descs.append(Desc(rng, op))
+    for op in (DBL, DCP):
+        descs.append(Desc(rng, op, big=True))
+    order = rng.permutation(len(descs))
+    descs = [descs[i] for i in order]
+    end = _layout(descs)
+    # io-vectors: accumulate pairs with repeated destinations, put pairs to distinct slots
+    iov_op = ACC_OPS[rnd % len(ACC_OPS)]
+    esz = _esz(iov_op)
+    m = int(rng.integers(1, 5))                       # elements per pair
+    nslot = 96
+    iov = {"op": iov_op, "m": m, "bytes": m * esz, "nslot": nslot,
+           "acc_dst": rng.integers(0, nslot, 400), "put_dst": rng.permutation(nslot)[:64],
+           "src": _values(rng, iov_op, 400 * m), "put_src": _values(rng, iov_op, 64 * m),
+           "init": _values(rng, iov_op, 2 * nslot * m)}
+    iov["off"] = (end + ALIGN - 1) // ALIGN * ALIGN
+    rmw_off = iov["off"] + 2 * nslot * m * esz
+    rmw_off = (rmw_off + ALIGN - 1) // ALIGN * ALIGN
+    total = rmw_off + 64
+    assert total <= SEG_BYTES, total
+    return descs, iov, rmw_off, total
+
+
+def _iov_expected(iov):
+    m = iov["m"]
+    slots = iov["init"].copy().reshape(2 * iov["nslot"], m)
+    a = np.asarray(ALPHA[iov["op"]], dtype=DTYPE[iov["op"]])
+    np.add.at(slots, iov["acc_dst"], a * iov["src"].reshape(-1, m))
+    slots[iov["nslot"] + iov["put_dst"]] = iov["put_src"].reshape(-1, m)
+    return slots.reshape(-1)
+
+
+def _owner_image(descs, iov, rmw_off, total, expected):
+    img = np.zeros(total, dtype=np.uint8)
+    for d in descs:
+        img[d.off:d.off + d.dspan] = d.expected() if expected else d.init
+    vals = _iov_expected(iov) if expected else iov["init"]
+    raw = vals.view(np.uint8)
+    img[iov["off"]:iov["off"] + raw.size] = raw
+    return img
+
+
+RMW_K = 12
+
+
+def _rmw_expected(src_rank):
+    img = np.zeros(64, dtype=np.uint8)
+    img[0:8] = np.array([RMW_K * (src_rank + 1)], dtype=np.int64).view(np.uint8)
+    img[8:12] = np.array([RMW_K * (src_rank + 2)], dtype=np.int32).view(np.uint8)
+    img[16:24] = np.array([1000 * src_rank + RMW_K - 1], dtype=np.int64).view(np.uint8)
+    return img
+
+
+def _counters(L):
+    from . import owner_counts, route_counts
+    out = (ctypes.c_ulonglong * 1)()
+    L.gaamd_diag(b"peer_gets", 0, out, 1)
+    c = dict(route_counts())
+    c.update({"owner_" + k: v for k, v in owner_counts().items()})
+    c["peer_gets"] = int(out[0])
+    return c
+
+
+def _sum(L, vals):
+    a = (ctypes.c_long * len(vals))(*[int(v) for v in vals])
+    L.armci_msg_lgop(a, len(vals), b"+")
+    return list(a)
+
+
+def _max(L, x):
+    a = (ctypes.c_double * 1)(float(x))
+    L.armci_msg_dgop(a, 1, b"max")
+    return a[0]
+
+
+def xdev_check(rank, size, seed=20260, budget_s=30.0, shifts=None):
+    """One pass of the check (collective over all ranks of the world group).
+    Returns a dict whose "result" is "exact" or "MISMATCH" (the same on every rank)."""
+    from . import DeviceBuffer, comex_malloc, comex_free, make_giov, scale_buffer, int_array, sync
+    L = _lib()
+    t0 = time.perf_counter()
+    shifts = _shifts(size) if shifts is None else shifts
+    c0 = _counters(L)
+    seg = comex_malloc(SEG_BYTES, size)
+    srcseg = comex_malloc(SRC_SEG_BYTES, size)
+    tally = {OP_NAME[op]: [0, 0] for op in ACC_OPS + (PUT,)}          # [patches, wrong bytes]
+    gets = [0, 0]
+    iovt = {"accv": [0, 0], "putv": [0, 0], "getv": [0, 0]}
+    rmw = [0, 0]
+    outside = 0
+    rounds_done = []
+    first_bad = None
+    for rnd, s in enumerate(shifts):
+        tgt, src_of_me = (rank + s) % size, (rank - s) % size
+        # -- the owner writes the initial image of what src_of_me will touch
+        o_descs, o_iov, o_rmw, o_total = _program(seed, rnd, src_of_me)
+        img = _owner_image(o_descs, o_iov, o_rmw, o_total, False)
+        assert L.gaamd_memcpy(ctypes.c_void_p(seg[rank]), img.ctypes.data_as(ctypes.c_void_p), img.nbytes) == 0
+        assert L.gaamd_memset(ctypes.c_void_p(seg[rank] + o_rmw), 0, 64) == 0
+        sync()
+        L.comex_barrier(0)
+        # -- the source: strided accumulates and puts into tgt
+        descs, iov, rmw_off, total = _program(seed, rnd, rank)
+        sbuf_bytes = sum((d.sspan + ALIGN - 1) // ALIGN * ALIGN for d in descs if d.src_kind == "buf")
+        sbuf = DeviceBuffer(max(ALIGN, sbuf_bytes))
+        hosts, keep = [], []
+        so, sso = 0, 0
+        for d in descs:
+            sb = d.src_bytes()
+            if d.src_kind == "buf":
+                d.soff = so
+                sbuf.upload(sb, so)
+                sp = sbuf.ptr + so + d.sphase
+                so += (d.sspan + ALIGN - 1) // ALIGN * ALIGN
+            elif d.src_kind == "seg":
+                d.soff = sso
+                assert L.gaamd_memcpy(ctypes.c_void_p(srcseg[rank] + sso), sb.ctypes.data_as(ctypes.c_void_p),
+                                      sb.nbytes) == 0
+                sp = srcseg[rank] + sso + d.sphase
+                sso += (d.sspan + ALIGN - 1) // ALIGN * ALIGN
+                assert sso <= SRC_SEG_BYTES
+            else:
+                hosts.append(sb)
+                sp = sb.ctypes.data + d.sphase
+            d.src_ptr = sp
+        sync()
+        handles = []
+        for d in descs:
+            dp = ctypes.c_void_p(seg[tgt] + d.off + d.dphase)
+            ss, ds, cnt = int_array(d.sstr), int_array(d.dstr), int_array(d.count)
+            keep += [ss, ds, cnt]
+            h = ctypes.c_int(-1)
+            if d.op == PUT:
+                rc = (L.comex_nbputs(ctypes.c_void_p(d.src_ptr), ss, dp, ds, cnt, d.levels, tgt, 0, ctypes.byref(h))
+                      if d.nb else L.comex_puts(ctypes.c_void_p(d.src_ptr), ss, dp, ds, cnt, d.levels, tgt, 0))
+            else:
+                ka, sp = scale_buffer(d.op, ALPHA[d.op])
+                keep.append(ka)
+                rc = (L.comex_nbaccs(d.op, sp, ctypes.c_void_p(d.src_ptr), ss, dp, ds, cnt, d.levels, tgt, 0,
+                                     ctypes.byref(h)) if d.nb else
+                      L.comex_accs(d.op, sp, ctypes.c_void_p(d.src_ptr), ss, dp, ds, cnt, d.levels, tgt, 0))
+            assert rc == 0, rc
+            if d.nb:
+                handles.append(h)
+        for h in handles:
+            assert L.comex_wait(ctypes.byref(h)) == 0
+        # -- io-vectors: accumulate pairs (repeated destinations), put pairs
+        m, nb_, esz = iov["m"], iov["bytes"], _esz(iov["op"])
+        isrc = DeviceBuffer((iov["src"].nbytes + iov["put_src"].nbytes + ALIGN) // ALIGN * ALIGN)
+        isrc.upload(iov["src"])
+        isrc.upload(iov["put_src"], iov["src"].nbytes)
+        sync()
+        base = seg[tgt] + iov["off"]
+        acc_pairs = ([isrc.ptr + k * nb_ for k in range(len(iov["acc_dst"]))],
+                     [base + int(j) * nb_ for j in iov["acc_dst"]], nb_)
+        put_pairs = ([isrc.ptr + iov["src"].nbytes + k * nb_ for k in range(len(iov["put_dst"]))],
+                     [base + (iov["nslot"] + int(j)) * nb_ for j in iov["put_dst"]], nb_)
+        ka, sp = scale_buffer(iov["op"], ALPHA[iov["op"]])
+        arr, kk = make_giov([acc_pairs])
+        assert L.comex_accv(iov["op"], sp, ctypes.cast(arr, ctypes.c_void_p), 1, tgt, 0) == 0
+        arr2, kk2 = make_giov([put_pairs])
+        assert L.comex_putv(ctypes.cast(arr2, ctypes.c_void_p), 1, tgt, 0) == 0
+        # -- rmw: fetch-and-add long and int, then swaps, one source per word
+        rb = seg[tgt] + rmw_off
+        loc = ctypes.c_long(0)
+        loci = ctypes.c_int(0)
+        for k in range(RMW_K):
+            assert L.comex_rmw(13, ctypes.byref(loc), ctypes.c_void_p(rb), rank + 1, tgt, 0) == 0
+            rmw[0] += 1
+            if loc.value != k * (rank + 1):
+                rmw[1] += 1
+            assert L.comex_rmw(12, ctypes.byref(loci), ctypes.c_void_p(rb + 8), rank + 2, tgt, 0) == 0
+            rmw[0] += 1
+            if loci.value != k * (rank + 2):
+                rmw[1] += 1
+        for k in range(RMW_K):
+            loc.value = 1000 * rank + k
+            assert L.comex_rmw(11, ctypes.byref(loc), ctypes.c_void_p(rb + 16), 0, tgt, 0) == 0
+            rmw[0] += 1
+            if loc.value != (0 if k == 0 else 1000 * rank + k - 1):
+                rmw[1] += 1
+        L.comex_barrier(0)
+        # -- the owner checks its segment: every patch, the io-vector slots, the rmw words,
+        #    and that no byte between the patches changed
+        want = _owner_image(o_descs, o_iov, o_rmw, o_total, True)
+        got = np.empty(o_total, dtype=np.uint8)
+        assert L.gaamd_memcpy(got.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(seg[rank]), o_total) == 0
+        for d in o_descs:
+            bad = int(np.count_nonzero(got[d.off:d.off + d.dspan] != want[d.off:d.off + d.dspan]))
+            tally[OP_NAME[d.op]][0] += 1
+            tally[OP_NAME[d.op]][1] += bad
+            if bad and first_bad is None:
+                first_bad = {"owner": rank, "source": src_of_me, "op": OP_NAME[d.op], "levels": d.levels,
+                             "count": d.count, "dst_stride": d.dstr, "dst_phase": d.dphase, "src": d.src_kind,
+                             "nb": d.nb, "wrong_bytes": bad}
+        mask = np.ones(o_total, dtype=bool)
+        for d in o_descs:
+            mask[d.off:d.off + d.dspan] = False
+        mask[o_iov["off"]:o_iov["off"] + o_iov["init"].nbytes] = False
+        mask[o_rmw:] = False
+        outside += int(np.count_nonzero(got[mask] != 0))
+        ioff, isz = o_iov["off"], o_iov["init"].nbytes
+        half = isz // 2
+        iovt["accv"][0] += 1
+        iovt["accv"][1] += int(np.count_nonzero(got[ioff:ioff + half] != want[ioff:ioff + half]))
+        iovt["putv"][0] += 1
+        iovt["putv"][1] += int(np.count_nonzero(got[ioff + half:ioff + isz] != want[ioff + half:ioff + isz]))
+        rw = np.empty(64, dtype=np.uint8)
+        assert L.gaamd_memcpy(rw.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(seg[rank] + o_rmw), 64) == 0
+        rmw[0] += 1
+        rmw[1] += int(np.count_nonzero(rw != _rmw_expected(src_of_me)))
+        # -- the source reads every patch back from tgt (strided gets), and the io-vector
+        #    slots (getv)
+        gbuf = DeviceBuffer(max(ALIGN, sum((d.sspan + ALIGN - 1) // ALIGN * ALIGN for d in descs)))
+        go = 0
+        handles = []
+        places = []
+        for i, d in enumerate(descs):
+            host = i % 3 == 2
+            hb = np.zeros(d.sspan, dtype=np.uint8) if host else None
+            dst = hb.ctypes.data + d.sphase if host else gbuf.ptr + go + d.sphase
+            ss, ds, cnt = int_array(d.sstr), int_array(d.dstr), int_array(d.count)
+            keep += [ss, ds, cnt]
+            sp_ = ctypes.c_void_p(seg[tgt] + d.off + d.dphase)
+            h = ctypes.c_int(-1)
+            if d.nb and not host:
+                assert L.comex_nbgets(sp_, ds, ctypes.c_void_p(dst), ss, cnt, d.levels, tgt, 0, ctypes.byref(h)) == 0
+                handles.append(h)
+            else:
+                assert L.comex_gets(sp_, ds, ctypes.c_void_p(dst), ss, cnt, d.levels, tgt, 0) == 0
+            places.append((d, hb, go))
+            go += (d.sspan + ALIGN - 1) // ALIGN * ALIGN
+        for h in handles:
+            assert L.comex_wait(ctypes.byref(h)) == 0
+        sync()
+        for d, hb, go_ in places:
+            if hb is None:
+                hb = gbuf.download(np.uint8, d.sspan, go_)
+            exp = d._typed(d.expected(), d.dphase)[d.elems(d.dstr, 0)]
+            got_el = d._typed(hb, d.sphase)[d.elems(d.sstr, 0)]
+            bad = int(np.count_nonzero(got_el.view(np.uint8) != exp.view(np.uint8)))
+            gets[0] += 1
+            gets[1] += bad
+            if bad and first_bad is None:
+                first_bad = {"get_from": tgt, "by": rank, "op": OP_NAME[d.op], "levels": d.levels, "count": d.count,
+                             "wrong_bytes": bad}
+        iv_exp = _iov_expected(iov)
+        back = np.zeros(2 * iov["nslot"] * m, dtype=DTYPE[iov["op"]])
+        get_pairs = ([base + k * nb_ for k in range(2 * iov["nslot"])],
+                     [back.ctypes.data + k * nb_ for k in range(2 * iov["nslot"])], nb_)
+        arr3, kk3 = make_giov([get_pairs])
+        assert L.comex_getv(ctypes.cast(arr3, ctypes.c_void_p), 1, tgt, 0) == 0
+        iovt["getv"][0] += 1
+        iovt["getv"][1] += int(np.count_nonzero(back.view(np.uint8) != iv_exp.view(np.uint8)))
+        del esz
+        sbuf.free()
+        isrc.free()
+        gbuf.free()
+        L.comex_barrier(0)
+        rounds_done.append(s)
+        if _max(L, time.perf_counter() - t0) > budget_s:
+            break
+    c1 = _counters(L)
+    comex_free(srcseg[rank])
+    comex_free(seg[rank])
+    keys = sorted(c1)
+    routes = dict(zip(keys, _sum(L, [c1[k] - c0[k] for k in keys])))
+    names = sorted(tally)
+    sums = _sum(L, [v for n in names for v in tally[n]] + gets + [v for k in ("accv", "putv", "getv")
+                                                                  for v in iovt[k]] + rmw + [outside])
+    it = iter(sums)
+    res_ops = {n: {"patches": next(it), "wrong_bytes": next(it)} for n in names}
+    res_gets = {"patches": next(it), "wrong_bytes": next(it)}
+    res_iov = {k: {"calls": next(it), "wrong_bytes": next(it)} for k in ("accv", "putv", "getv")}
+    res_rmw = {"checks": next(it), "wrong": next(it)}
+    outside_all = next(it)
+    wrong = (sum(v["wrong_bytes"] for v in res_ops.values()) + res_gets["wrong_bytes"]
+             + sum(v["wrong_bytes"] for v in res_iov.values()) + res_rmw["wrong"] + outside_all)
+    res = {"result": "exact" if wrong == 0 else "MISMATCH", "shifts": rounds_done, "seed": seed,
+           "strided": res_ops, "gets": res_gets, "iov": res_iov, "rmw": res_rmw,
+           "bytes_outside_patches_changed": outside_all, "routes_all_ranks": routes,
+           "seconds": round(_max(L, time.perf_counter() - t0), 2)}
+    # the first wrong patch some rank saw (the lowest such rank's)
+    who = _max(L, -rank if first_bad is not None else -1e9)
+    if wrong and who > -1e9 and -int(who) == rank:
+        res["first_wrong_patch_on_this_rank"] = first_bad
+    return res
+
+
+def xdev_check_diagnosed(rank, size, seed=20260, budget_s=30.0, shifts=None):
+    """xdev_check, and on MISMATCH the same check (same seed) once more in this process
+    under the conservative publication mode: "clears: visibility" if it then reads
+    exact, "persists: logic" if not.  The mode is restored afterwards."""
+    L = _lib()
+    res = xdev_check(rank, size, seed, budget_s, shifts)
+    if res["result"] == "exact":
+        return res
+    old = (ctypes.c_ulonglong * 1)()
+    L.gaamd_diag(b"publish", 1, old, 1)
+    try:
+        again = xdev_check(rank, size, seed, budget_s, shifts)
+    finally:
+        L.gaamd_diag(b"publish", int(old[0]), None, 0)
+    res["conservative_rerun"] = again
+    res["diagnosis"] = ("clears: visibility -- exact once every post and fence carries a system-scope release"
+                        if again["result"] == "exact" else
+                        "persists: logic -- wrong under the conservative publication mode too")
+    return res

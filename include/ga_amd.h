@@ -194,6 +194,18 @@ const char *gaamd_build_id(void);
  *   "pinned_threads" out[0] (nout >= 1): threads that hold pinned bounce buffers or
  *                   a non-blocking ring now (a thread's are freed when it ends, every
  *                   thread's at comex_finalize).
+ *   "publish"       1: the conservative publication mode -- every direct-source
+ *                   post, every packed-chunk post and every fence first records a
+ *                   system-scope release (hipEventReleaseToSystem) on each library
+ *                   stream and waits for them (the markers round 5 measured and took
+ *                   out of the default path); 0: the default; -1 leaves it.  out[0]
+ *                   (nout >= 1) receives the previous setting.  Used to classify a
+ *                   cross-GPU mismatch as visibility (clears) or logic (persists).
+ *   "drop_chunk"    N > 0: the owner's progress thread counts every N-th packed chunk
+ *                   applied without running its kernel (a test hook: a logic fault);
+ *                   0: off.
+ *   "peer_gets"     out[0] (nout >= 1): strided gets this rank read from another GPU's
+ *                   memory with system-scope loads.
  *   "vmm_window"    out[0], out[1] (nout >= 2): bytes of the vmm allocator's private
  *                   address window taken so far and bytes left.  Every mapping (this
  *                   rank's blocks and its imports of peers' blocks) takes
