@@ -587,13 +587,23 @@ def c5_extras(args, dist, wd=None):
     the owner's unpack-acc reading it over xGMI).  Few steps: these are reported
     beside the headline, not as `value`."""
     out = {}
-    # the exchange's exactness FIRST, on a small GA (4096^2, both routes) before any
-    # timed C5 step (VERDICT r4 item 5): on the first run over separate GPUs a
-    # visibility bug reads as exchange_precheck MISMATCH, not as a plausible rate
+    # every cross-GPU operation FIRST (VERDICT r5 item 1): remote strided acc of every
+    # type, put and get with seeded random descriptors, accv/putv/getv, rmw, between
+    # rank pairs, exact by closed form (ga_amd/xcheck.py, no oracle), the routes it
+    # exercised summed over the ranks; a MISMATCH is rerun at once under the
+    # conservative publication mode and classified (VERDICT r5 item 2)
+    if not args.no_xcheck:
+        if wd is not None:
+            wd.phase = "xdev_check"
+        from ga_amd.xcheck import xdev_check_diagnosed
+        out["xdev_check"] = xdev_check_diagnosed(dist.rank, dist.size, budget_s=args.xcheck_s)
+    # the exchange's exactness on a small GA (4096^2, both routes) before any timed C5
+    # step (VERDICT r4 item 5): on the first run over separate GPUs a visibility bug
+    # reads as exchange_precheck MISMATCH, not as a plausible rate
     if wd is not None:
         wd.phase = "exchange_precheck"
     assert ga_amd_lib().GA_Initialize() == 0
-    out["exchange_precheck"] = {route: c5_exchange_check(dist, src_seg, n=4096) for route, src_seg in
+    out["exchange_precheck"] = {route: exchange_check_diagnosed(dist, src_seg, n=4096) for route, src_seg in
                                 (("buffer_src", False), ("segment_src", True))}
     saved = args.src_seg
     m2 = max(1, args.c5_steps // 2)
@@ -649,7 +659,7 @@ def c5_extras(args, dist, wd=None):
     n_chk = args.ga_dims if args.ga_dims else GA_DIMS[0]
     if wd is not None:
         wd.phase = "exchange_check"
-    out["exchange_check"] = {route: c5_exchange_check(dist, src_seg, n=n_chk) for route, src_seg in
+    out["exchange_check"] = {route: exchange_check_diagnosed(dist, src_seg, n=n_chk) for route, src_seg in
                              (("buffer_src", False), ("segment_src", True))}
     # diagnostics only (BENCH_CHECK_LOOPS=n): the exchange check n more times per route,
     # with the first mismatch's details (never the driver's runs)
@@ -667,6 +677,26 @@ def c5_extras(args, dist, wd=None):
         out["exchange_check_loops"] = rep
     ga_amd_lib().GA_Terminate()
     return out
+
+
+def exchange_check_diagnosed(dist, src_seg, n):
+    """c5_exchange_check, and on MISMATCH once more in this process under the
+    conservative publication mode (gaamd_diag "publish": a system-scope release on
+    every library stream before every post and fence): a mismatch that clears is a
+    visibility fault, one that persists a logic fault."""
+    res = c5_exchange_check(dist, src_seg, n=n)
+    if res["result"] == "exact":
+        return res
+    L = ga_amd_lib()
+    old = (ctypes.c_ulonglong * 1)()
+    L.gaamd_diag(b"publish", 1, old, 1)
+    try:
+        again = c5_exchange_check(dist, src_seg, n=n)
+    finally:
+        L.gaamd_diag(b"publish", int(old[0]), None, 0)
+    res["conservative_rerun"] = again
+    res["diagnosis"] = ("clears: visibility" if again["result"] == "exact" else "persists: logic")
+    return res
 
 
 def ga_amd_lib():
@@ -990,7 +1020,10 @@ def main():
     ap.add_argument("--ga-dims", type=int, default=0, help="C5: square GA of this size instead of 32768^2")
     ap.add_argument("--c5-steps", type=int, default=4, help="N>1: timed C5 M1 steps (M2: half as many)")
     ap.add_argument("--no-extras", action="store_true", help="N>1: skip the C5 M1/M2 measurements")
-    ap.add_argument("--extras-timeout", type=float, default=180.0,
+    ap.add_argument("--no-xcheck", action="store_true", help="N>1: skip the cross-GPU self-check (xdev_check)")
+    ap.add_argument("--xcheck-s", type=float, default=30.0,
+                    help="N>1: seconds after which the cross-GPU self-check stops after its current round")
+    ap.add_argument("--extras-timeout", type=float, default=300.0,
                     help="N>1: seconds the C5 extras may take before the headline line is printed without them")
     ap.add_argument("--verbose", action="store_true", help="progress lines on stderr")
     args = ap.parse_args()

@@ -118,6 +118,8 @@ def main():
         stale_fix_test(L, rank, size)
     elif mode == "oddseg":
         odd_segment_test(L, rank, size)
+    elif mode == "xcheck":
+        xcheck_test(L, rank, size)
     elif mode in ("armcimisc", "armcimisc-gloo"):
         armci_misc_test(L, rank, size)
     elif mode in ("rdesc", "rdesc-gloo"):
@@ -812,6 +814,41 @@ def stale_fix_test(L, rank, size):
     # process leaves through the exit hook (STALEFIX_NO_FINALIZE=1)
     if os.environ.get("STALEFIX_NO_FINALIZE") != "1":
         assert ga_amd.comex_finalize() == 0
+
+
+def xcheck_test(L, rank, size):
+    """ga_amd/xcheck.py, the check bench.py's N > 1 extras open with: every remote
+    operation between rank pairs, exact by closed form, route counters summed over
+    ranks.  XCHECK_DROP=N: the owners drop every N-th packed chunk (gaamd_diag
+    "drop_chunk"), so the check must read MISMATCH and the conservative rerun must
+    classify it "persists: logic".  Rank 0 prints the report as one XCHECK line."""
+    import json
+    import ga_amd
+    from ga_amd.xcheck import xdev_check_diagnosed
+    assert ga_amd.comex_init() == 0
+    drop = int(os.environ.get("XCHECK_DROP", "0"))
+    if drop:
+        assert L.gaamd_diag(b"drop_chunk", drop, None, 0) == 0
+    res = xdev_check_diagnosed(rank, size, seed=int(os.environ.get("XCHECK_SEED", "20260")), budget_s=90.0)
+    if rank == 0:
+        print("XCHECK " + json.dumps(res), flush=True)
+    if drop:
+        assert res["result"] == "MISMATCH", res
+        assert res["diagnosis"].startswith("persists: logic"), res
+        assert res["conservative_rerun"]["result"] == "MISMATCH"
+        say(rank, "dropped chunks read MISMATCH, classified " + res["diagnosis"][:16])
+    else:
+        assert res["result"] == "exact", json.dumps(res)[:3000]
+        routes = res["routes_all_ranks"]
+        assert routes["peer_gets"] + routes["one_pass"] + routes["packed"] > 0, routes
+        if L.gaamd_device_count() >= 1 and os.environ.get("COMEX_AMD_PEER_LOADS") == "all":
+            # every peer another GPU: puts and accumulates packed, >= 1 MiB segment sources
+            # direct, gets read with system-scope loads
+            assert routes["packed"] > 0 and routes["direct_src"] > 0 and routes["peer_gets"] > 0, routes
+            assert routes["owner_packed"] > 0 and routes["owner_direct_src"] > 0, routes
+            assert routes["iov"] > 0 and routes["rmw"] > 0, routes
+    ga_amd.comex_barrier()
+    assert ga_amd.comex_finalize() == 0
 
 
 def odd_segment_test(L, rank, size):

@@ -146,6 +146,7 @@ def test_remote_across_devices():
     launch("remote", n=n, timeout=180, extra_env={"TEST_DISTINCT_DEVICES": "1"})
     launch("order", n=n, timeout=180)
     launch("rdesc", n=2, timeout=170)   # random descriptors from GPU 0 into GPU 1's segment
+    launch("xcheck", n=n, timeout=240)  # the bench's cross-GPU self-check, every rank pair shift
     launch("c5full", n=n, timeout=420, extra_env={"COMEX_AMD_STAGING_MB": "256", "TEST_DISTINCT_DEVICES": "1"})
 
 
@@ -542,6 +543,26 @@ def test_segment_cache_reuse(n, cache):
     their size; remote accumulates into reused segments stay exact (and with the cache
     off, every segment is a fresh block)."""
     launch("segcache", n=n, timeout=120, extra_env={"COMEX_AMD_SEGMENT_CACHE_MB": cache})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,peer", [(2, "all"), (3, "all"), (2, "auto")])
+def test_xdev_self_check(n, peer):
+    """the self-check bench.py's N > 1 extras open with -- remote
+    strided acc (every type) / put / get with random descriptors, accv / putv / getv,
+    rmw, between rank pairs -- exact by closed form on one MI355X; with every peer
+    treated as another GPU (PEER_LOADS=all) the packed, direct-source and system-scope
+    get routes all ran (route counters summed over the ranks)."""
+    outs = launch("xcheck", n=n, timeout=200, extra_env={"COMEX_AMD_PEER_LOADS": peer})
+    assert any(l.startswith("XCHECK ") for l in outs[0].splitlines())
+
+
+@pytest.mark.gpu
+def test_xdev_self_check_classifies_a_dropped_chunk():
+    """the owners drop every 7th packed chunk (gaamd_diag
+    "drop_chunk"); the check reads MISMATCH, reruns in the same processes under the
+    conservative publication mode, reads MISMATCH again and says "persists: logic"."""
+    launch("xcheck", n=2, timeout=200, extra_env={"COMEX_AMD_PEER_LOADS": "all", "XCHECK_DROP": "7"})
 
 
 @pytest.mark.gpu
