@@ -200,9 +200,9 @@ def toggle_counts():
 
 def iov_path_counts():
     """local io-vector launches with repeated-destination ordering, by path"""
-    c = (ctypes.c_ulonglong * 3)()
+    c = (ctypes.c_ulonglong * 4)()
     lib().gaamd_iov_path_counts(c)
-    return {"hashed": c[0], "hashed_then_radix": c[1], "radix": c[2]}
+    return {"hashed": c[0], "hashed_then_radix": c[1], "radix": c[2], "lds": c[3]}
 
 
 def owner_counts():

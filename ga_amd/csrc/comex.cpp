@@ -1213,7 +1213,7 @@ int gaamd_diag(const char *key, long long value, unsigned long long *out, int no
 }
 
 int gaamd_iov_path_counts(unsigned long long counts[3]) {
-    for (int k = 0; k < 3; ++k) counts[k] = g_iov_path[k].load(std::memory_order_relaxed);
+    for (int k = 0; k < 4; ++k) counts[k] = g_iov_path[k].load(std::memory_order_relaxed);
     return 0;
 }
 

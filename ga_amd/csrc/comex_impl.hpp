@@ -187,7 +187,7 @@ extern std::atomic<unsigned long long> g_one_pass;
 // ---- io-vector transfers (iov.cpp) -------------------------------------------
 int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int proc, int group, comex_request_t *hdl);
 void iov_finalize();
-extern std::atomic<unsigned long long> g_iov_path[3];   // gaamd_iov_path_counts
+extern std::atomic<unsigned long long> g_iov_path[4];   // gaamd_iov_path_counts
 extern std::atomic<unsigned long long> g_iov_host_sides;   // gaamd_diag("iov_host_sides")
 bool host_cpu_range_probe(uint64_t lo, uint64_t hi, bool write);   // gaamd_diag("host_range")
 

@@ -71,6 +71,7 @@ constexpr uint32_t kIovRunSkip = 0xffffffffu;   // k_iov_runs: a run of this key
 
 // the hashed path's state for one launch (see k_iovh_insert below)
 struct IovHashArgs {
+    bool lds;              // k_iov_lds (one workgroup) instead of the hashed apply + conflicts
     uint64_t dlo;
     uint32_t shift;
     bool pow2;
@@ -267,6 +268,145 @@ __global__ __launch_bounds__(1024) void k_iovh_conf(const IovDesc d, const OP op
     }
 }
 
+// ---------------------------------------------------------------------------
+// One-workgroup io-vector path: up to kIovLdsMax pairs whose
+// destinations may repeat are ordered AND applied by one launch of one 1024-thread
+// workgroup, everything it orders held in LDS -- the hashed path's three launches
+// (insert, apply, conflicts: 17.6 + 5.1 + 4.1 us at 16 Ki pairs, profiles/r05/iov3)
+// and their device-scope atomics on an HBM table were what kept a 16 Ki-pair
+// scatter-accumulate behind the reference's one-core loop.
+//   keys  : each pair's destination unit (dst - dlo) / bytes, read once from the
+//           list (through the mapped pinned staging: no upload launch)
+//   table : open addressing, 2^15 16-bit slots (pair index; top bit: the slot's key
+//           has more than one pair), claimed with an LDS compare-and-swap
+//   apply : a pair alone on its destination is applied at once, its vectors spread
+//           over all lanes; the pairs of repeated destinations are listed (over the
+//           table, no longer needed), sorted by (key, index) with an LDS bitonic sort,
+//           and each destination's pairs applied in index order by one lane -- the
+//           reference's order (comex.c:7342-7351: one _acc per pair, in order).
+// A destination is rebuilt from its key (dlo + key * bytes: the caller guarantees
+// every destination a whole number of pairs from dlo), so the list is read once.
+constexpr uint32_t kIovLdsLog = 15;                       // table slots: 2^15 = 2 x pairs
+constexpr uint32_t kIovLdsEmpty = 0xffffu;
+
+template <class OP, int W, bool SYS>
+__device__ __forceinline__ void iov_lds_pair(const IovDesc &d, const OP &op, uint32_t i, char *dp) {
+    const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
+    for (uint32_t v = 0; v < d.nvec; ++v) {
+        typename Vec<W>::T x = src_load<W, SYS>(sp + (size_t)v * W), y = x;
+        if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
+        vstore<W, false>(dp + (size_t)v * W, op.template apply<W>(y, x));
+    }
+}
+
+template <class OP, int W, bool SYS>
+__global__ __launch_bounds__(1024) void k_iov_lds(const IovDesc d, const OP op, uint64_t dlo, uint32_t shift,
+                                                  bool pow2) {
+    __shared__ uint32_t keys[kIovLdsMax];
+    __shared__ uint32_t tab[(1u << kIovLdsLog) / 2];      // two 16-bit slots per word; later the conflict list
+    __shared__ uint32_t rep[kIovLdsMax / 32];             // pair i's destination repeats
+    __shared__ uint32_t nconf;
+    const uint32_t t = threadIdx.x, n = d.n;
+    constexpr uint32_t mask = (1u << kIovLdsLog) - 1u;
+    for (uint32_t w = t; w < (1u << kIovLdsLog) / 2; w += 1024) tab[w] = 0xffffffffu;
+    for (uint32_t w = t; w < kIovLdsMax / 32; w += 1024) rep[w] = 0;
+    if (t == 0) nconf = 0;
+    for (uint32_t i = t; i < n; i += 1024) {
+        const uint64_t off = d.dst_list[i] - dlo;
+        keys[i] = (uint32_t)(pow2 ? (off >> shift) : off / (uint64_t)d.bytes);
+    }
+    __syncthreads();
+    // insert: the lane whose compare-and-swap claims an empty slot is its key's first
+    // pair; a lane that finds its key in a slot marks that slot repeated
+    for (uint32_t i = t; i < n; i += 1024) {
+        const uint32_t key = keys[i];
+        uint32_t h = (key * 0x9E3779B1u) >> (32 - kIovLdsLog);
+        for (;;) {
+            uint32_t *wp = &tab[h >> 1];
+            const uint32_t sh = (h & 1u) * 16u;
+            const uint32_t cur = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t e = (cur >> sh) & 0xffffu;
+            if (e == kIovLdsEmpty) {
+                if (atomicCAS(wp, cur, (cur & ~(0xffffu << sh)) | (i << sh)) == cur) break;
+                continue;                                   // the word changed under us: look again
+            }
+            if (keys[e & 0x7fffu] == key) {
+                atomicOr(wp, 0x8000u << sh);
+                break;
+            }
+            h = (h + 1u) & mask;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += 1024) {
+        const uint32_t key = keys[i];
+        uint32_t h = (key * 0x9E3779B1u) >> (32 - kIovLdsLog), e;
+        for (;; h = (h + 1u) & mask) {
+            e = (tab[h >> 1] >> ((h & 1u) * 16u)) & 0xffffu;
+            if (keys[e & 0x7fffu] == key) break;            // the key's slot (it was inserted)
+        }
+        if (e & 0x8000u) atomicOr(&rep[i >> 5], 1u << (i & 31u));
+    }
+    __syncthreads();
+    uint32_t *conf = tab;                                   // the table is done with
+    // pairs alone on their destination: every vector of them at once, four per lane in flight
+    constexpr int U = 4;
+    for (uint32_t base = 0; base < d.items; base += 1024u * U) {
+        typename Vec<W>::T a[U], b[U];
+        char *dps[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint32_t g = base + (uint32_t)k * 1024u + t;
+            dps[k] = nullptr;
+            if (g >= d.items) continue;
+            const uint32_t i = d.nvec_div.div(g), v = g - i * d.nvec;
+            if ((rep[i >> 5] >> (i & 31u)) & 1u) {
+                if (v == 0) conf[atomicAdd(&nconf, 1u)] = i;
+                continue;
+            }
+            const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
+            dps[k] = (char *)(dlo + (uint64_t)keys[i] * (uint64_t)d.bytes) + (size_t)v * W;
+            a[k] = src_load<W, SYS>(sp + (size_t)v * W);
+            if constexpr (OP::kReadsDst) b[k] = vload<W, false>(dps[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (dps[k]) vstore<W, false>(dps[k], op.template apply<W>(b[k], a[k]));
+    }
+    __syncthreads();
+    const uint32_t m = nconf;
+    if (m == 0) return;
+    uint32_t P = 1;
+    while (P < m) P <<= 1;
+    for (uint32_t u = m + t; u < P; u += 1024) conf[u] = 0xffffffffu;   // sorts last
+    __syncthreads();
+    // bitonic sort of the listed pairs by (key, pair index)
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t u = t; u < P; u += 1024) {
+                const uint32_t l = u ^ j;
+                if (l <= u) continue;
+                const uint32_t x = conf[u], y = conf[l];
+                const bool gt = x == 0xffffffffu ? y != 0xffffffffu
+                              : y == 0xffffffffu ? false
+                              : (keys[x] != keys[y] ? keys[x] > keys[y] : x > y);
+                if (gt == ((u & k) == 0)) {
+                    conf[u] = y;
+                    conf[l] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // one lane per repeated destination: its pairs in index order
+    for (uint32_t u = t; u < m; u += 1024) {
+        const uint32_t key = keys[conf[u]];
+        if (u > 0 && keys[conf[u - 1]] == key) continue;
+        char *dp = (char *)(dlo + (uint64_t)key * (uint64_t)d.bytes);
+        for (uint32_t w = u; w < m && keys[conf[w]] == key; ++w) iov_lds_pair<OP, W, SYS>(d, op, conf[w], dp);
+    }
+}
+
 // the fallback's keys: pairs k_iovh_apply already applied (their slot not marked
 // repeated) get the sentinel key, sorted last and skipped by k_iov_runs
 __global__ __launch_bounds__(256) void k_iov_keys_masked(const uint64_t *dst_list, uint64_t dlo, uint32_t bytes,
@@ -281,7 +421,9 @@ __global__ __launch_bounds__(256) void k_iov_keys_masked(const uint64_t *dst_lis
 
 template <class OP, int W, bool SYS>
 static hipError_t iov_ws(const IovDesc &d, const OP &op, bool serial, hipStream_t st, const IovHashArgs *ha) {
-    if (ha) {
+    if (ha && ha->lds) {
+        hipLaunchKernelGGL((k_iov_lds<OP, W, SYS>), dim3(1), dim3(1024), 0, st, d, op, ha->dlo, ha->shift, ha->pow2);
+    } else if (ha) {
         hipLaunchKernelGGL((k_iovh_apply<OP, W, SYS>), dim3((d.n + kIovhBS - 1) / kIovhBS), dim3(kIovhBS), 0, st, d, op,
                            ha->dlo,
                            ha->shift, ha->pow2, ha->epoch, ha->dup, ha->slot, ha->conf, ha->count);
@@ -603,11 +745,36 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
                        (uint64_t *)d.src_list);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return -100 - (int)e;
-    IovHashArgs ha{dlo, shift, pow2, h->epoch, dup, slot, conf, count, h->flag_dev};
+    IovHashArgs ha{false, dlo, shift, pow2, h->epoch, dup, slot, conf, count, h->flag_dev};
     h->dlo = dlo;
     h->n = d.n;
     h->shift = shift;
     h->pow2 = pow2;
+    return iov_dispatch(op, scale, W, d, false, src_peer, stream, &ha);
+}
+
+int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
+                   hipStream_t stream, bool src_peer) {
+    const int esz = elem_size(op);
+    if (!esz || d.bytes <= 0 || d.bytes > kIovRunsMaxBytes || !d.dst_list) return -4;
+    if (op != kOpCopy && !scale) return -5;
+    if (d.n > kIovLdsMax || units > (1ull << 32)) return 1;   // another path
+    const int64_t row = (op == kOpCopy) ? d.bytes : (int64_t)(d.bytes / esz) * esz;   // acc.h:122
+    if (d.n == 0 || row == 0) return 0;
+    uint64_t a = align_or | (uint64_t)row | 16;
+    if (!d.src_list) a |= (uint64_t)(uintptr_t)d.src_base | (uint64_t)d.bytes;
+    int W = (int)lowbit(a);
+    if (W > 16) W = 16;
+    if (W < esz) {
+        if (W < 4) return -8;
+        W = esz;
+    }
+    d.nvec = (uint32_t)(row / W);
+    d.nvec_div = make_fastdiv(d.nvec);
+    d.items = d.n * d.nvec;
+    const bool pow2 = (d.bytes & (d.bytes - 1)) == 0;
+    const uint32_t shift = pow2 ? (uint32_t)__builtin_ctz((unsigned)d.bytes) : 0;
+    IovHashArgs ha{true, dlo, shift, pow2, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
     return iov_dispatch(op, scale, W, d, false, src_peer, stream, &ha);
 }
 

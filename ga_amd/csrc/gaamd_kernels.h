@@ -72,6 +72,9 @@ struct Tuning {
     // every wave of a workgroup and applied in order from LDS (k_ordered_cols_lds); 1 one lane
     // per column slice loading its own rows (k_ordered_cols); 0 the one-workgroup kernel
     int ordered_cols = 2;
+    // io-vectors of at most kIovLdsMax pairs whose destinations may repeat: 1 (default) the
+    // one-workgroup LDS kernel, 0 the hashed three-launch path (kept for A/B and fallback)
+    int iov_lds = 1;
 };
 Tuning &tuning();
 
@@ -186,5 +189,11 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
                       uint64_t units, hipStream_t stream, bool src_peer = false, const uint64_t *dst_in = nullptr,
                       const uint64_t *src_in = nullptr);
 bool iov_hash_overflowed(const IovHash *h);
+// The same contract for up to kIovLdsMax pairs in ONE launch of one workgroup (the
+// ordering held in LDS, k_iov_lds); d.dst_list / d.src_list may point into mapped
+// pinned memory (read once).  Returns 1 when n is outside its range.
+constexpr uint32_t kIovLdsMax = 16384;
+int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
+                   hipStream_t stream, bool src_peer = false);
 
 }  // namespace gaamd

@@ -27,7 +27,7 @@ static char *g_iov_scratch = nullptr;
 static size_t g_iov_scratch_bytes = 0;
 // gaamd_iov_path_counts: local io-vector launches with repeated-destination
 // ordering, by path: hashed, hashed + radix fallback (conflicts overflowed), radix
-std::atomic<unsigned long long> g_iov_path[3];
+std::atomic<unsigned long long> g_iov_path[4];
 
 static char *g_iov_host = nullptr;
 static size_t g_iov_host_bytes = 0;
@@ -466,7 +466,7 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         else if (!src_listed) d.src_base = up_dev + o_src;
         if (d.dst_list) d.dst_list = (const uint64_t *)(up_dev + o_dst);
     } else if (runs) {
-        if (!src_listed && o_res > o_src) upload_pinned(dev + o_src, up + o_src, o_res - o_src, r.streams[si]);
+        // (packed sources go up below unless the one-workgroup kernel reads them in place)
     } else if (up_hi > up_lo) {
         upload_pinned(dev + up_lo, up + up_lo, up_hi - up_lo, r.streams[si]);
     }
@@ -477,10 +477,22 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         // destination), or the radix path above 2^19 pairs
         static IovHash *g_hash = nullptr;
         rc = 1;
-        {
+        char *up_dev = nullptr;   // the device view of the pinned upload buffer
+        GA_HIP(hipHostGetDevicePointer((void **)&up_dev, up, 0));
+        if (n <= (int)kIovLdsMax && !src_peer && tuning().iov_lds) {
+            // up to 16 Ki pairs: ordered and applied by one launch of one workgroup, the
+            // lists (and packed sources) read in place from the pinned staging
+            IovDesc z = d;
+            z.dst_list = (const uint64_t *)(up_dev + o_dst);
+            if (d.src_list) z.src_list = (const uint64_t *)(up_dev + o_src);
+            else if (!src_listed) z.src_base = up_dev + o_src;
+            rc = launch_iov_lds(cop, scale, z, align_or, dlo, units, r.streams[si]);
+            if (rc == 0) g_iov_path[3].fetch_add(1, std::memory_order_relaxed);
+        }
+        if (rc == 1 && !src_listed && o_res > o_src)
+            upload_pinned(dev + o_src, up + o_src, o_res - o_src, r.streams[si]);
+        if (rc == 1) {
             if (!g_hash) g_hash = iov_hash_create();
-            char *up_dev = nullptr;   // the device view of the pinned upload buffer
-            GA_HIP(hipHostGetDevicePointer((void **)&up_dev, up, 0));
             rc = launch_iov_hashed(g_hash, cop, scale, d, align_or, dlo, units, r.streams[si], src_peer,
                                    (const uint64_t *)(up_dev + o_dst),
                                    d.src_list ? (const uint64_t *)(up_dev + o_src) : nullptr);

@@ -138,6 +138,7 @@ static int *tuning_field(const char *key) {
     if (!strcmp(key, "align")) return &t.align;
     if (!strcmp(key, "flat_line_min")) return &t.flat_line_min;
     if (!strcmp(key, "ordered_cols")) return &t.ordered_cols;
+    if (!strcmp(key, "iov_lds")) return &t.iov_lds;
     return nullptr;
 }
 

@@ -310,8 +310,12 @@ static void progress_loop() {
                 d.dst_list = (const uint64_t *)(packed + iov_list_off(q.count[1], q.count[0]));
                 d.bytes = q.count[0];
                 d.n = (uint32_t)q.count[1];
-                int rc;
-                if (q.iov_serial == 2) {
+                int rc = 1;
+                const uint64_t units = (q.dst_hi - q.dst_addr) / (uint64_t)d.bytes + 1;
+                if (q.iov_serial == 2 && d.n <= kIovLdsMax && tuning().iov_lds)
+                    // up to 16 Ki pairs: ordered and applied by one workgroup, in LDS
+                    rc = launch_iov_lds(q.op, q.scale, d, q.iov_align, q.dst_addr, units, r.streams[si]);
+                if (q.iov_serial == 2 && rc == 1) {
                     // repeated destinations ordered on the GPU; the progress thread's own sort
                     // scratch, free once the previous runs kernel has finished
                     const size_t need = iov_runs_work_bytes(d.n);
@@ -322,11 +326,10 @@ static void progress_loop() {
                         GA_HIP(hipMalloc((void **)&prog_work, prog_work_bytes));
                     }
                     if (!prog_work_ev) GA_HIP(hipEventCreateWithFlags(&prog_work_ev, kOwnerEventFlags));
-                    rc = launch_iov_runs(q.op, q.scale, d, q.iov_align, q.dst_addr,
-                                         (q.dst_hi - q.dst_addr) / (uint64_t)d.bytes + 1, prog_work, prog_work_bytes,
+                    rc = launch_iov_runs(q.op, q.scale, d, q.iov_align, q.dst_addr, units, prog_work, prog_work_bytes,
                                          r.streams[si]);
                     GA_HIP(hipEventRecord(prog_work_ev, r.streams[si]));
-                } else {
+                } else if (rc == 1) {
                     rc = launch_iov(q.op, q.scale, d, q.iov_align, q.iov_serial != 0, r.streams[si]);
                 }
                 if (rc) fatal("io-vector accumulate launch failed (%d)", rc);

@@ -96,11 +96,12 @@ int gaamd_route_counts(unsigned long long counts[4]);
  * [1] io-vector descriptors split pair by pair (COMEX_ENABLE_{ACC,PUT,GET}_IOV=0),
  * [2] gets through the owner (COMEX_ENABLE_GET_SELF/SMP=0). */
 int gaamd_toggle_counts(unsigned long long counts[3]);
-/* Local io-vector launches whose destinations may repeat (>= 4096 pairs), by path:
- * [0] hashed (only pairs sharing a destination sorted, in LDS), [1] hashed, then
- * the radix path for the pairs it could not order (more than 8192 such pairs),
- * [2] the radix path (over 2^19 pairs). */
-int gaamd_iov_path_counts(unsigned long long counts[3]);
+/* Local io-vector launches whose destinations may repeat (>= 2048 pairs, or fewer
+ * with a repeat), by path: [0] hashed (only pairs sharing a destination sorted, in
+ * LDS), [1] hashed, then the radix path for the pairs it could not order (more than
+ * 8192 such pairs), [2] the radix path (over 2^19 pairs), [3] one workgroup ordering
+ * and applying everything in LDS (up to 16 Ki pairs, one launch). */
+int gaamd_iov_path_counts(unsigned long long counts[4]);
 /* one-pass accumulates this rank applied into the segment of a rank on the same GPU */
 unsigned long long gaamd_one_pass_count(void);
 /* comex_malloc calls served by a freed segment block kept for reuse (with its IPC export) */

@@ -881,3 +881,50 @@ def test_accv_host_source_over_split_mappings(gpu_lib, oracle):
     assert np.array_equal(db.download(np.uint8, dst.size), want)
     del g
     assert libc.munmap(ctypes.c_void_p(base), size) == 0
+
+
+@pytest.mark.parametrize("op,nbytes,slots,n,src", [
+    (C.DBL, 8, 10 ** 6, 16384, "seq"), (C.DBL, 8, 3000, 16384, "perm"), (C.FLT, 4, 100, 16384, "seq"),
+    (C.DCP, 16, 2000, 8192, "perm"), (C.INT, 12, 700, 4096, "seq"), (C.LNG, 8, 50, 2048, "perm"),
+    (C.CPL, 24, 5000, 12000, "seq"), (C.DBL, 256, 300, 3000, "perm"), (C.DBL, 8, 1, 4096, "seq"),
+    (C.DBL, 8, 200, 1000, "host"), (C.FLT, 4, 1 << 20, 16384, "host")])
+def test_accv_one_workgroup_path(gpu_lib, oracle, op, nbytes, slots, n, src):
+    """up to 16 Ki pairs whose destinations may repeat are ordered and
+    applied by ONE launch of one 1024-thread workgroup (k_iov_lds: keys and a hash table
+    in LDS, pairs alone on their destination applied at once, the repeated ones sorted by
+    (destination, index) in LDS and applied in input order).  Sources contiguous (GA's
+    `v`), permuted, or gathered from pageable host memory; from one destination for
+    every pair to nearly all distinct; bit-exact against the pairs applied one by one,
+    and the same bytes as the hashed three-launch path (tuning iov_lds=0)."""
+    rng = np.random.default_rng(n * 31 + slots)
+    srcb = C.fill_bytes(op, n * nbytes, 21)
+    dst = C.fill_bytes(op, slots * nbytes, 22)
+    db = ga_amd.DeviceBuffer(dst.size)
+    if src == "host":
+        sbase, sb = srcb.ctypes.data, None
+    else:
+        sb = ga_amd.DeviceBuffer(srcb.size)
+        sb.upload(srcb)
+        sbase = sb.ptr
+    so = (rng.permutation(n) if src == "perm" else np.arange(n)).astype(np.uint64) * nbytes
+    do = rng.integers(0, slots, n).astype(np.uint64) * nbytes
+    g = _giov_np(so + np.uint64(sbase), do + np.uint64(db.ptr), nbytes)
+    keep, sp = ga_amd.scale_buffer(op, C.SCALE[op])
+    want = dst.copy()
+    _oracle_acc_pairs(oracle, op, C.SCALE[op], srcb, want, list(zip(so.tolist(), do.tolist())), nbytes)
+    outs = []
+    for lds in (1, 0):
+        old = ga_amd.set_tuning("iov_lds", lds)
+        try:
+            db.upload(dst)
+            paths0 = ga_amd.iov_path_counts()
+            assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
+            ga_amd.comex_fence_all()
+            paths1 = ga_amd.iov_path_counts()
+        finally:
+            ga_amd.set_tuning("iov_lds", old)
+        assert (paths1["lds"] - paths0["lds"]) == lds, (lds, paths0, paths1)
+        got = db.download(np.uint8, dst.size)
+        assert same_bits_nan_aware(got, want, op), f"iov_lds={lds}"
+        outs.append(got)
+    assert np.array_equal(outs[0], outs[1])

@@ -37,6 +37,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--slots", type=int, default=0,
                     help="destinations drawn from this many f64 slots (repeats) instead of the whole 1 GiB")
+    ap.add_argument("--ab", action="store_true",
+                    help="interleaved A/B of the one-workgroup LDS path (tuning iov_lds=1) against the hashed "
+                         "three-launch path (iov_lds=0): 5 alternations of --steps calls each")
+    ap.add_argument("--nb", action="store_true",
+                    help="also time --steps non-blocking calls back to back (comex_nbaccv, one wait at the end)")
     ap.add_argument("--ga", action="store_true",
                     help="NGA_Scatter_acc_flat / NGA_Gather_flat of n elements of a 16384^2 f64 GA (host v)")
     args = ap.parse_args()
@@ -71,17 +76,41 @@ def main():
             rc = L.comex_accv(DBL, sp, ctypes.byref(g), 1, 0, 0)
             assert rc == 0, rc
 
-        call()
-        ga_amd.sync()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
+        def timed():
             call()
-        ga_amd.sync()
-        el = (time.perf_counter() - t0) / args.steps
+            ga_amd.sync()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                call()
+            ga_amd.sync()
+            return (time.perf_counter() - t0) / args.steps
+
+        paths0 = ga_amd.iov_path_counts()
+        el = timed()
+        paths1 = ga_amd.iov_path_counts()
         line = {"tool": "scatter_bench", "pairs": n, "bytes_per_pair": 8, "repeated_destinations": int(dups),
                 "src": args.src, "steps": args.steps, "ms_per_call": round(el * 1e3, 3),
                 "Mpairs_per_s": round(n / el / 1e6, 2), "GBps_alg": round(24 * n / el / 1e9, 2),
-                "kernel": ga_amd.last_launch()}
+                "kernel": ga_amd.last_launch(),
+                "iov_path": [k for k in paths1 if paths1[k] > paths0[k]]}
+        if args.ab:
+            runs = {1: [], 0: []}
+            for _ in range(5):
+                for lds in (1, 0):
+                    old = ga_amd.set_tuning("iov_lds", lds)
+                    runs[lds].append(timed())
+                    ga_amd.set_tuning("iov_lds", old)
+            line["ab_ms_per_call"] = {"lds_one_launch": [round(x * 1e3, 4) for x in runs[1]],
+                                      "hashed_three_launches": [round(x * 1e3, 4) for x in runs[0]]}
+        if args.nb:
+            hs = [ctypes.c_int(-1) for _ in range(args.steps)]
+            call()
+            ga_amd.sync()
+            t0 = time.perf_counter()
+            for h in hs:
+                assert L.comex_nbaccv(DBL, sp, ctypes.byref(g), 1, 0, 0, ctypes.byref(h)) == 0
+            assert L.comex_wait_all(0) == 0
+            line["nb_ms_per_call"] = round((time.perf_counter() - t0) / args.steps * 1e3, 4)
         if not args.no_cpu:
             from oracle import Ref, ref_available
             if ref_available():
