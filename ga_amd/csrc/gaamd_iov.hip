@@ -311,9 +311,22 @@ __global__ __launch_bounds__(1024) void k_iov_lds(const IovDesc d, const OP op, 
     for (uint32_t w = t; w < (1u << kIovLdsLog) / 2; w += 1024) tab[w] = 0xffffffffu;
     for (uint32_t w = t; w < kIovLdsMax / 32; w += 1024) rep[w] = 0;
     if (t == 0) nconf = 0;
-    for (uint32_t i = t; i < n; i += 1024) {
-        const uint64_t off = d.dst_list[i] - dlo;
-        keys[i] = (uint32_t)(pow2 ? (off >> shift) : off / (uint64_t)d.bytes);
+    {
+        // every list load of this lane in flight at once (the list may sit across PCIe in
+        // the mapped pinned staging: one round trip, not one per pair)
+        constexpr int K = kIovLdsMax / 1024;
+        uint64_t a[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t i = t + (uint32_t)k * 1024u;
+            a[k] = i < n ? __builtin_nontemporal_load(d.dst_list + i) : dlo;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t i = t + (uint32_t)k * 1024u;
+            const uint64_t off = a[k] - dlo;
+            if (i < n) keys[i] = (uint32_t)(pow2 ? (off >> shift) : off / (uint64_t)d.bytes);
+        }
     }
     __syncthreads();
     // insert: the lane whose compare-and-swap claims an empty slot is its key's first
@@ -349,10 +362,12 @@ __global__ __launch_bounds__(1024) void k_iov_lds(const IovDesc d, const OP op, 
     }
     __syncthreads();
     uint32_t *conf = tab;                                   // the table is done with
-    // pairs alone on their destination: every vector of them at once, four per lane in flight
-    constexpr int U = 4;
+    // pairs alone on their destination: every vector of them at once, U per lane in flight
+    // (source addresses first -- a listed source is one more round trip -- then the data)
+    constexpr int U = W == 16 ? 8 : 16;
     for (uint32_t base = 0; base < d.items; base += 1024u * U) {
         typename Vec<W>::T a[U], b[U];
+        const char *sps[U];
         char *dps[U];
 #pragma unroll
         for (int k = 0; k < U; ++k) {
@@ -364,9 +379,14 @@ __global__ __launch_bounds__(1024) void k_iov_lds(const IovDesc d, const OP op, 
                 if (v == 0) conf[atomicAdd(&nconf, 1u)] = i;
                 continue;
             }
-            const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
+            sps[k] = (d.src_list ? (const char *)__builtin_nontemporal_load(d.src_list + i)
+                                 : d.src_base + (size_t)i * d.bytes) + (size_t)v * W;
             dps[k] = (char *)(dlo + (uint64_t)keys[i] * (uint64_t)d.bytes) + (size_t)v * W;
-            a[k] = src_load<W, SYS>(sp + (size_t)v * W);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            if (!dps[k]) continue;
+            a[k] = src_load<W, SYS>(sps[k]);
             if constexpr (OP::kReadsDst) b[k] = vload<W, false>(dps[k]);
         }
 #pragma unroll

@@ -95,6 +95,15 @@ __device__ __forceinline__ void row_offsets(const Desc &d, uint32_t r, int64_t &
     }
 }
 
+// Stores of the streaming kernels are non-temporal, like their loads.  Round 6 tried
+// default-policy stores: a one-stream probe read them faster on every row length
+// (tools/short_rows_probe.hip, profiles/r06/short_rows/), but in the library, whose
+// launches overlap on two streams, they lost everywhere but on the shortest rows
+// (headline H 0.750 against 0.80 over 300 steps, 64-byte rows 0.334 against 0.414,
+// profiles/r06/plain_stores/).  Rows of at most 32 bytes take the flat kernel's SHORT
+// form instead: plain loads and non-temporal stores, 0.337 against 0.283.
+constexpr bool kNtStore = true;
+
 // the U vectors of one thread: all loads first, then the ops and the stores.
 // `full` (wave-uniform) says the whole chunk lies inside the row, so the
 // vectors need no predicate and their addresses fold into immediate offsets.
@@ -124,7 +133,7 @@ __device__ __forceinline__ void chunk_op(const char *sp, char *dp, int64_t v0, u
             }
         }
 #pragma unroll
-        for (int k = 0; k < U; ++k) vstore<W, true>(d0 + k * BS * W, op.template apply<W>(b[k], a[k]));
+        for (int k = 0; k < U; ++k) vstore<W, kNtStore>(d0 + k * BS * W, op.template apply<W>(b[k], a[k]));
         return;
     }
     // row head/tail: one vector at a time (keeps the register budget of the full path)
@@ -135,7 +144,7 @@ __device__ __forceinline__ void chunk_op(const char *sp, char *dp, int64_t v0, u
         if constexpr (SYS) x = vload_sys<W>(s0 + k * BS * W);
         else x = vload<W, true>(s0 + k * BS * W);
         if constexpr (!OP::kReadsDst) y = x;
-        vstore<W, true>(d0 + k * BS * W, op.template apply<W>(y, x));
+        vstore<W, kNtStore>(d0 + k * BS * W, op.template apply<W>(y, x));
     }
 }
 
@@ -218,7 +227,7 @@ __global__ __launch_bounds__(BS) void k_rows2d(const Desc2D d, const OP op) {
         b = a;
         if constexpr (OP::kReadsDst) b = vload<W, true>(dp);
     }
-    vstore<W, true>(dp, op.template apply<W>(b, a));
+    vstore<W, kNtStore>(dp, op.template apply<W>(b, a));
 }
 
 // DIRECT N-D kernel (2 or 3 stride levels, every row whole chunks): as
@@ -254,14 +263,15 @@ __global__ __launch_bounds__(BS) void k_rowsnd(const DescND<LV> d, const OP op) 
     char *dp = d.dst + dof + v * W;
     typename Vec<W>::T a = vload<W, true>(sp), b = a;
     if constexpr (OP::kReadsDst) b = vload<W, true>(dp);
-    vstore<W, true>(dp, op.template apply<W>(b, a));
+    vstore<W, kNtStore>(dp, op.template apply<W>(b, a));
 }
 
 // FLAT kernel: vectors of all rows flattened, each lane decodes its own row;
-// non-temporal accesses (+12-24 % on 64 B-1 KiB rows, profiles/r01/flat_nt_ab.jsonl).
-template <class OP, int W, int U, int BS, int LV>
+// non-temporal loads (+12-24 % on 64 B-1 KiB rows, profiles/r01/flat_nt_ab.jsonl), stores
+// as kNtStore -- or, SHORT (rows of at most 32 bytes), plain loads and non-temporal stores.
+template <class OP, int W, int U, int BS, int LV, bool SHORT = false>
 __global__ __launch_bounds__(BS) void k_flat(const Desc d, const OP op) {
-    constexpr bool NT = true;
+    constexpr bool NT = !SHORT, NTS = SHORT ? true : kNtStore;
     typedef typename Vec<W>::T V;
     const uint32_t span = (uint32_t)BS * U;
     for (uint32_t base = blockIdx.x * span; base < (uint32_t)d.items; base += gridDim.x * span) {
@@ -283,7 +293,7 @@ __global__ __launch_bounds__(BS) void k_flat(const Desc d, const OP op) {
         }
 #pragma unroll
         for (int k = 0; k < U; ++k)
-            if (dps[k]) vstore<W, NT>(dps[k], op.template apply<W>(b[k], a[k]));
+            if (dps[k]) vstore<W, NTS>(dps[k], op.template apply<W>(b[k], a[k]));
     }
 }
 
@@ -859,7 +869,9 @@ static hipError_t dispatch_w(const Plan &p, const Desc &d, const OP &op, uint64_
         if (p.kind == KK_FLAT) {
             constexpr int UF = (W == 16) ? 1 : 4;
             constexpr int FB = (W == 16) ? 64 : 256;
-            if (d.levels == 1)
+            if (d.levels == 1 && (uint64_t)d.nvec * W <= 32)
+                hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 1, true>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
+            else if (d.levels == 1)
                 hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 1>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);
             else if (d.levels == 2)
                 hipLaunchKernelGGL((k_flat<OP, W, UF, FB, 2>), dim3((uint32_t)blocks), dim3(FB), 0, st, d, op);

@@ -153,9 +153,9 @@ def _layout(descs, start=0):
 
 
 def _shifts(size):
-    if size < 2:
-        return []
-    return sorted({1, size // 2, size - 1})[:3]
+    """every ordered rank pair: rank r sends to r + s for s = 1 .. size - 1 (one round each;
+    the budget may end the check after any round)"""
+    return list(range(1, size))
 
 
 def _program(seed, rnd, src_rank):
@@ -164,7 +164,7 @@ def _program(seed, rnd, src_rank):
     rng = np.random.default_rng([seed, rnd, src_rank])
     descs = []
     for op in ACC_OPS + (PUT,):
-        for _ in range(3):
+        for _ in range(5):
             descs.append(Desc(rng, op))
     for op in (DBL, DCP):
         descs.append(Desc(rng, op, big=True))
