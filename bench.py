@@ -1165,6 +1165,10 @@ def make_line(args, dist, r, ga_amd):
                      "kernel_ms_avg": round(r["avg_kernel_s"] * 1e3, 4),
                      "timing": ("HIP events at both ends of every library stream around K more launches of the "
                                 "same step right after the value region (first start to last end) / K"),
+                     "frac_kind": ("event-pair figure: an HIP event pair per library stream around K extra launches; "
+                                   "the rocprofv3 summaries under profiles/ give the per-launch AverageNs on one "
+                                   "stream and the merged busy time per dispatch on the default two streams, which "
+                                   "bracket it"),
                      "streams": r["streams"],
                      "rocprof_check": ("consecutive launches overlap on the library streams: compare kernel_ms_avg "
                                        "with the merged busy time per dispatch of the rocprofv3 kernel trace "

@@ -486,7 +486,14 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
             z.dst_list = (const uint64_t *)(up_dev + o_dst);
             if (d.src_list) z.src_list = (const uint64_t *)(up_dev + o_src);
             else if (!src_listed) z.src_base = up_dev + o_src;
-            rc = launch_iov_lds(cop, scale, z, align_or, dlo, units, r.streams[si]);
+            static uint32_t *g_lds_counter = nullptr;   // the hand-off counter of this path's launches
+            if (!g_lds_counter) {
+                GA_HIP(hipMalloc((void **)&g_lds_counter, 256));
+                GA_HIP(hipMemset(g_lds_counter, 0, 256));
+            }
+            if (work < iov_lds_scratch_bytes((uint32_t)n)) fatal("io-vector scratch too small for the LDS path");
+            rc = launch_iov_lds(cop, scale, z, align_or, dlo, units, r.streams[si], false, dev + o_work,
+                                g_lds_counter);
             if (rc == 0) g_iov_path[3].fetch_add(1, std::memory_order_relaxed);
         }
         if (rc == 1 && !src_listed && o_res > o_src)
