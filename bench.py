@@ -596,7 +596,10 @@ def c5_extras(args, dist, wd=None):
         if wd is not None:
             wd.phase = "xdev_check"
         from ga_amd.xcheck import xdev_check_diagnosed
-        out["xdev_check"] = xdev_check_diagnosed(dist.rank, dist.size, budget_s=args.xcheck_s)
+        try:
+            out["xdev_check"] = xdev_check_diagnosed(dist.rank, dist.size, budget_s=args.xcheck_s)
+        except Exception as e:   # a failed call is a finding, not a lost line (the watchdog covers a hang)
+            out["xdev_check"] = {"result": "ERROR", "rank": dist.rank, "error": repr(e)[:500]}
     # the exchange's exactness on a small GA (4096^2, both routes) before any timed C5
     # step: on the first run over separate GPUs a visibility bug
     # reads as exchange_precheck MISMATCH, not as a plausible rate

@@ -705,8 +705,9 @@ int comex_init() {
             if (r.same_node(q) && r.peer_src(q)) ++peers;
         // owner pulls from peer GPUs: one stream per source rank, so the chunks of
         // different peers (different xGMI links) are applied side by side
-        const char *ps = getenv("COMEX_AMD_PULL_STREAMS");
-        const int pull = std::min(peers, ps ? atoi(ps) : 6);
+        // (at most 6: GPU_MAX_HW_QUEUES is 4 here, more streams share hardware queues;
+        // the former COMEX_AMD_PULL_STREAMS knob, settled)
+        const int pull = std::min(peers, 6);
         // 2 library streams: independent ops overlap kernel edges; 1 when
         // other ranks of the job share this GPU: their processes fill it anyway, and two
         // streams per process made a small blocking call wait 55-80 us for its kernel
@@ -729,8 +730,10 @@ int comex_init() {
     const char *bs = getenv("COMEX_AMD_BLOCKING_SYNC");
     r.blocking_sync = !bs || atoi(bs) != 0;
     {
-        const char *ds = getenv("COMEX_AMD_DIRECT_SRC");
-        r.direct_src = !ds || atoi(ds) != 0;
+        // the direct-source route is always on (the former COMEX_AMD_DIRECT_SRC knob:
+        // its A/B settled in round 2; COMEX_ENABLE_ACC_SMP=0 still turns it off, as the
+        // reference's SMP toggle does)
+        r.direct_src = true;
         auto flag = [](const char *name) {
             const char *v = getenv(name);
             return !v || atoi(v) != 0;

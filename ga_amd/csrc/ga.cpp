@@ -466,14 +466,9 @@ template <class T> static T *grow(std::vector<T> &v, size_t n) {
 // cheaper than storing each element's owner and offset between the passes: the
 // call is bound by host memory traffic, 32 bytes per element this way against 48
 // (NGA_Scatter_acc_flat of 4 Mi elements: profiles/r05/scatter2, scatter3).
-static int gs_threads() {
-    static const int n = [] {
-        const char *e = getenv("COMEX_AMD_GS_THREADS");
-        const int v = e ? atoi(e) : 8;
-        return v < 1 ? 1 : (v > 64 ? 64 : v);
-    }();
-    return n;
-}
+// host threads that locate owners and group pairs (one per 128 Ki elements, up to 8;
+// the former COMEX_AMD_GS_THREADS knob, settled: the box's host share is 16 cores)
+static int gs_threads() { return 8; }
 
 struct GsCtx {
     const GArray *a;

@@ -178,13 +178,8 @@ struct ViewCache {
 // contiguous ranges over a few threads: fn(t, i0, i1) for t < T, T = one thread
 // per 256 Ki pairs, at most 8.  Each range's results are combined by the caller
 // in range order, so the outcome does not depend on T.
-static int par_threads(long n) {
-    static const long cap = [] {   // COMEX_AMD_HOST_THREADS: at most this many (1..8, default 8)
-        const char *e = getenv("COMEX_AMD_HOST_THREADS");
-        const long v = e ? atol(e) : 8;
-        return v < 1 ? 1L : (v > 8 ? 8L : v);
-    }();
-    return (int)std::max(1L, std::min(cap, n >> 18));
+static int par_threads(long n) {   // one per 256 Ki pairs, at most 8 (the former COMEX_AMD_HOST_THREADS)
+    return (int)std::max(1L, std::min(8L, n >> 18));
 }
 template <class F> static void par_for(long n, int T, F fn) {
     if (T <= 1) { fn(0, 0L, n); return; }

@@ -185,10 +185,7 @@ static void *device_alloc(size_t bytes);
 
 void export_alloc(void **p, size_t bytes, hipIpcMemHandle_t *h, const char *what) {
     Runtime &r = rt();
-    static const bool retry = [] {
-        const char *e = getenv("COMEX_AMD_IPC_RETRY");
-        return !e || atoi(e) != 0;
-    }();
+    constexpr bool retry = true;   // the former COMEX_AMD_IPC_RETRY knob (its 0 only aborted sooner)
     std::vector<void *> held;
     trace(2, "hipIpcGetMemHandle of a %zu-byte %s at %p", bytes, what, *p);
     hipError_t e = hipIpcGetMemHandle(h, *p);
@@ -273,10 +270,7 @@ static size_t block_cache_cap() {
 }
 
 static size_t free_watermark() {
-    static const size_t v = [] {
-        if (const char *e = getenv("COMEX_AMD_SEGMENT_FREE_MIN_MB")) return (size_t)atof(e) << 20;
-        return device_total() / 16;
-    }();
+    static const size_t v = device_total() / 16;   // the former COMEX_AMD_SEGMENT_FREE_MIN_MB
     return v;
 }
 

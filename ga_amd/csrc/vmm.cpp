@@ -82,11 +82,7 @@ size_t g_retired_bytes = 0;
 uintptr_t g_window = 0;            // next hint in the private window
 
 size_t retain_cap() {
-    static const size_t cap = [] {
-        const char *e = getenv("COMEX_AMD_VMM_RETAIN_GB");
-        return (size_t)(e ? atoll(e) : 16384) << 30;
-    }();
-    return cap;
+    return (size_t)16384 << 30;   // 16 TiB (the former COMEX_AMD_VMM_RETAIN_GB knob)
 }
 
 uintptr_t g_window_end = 0, g_window_start = 0;
