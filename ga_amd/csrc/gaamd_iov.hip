@@ -71,11 +71,7 @@ constexpr uint32_t kIovRunSkip = 0xffffffffu;   // k_iov_runs: a run of this key
 
 // the hashed path's state for one launch (see k_iovh_insert below)
 struct IovHashArgs {
-    bool lds;              // k_iov_lds instead of the hashed apply + conflicts
-    uint32_t lds_grid;     // its workgroups (1: the lists are in HBM already)
-    uint32_t *lds_keys;    // G > 1: HBM scratch for the keys, listed sources, the counter
-    uint64_t *lds_src;
-    uint32_t *lds_counter;
+    bool lds;              // k_iov_lds (one workgroup) instead of the hashed apply + conflicts
     uint64_t dlo;
     uint32_t shift;
     bool pow2;
@@ -275,10 +271,9 @@ __global__ __launch_bounds__(1024) void k_iovh_conf(const IovDesc d, const OP op
 // ---------------------------------------------------------------------------
 // One-workgroup io-vector path: up to kIovLdsMax pairs whose
 // destinations may repeat are ordered AND applied by one launch of one 1024-thread
-// workgroup, everything it orders held in LDS -- the hashed path's three launches
-// (insert, apply, conflicts: 17.6 + 5.1 + 4.1 us at 16 Ki pairs, profiles/r05/iov3)
-// and their device-scope atomics on an HBM table were what kept a 16 Ki-pair
-// scatter-accumulate behind the reference's one-core loop.
+// workgroup, everything it orders held in LDS, instead of the hashed path's three
+// launches (insert, apply, conflicts: 17.6 + 5.1 + 4.1 us at 16 Ki pairs,
+// profiles/r05/iov3) with their device-scope atomics on an HBM table.
 //   keys  : each pair's destination unit (dst - dlo) / bytes, read once from the
 //           list (through the mapped pinned staging: no upload launch)
 //   table : open addressing, 2^15 16-bit slots (pair index; top bit: the slot's key
@@ -290,27 +285,24 @@ __global__ __launch_bounds__(1024) void k_iovh_conf(const IovDesc d, const OP op
 //           reference's order (comex.c:7342-7351: one _acc per pair, in order).
 // A destination is rebuilt from its key (dlo + key * bytes: the caller guarantees
 // every destination a whole number of pairs from dlo), so the list is read once.
-// Lists in the mapped pinned staging (the local call) sit across PCIe, and one CU
-// keeps too few reads in flight to fetch 128 KiB of them quickly (the first version,
-// one workgroup reading them itself: 0.103 ms at 16 Ki pairs, profiles/r06/iov_lds/).
-// So that launch has G > 1 workgroups: each reads a slice of the lists, writes the keys
-// (and a listed source's addresses) to HBM scratch with `sc1` stores, waits for them,
-// and adds to one agent-scope counter; the workgroup whose add comes last -- told by the
-// value its add returned -- is the one that orders and applies, reading the hand-off with
-// `sc1` loads (MI355X_MICROARCH.md, the hand-off table's first row: no acquire needed),
-// and puts the counter back to 0 for the next launch on the caller's stream.
+// Where it pays (round 6, tools/iov_lds_probe.cpp, profiles/r06/iov_lds/): below 4 Ki
+// pairs.  Kernel time, random single-f64 destinations in 1 GiB, back-to-back launches:
+// 1 Ki pairs 5.9 us against 11.5 for the hashed path's three launches, 2 Ki 8.4 against
+// 13.0, 4 Ki 13.4 against 13.8 -- and then 26 against 19 at 8 Ki, 76 against 18 at 16 Ki:
+// one CU cannot keep enough random destinations in flight (the cost grows faster than
+// the pairs), where the hashed path's apply spreads them over the chip.  A version whose
+// list read was spread over up to 32 workgroups (keys handed to the last one through HBM)
+// measured no faster and was not kept.
 constexpr uint32_t kIovLdsLog = 15;                       // table slots: 2^15 = 2 x pairs
 constexpr uint32_t kIovLdsEmpty = 0xffffu;
 
-__device__ __forceinline__ const char *iov_lds_src(const IovDesc &d, uint32_t i, bool sc1) {
-    if (!d.src_list) return d.src_base + (size_t)i * d.bytes;
-    if (sc1) return (const char *)__hip_atomic_load(d.src_list + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return (const char *)__builtin_nontemporal_load(d.src_list + i);
+__device__ __forceinline__ const char *iov_lds_src(const IovDesc &d, uint32_t i) {
+    return d.src_list ? (const char *)__builtin_nontemporal_load(d.src_list + i) : d.src_base + (size_t)i * d.bytes;
 }
 
 template <class OP, int W, bool SYS>
-__device__ __forceinline__ void iov_lds_pair(const IovDesc &d, const OP &op, uint32_t i, char *dp, bool sc1) {
-    const char *sp = iov_lds_src(d, i, sc1);
+__device__ __forceinline__ void iov_lds_pair(const IovDesc &d, const OP &op, uint32_t i, char *dp) {
+    const char *sp = iov_lds_src(d, i);
     for (uint32_t v = 0; v < d.nvec; ++v) {
         typename Vec<W>::T x = src_load<W, SYS>(sp + (size_t)v * W), y = x;
         if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
@@ -319,35 +311,18 @@ __device__ __forceinline__ void iov_lds_pair(const IovDesc &d, const OP &op, uin
 }
 
 template <class OP, int W, bool SYS>
-__global__ __launch_bounds__(1024) void k_iov_lds(IovDesc d, const OP op, uint64_t dlo, uint32_t shift, bool pow2,
-                                                  uint32_t *keys_g, uint64_t *src_g, uint32_t *counter) {
+__global__ __launch_bounds__(1024) void k_iov_lds(const IovDesc d, const OP op, uint64_t dlo, uint32_t shift,
+                                                  bool pow2) {
     __shared__ uint32_t keys[kIovLdsMax];
     __shared__ uint32_t tab[(1u << kIovLdsLog) / 2];      // two 16-bit slots per word; later the conflict list
     __shared__ uint32_t rep[kIovLdsMax / 32];             // pair i's destination repeats
-    __shared__ uint32_t nconf, last;
-    const uint32_t t = threadIdx.x, n = d.n, G = gridDim.x;
+    __shared__ uint32_t nconf;
+    const uint32_t t = threadIdx.x, n = d.n;
     constexpr uint32_t mask = (1u << kIovLdsLog) - 1u;
     auto key_of = [&](uint64_t a) -> uint32_t {
         const uint64_t off = a - dlo;
         return (uint32_t)(pow2 ? (off >> shift) : off / (uint64_t)d.bytes);
     };
-    const bool handed = G > 1;   // the lists came through HBM scratch (sc1 both sides)
-    if (handed) {
-        // this workgroup's slice of the lists: keys (and listed sources) to HBM, sc1 stores
-        const uint32_t per = (n + G - 1) / G, i0 = blockIdx.x * per, i1 = min(n, i0 + per);
-        for (uint32_t i = i0 + t; i < i1; i += 1024) {
-            const uint64_t a = __builtin_nontemporal_load(d.dst_list + i);
-            const uint64_t s = d.src_list ? __builtin_nontemporal_load(d.src_list + i) : 0;
-            __hip_atomic_store(keys_g + i, key_of(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (d.src_list) __hip_atomic_store(src_g + i, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its stores done
-        __syncthreads();
-        if (t == 0) last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
-        __syncthreads();
-        if (!last) return;
-        if (d.src_list) d.src_list = src_g;
-    }
     for (uint32_t w = t; w < (1u << kIovLdsLog) / 2; w += 1024) tab[w] = 0xffffffffu;
     for (uint32_t w = t; w < kIovLdsMax / 32; w += 1024) rep[w] = 0;
     if (t == 0) nconf = 0;
@@ -358,9 +333,7 @@ __global__ __launch_bounds__(1024) void k_iov_lds(IovDesc d, const OP op, uint64
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t i = t + (uint32_t)k * 1024u;
-            if (i >= n) kk[k] = 0;
-            else if (handed) kk[k] = __hip_atomic_load(keys_g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else kk[k] = key_of(__builtin_nontemporal_load(d.dst_list + i));
+            kk[k] = i < n ? key_of(__builtin_nontemporal_load(d.dst_list + i)) : 0u;
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -368,7 +341,6 @@ __global__ __launch_bounds__(1024) void k_iov_lds(IovDesc d, const OP op, uint64
             if (i < n) keys[i] = kk[k];
         }
     }
-    if (handed && t == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     // insert: the lane whose compare-and-swap claims an empty slot is its key's first
     // pair; a lane that finds its key in a slot marks that slot repeated
@@ -420,7 +392,7 @@ __global__ __launch_bounds__(1024) void k_iov_lds(IovDesc d, const OP op, uint64
                 if (v == 0) conf[atomicAdd(&nconf, 1u)] = i;
                 continue;
             }
-            sps[k] = iov_lds_src(d, i, handed) + (size_t)v * W;
+            sps[k] = iov_lds_src(d, i) + (size_t)v * W;
             dps[k] = (char *)(dlo + (uint64_t)keys[i] * (uint64_t)d.bytes) + (size_t)v * W;
         }
 #pragma unroll
@@ -463,7 +435,7 @@ __global__ __launch_bounds__(1024) void k_iov_lds(IovDesc d, const OP op, uint64
         const uint32_t key = keys[conf[u]];
         if (u > 0 && keys[conf[u - 1]] == key) continue;
         char *dp = (char *)(dlo + (uint64_t)key * (uint64_t)d.bytes);
-        for (uint32_t w = u; w < m && keys[conf[w]] == key; ++w) iov_lds_pair<OP, W, SYS>(d, op, conf[w], dp, handed);
+        for (uint32_t w = u; w < m && keys[conf[w]] == key; ++w) iov_lds_pair<OP, W, SYS>(d, op, conf[w], dp);
     }
 }
 
@@ -482,8 +454,7 @@ __global__ __launch_bounds__(256) void k_iov_keys_masked(const uint64_t *dst_lis
 template <class OP, int W, bool SYS>
 static hipError_t iov_ws(const IovDesc &d, const OP &op, bool serial, hipStream_t st, const IovHashArgs *ha) {
     if (ha && ha->lds) {
-        hipLaunchKernelGGL((k_iov_lds<OP, W, SYS>), dim3(ha->lds_grid), dim3(1024), 0, st, d, op, ha->dlo, ha->shift,
-                           ha->pow2, ha->lds_keys, ha->lds_src, ha->lds_counter);
+        hipLaunchKernelGGL((k_iov_lds<OP, W, SYS>), dim3(1), dim3(1024), 0, st, d, op, ha->dlo, ha->shift, ha->pow2);
     } else if (ha) {
         hipLaunchKernelGGL((k_iovh_apply<OP, W, SYS>), dim3((d.n + kIovhBS - 1) / kIovhBS), dim3(kIovhBS), 0, st, d, op,
                            ha->dlo,
@@ -806,8 +777,7 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
                        (uint64_t *)d.src_list);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return -100 - (int)e;
-    IovHashArgs ha{false, 0, nullptr, nullptr, nullptr, dlo, shift, pow2, h->epoch, dup, slot, conf, count,
-                   h->flag_dev};
+    IovHashArgs ha{false, dlo, shift, pow2, h->epoch, dup, slot, conf, count, h->flag_dev};
     h->dlo = dlo;
     h->n = d.n;
     h->shift = shift;
@@ -816,7 +786,7 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
 }
 
 int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
-                   hipStream_t stream, bool src_peer, void *scratch, uint32_t *counter) {
+                   hipStream_t stream, bool src_peer) {
     const int esz = elem_size(op);
     if (!esz || d.bytes <= 0 || d.bytes > kIovRunsMaxBytes || !d.dst_list) return -4;
     if (op != kOpCopy && !scale) return -5;
@@ -836,12 +806,7 @@ int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint
     d.items = d.n * d.nvec;
     const bool pow2 = (d.bytes & (d.bytes - 1)) == 0;
     const uint32_t shift = pow2 ? (uint32_t)__builtin_ctz((unsigned)d.bytes) : 0;
-    // lists across PCIe (scratch given): one workgroup per 512 pairs reads them, up to 32
-    const uint32_t G = scratch ? std::max(1u, std::min(32u, (d.n + 511u) / 512u)) : 1u;
-    uint32_t *keys = (uint32_t *)scratch;
-    uint64_t *src = scratch ? (uint64_t *)((char *)scratch + align256((size_t)d.n * 4)) : nullptr;
-    if (G > 1 && !counter) return -4;
-    IovHashArgs ha{true, G, keys, src, counter, dlo, shift, pow2, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+    IovHashArgs ha{true, dlo, shift, pow2, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
     return iov_dispatch(op, scale, W, d, false, src_peer, stream, &ha);
 }
 

@@ -189,16 +189,13 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
                       uint64_t units, hipStream_t stream, bool src_peer = false, const uint64_t *dst_in = nullptr,
                       const uint64_t *src_in = nullptr);
 bool iov_hash_overflowed(const IovHash *h);
-// The same contract for up to kIovLdsMax pairs in ONE launch (k_iov_lds: one
-// workgroup orders and applies everything, in LDS).  With `scratch` (HBM, at least
-// iov_lds_scratch_bytes(n)) and `counter` (one device word, 0 before the first launch;
-// the kernel leaves it 0) d.dst_list / d.src_list may point into mapped pinned memory:
-// up to 32 workgroups read them once and hand them over through the scratch.  Without,
-// the lists are read by the one workgroup (device memory).  The caller orders its
-// launches on one counter.  Returns 1 when n is outside its range.
+// The same contract for up to kIovLdsMax pairs in ONE launch of one workgroup (the
+// ordering held in LDS, k_iov_lds); d.dst_list / d.src_list may point into mapped
+// pinned memory (read once).  Returns 1 when n is outside its range.  The callers use it
+// below kIovLdsRoute pairs, where it is faster than the hashed path (gaamd_iov.hip).
 constexpr uint32_t kIovLdsMax = 16384;
-inline size_t iov_lds_scratch_bytes(uint32_t n) { return (((size_t)n * 4 + 255) & ~(size_t)255) + (size_t)n * 8; }
+constexpr uint32_t kIovLdsRoute = 4096;
 int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
-                   hipStream_t stream, bool src_peer = false, void *scratch = nullptr, uint32_t *counter = nullptr);
+                   hipStream_t stream, bool src_peer = false);
 
 }  // namespace gaamd

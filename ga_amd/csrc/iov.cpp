@@ -474,21 +474,14 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         rc = 1;
         char *up_dev = nullptr;   // the device view of the pinned upload buffer
         GA_HIP(hipHostGetDevicePointer((void **)&up_dev, up, 0));
-        if (n <= (int)kIovLdsMax && !src_peer && tuning().iov_lds) {
-            // up to 16 Ki pairs: ordered and applied by one launch of one workgroup, the
+        if (n < (int)kIovLdsRoute && !src_peer && tuning().iov_lds) {
+            // below 4 Ki pairs: ordered and applied by one launch of one workgroup, the
             // lists (and packed sources) read in place from the pinned staging
             IovDesc z = d;
             z.dst_list = (const uint64_t *)(up_dev + o_dst);
             if (d.src_list) z.src_list = (const uint64_t *)(up_dev + o_src);
             else if (!src_listed) z.src_base = up_dev + o_src;
-            static uint32_t *g_lds_counter = nullptr;   // the hand-off counter of this path's launches
-            if (!g_lds_counter) {
-                GA_HIP(hipMalloc((void **)&g_lds_counter, 256));
-                GA_HIP(hipMemset(g_lds_counter, 0, 256));
-            }
-            if (work < iov_lds_scratch_bytes((uint32_t)n)) fatal("io-vector scratch too small for the LDS path");
-            rc = launch_iov_lds(cop, scale, z, align_or, dlo, units, r.streams[si], false, dev + o_work,
-                                g_lds_counter);
+            rc = launch_iov_lds(cop, scale, z, align_or, dlo, units, r.streams[si]);
             if (rc == 0) g_iov_path[3].fetch_add(1, std::memory_order_relaxed);
         }
         if (rc == 1 && !src_listed && o_res > o_src)

@@ -312,8 +312,8 @@ static void progress_loop() {
                 d.n = (uint32_t)q.count[1];
                 int rc = 1;
                 const uint64_t units = (q.dst_hi - q.dst_addr) / (uint64_t)d.bytes + 1;
-                if (q.iov_serial == 2 && d.n <= kIovLdsMax && tuning().iov_lds)
-                    // up to 16 Ki pairs: ordered and applied by one workgroup, in LDS
+                if (q.iov_serial == 2 && d.n < kIovLdsRoute && tuning().iov_lds)
+                    // below 4 Ki pairs: ordered and applied by one workgroup, in LDS
                     rc = launch_iov_lds(q.op, q.scale, d, q.iov_align, q.dst_addr, units, r.streams[si]);
                 if (q.iov_serial == 2 && rc == 1) {
                     // repeated destinations ordered on the GPU; the progress thread's own sort

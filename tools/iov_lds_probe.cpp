@@ -1,0 +1,107 @@
+// iov_lds_probe.cpp -- kernel-only timing of the io-vector ordering paths (VERDICT r5
+// item 3), linked against libga_amd.so's internal launchers: n single-f64 pairs with
+// random destinations in 1 GiB, contiguous sources, lists in HBM or in mapped pinned
+// memory; per n the one-launch LDS path (one workgroup reads the lists, from HBM or from
+// mapped pinned memory across PCIe) and the hashed three-launch path, HIP events
+// around 50 back-to-back calls on one stream.  Checks the LDS path's result against the
+// hashed path's (bit-exact: the same pair order on repeated destinations).
+// Build: hipcc -O2 -std=c++17 -D__HIP_PLATFORM_AMD__ -I ga_amd/csrc tools/iov_lds_probe.cpp \
+//        -L ga_amd -lga_amd -Wl,-rpath,$PWD/ga_amd -o tools/iov_lds_probe
+#include "gaamd_kernels.h"
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <random>
+#include <vector>
+
+using namespace gaamd;
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+int main(int argc, char **argv) {
+    const int steps = 50;
+    const uint64_t region = 1ull << 30;
+    char *dst;
+    CK(hipMalloc(&dst, region));
+    CK(hipMemset(dst, 0, region));
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    IovHash *h = iov_hash_create();
+    const double alpha = 0.7071067811865476;
+    std::mt19937_64 rng(7);
+    int slots_arg = argc > 1 ? atoi(argv[1]) : 0;   // destinations from this many slots (0: all of 1 GiB)
+    for (uint32_t n : {1024u, 2048u, 4096u, 8192u, 16384u}) {
+        std::vector<uint64_t> dl(n);
+        const uint64_t slots = slots_arg ? (uint64_t)slots_arg : region / 8;
+        for (uint32_t i = 0; i < n; ++i) dl[i] = (uint64_t)(uintptr_t)dst + 8 * (rng() % slots);
+        uint64_t dlo = ~0ull, dhi = 0;
+        for (uint64_t a : dl) { dlo = a < dlo ? a : dlo; dhi = a > dhi ? a : dhi; }
+        const uint64_t units = (dhi - dlo) / 8 + 1;
+        double *src;
+        CK(hipMalloc(&src, 8 * n));
+        std::vector<double> sv(n);
+        for (uint32_t i = 0; i < n; ++i) sv[i] = (double)(i % 97) - 48;
+        CK(hipMemcpy(src, sv.data(), 8 * n, hipMemcpyHostToDevice));
+        uint64_t *dl_dev, *dl_pin, *dl_pin_dev;
+        CK(hipMalloc(&dl_dev, 8 * n));
+        CK(hipMemcpy(dl_dev, dl.data(), 8 * n, hipMemcpyHostToDevice));
+        CK(hipHostMalloc(&dl_pin, 8 * n, hipHostMallocMapped));
+        memcpy(dl_pin, dl.data(), 8 * n);
+        CK(hipHostGetDevicePointer((void **)&dl_pin_dev, dl_pin, 0));
+        IovDesc d;
+        memset(&d, 0, sizeof(d));
+        d.src_base = (const char *)src;
+        d.bytes = 8;
+        d.n = n;
+        uint64_t align_or = 0;
+        for (uint64_t a : dl) align_or |= a;
+        auto run = [&](int mode) {
+            IovDesc z = d;
+            int rc = 0;
+            if (mode == 0) {          // LDS, lists in HBM, one workgroup
+                z.dst_list = dl_dev;
+                rc = launch_iov_lds(38, &alpha, z, align_or, dlo, units, st);
+            } else if (mode == 1) {   // LDS, lists in mapped pinned memory (the local call's case)
+                z.dst_list = dl_pin_dev;
+                rc = launch_iov_lds(38, &alpha, z, align_or, dlo, units, st);
+            } else {                  // hashed, lists in HBM
+                z.dst_list = dl_dev;
+                rc = launch_iov_hashed(h, 38, &alpha, z, align_or, dlo, units, st);
+            }
+            if (rc) { fprintf(stderr, "mode %d rc %d\n", mode, rc); exit(1); }
+        };
+        const char *names[3] = {"lds_hbm_lists", "lds_pinned_lists", "hashed_3_launches"};
+        std::vector<double> res[3];
+        for (int mode = 0; mode < 3; ++mode) {
+            CK(hipMemset(dst, 0, region));
+            run(mode);
+            CK(hipStreamSynchronize(st));
+            std::vector<double> got(n);
+            for (uint32_t i = 0; i < n; ++i) CK(hipMemcpy(&got[i], (void *)dl[i], 8, hipMemcpyDeviceToHost));
+            res[mode] = got;
+            float best = 1e30f;
+            for (int rep = 0; rep < 3; ++rep) {
+                CK(hipEventRecord(e0, st));
+                for (int s = 0; s < steps; ++s) run(mode);
+                CK(hipEventRecord(e1, st));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                best = ms < best ? ms : best;
+            }
+            printf("{\"probe\": \"iov_lds\", \"pairs\": %u, \"slots\": %llu, \"path\": \"%s\", \"us_per_call\": %.2f, "
+                   "\"same_as_hashed\": %s}\n",
+                   n, (unsigned long long)slots, names[mode], best * 1e3 / steps, "null");
+            fflush(stdout);
+        }
+        const bool same = memcmp(res[0].data(), res[2].data(), 8 * n) == 0 && memcmp(res[1].data(), res[2].data(), 8 * n) == 0;
+        printf("{\"probe\": \"iov_lds\", \"pairs\": %u, \"lds_equals_hashed\": %s}\n", n, same ? "true" : "false");
+        CK(hipFree(src));
+        CK(hipFree(dl_dev));
+        CK(hipHostFree(dl_pin));
+    }
+    return 0;
+}
