@@ -808,6 +808,10 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
     // io-vector kernels may sit on any library stream (sched_pick per descriptor):
     // a handle is recorded after a join, so it covers all of them; a blocking call
     // completes locally before returning
+    // (a blocking call completes by synchronising the streams: the completion flag the
+    // strided calls wait on measured 7-18 us SLOWER here, interleaved A/B,
+    // profiles/r06/iov_flag_ab/ -- the io-vector kernels read the lists across PCIe from
+    // pinned memory while the host polls a pinned flag)
     const bool blocking = !hdl && r.blocking_sync;
     {
         std::lock_guard<std::mutex> g(r.launch_mu);

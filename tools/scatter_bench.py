@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--ab", action="store_true",
                     help="interleaved A/B of the one-workgroup LDS path (tuning iov_lds=1) against the hashed "
                          "three-launch path (iov_lds=0): 5 alternations of --steps calls each")
+    ap.add_argument("--ab-key", default="iov_lds",
+                    help="the tuning key --ab alternates between 1 and 0 (iov_lds, iov_flag)")
     ap.add_argument("--nb", action="store_true",
                     help="also time --steps non-blocking calls back to back (comex_nbaccv, one wait at the end)")
     ap.add_argument("--ga", action="store_true",
@@ -96,12 +98,15 @@ def main():
         if args.ab:
             runs = {1: [], 0: []}
             for _ in range(5):
-                for lds in (1, 0):
-                    old = ga_amd.set_tuning("iov_lds", lds)
-                    runs[lds].append(timed())
-                    ga_amd.set_tuning("iov_lds", old)
-            line["ab_ms_per_call"] = {"lds_one_launch": [round(x * 1e3, 4) for x in runs[1]],
-                                      "hashed_three_launches": [round(x * 1e3, 4) for x in runs[0]]}
+                for val in (1, 0):
+                    old = ga_amd.set_tuning(args.ab_key, val)
+                    runs[val].append(timed())
+                    ga_amd.set_tuning(args.ab_key, old)
+            names = {"iov_lds": ("lds_one_launch", "hashed_three_launches"),
+                     "iov_flag": ("flag_wait", "stream_sync")}.get(args.ab_key, ("on", "off"))
+            line["ab_key"] = args.ab_key
+            line["ab_ms_per_call"] = {names[0]: [round(x * 1e3, 4) for x in runs[1]],
+                                      names[1]: [round(x * 1e3, 4) for x in runs[0]]}
         if args.nb:
             hs = [ctypes.c_int(-1) for _ in range(args.steps)]
             call()
