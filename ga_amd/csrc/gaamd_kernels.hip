@@ -96,12 +96,14 @@ __device__ __forceinline__ void row_offsets(const Desc &d, uint32_t r, int64_t &
 }
 
 // Stores of the streaming kernels are non-temporal, like their loads.  Round 6 tried
-// default-policy stores: a one-stream probe read them faster on every row length
-// (tools/short_rows_probe.hip, profiles/r06/short_rows/), but in the library, whose
-// launches overlap on two streams, they lost everywhere but on the shortest rows
-// (headline H 0.750 against 0.80 over 300 steps, 64-byte rows 0.334 against 0.414,
-// profiles/r06/plain_stores/).  Rows of at most 32 bytes take the flat kernel's SHORT
-// form instead: plain loads and non-temporal stores, 0.337 against 0.283.
+// default-policy stores: a stand-alone probe (tools/short_rows_probe.hip, constant
+// data, profiles/r06/short_rows/) read them faster on every row length, but the
+// library built with them lost on every row length but the shortest, on one stream and
+// on two alike (64-byte rows 0.36-0.39 against 0.41-0.43, 16 KiB rows 0.72-0.76 against
+// 0.79-0.81, interleaved in one call, profiles/r06/store_policy_ab/; the headline 0.75
+// against 0.80 over 300 steps, profiles/r06/plain_stores/).  Rows of at most 32 bytes
+// take the flat kernel's SHORT form instead: plain loads and non-temporal stores, 0.337
+// against 0.283.
 constexpr bool kNtStore = true;
 
 // the U vectors of one thread: all loads first, then the ops and the stores.
