@@ -25,6 +25,45 @@ __device__ __forceinline__ typename Vec<W>::T src_load(const char *p) {
     else return vload<W, false>(p);
 }
 
+// Applies `cnt` pairs that share ONE destination dp, pair idx(0) first: the destination
+// is read once, the pairs are applied in a register in that order and the result stored
+// once.  The same operations on the same values in the same order as one read-modify-
+// write per pair (the reference's, comex.c:7342-7351), so bit-exact, but a run of r pairs
+// costs r independent source loads (16 in flight) and one round trip to the destination
+// instead of r dependent round trips (round 6: a heavy-repeat scatter -- 200 slots for
+// 64 Ki pairs -- spent its time in exactly that chain).  Sources never overlap the
+// destinations on the ordered paths (the host sends such calls to the serial kernel).
+template <class OP, int W, bool SYS, class IDX>
+__device__ __forceinline__ void iov_apply_chain(const IovDesc &d, const OP &op, char *dp, uint32_t cnt, IDX idx) {
+    typedef typename Vec<W>::T V;
+    auto src = [&](uint32_t j) -> const char * {
+        const uint32_t i = idx(j);
+        return d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
+    };
+    for (uint32_t v = 0; v < d.nvec; ++v) {
+        V y{};
+        if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
+        uint32_t j = 0;
+        constexpr uint32_t B = 16, b = 4;
+        for (; j + B <= cnt; j += B) {
+            V x[B];
+#pragma unroll
+            for (uint32_t k = 0; k < B; ++k) x[k] = src_load<W, SYS>(src(j + k) + (size_t)v * W);
+#pragma unroll
+            for (uint32_t k = 0; k < B; ++k) y = op.template apply<W>(y, x[k]);
+        }
+        for (; j + b <= cnt; j += b) {
+            V x[b];
+#pragma unroll
+            for (uint32_t k = 0; k < b; ++k) x[k] = src_load<W, SYS>(src(j + k) + (size_t)v * W);
+#pragma unroll
+            for (uint32_t k = 0; k < b; ++k) y = op.template apply<W>(y, x[k]);
+        }
+        for (; j < cnt; ++j) y = op.template apply<W>(y, src_load<W, SYS>(src(j) + (size_t)v * W));
+        vstore<W, false>(dp + (size_t)v * W, y);
+    }
+}
+
 template <class OP, int W, int U, bool SYS = false>
 __global__ __launch_bounds__(256) void k_iov(const IovDesc d, const OP op) {
     typedef typename Vec<W>::T V;
@@ -72,6 +111,8 @@ constexpr uint32_t kIovRunSkip = 0xffffffffu;   // k_iov_runs: a run of this key
 // the hashed path's state for one launch (see k_iovh_insert below)
 struct IovHashArgs {
     bool lds;              // k_iov_lds (one workgroup) instead of the hashed apply + conflicts
+    uint32_t part_lg;      // > 0 with part_keys: k_iov_keyof + k_iov_part on 2^part_lg partitions
+    uint32_t *part_keys;   // their scratch: keys (4 bytes a pair) and buckets; counters in `count`
     uint64_t dlo;
     uint32_t shift;
     bool pow2;
@@ -99,16 +140,10 @@ __global__ __launch_bounds__(256) void k_iov_runs(const IovDesc d, const OP op) 
     if (j0 >= d.n) return;
     const uint32_t key = d.run_key[j0];
     if (key == kIovRunSkip || (j0 > 0 && d.run_key[j0 - 1] == key)) return;
-    for (uint32_t j = j0; j < d.n && d.run_key[j] == key; ++j) {
-        const uint32_t i = d.run_perm[j];
-        const char *sp = d.src_list ? (const char *)d.src_list[i] : d.src_base + (size_t)i * d.bytes;
-        char *dp = (char *)d.dst_list[i];
-        for (uint32_t v = 0; v < d.nvec; ++v) {
-            typename Vec<W>::T x = src_load<W, SYS>(sp + (size_t)v * W), y = x;
-            if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
-            vstore<W, false>(dp + (size_t)v * W, op.template apply<W>(y, x));
-        }
-    }
+    uint32_t cnt = 1;
+    while (j0 + cnt < d.n && d.run_key[j0 + cnt] == key) ++cnt;
+    const uint32_t *perm = d.run_perm + j0;
+    iov_apply_chain<OP, W, SYS>(d, op, (char *)d.dst_list[perm[0]], cnt, [&](uint32_t j) { return perm[j]; });
 }
 
 // ---------------------------------------------------------------------------
@@ -264,7 +299,10 @@ __global__ __launch_bounds__(1024) void k_iovh_conf(const IovDesc d, const OP op
     for (uint32_t t = threadIdx.x; t < m; t += 1024) {
         const uint32_t key = (uint32_t)(s[t] >> 32);
         if (t > 0 && (uint32_t)(s[t - 1] >> 32) == key) continue;
-        for (uint32_t u = t; u < m && (uint32_t)(s[u] >> 32) == key; ++u) iov_apply_pair<OP, W, SYS>(d, op, (uint32_t)s[u]);
+        uint32_t cnt = 1;
+        while (t + cnt < m && (uint32_t)(s[t + cnt] >> 32) == key) ++cnt;
+        iov_apply_chain<OP, W, SYS>(d, op, (char *)d.dst_list[(uint32_t)s[t]], cnt,
+                                    [&](uint32_t j) { return (uint32_t)s[t + j]; });
     }
 }
 
@@ -285,14 +323,13 @@ __global__ __launch_bounds__(1024) void k_iovh_conf(const IovDesc d, const OP op
 //           reference's order (comex.c:7342-7351: one _acc per pair, in order).
 // A destination is rebuilt from its key (dlo + key * bytes: the caller guarantees
 // every destination a whole number of pairs from dlo), so the list is read once.
-// Where it pays (round 6, tools/iov_lds_probe.cpp, profiles/r06/iov_lds/): below 4 Ki
-// pairs.  Kernel time, random single-f64 destinations in 1 GiB, back-to-back launches:
-// 1 Ki pairs 5.9 us against 11.5 for the hashed path's three launches, 2 Ki 8.4 against
-// 13.0, 4 Ki 13.4 against 13.8 -- and then 26 against 19 at 8 Ki, 76 against 18 at 16 Ki:
-// one CU cannot keep enough random destinations in flight (the cost grows faster than
-// the pairs), where the hashed path's apply spreads them over the chip.  A version whose
-// list read was spread over up to 32 workgroups (keys handed to the last one through HBM)
-// measured no faster and was not kept.
+// Where it pays (round 6, tools/iov_lds_probe.cpp, profiles/r06/iov_lds/): small
+// io-vectors.  Kernel time, random single-f64 destinations in 1 GiB, back-to-back
+// launches: 1 Ki pairs 5.9 us against 11.5 for the hashed path's three launches, 2 Ki 8.4
+// against 13.0, 4 Ki 13.4 against 13.8 -- and then 26 against 19 at 8 Ki, 76 against 18
+// at 16 Ki: one CU cannot keep enough random destinations in flight.  From 1 Ki pairs the
+// partitioned path below is used instead (about the same at 1 Ki, faster above, and far
+// faster on heavy repeats: 200 destinations, 2 Ki pairs 23 us against 62 here).
 constexpr uint32_t kIovLdsLog = 15;                       // table slots: 2^15 = 2 x pairs
 constexpr uint32_t kIovLdsEmpty = 0xffffu;
 
@@ -310,43 +347,28 @@ __device__ __forceinline__ void iov_lds_pair(const IovDesc &d, const OP &op, uin
     }
 }
 
-template <class OP, int W, bool SYS>
-__global__ __launch_bounds__(1024) void k_iov_lds(const IovDesc d, const OP op, uint64_t dlo, uint32_t shift,
-                                                  bool pow2) {
-    __shared__ uint32_t keys[kIovLdsMax];
-    __shared__ uint32_t tab[(1u << kIovLdsLog) / 2];      // two 16-bit slots per word; later the conflict list
-    __shared__ uint32_t rep[kIovLdsMax / 32];             // pair i's destination repeats
-    __shared__ uint32_t nconf;
-    const uint32_t t = threadIdx.x, n = d.n;
+// Double hashing: a key's probe step is odd (so it visits every slot of the power-of-two
+// table) and depends on the key.  Linear probing (step 1) let clusters grow at the
+// table's load of one half: with random destinations every 64-lane wave waited for its
+// longest probe, and marking 16 Ki keys took 37 us against 8 for keys that never collide
+// (tools/lds_mark_probe.hip, profiles/r06/iov_lds/lds_mark_*.jsonl).
+__device__ __forceinline__ uint32_t iov_lds_step(uint32_t key) {
+    return ((key * 0x85EBCA6Bu) >> (32 - kIovLdsLog)) | 1u;
+}
+
+// the LDS table of k_iov_lds / k_iov_order: keys[0..n) in LDS -> rep (bit i: pair i's
+// destination has more than one pair).  Insert: the lane whose compare-and-swap claims
+// an empty slot is its key's first pair; a lane that finds its key in a slot marks that
+// slot repeated.  Then every pair looks its key up again and copies the mark.  (Every
+// lane with a given key walks the same probe sequence, so they meet at its first empty
+// slot; no slot is emptied again, so the lookup finds the key before any empty slot.)
+__device__ __forceinline__ void iov_lds_mark(const uint32_t *keys, uint32_t *tab, uint32_t *rep, uint32_t n) {
+    const uint32_t t = threadIdx.x;
     constexpr uint32_t mask = (1u << kIovLdsLog) - 1u;
-    auto key_of = [&](uint64_t a) -> uint32_t {
-        const uint64_t off = a - dlo;
-        return (uint32_t)(pow2 ? (off >> shift) : off / (uint64_t)d.bytes);
-    };
-    for (uint32_t w = t; w < (1u << kIovLdsLog) / 2; w += 1024) tab[w] = 0xffffffffu;
-    for (uint32_t w = t; w < kIovLdsMax / 32; w += 1024) rep[w] = 0;
-    if (t == 0) nconf = 0;
-    {
-        // every list load of this lane in flight at once
-        constexpr int K = kIovLdsMax / 1024;
-        uint32_t kk[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t i = t + (uint32_t)k * 1024u;
-            kk[k] = i < n ? key_of(__builtin_nontemporal_load(d.dst_list + i)) : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t i = t + (uint32_t)k * 1024u;
-            if (i < n) keys[i] = kk[k];
-        }
-    }
-    __syncthreads();
-    // insert: the lane whose compare-and-swap claims an empty slot is its key's first
-    // pair; a lane that finds its key in a slot marks that slot repeated
     for (uint32_t i = t; i < n; i += 1024) {
         const uint32_t key = keys[i];
         uint32_t h = (key * 0x9E3779B1u) >> (32 - kIovLdsLog);
+        const uint32_t step = iov_lds_step(key);
         for (;;) {
             uint32_t *wp = &tab[h >> 1];
             const uint32_t sh = (h & 1u) * 16u;
@@ -360,20 +382,90 @@ __global__ __launch_bounds__(1024) void k_iov_lds(const IovDesc d, const OP op, 
                 atomicOr(wp, 0x8000u << sh);
                 break;
             }
-            h = (h + 1u) & mask;
+            h = (h + step) & mask;
         }
     }
     __syncthreads();
     for (uint32_t i = t; i < n; i += 1024) {
         const uint32_t key = keys[i];
         uint32_t h = (key * 0x9E3779B1u) >> (32 - kIovLdsLog), e;
-        for (;; h = (h + 1u) & mask) {
+        const uint32_t step = iov_lds_step(key);
+        for (;; h = (h + step) & mask) {
             e = (tab[h >> 1] >> ((h & 1u) * 16u)) & 0xffffu;
             if (keys[e & 0x7fffu] == key) break;            // the key's slot (it was inserted)
         }
         if (e & 0x8000u) atomicOr(&rep[i >> 5], 1u << (i & 31u));
     }
     __syncthreads();
+}
+
+// the listed pairs of repeated destinations conf[0..m), sorted by (key, pair index) with
+// an LDS bitonic sort, then one lane per destination applies its pairs in index order
+template <class OP, int W, bool SYS>
+__device__ __forceinline__ void iov_lds_runs(const IovDesc &d, const OP &op, uint64_t dlo, const uint32_t *keys,
+                                             uint32_t *conf, uint32_t m) {
+    const uint32_t t = threadIdx.x;
+    if (m == 0) return;
+    uint32_t P = 1;
+    while (P < m) P <<= 1;
+    for (uint32_t u = m + t; u < P; u += 1024) conf[u] = 0xffffffffu;   // sorts last
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t u = t; u < P; u += 1024) {
+                const uint32_t l = u ^ j;
+                if (l <= u) continue;
+                const uint32_t x = conf[u], y = conf[l];
+                const bool gt = x == 0xffffffffu ? y != 0xffffffffu
+                              : y == 0xffffffffu ? false
+                              : (keys[x] != keys[y] ? keys[x] > keys[y] : x > y);
+                if (gt == ((u & k) == 0)) {
+                    conf[u] = y;
+                    conf[l] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t u = t; u < m; u += 1024) {
+        const uint32_t key = keys[conf[u]];
+        if (u > 0 && keys[conf[u - 1]] == key) continue;
+        char *dp = (char *)(dlo + (uint64_t)key * (uint64_t)d.bytes);
+        uint32_t cnt = 1;
+        while (u + cnt < m && keys[conf[u + cnt]] == key) ++cnt;
+        iov_apply_chain<OP, W, SYS>(d, op, dp, cnt, [&](uint32_t j) { return conf[u + j]; });
+    }
+}
+
+template <class OP, int W, bool SYS>
+__global__ __launch_bounds__(1024) void k_iov_lds(const IovDesc d, const OP op, uint64_t dlo, uint32_t shift,
+                                                  bool pow2) {
+    __shared__ uint32_t keys[kIovLdsMax];
+    __shared__ uint32_t tab[(1u << kIovLdsLog) / 2];      // two 16-bit slots per word; later the conflict list
+    __shared__ uint32_t rep[kIovLdsMax / 32];             // pair i's destination repeats
+    __shared__ uint32_t nconf;
+    const uint32_t t = threadIdx.x, n = d.n;
+    for (uint32_t w = t; w < (1u << kIovLdsLog) / 2; w += 1024) tab[w] = 0xffffffffu;
+    for (uint32_t w = t; w < kIovLdsMax / 32; w += 1024) rep[w] = 0;
+    if (t == 0) nconf = 0;
+    {
+        // every list load of this lane in flight at once
+        constexpr int K = kIovLdsMax / 1024;
+        uint32_t kk[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t i = t + (uint32_t)k * 1024u;
+            const uint64_t off = i < n ? __builtin_nontemporal_load(d.dst_list + i) - dlo : 0;
+            kk[k] = (uint32_t)(pow2 ? (off >> shift) : off / (uint64_t)d.bytes);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t i = t + (uint32_t)k * 1024u;
+            if (i < n) keys[i] = kk[k];
+        }
+    }
+    __syncthreads();
+    iov_lds_mark(keys, tab, rep, n);
     uint32_t *conf = tab;                                   // the table is done with
     // pairs alone on their destination: every vector of them at once, U per lane in flight
     // (source addresses first -- a listed source is one more round trip -- then the data)
@@ -406,36 +498,246 @@ __global__ __launch_bounds__(1024) void k_iov_lds(const IovDesc d, const OP op, 
             if (dps[k]) vstore<W, false>(dps[k], op.template apply<W>(b[k], a[k]));
     }
     __syncthreads();
-    const uint32_t m = nconf;
-    if (m == 0) return;
-    uint32_t P = 1;
-    while (P < m) P <<= 1;
-    for (uint32_t u = m + t; u < P; u += 1024) conf[u] = 0xffffffffu;   // sorts last
+    iov_lds_runs<OP, W, SYS>(d, op, dlo, keys, conf, nconf);
+}
+
+// ---------------------------------------------------------------------------
+// Partitioned io-vector path (round 6) for kIovLdsRoute .. kIovPartMax pairs whose
+// destinations may repeat.  Repeats can only meet on one key, so the keys are split by a
+// hash into G partitions of about kIovPartMean pairs, and each workgroup orders and
+// applies ONE partition on its own: no table, no cross-workgroup hand-off, and the
+// random destinations spread over G CUs.
+//   k_iov_keyof : key = (dst_list[i] - dlo) / bytes, the list read once (chip-wide; it
+//                 may sit across PCIe in the mapped pinned staging); keys[i] = key, and
+//                 (key, i) appended to its partition's bucket (an atomic on its counter:
+//                 an array per calling thread and device, zero at rest -- k_iov_part
+//                 zeroes its own after use, so no clearing launch)
+//   k_iov_part  : workgroup w reads its bucket into LDS, sorts it by (key, index) -- a
+//                 bitonic sort of about kIovPartMean entries -- and one lane per distinct
+//                 key applies its pairs in index order (iov_apply_chain), the
+//                 reference's (comex.c:7342-7351).  A bucket that overflowed (a skewed
+//                 scatter: thousands of pairs on a few destinations) is done in windows
+//                 of the input instead: the window's pairs of the partition gathered,
+//                 sorted and applied, window after window -- input order per key kept.
+// A first version without buckets (each workgroup scanned every key for its own) grew
+// with n x G: 53 us at 64 Ki random pairs against 26 for the hashed path; one with a
+// memset clearing the counters before each call: 25 us at 4 Ki pairs, 39 at 64 Ki.
+constexpr uint32_t kIovPartMean = 128;      // pairs per partition on average
+constexpr uint32_t kIovPartCap = 1024;      // bucket entries (LDS: the entries and the repeated ones, 16 KiB)
+constexpr uint32_t kIovPartBS = 128;        // k_iov_part threads
+constexpr uint32_t kIovPartGMax = 1024;     // partitions at most (kIovPartMax / kIovPartMean = 512)
+
+// The counters: zero at rest, so one array serves one caller at a time -- each calling
+// thread gets its own per device (the local io-vector path under launch_mu and the
+// progress thread's owner-side applies may run together), taken from a pool and returned
+// to it, still zero, when the thread ends (no device free at thread exit).  A caller
+// orders its own calls: the local path synchronises the streams first, the progress
+// thread waits for its previous apply (prog_work_ev).
+struct IovPartCounts {
+    uint32_t *dev[64] = {};
+    ~IovPartCounts();
+};
+static std::mutex g_part_mu;
+static std::vector<uint32_t *> g_part_pool[64];
+IovPartCounts::~IovPartCounts() {
+    std::lock_guard<std::mutex> g(g_part_mu);
+    for (int i = 0; i < 64; ++i)
+        if (dev[i]) g_part_pool[i].push_back(dev[i]);
+}
+static uint32_t *iov_part_counts() {
+    static thread_local IovPartCounts mine;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    if (mine.dev[dev]) return mine.dev[dev];
+    std::lock_guard<std::mutex> g(g_part_mu);
+    if (!g_part_pool[dev].empty()) {
+        mine.dev[dev] = g_part_pool[dev].back();
+        g_part_pool[dev].pop_back();
+        return mine.dev[dev];
+    }
+    uint32_t *p = nullptr;
+    if (hipMalloc((void **)&p, kIovPartGMax * 4) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, kIovPartGMax * 4) != hipSuccess) return nullptr;
+    mine.dev[dev] = p;
+    return p;
+}
+
+__device__ __forceinline__ uint32_t iov_part_of(uint32_t key, uint32_t lg) {
+    return lg ? (key * 0x9E3779B1u) >> (32 - lg) : 0u;
+}
+
+// 1024 threads x kKeyofPer pairs a workgroup: the ranks within a partition from an LDS
+// histogram, then ONE device atomic per (workgroup, partition) reserves the bucket
+// range (one returning atomic per pair instead -- 128 on each counter -- took ~10 us at
+// 4 Ki pairs, this 5)
+constexpr uint32_t kKeyofPer = 4;
+__global__ __launch_bounds__(1024) void k_iov_keyof(const uint64_t *dst_list, uint64_t dlo, uint32_t shift, bool pow2,
+                                                    uint32_t bytes, uint32_t n, uint32_t lg, uint32_t *counts,
+                                                    uint32_t *keys, uint64_t *bucket) {
+    __shared__ uint32_t hist[kIovPartGMax];
+    const uint32_t t = threadIdx.x, G = 1u << lg;
+    for (uint32_t p = t; p < G; p += 1024) hist[p] = 0;
+    uint64_t a[kKeyofPer];
+    const uint32_t i0 = blockIdx.x * 1024u * kKeyofPer + t;
+#pragma unroll
+    for (uint32_t k = 0; k < kKeyofPer; ++k) {
+        const uint32_t i = i0 + k * 1024u;
+        a[k] = i < n ? __builtin_nontemporal_load(dst_list + i) : 0;
+    }
     __syncthreads();
-    // bitonic sort of the listed pairs by (key, pair index)
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t u = t; u < P; u += 1024) {
-                const uint32_t l = u ^ j;
-                if (l <= u) continue;
-                const uint32_t x = conf[u], y = conf[l];
-                const bool gt = x == 0xffffffffu ? y != 0xffffffffu
-                              : y == 0xffffffffu ? false
-                              : (keys[x] != keys[y] ? keys[x] > keys[y] : x > y);
-                if (gt == ((u & k) == 0)) {
-                    conf[u] = y;
-                    conf[l] = x;
+    uint32_t key[kKeyofPer], part[kKeyofPer], rank[kKeyofPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kKeyofPer; ++k) {
+        const uint32_t i = i0 + k * 1024u;
+        if (i >= n) continue;
+        const uint64_t off = a[k] - dlo;
+        key[k] = (uint32_t)(pow2 ? (off >> shift) : off / bytes);
+        keys[i] = key[k];
+        part[k] = iov_part_of(key[k], lg);
+        rank[k] = atomicAdd(&hist[part[k]], 1u);
+    }
+    __syncthreads();
+    for (uint32_t p = t; p < G; p += 1024)
+        if (hist[p]) hist[p] = atomicAdd(counts + p, hist[p]);   // now the range's start
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kKeyofPer; ++k) {
+        const uint32_t i = i0 + k * 1024u;
+        if (i >= n) continue;
+        const uint32_t s = hist[part[k]] + rank[k];
+        if (s < kIovPartCap) bucket[(size_t)part[k] * kIovPartCap + s] = ((uint64_t)key[k] << 32) | i;
+    }
+}
+
+// ent[0..m) (key:index) of one partition: an LDS hash table (16-bit slots: entry index,
+// top bit = the key has more than one entry; double hashing as iov_lds_mark) finds the
+// entries whose key repeats; every other entry is its destination's only pair and is
+// applied at once, the repeated ones are sorted by (key, index) in `aux`, their
+// source-side products computed by all lanes, and one lane per distinct key adds them to
+// its destination in index order (a run of hundreds of pairs on one destination: one
+// lane's chain of source loads took ~90 us at 32 Ki pairs on 200 destinations).  (Sorting every entry instead -- a bitonic sort of about
+// kIovPartMean -- cost ~13 us a partition at 128 threads and ~21 at 64: latency of the
+// barrier stages, where a random scatter has no repeats to order.)  Every thread of the
+// workgroup calls it (barriers inside).
+constexpr uint32_t kIovPartTabLog = 11;     // 2048 slots for at most kIovPartCap entries
+template <class OP, int W, bool SYS>
+__device__ __forceinline__ void iov_part_apply(const IovDesc &d, const OP &op, uint64_t dlo, const uint64_t *ent,
+                                               uint32_t m, uint32_t *tab, uint64_t *aux, uint32_t *naux,
+                                               typename Vec<W>::T *pv) {
+    const uint32_t t = threadIdx.x;
+    constexpr uint32_t mask = (1u << kIovPartTabLog) - 1u;
+    for (uint32_t w = t; w < (1u << kIovPartTabLog) / 2; w += kIovPartBS) tab[w] = 0xffffffffu;
+    if (t == 0) *naux = 0;
+    __syncthreads();
+    for (uint32_t u = t; u < m; u += kIovPartBS) {
+        const uint32_t key = (uint32_t)(ent[u] >> 32);
+        uint32_t h = (key * 0x85EBCA6Bu) >> (32 - kIovPartTabLog);
+        const uint32_t step = ((key * 0xC2B2AE35u) >> (32 - kIovPartTabLog)) | 1u;
+        for (;;) {
+            uint32_t *wp = &tab[h >> 1];
+            const uint32_t sh = (h & 1u) * 16u;
+            const uint32_t cur = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t e = (cur >> sh) & 0xffffu;
+            if (e == kIovLdsEmpty) {
+                if (atomicCAS(wp, cur, (cur & ~(0xffffu << sh)) | (u << sh)) == cur) break;
+                continue;                                   // the word changed under us: look again
+            }
+            if ((uint32_t)(ent[e & 0x7fffu] >> 32) == key) {
+                atomicOr(wp, 0x8000u << sh);
+                break;
+            }
+            h = (h + step) & mask;
+        }
+    }
+    __syncthreads();
+    for (uint32_t u = t; u < m; u += kIovPartBS) {
+        const uint64_t en = ent[u];
+        const uint32_t key = (uint32_t)(en >> 32);
+        uint32_t h = (key * 0x85EBCA6Bu) >> (32 - kIovPartTabLog), e;
+        const uint32_t step = ((key * 0xC2B2AE35u) >> (32 - kIovPartTabLog)) | 1u;
+        for (;; h = (h + step) & mask) {
+            e = (tab[h >> 1] >> ((h & 1u) * 16u)) & 0xffffu;
+            if ((uint32_t)(ent[e & 0x7fffu] >> 32) == key) break;   // the key's slot
+        }
+        if (e & 0x8000u) aux[atomicAdd(naux, 1u)] = en;
+        else iov_lds_pair<OP, W, SYS>(d, op, (uint32_t)en, (char *)(dlo + (uint64_t)key * (uint64_t)d.bytes));
+    }
+    __syncthreads();
+    const uint32_t mr = *naux;
+    if (mr) {
+        uint32_t P = 1;
+        while (P < mr) P <<= 1;
+        for (uint32_t u = mr + t; u < P; u += kIovPartBS) aux[u] = ~0ull;   // sorts last
+        __syncthreads();
+        for (uint32_t k = 2; k <= P; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t u = t; u < P; u += kIovPartBS) {
+                    const uint32_t l = u ^ j;
+                    if (l <= u) continue;
+                    const uint64_t x = aux[u], y = aux[l];
+                    if ((x > y) == ((u & k) == 0)) {
+                        aux[u] = y;
+                        aux[l] = x;
+                    }
                 }
+                __syncthreads();
+            }
+        }
+        // vector v of every repeated pair: the source-only part of the operation (the
+        // products) by all lanes into LDS, then one lane per destination adds them in index
+        // order -- op.pre / op.add, the same operations as op.apply (gaamd_device.hpp)
+        for (uint32_t v = 0; v < d.nvec; ++v) {
+            for (uint32_t u = t; u < mr; u += kIovPartBS)
+                pv[u] = op.template pre<W>(src_load<W, SYS>(iov_lds_src(d, (uint32_t)aux[u]) + (size_t)v * W));
+            __syncthreads();
+            for (uint32_t u = t; u < mr; u += kIovPartBS) {
+                const uint32_t key = (uint32_t)(aux[u] >> 32);
+                if (u > 0 && (uint32_t)(aux[u - 1] >> 32) == key) continue;
+                char *dp = (char *)(dlo + (uint64_t)key * (uint64_t)d.bytes) + (size_t)v * W;
+                typename Vec<W>::T y{};
+                if constexpr (OP::kReadsDst) y = vload<W, false>(dp);
+                for (uint32_t j = u; j < mr && (uint32_t)(aux[j] >> 32) == key; ++j) y = op.template add<W>(y, pv[j]);
+                vstore<W, false>(dp, y);
             }
             __syncthreads();
         }
     }
-    // one lane per repeated destination: its pairs in index order
-    for (uint32_t u = t; u < m; u += 1024) {
-        const uint32_t key = keys[conf[u]];
-        if (u > 0 && keys[conf[u - 1]] == key) continue;
-        char *dp = (char *)(dlo + (uint64_t)key * (uint64_t)d.bytes);
-        for (uint32_t w = u; w < m && keys[conf[w]] == key; ++w) iov_lds_pair<OP, W, SYS>(d, op, conf[w], dp);
+    __syncthreads();
+}
+
+template <class OP, int W, bool SYS>
+__global__ __launch_bounds__(kIovPartBS) void k_iov_part(const IovDesc d, const OP op, uint64_t dlo, uint32_t lg,
+                                                         uint32_t *counts, const uint32_t *keys,
+                                                         const uint64_t *bucket) {
+    __shared__ uint64_t ent[kIovPartCap], aux[kIovPartCap];
+    __shared__ uint32_t tab[(1u << kIovPartTabLog) / 2];
+    __shared__ uint32_t cnt, naux;
+    __shared__ typename Vec<W>::T pv[kIovPartCap];
+    const uint32_t t = threadIdx.x, w = blockIdx.x;
+    // the bucket's first kIovPartBS entries loaded with the count, not after it
+    const uint64_t *bk = bucket + (size_t)w * kIovPartCap;
+    const uint64_t e0 = bk[t];
+    const uint32_t m = counts[w];
+    if (m == 0) return;
+    __syncthreads();
+    if (t == 0) counts[w] = 0;   // zero at rest for the next call (stream-ordered after this one)
+    if (m <= kIovPartCap) {
+        if (t < m) ent[t] = e0;
+        for (uint32_t u = t + kIovPartBS; u < m; u += kIovPartBS) ent[u] = bk[u];
+        iov_part_apply<OP, W, SYS>(d, op, dlo, ent, m, tab, aux, &naux, pv);
+        return;
+    }
+    // overflowed: windows of kIovPartCap input pairs (at most kIovPartCap of them match)
+    for (uint32_t base = 0; base < d.n; base += kIovPartCap) {
+        if (t == 0) cnt = 0;
+        __syncthreads();
+        for (uint32_t i = base + t; i < base + kIovPartCap && i < d.n; i += kIovPartBS) {
+            const uint32_t key = keys[i];
+            if (iov_part_of(key, lg) == w) ent[atomicAdd(&cnt, 1u)] = ((uint64_t)key << 32) | i;
+        }
+        __syncthreads();
+        const uint32_t mw = cnt;
+        if (mw) iov_part_apply<OP, W, SYS>(d, op, dlo, ent, mw, tab, aux, &naux, pv);   // mw is uniform
     }
 }
 
@@ -453,7 +755,18 @@ __global__ __launch_bounds__(256) void k_iov_keys_masked(const uint64_t *dst_lis
 
 template <class OP, int W, bool SYS>
 static hipError_t iov_ws(const IovDesc &d, const OP &op, bool serial, hipStream_t st, const IovHashArgs *ha) {
-    if (ha && ha->lds) {
+    if (ha && ha->part_keys) {
+        // scratch: keys (4 B a pair) | buckets (G x kIovPartCap x 8 B)
+        char *sc = (char *)ha->part_keys;
+        const uint32_t G = 1u << ha->part_lg;
+        uint32_t *counts = ha->count, *keys = (uint32_t *)sc;
+        uint64_t *bucket = (uint64_t *)(sc + (((size_t)d.n * 4 + 255) & ~(size_t)255));
+        hipLaunchKernelGGL(k_iov_keyof, dim3((d.n + 1024u * kKeyofPer - 1) / (1024u * kKeyofPer)), dim3(1024), 0, st,
+                           d.dst_list, ha->dlo, ha->shift,
+                           ha->pow2, (uint32_t)d.bytes, d.n, ha->part_lg, counts, keys, bucket);
+        hipLaunchKernelGGL((k_iov_part<OP, W, SYS>), dim3(G), dim3(kIovPartBS), 0, st, d, op, ha->dlo, ha->part_lg,
+                           counts, keys, bucket);
+    } else if (ha && ha->lds) {
         hipLaunchKernelGGL((k_iov_lds<OP, W, SYS>), dim3(1), dim3(1024), 0, st, d, op, ha->dlo, ha->shift, ha->pow2);
     } else if (ha) {
         hipLaunchKernelGGL((k_iovh_apply<OP, W, SYS>), dim3((d.n + kIovhBS - 1) / kIovhBS), dim3(kIovhBS), 0, st, d, op,
@@ -658,6 +971,12 @@ static int radix_sort_pairs(uint32_t *const k[2], uint32_t *const v[2], uint32_t
     return cur;
 }
 
+size_t iov_lds_scratch_bytes(uint32_t n) {
+    uint32_t lg = 0;
+    while ((n >> lg) > kIovPartMean) ++lg;
+    return (((size_t)n * 4 + 255) & ~(size_t)255) + ((size_t)kIovPartCap * 8 << lg);
+}
+
 size_t iov_runs_work_bytes(uint32_t n) { return 4 * align256((size_t)n * 4) + align256(iov_sort_temp_bytes(n)); }
 
 int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
@@ -777,7 +1096,7 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
                        (uint64_t *)d.src_list);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return -100 - (int)e;
-    IovHashArgs ha{false, dlo, shift, pow2, h->epoch, dup, slot, conf, count, h->flag_dev};
+    IovHashArgs ha{false, 0, nullptr, dlo, shift, pow2, h->epoch, dup, slot, conf, count, h->flag_dev};
     h->dlo = dlo;
     h->n = d.n;
     h->shift = shift;
@@ -786,11 +1105,11 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
 }
 
 int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
-                   hipStream_t stream, bool src_peer) {
+                   hipStream_t stream, bool src_peer, void *scratch) {
     const int esz = elem_size(op);
     if (!esz || d.bytes <= 0 || d.bytes > kIovRunsMaxBytes || !d.dst_list) return -4;
     if (op != kOpCopy && !scale) return -5;
-    if (d.n > kIovLdsMax || units > (1ull << 32)) return 1;   // another path
+    if (units > (1ull << 32)) return 1;   // another path
     const int64_t row = (op == kOpCopy) ? d.bytes : (int64_t)(d.bytes / esz) * esz;   // acc.h:122
     if (d.n == 0 || row == 0) return 0;
     uint64_t a = align_or | (uint64_t)row | 16;
@@ -806,7 +1125,21 @@ int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint
     d.items = d.n * d.nvec;
     const bool pow2 = (d.bytes & (d.bytes - 1)) == 0;
     const uint32_t shift = pow2 ? (uint32_t)__builtin_ctz((unsigned)d.bytes) : 0;
-    IovHashArgs ha{true, dlo, shift, pow2, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+    // from kIovLdsRoute pairs (with scratch, iov_lds_scratch_bytes): the partitioned path,
+    // about kIovPartMean pairs a partition
+    uint32_t lg = 0;
+    uint32_t *keys = nullptr, *counts = nullptr;
+    if (scratch && d.n >= kIovLdsRoute) {
+        if (d.n > kIovPartMax) return 1;
+        while ((d.n >> lg) > kIovPartMean) ++lg;
+        if ((1u << lg) > kIovPartGMax) return -6;
+        counts = iov_part_counts();
+        if (!counts) return -7;
+        keys = (uint32_t *)scratch;
+    } else if (d.n > kIovLdsMax) {
+        return 1;
+    }
+    IovHashArgs ha{true, lg, keys, dlo, shift, pow2, 0, nullptr, nullptr, nullptr, counts, nullptr};
     return iov_dispatch(op, scale, W, d, false, src_peer, stream, &ha);
 }
 

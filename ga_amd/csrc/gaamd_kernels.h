@@ -189,13 +189,19 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
                       uint64_t units, hipStream_t stream, bool src_peer = false, const uint64_t *dst_in = nullptr,
                       const uint64_t *src_in = nullptr);
 bool iov_hash_overflowed(const IovHash *h);
-// The same contract for up to kIovLdsMax pairs in ONE launch of one workgroup (the
-// ordering held in LDS, k_iov_lds); d.dst_list / d.src_list may point into mapped
-// pinned memory (read once).  Returns 1 when n is outside its range.  The callers use it
-// below kIovLdsRoute pairs, where it is faster than the hashed path (gaamd_iov.hip).
+// The same contract with the ordering held in LDS; d.dst_list / d.src_list may point
+// into mapped pinned memory (read once).  Below kIovLdsRoute pairs, or without scratch,
+// ONE launch of one workgroup (k_iov_lds, up to kIovLdsMax pairs); from kIovLdsRoute
+// to kIovPartMax pairs with `scratch` (HBM, iov_lds_scratch_bytes(n)), two launches:
+// the keys into hash-partition buckets (k_iov_keyof), then one workgroup per partition
+// orders and applies its pairs (k_iov_part).  Returns 1 when n is outside its range.
+// Calls from one thread must be ordered (each completes before the next starts): the
+// partition counters are per thread and zero between calls.
 constexpr uint32_t kIovLdsMax = 16384;
-constexpr uint32_t kIovLdsRoute = 4096;
+constexpr uint32_t kIovLdsRoute = 1024;
+constexpr uint32_t kIovPartMax = 1u << 16;
+size_t iov_lds_scratch_bytes(uint32_t n);   // keys and partition buckets (~68 B a pair)
 int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
-                   hipStream_t stream, bool src_peer = false);
+                   hipStream_t stream, bool src_peer = false, void *scratch = nullptr);
 
 }  // namespace gaamd

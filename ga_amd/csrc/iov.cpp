@@ -422,7 +422,9 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     }
     phase("classify");
     const size_t o_work = (o_res + (dst_listed ? 0 : pk) + 255) & ~(size_t)255;   // sort work: 256-aligned
-    const size_t work = runs ? iov_runs_work_bytes((uint32_t)n) : 0;
+    const size_t work = !runs ? 0
+                      : std::max(iov_runs_work_bytes((uint32_t)n),
+                                 n <= (int)kIovPartMax ? iov_lds_scratch_bytes((uint32_t)n) : (size_t)0);
     char *dev = iov_scratch(o_work + work);
     IovDesc d;
     memset(&d, 0, sizeof(d));
@@ -474,14 +476,16 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         rc = 1;
         char *up_dev = nullptr;   // the device view of the pinned upload buffer
         GA_HIP(hipHostGetDevicePointer((void **)&up_dev, up, 0));
-        if (n < (int)kIovLdsRoute && !src_peer && tuning().iov_lds) {
-            // below 4 Ki pairs: ordered and applied by one launch of one workgroup, the
-            // lists (and packed sources) read in place from the pinned staging
+        if (n <= (int)kIovPartMax && !src_peer && tuning().iov_lds) {
+            // up to 64 Ki pairs: ordered in LDS, the lists (and packed sources) read in
+            // place from the pinned staging -- below 1 Ki pairs one launch of one
+            // workgroup, from 1 Ki the keys and then one workgroup per hash partition
             IovDesc z = d;
             z.dst_list = (const uint64_t *)(up_dev + o_dst);
             if (d.src_list) z.src_list = (const uint64_t *)(up_dev + o_src);
             else if (!src_listed) z.src_base = up_dev + o_src;
-            rc = launch_iov_lds(cop, scale, z, align_or, dlo, units, r.streams[si]);
+            if (work < iov_lds_scratch_bytes((uint32_t)n)) fatal("io-vector scratch too small for the LDS path");
+            rc = launch_iov_lds(cop, scale, z, align_or, dlo, units, r.streams[si], false, dev + o_work);
             if (rc == 0) g_iov_path[3].fetch_add(1, std::memory_order_relaxed);
         }
         if (rc == 1 && !src_listed && o_res > o_src)

@@ -313,12 +313,15 @@ static void progress_loop() {
                 int rc = 1;
                 const uint64_t units = (q.dst_hi - q.dst_addr) / (uint64_t)d.bytes + 1;
                 if (q.iov_serial == 2 && d.n < kIovLdsRoute && tuning().iov_lds)
-                    // below 4 Ki pairs: ordered and applied by one workgroup, in LDS
+                    // below 1 Ki pairs: ordered and applied by one workgroup, in LDS
                     rc = launch_iov_lds(q.op, q.scale, d, q.iov_align, q.dst_addr, units, r.streams[si]);
                 if (q.iov_serial == 2 && rc == 1) {
-                    // repeated destinations ordered on the GPU; the progress thread's own sort
-                    // scratch, free once the previous runs kernel has finished
-                    const size_t need = iov_runs_work_bytes(d.n);
+                    // repeated destinations ordered on the GPU: up to kIovPartMax pairs by
+                    // hash partitions in LDS, above by the radix path; the progress thread's
+                    // own scratch, free once its previous apply has finished (which also
+                    // orders the partition counters, zero at rest, between its calls)
+                    const bool part = d.n <= kIovPartMax && tuning().iov_lds;
+                    const size_t need = std::max(iov_runs_work_bytes(d.n), part ? iov_lds_scratch_bytes(d.n) : 0);
                     if (prog_work_ev) GA_HIP(hipEventSynchronize(prog_work_ev));
                     if (need > prog_work_bytes) {
                         if (prog_work) GA_HIP(hipFree(prog_work));
@@ -326,8 +329,12 @@ static void progress_loop() {
                         GA_HIP(hipMalloc((void **)&prog_work, prog_work_bytes));
                     }
                     if (!prog_work_ev) GA_HIP(hipEventCreateWithFlags(&prog_work_ev, kOwnerEventFlags));
-                    rc = launch_iov_runs(q.op, q.scale, d, q.iov_align, q.dst_addr, units, prog_work, prog_work_bytes,
-                                         r.streams[si]);
+                    if (part)
+                        rc = launch_iov_lds(q.op, q.scale, d, q.iov_align, q.dst_addr, units, r.streams[si], false,
+                                            prog_work);
+                    if (rc == 1)
+                        rc = launch_iov_runs(q.op, q.scale, d, q.iov_align, q.dst_addr, units, prog_work,
+                                             prog_work_bytes, r.streams[si]);
                     GA_HIP(hipEventRecord(prog_work_ev, r.streams[si]));
                 } else if (rc == 1) {
                     rc = launch_iov(q.op, q.scale, d, q.iov_align, q.iov_serial != 0, r.streams[si]);

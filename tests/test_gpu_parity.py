@@ -686,10 +686,11 @@ def _giov_np(src_addrs, dst_addrs, nbytes):
 def test_accv_large_repeated_destinations(gpu_lib, oracle, op, nbytes, slots, shift):
     """GA scatter-acc sizes: 40 000 pairs in one descriptor, destinations drawn from
     `slots` (many repeats), bit-exact against the pairs applied one by one in order.
-    From 4096 pairs the launcher sorts destinations on the GPU and applies each
-    destination's pairs in input order (launch_iov_runs); 320-byte pairs and
-    destinations not congruent modulo the pair size (`shift`: some start half a
-    pair later) take the host-checked path instead."""
+    The GPU orders repeated destinations and applies each destination's pairs in input
+    order: the partitioned LDS path (round 6), and the hashed path (+ the radix path
+    for heavy repeats) with tuning iov_lds=0; 320-byte pairs and destinations not
+    congruent modulo the pair size (`shift`: some start half a pair later) take the
+    host-checked path instead."""
     rng = np.random.default_rng(nbytes * 7 + slots)
     n = 40000
     src = C.fill_bytes(op, n * nbytes, 5)
@@ -712,12 +713,21 @@ def test_accv_large_repeated_destinations(gpu_lib, oracle, op, nbytes, slots, sh
     got = db.download(np.uint8, dst.size)
     assert same_bits_nan_aware(got, want, op)
     if nbytes <= 256 and not shift:
-        # the hashed path orders the pairs that share a destination: up to 8192 of them
-        # in LDS (1e6 slots: ~800 such pairs), more (every pair repeats) through the
-        # radix path for what the hashed launch left
+        # up to 64 Ki pairs the partitioned LDS path orders them (round 6); the hashed
+        # path (and the radix path for what it leaves) with iov_lds=0, below
+        assert paths1["lds"] == paths0["lds"] + 1, (paths0, paths1)
+        old = ga_amd.set_tuning("iov_lds", 0)
+        try:
+            db.upload(dst)
+            assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
+            ga_amd.comex_fence_all()
+        finally:
+            ga_amd.set_tuning("iov_lds", old)
+        assert same_bits_nan_aware(db.download(np.uint8, dst.size), want, op)
+        paths2 = ga_amd.iov_path_counts()
         conflicting = n - int(np.sum(np.unique(do, return_counts=True)[1] == 1))
         key = "hashed" if conflicting <= 8192 else "hashed_then_radix"
-        assert paths1[key] == paths0[key] + 1, (conflicting, paths0, paths1)
+        assert paths2[key] == paths1[key] + 1, (conflicting, paths1, paths2)
 
 
 @pytest.mark.parametrize("op,nbytes,slots,n", [(C.DBL, 8, 150000, 600037), (C.FLT, 4, 900, 530001),
@@ -887,14 +897,17 @@ def test_accv_host_source_over_split_mappings(gpu_lib, oracle):
     (C.DBL, 8, 10 ** 6, 16384, "seq"), (C.DBL, 8, 3000, 16384, "perm"), (C.FLT, 4, 100, 16384, "seq"),
     (C.DCP, 16, 2000, 8192, "perm"), (C.INT, 12, 700, 4096, "seq"), (C.LNG, 8, 50, 2048, "perm"),
     (C.CPL, 24, 5000, 12000, "seq"), (C.DBL, 256, 300, 3000, "perm"), (C.DBL, 8, 1, 4095, "seq"),
-    (C.DBL, 8, 200, 1000, "host"), (C.FLT, 4, 1 << 20, 3500, "host"), (C.LNG, 8, 3, 64, "perm"),
-    (C.INT, 4, 1 << 20, 3000, "perm")])
+    (C.DBL, 8, 1, 4096, "seq"), (C.DBL, 8, 200, 1000, "host"), (C.FLT, 4, 1 << 20, 16384, "host"),
+    (C.LNG, 8, 3, 64, "perm"), (C.INT, 4, 1 << 20, 3000, "perm"), (C.DCP, 16, 1 << 20, 9000, "perm"),
+    (C.DBL, 8, 10 ** 6, 65536, "seq"), (C.FLT, 4, 7, 30000, "perm"), (C.CPL, 8, 40000, 50000, "host")])
 def test_accv_one_workgroup_path(gpu_lib, oracle, op, nbytes, slots, n, src):
-    """below 4 Ki pairs, io-vectors whose destinations may repeat are
-    ordered and applied by ONE launch of one 1024-thread workgroup (k_iov_lds: keys and a
-    hash table in LDS, pairs alone on their destination applied at once, the repeated ones
-    sorted by (destination, index) in LDS and applied in input order); from 4 Ki pairs the
-    hashed path (one CU cannot keep enough random destinations in flight there).  Sources contiguous (GA's
+    """io-vectors of up to 64 Ki pairs whose destinations may repeat are
+    ordered in LDS: below 1 Ki pairs ONE launch of one 1024-thread workgroup (k_iov_lds:
+    keys and a hash table in LDS, repeated pairs sorted by (destination, index), applied
+    in input order); from 1 Ki pairs the keys into hash-partition buckets, then one
+    workgroup per partition finds its repeated keys in an LDS table, sorts only those and
+    applies them (k_iov_keyof + k_iov_part; a skewed partition -- 7 destinations for
+    30 000 pairs -- in windows of the input).  Sources contiguous (GA's
     `v`), permuted, or gathered from pageable host memory; from one destination for
     every pair to nearly all distinct; bit-exact against the pairs applied one by one,
     and the same bytes as the hashed three-launch path (tuning iov_lds=0)."""
@@ -925,7 +938,7 @@ def test_accv_one_workgroup_path(gpu_lib, oracle, op, nbytes, slots, n, src):
             paths1 = ga_amd.iov_path_counts()
         finally:
             ga_amd.set_tuning("iov_lds", old)
-        assert (paths1["lds"] - paths0["lds"]) == (lds if n < 4096 else 0), (lds, n, paths0, paths1)
+        assert (paths1["lds"] - paths0["lds"]) == lds, (lds, n, paths0, paths1)
         got = db.download(np.uint8, dst.size)
         assert same_bits_nan_aware(got, want, op), f"iov_lds={lds}"
         outs.append(got)
