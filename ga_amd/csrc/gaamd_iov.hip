@@ -120,7 +120,7 @@ struct IovHashArgs {
     const uint32_t *dup;
     const uint32_t *slot;
     uint64_t *conf;
-    uint32_t *count, *overflow;
+    uint32_t *count, *overflow;   // partitioned path: its counters, and (deferring) the overflow flag
 };
 
 // launch_iov_runs: sort keys = destination index relative to dlo, values = pair index
@@ -525,7 +525,7 @@ __global__ __launch_bounds__(1024) void k_iov_lds(const IovDesc d, const OP op, 
 constexpr uint32_t kIovPartMean = 128;      // pairs per partition on average
 constexpr uint32_t kIovPartCap = 1024;      // bucket entries (LDS: the entries and the repeated ones, 16 KiB)
 constexpr uint32_t kIovPartBS = 128;        // k_iov_part threads
-constexpr uint32_t kIovPartGMax = 1024;     // partitions at most (kIovPartMax / kIovPartMean = 512)
+constexpr uint32_t kIovPartGMax = 8192;     // partitions at most (kIovPartMax / kIovPartMean)
 
 // The counters: zero at rest, so one array serves one caller at a time -- each calling
 // thread gets its own per device (the local io-vector path under launch_mu and the
@@ -573,7 +573,7 @@ __device__ __forceinline__ uint32_t iov_part_of(uint32_t key, uint32_t lg) {
 constexpr uint32_t kKeyofPer = 4;
 __global__ __launch_bounds__(1024) void k_iov_keyof(const uint64_t *dst_list, uint64_t dlo, uint32_t shift, bool pow2,
                                                     uint32_t bytes, uint32_t n, uint32_t lg, uint32_t *counts,
-                                                    uint32_t *keys, uint64_t *bucket) {
+                                                    uint32_t *keys, uint64_t *bucket, uint32_t *overflow) {
     __shared__ uint32_t hist[kIovPartGMax];
     const uint32_t t = threadIdx.x, G = 1u << lg;
     for (uint32_t p = t; p < G; p += 1024) hist[p] = 0;
@@ -598,7 +598,11 @@ __global__ __launch_bounds__(1024) void k_iov_keyof(const uint64_t *dst_list, ui
     }
     __syncthreads();
     for (uint32_t p = t; p < G; p += 1024)
-        if (hist[p]) hist[p] = atomicAdd(counts + p, hist[p]);   // now the range's start
+        if (hist[p]) {
+            const uint32_t h = hist[p];
+            hist[p] = atomicAdd(counts + p, h);   // now the range's start
+            if (overflow && hist[p] + h > kIovPartCap) *overflow = 1u;   // (mapped pinned: the host reads it)
+        }
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < kKeyofPer; ++k) {
@@ -708,7 +712,7 @@ __device__ __forceinline__ void iov_part_apply(const IovDesc &d, const OP &op, u
 template <class OP, int W, bool SYS>
 __global__ __launch_bounds__(kIovPartBS) void k_iov_part(const IovDesc d, const OP op, uint64_t dlo, uint32_t lg,
                                                          uint32_t *counts, const uint32_t *keys,
-                                                         const uint64_t *bucket) {
+                                                         const uint64_t *bucket, bool defer) {
     __shared__ uint64_t ent[kIovPartCap], aux[kIovPartCap];
     __shared__ uint32_t tab[(1u << kIovPartTabLog) / 2];
     __shared__ uint32_t cnt, naux;
@@ -719,6 +723,9 @@ __global__ __launch_bounds__(kIovPartBS) void k_iov_part(const IovDesc d, const 
     const uint64_t e0 = bk[t];
     const uint32_t m = counts[w];
     if (m == 0) return;
+    // an overflowed partition of a large call is left, count and all, to the caller's
+    // radix fallback (launch_iov_runs with this call's IovPartState as the mask)
+    if (defer && m > kIovPartCap) return;
     __syncthreads();
     if (t == 0) counts[w] = 0;   // zero at rest for the next call (stream-ordered after this one)
     if (m <= kIovPartCap) {
@@ -727,7 +734,9 @@ __global__ __launch_bounds__(kIovPartBS) void k_iov_part(const IovDesc d, const 
         iov_part_apply<OP, W, SYS>(d, op, dlo, ent, m, tab, aux, &naux, pv);
         return;
     }
-    // overflowed: windows of kIovPartCap input pairs (at most kIovPartCap of them match)
+    // overflowed: windows of kIovPartCap input pairs (at most kIovPartCap of them match);
+    // n / kIovPartCap windows for this one workgroup, so only for calls of up to
+    // kIovPartWindowMax pairs -- larger ones defer (above)
     for (uint32_t base = 0; base < d.n; base += kIovPartCap) {
         if (t == 0) cnt = 0;
         __syncthreads();
@@ -753,6 +762,18 @@ __global__ __launch_bounds__(256) void k_iov_keys_masked(const uint64_t *dst_lis
     vals[i] = i;
 }
 
+// the partition fallback's keys: pairs of partitions that did not overflow were applied
+// by k_iov_part and get the sentinel key
+__global__ __launch_bounds__(256) void k_iov_keys_partmask(const uint64_t *dst_list, uint64_t dlo, uint32_t bytes,
+                                                           uint32_t n, const uint32_t *counts, uint32_t lg,
+                                                           uint32_t *keys, uint32_t *vals) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t key = (uint32_t)((dst_list[i] - dlo) / bytes);
+    keys[i] = counts[iov_part_of(key, lg)] > kIovPartCap ? key : kIovRunSkip;
+    vals[i] = i;
+}
+
 template <class OP, int W, bool SYS>
 static hipError_t iov_ws(const IovDesc &d, const OP &op, bool serial, hipStream_t st, const IovHashArgs *ha) {
     if (ha && ha->part_keys) {
@@ -763,9 +784,9 @@ static hipError_t iov_ws(const IovDesc &d, const OP &op, bool serial, hipStream_
         uint64_t *bucket = (uint64_t *)(sc + (((size_t)d.n * 4 + 255) & ~(size_t)255));
         hipLaunchKernelGGL(k_iov_keyof, dim3((d.n + 1024u * kKeyofPer - 1) / (1024u * kKeyofPer)), dim3(1024), 0, st,
                            d.dst_list, ha->dlo, ha->shift,
-                           ha->pow2, (uint32_t)d.bytes, d.n, ha->part_lg, counts, keys, bucket);
+                           ha->pow2, (uint32_t)d.bytes, d.n, ha->part_lg, counts, keys, bucket, ha->overflow);
         hipLaunchKernelGGL((k_iov_part<OP, W, SYS>), dim3(G), dim3(kIovPartBS), 0, st, d, op, ha->dlo, ha->part_lg,
-                           counts, keys, bucket);
+                           counts, keys, bucket, ha->overflow != nullptr);
     } else if (ha && ha->lds) {
         hipLaunchKernelGGL((k_iov_lds<OP, W, SYS>), dim3(1), dim3(1024), 0, st, d, op, ha->dlo, ha->shift, ha->pow2);
     } else if (ha) {
@@ -980,7 +1001,8 @@ size_t iov_lds_scratch_bytes(uint32_t n) {
 size_t iov_runs_work_bytes(uint32_t n) { return 4 * align256((size_t)n * 4) + align256(iov_sort_temp_bytes(n)); }
 
 int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
-                    void *work, size_t work_bytes, hipStream_t stream, bool src_peer, const IovHash *mask) {
+                    void *work, size_t work_bytes, hipStream_t stream, bool src_peer, const IovHash *mask,
+                    const IovPartState *pmask) {
     const int esz = elem_size(op);
     if (!esz || d.bytes <= 0 || d.bytes > kIovRunsMaxBytes || !d.dst_list) return -4;
     if (op != kOpCopy && !scale) return -5;
@@ -1014,6 +1036,17 @@ int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uin
         const uint32_t *slot = (const uint32_t *)(mask->mem + iovh_off_slot((uint32_t)P));
         hipLaunchKernelGGL(k_iov_keys_masked, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, d.dst_list, dlo,
                            (uint32_t)d.bytes, d.n, mask->epoch, dup, slot, kin, vin);
+        end_bit = 32;
+    } else if (pmask) {
+        // the pairs of partitions k_iov_part applied sort last (sentinel key); then the
+        // deferred partitions' counters back to zero
+        if (!pmask->counts || units >= (uint64_t)kIovRunSkip) return -9;
+        hipLaunchKernelGGL(k_iov_keys_partmask, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, d.dst_list, dlo,
+                           (uint32_t)d.bytes, d.n, pmask->counts, pmask->lg, kin, vin);
+        hipError_t e0 = hipGetLastError();
+        if (e0 != hipSuccess) return -100 - (int)e0;
+        e0 = hipMemsetAsync(pmask->counts, 0, (size_t)4 << pmask->lg, stream);
+        if (e0 != hipSuccess) return -100 - (int)e0;
         end_bit = 32;
     } else {
         hipLaunchKernelGGL(k_iov_keys, dim3((d.n + 255u) / 256u), dim3(256), 0, stream, d.dst_list, dlo,
@@ -1105,7 +1138,7 @@ int launch_iov_hashed(IovHash *h, int op, const void *scale, IovDesc d, uint64_t
 }
 
 int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
-                   hipStream_t stream, bool src_peer, void *scratch) {
+                   hipStream_t stream, bool src_peer, void *scratch, IovPartState *defer) {
     const int esz = elem_size(op);
     if (!esz || d.bytes <= 0 || d.bytes > kIovRunsMaxBytes || !d.dst_list) return -4;
     if (op != kOpCopy && !scale) return -5;
@@ -1136,10 +1169,16 @@ int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint
         counts = iov_part_counts();
         if (!counts) return -7;
         keys = (uint32_t *)scratch;
+        if (d.n > kIovPartWindowMax && !(defer && defer->flag_dev)) return -10;   // must defer
+        if (defer) {
+            defer->counts = counts;
+            defer->lg = lg;
+        }
     } else if (d.n > kIovLdsMax) {
         return 1;
     }
-    IovHashArgs ha{true, lg, keys, dlo, shift, pow2, 0, nullptr, nullptr, nullptr, counts, nullptr};
+    IovHashArgs ha{true, lg, keys, dlo, shift, pow2, 0, nullptr, nullptr, nullptr, counts,
+                   (keys && defer) ? defer->flag_dev : nullptr};
     return iov_dispatch(op, scale, W, d, false, src_peer, stream, &ha);
 }
 

@@ -167,12 +167,13 @@ int launch_iov(int op, const void *scale, IovDesc d, uint64_t align_or, bool ser
 // < 2^32, d.bytes <= kIovRunsMaxBytes, and no source inside a destination.
 constexpr int kIovRunsMaxBytes = 256;
 size_t iov_runs_work_bytes(uint32_t n);
+struct IovPartState;   // the partitioned path's deferred overflow (below)
 struct IovHash;   // the hashed path's table (one per calling thread; kept across calls)
 // mask: the table of a hashed launch whose conflicts overflowed (iov_hash_overflowed):
 // the pairs it applied already are skipped
 int launch_iov_runs(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
                     void *work, size_t work_bytes, hipStream_t stream, bool src_peer = false,
-                    const IovHash *mask = nullptr);
+                    const IovHash *mask = nullptr, const IovPartState *pmask = nullptr);
 // The same contract as launch_iov_runs without the sort for up to 2^19 pairs: a
 // hash table finds the destinations with more than one pair; pairs alone on
 // theirs are applied at once, the rest (up to 8192) sorted by (destination,
@@ -197,11 +198,23 @@ bool iov_hash_overflowed(const IovHash *h);
 // orders and applies its pairs (k_iov_part).  Returns 1 when n is outside its range.
 // Calls from one thread must be ordered (each completes before the next starts): the
 // partition counters are per thread and zero between calls.
+// A partition of more than its bucket's pairs (heavy repeats) is done in windows of the
+// input by its workgroup: n / 1024 windows, so only up to kIovPartWindowMax pairs.  Larger
+// calls pass `defer` with a mapped pinned flag: such partitions are then left untouched
+// (counters kept), the flag raised, and after the stream completed the caller applies
+// them with launch_iov_runs(..., pmask = defer) (which zeroes the counters again).
+struct IovPartState {
+    uint32_t *flag_dev = nullptr;   // in: device view of a zeroed mapped pinned word
+    uint32_t *counts = nullptr;     // out: the call's partition counters
+    uint32_t lg = 0;                // out: log2 of its partitions
+};
+constexpr uint32_t kIovPartWindowMax = 1u << 16;
 constexpr uint32_t kIovLdsMax = 16384;
 constexpr uint32_t kIovLdsRoute = 1024;
-constexpr uint32_t kIovPartMax = 1u << 16;
+constexpr uint32_t kIovPartMax = 1u << 20;
 size_t iov_lds_scratch_bytes(uint32_t n);   // keys and partition buckets (~68 B a pair)
 int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
-                   hipStream_t stream, bool src_peer = false, void *scratch = nullptr);
+                   hipStream_t stream, bool src_peer = false, void *scratch = nullptr,
+                   IovPartState *defer = nullptr);
 
 }  // namespace gaamd

@@ -477,7 +477,7 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         char *up_dev = nullptr;   // the device view of the pinned upload buffer
         GA_HIP(hipHostGetDevicePointer((void **)&up_dev, up, 0));
         if (n <= (int)kIovPartMax && !src_peer && tuning().iov_lds) {
-            // up to 64 Ki pairs: ordered in LDS, the lists (and packed sources) read in
+            // up to 1 Mi pairs: ordered in LDS, the lists (and packed sources) read in
             // place from the pinned staging -- below 1 Ki pairs one launch of one
             // workgroup, from 1 Ki the keys and then one workgroup per hash partition
             IovDesc z = d;
@@ -485,8 +485,32 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
             if (d.src_list) z.src_list = (const uint64_t *)(up_dev + o_src);
             else if (!src_listed) z.src_base = up_dev + o_src;
             if (work < iov_lds_scratch_bytes((uint32_t)n)) fatal("io-vector scratch too small for the LDS path");
-            rc = launch_iov_lds(cop, scale, z, align_or, dlo, units, r.streams[si], false, dev + o_work);
+            // above kIovPartWindowMax pairs, partitions with more pairs than their bucket
+            // (heavy repeats) are deferred to the radix path, masked, once the stream is done
+            static uint32_t *s_flag_host = nullptr, *s_flag_dev = nullptr;
+            IovPartState ps;
+            const bool defer = n > (int)kIovPartWindowMax;
+            if (defer) {
+                if (!s_flag_host) {
+                    GA_HIP(hipHostMalloc((void **)&s_flag_host, 64, hipHostMallocMapped));
+                    GA_HIP(hipHostGetDevicePointer((void **)&s_flag_dev, s_flag_host, 0));
+                }
+                *(volatile uint32_t *)s_flag_host = 0;
+                ps.flag_dev = s_flag_dev;
+            }
+            rc = launch_iov_lds(cop, scale, z, align_or, dlo, units, r.streams[si], false, dev + o_work,
+                                defer ? &ps : nullptr);
             if (rc == 0) g_iov_path[3].fetch_add(1, std::memory_order_relaxed);
+            if (rc == 0 && defer) {
+                GA_HIP(hipStreamSynchronize(r.streams[si]));
+                if (*(volatile uint32_t *)s_flag_host) {
+                    // counted as "lds" and "radix" both
+                    if (up_hi > up_lo) upload_pinned(dev + up_lo, up + up_lo, up_hi - up_lo, r.streams[si]);
+                    g_iov_path[2].fetch_add(1, std::memory_order_relaxed);
+                    rc = launch_iov_runs(cop, scale, d, align_or, dlo, units, dev + o_work, work, r.streams[si],
+                                         false, nullptr, &ps);
+                }
+            }
         }
         if (rc == 1 && !src_listed && o_res > o_src)
             upload_pinned(dev + o_src, up + o_src, o_res - o_src, r.streams[si]);

@@ -316,11 +316,11 @@ static void progress_loop() {
                     // below 1 Ki pairs: ordered and applied by one workgroup, in LDS
                     rc = launch_iov_lds(q.op, q.scale, d, q.iov_align, q.dst_addr, units, r.streams[si]);
                 if (q.iov_serial == 2 && rc == 1) {
-                    // repeated destinations ordered on the GPU: up to kIovPartMax pairs by
-                    // hash partitions in LDS, above by the radix path; the progress thread's
+                    // repeated destinations ordered on the GPU: up to kIovPartWindowMax pairs
+                    // by hash partitions in LDS, above by the radix path; the progress thread's
                     // own scratch, free once its previous apply has finished (which also
                     // orders the partition counters, zero at rest, between its calls)
-                    const bool part = d.n <= kIovPartMax && tuning().iov_lds;
+                    const bool part = d.n <= kIovPartWindowMax && tuning().iov_lds;
                     const size_t need = std::max(iov_runs_work_bytes(d.n), part ? iov_lds_scratch_bytes(d.n) : 0);
                     if (prog_work_ev) GA_HIP(hipEventSynchronize(prog_work_ev));
                     if (need > prog_work_bytes) {

@@ -99,8 +99,9 @@ int gaamd_toggle_counts(unsigned long long counts[3]);
 /* Local io-vector launches whose destinations may repeat (>= 2048 pairs, or fewer
  * with a repeat), by path: [0] hashed (only pairs sharing a destination sorted, in
  * LDS), [1] hashed, then the radix path for the pairs it could not order (more than
- * 8192 such pairs), [2] the radix path (over 2^19 pairs), [3] one workgroup ordering
- * and applying everything in LDS (up to 16 Ki pairs, one launch). */
+ * 8192 such pairs), [2] the radix path (above the other paths' range, or for the
+ * partitions [3] deferred), [3] ordered in LDS: one workgroup below 1 Ki pairs, hash
+ * partitions up to 1 Mi pairs (tuning iov_lds=0 routes to [0]-[2] instead). */
 int gaamd_iov_path_counts(unsigned long long counts[4]);
 /* one-pass accumulates this rank applied into the segment of a rank on the same GPU */
 unsigned long long gaamd_one_pass_count(void);

@@ -733,29 +733,37 @@ def test_accv_large_repeated_destinations(gpu_lib, oracle, op, nbytes, slots, sh
 @pytest.mark.parametrize("op,nbytes,slots,n", [(C.DBL, 8, 150000, 600037), (C.FLT, 4, 900, 530001),
                                                (C.LNG, 8, 70000, 4 * 2 ** 18 + 5)])
 def test_accv_radix_path(gpu_lib, oracle, op, nbytes, slots, n):
-    """Above 2^19 pairs the hashed path is skipped: every destination is sorted on the
-    GPU by the library's own stable LSD radix sort (k_rs_*; 8-bit digits, 2 passes at
+    """Above 2^19 pairs the hashed path is skipped: with tuning iov_lds=0 (and by default
+    above 2^20 pairs, where the partitioned LDS path stops) every destination is sorted on
+    the GPU by the library's own stable LSD radix sort (k_rs_*; 8-bit digits, 2 passes at
     900 slots, 3 at 70 000 and 150 000; ragged last tile) and each destination's pairs
-    applied in input order -- bit-exact against the pairs applied one by one."""
+    applied in input order -- bit-exact against the pairs applied one by one; by default,
+    up to 2^20 pairs, the partitioned path gives the same bytes."""
     rng = np.random.default_rng(n)
     src = C.fill_bytes(op, n * nbytes, 11)
     dst = C.fill_bytes(op, slots * nbytes, 12)
     sb, db = ga_amd.DeviceBuffer(src.size), ga_amd.DeviceBuffer(dst.size)
     sb.upload(src)
-    db.upload(dst)
     so = np.arange(n, dtype=np.uint64) * nbytes
     do = rng.integers(0, slots, n).astype(np.uint64) * nbytes
     g = _giov_np(so + np.uint64(sb.ptr), do + np.uint64(db.ptr), nbytes)
     keep, sp = ga_amd.scale_buffer(op, C.SCALE[op])
-    paths0 = ga_amd.iov_path_counts()
-    assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
-    ga_amd.comex_fence_all()
-    paths1 = ga_amd.iov_path_counts()
-    assert paths1["radix"] == paths0["radix"] + 1, (paths0, paths1)
     want = dst.copy()
     _oracle_acc_pairs(oracle, op, C.SCALE[op], src, want, zip(so.tolist(), do.tolist()), nbytes)
-    got = db.download(np.uint8, dst.size)
-    assert same_bits_nan_aware(got, want, op)
+    for lds in (0, 1):
+        db.upload(dst)
+        old = ga_amd.set_tuning("iov_lds", lds)
+        try:
+            paths0 = ga_amd.iov_path_counts()
+            assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
+            ga_amd.comex_fence_all()
+            paths1 = ga_amd.iov_path_counts()
+        finally:
+            ga_amd.set_tuning("iov_lds", old)
+        key = "lds" if lds and n <= 1 << 20 else "radix"
+        assert paths1[key] == paths0[key] + 1, (lds, paths0, paths1)
+        got = db.download(np.uint8, dst.size)
+        assert same_bits_nan_aware(got, want, op), f"iov_lds={lds}"
 
 
 @pytest.mark.parametrize("n", [50, 20000, 200000])
@@ -943,3 +951,44 @@ def test_accv_one_workgroup_path(gpu_lib, oracle, op, nbytes, slots, n, src):
         assert same_bits_nan_aware(got, want, op), f"iov_lds={lds}"
         outs.append(got)
     assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("op,nbytes,slots,n,deferred", [
+    (C.DBL, 8, 200, 300000, True), (C.DBL, 8, 10 ** 7, 300000, False), (C.DCP, 16, 50, 150000, True),
+    (C.FLT, 4, 3000, 1 << 20, None), (C.INT, 12, 2, 70000, True)])
+def test_accv_partitions_large(gpu_lib, oracle, op, nbytes, slots, n, deferred):
+    """The partitioned path above kIovPartWindowMax (64 Ki) pairs: a partition holding more
+    pairs than its bucket (heavy repeats -- 200 destinations for 300 000 pairs) is left to
+    the radix path, masked, once the stream has completed (path counters "lds" and
+    "radix" both advance); random destinations never defer.  Bit-exact against the pairs
+    applied one by one in input order (comex.c:7342-7351)."""
+    rng = np.random.default_rng(n + slots)
+    srcb = C.fill_bytes(op, n * nbytes, 31)
+    dst = C.fill_bytes(op, slots * nbytes, 32) if slots <= 10 ** 6 else None
+    span = slots if dst is not None else n * 4
+    if dst is None:
+        dst = C.fill_bytes(op, span * nbytes, 32)
+    sb = ga_amd.DeviceBuffer(srcb.size)
+    sb.upload(srcb)
+    db = ga_amd.DeviceBuffer(dst.size)
+    db.upload(dst)
+    so = np.arange(n, dtype=np.uint64) * nbytes
+    do = rng.integers(0, span, n).astype(np.uint64) * nbytes
+    g = _giov_np(so + np.uint64(sb.ptr), do + np.uint64(db.ptr), nbytes)
+    keep, sp = ga_amd.scale_buffer(op, C.SCALE[op])
+    want = dst.copy()
+    _oracle_acc_pairs(oracle, op, C.SCALE[op], srcb, want, list(zip(so.tolist(), do.tolist())), nbytes)
+    p0 = ga_amd.iov_path_counts()
+    assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
+    ga_amd.comex_fence_all()
+    p1 = ga_amd.iov_path_counts()
+    assert p1["lds"] == p0["lds"] + 1, (p0, p1)
+    if deferred is not None:
+        assert p1["radix"] == p0["radix"] + int(deferred), (p0, p1)
+    assert same_bits_nan_aware(db.download(np.uint8, dst.size), want, op)
+    # the counters are zero again: a second call on the same destinations
+    want2 = want.copy()
+    _oracle_acc_pairs(oracle, op, C.SCALE[op], srcb, want2, list(zip(so.tolist(), do.tolist())), nbytes)
+    assert gpu_lib.comex_accv(op, sp, ctypes.byref(g), 1, 0, 0) == 0
+    ga_amd.comex_fence_all()
+    assert same_bits_nan_aware(db.download(np.uint8, dst.size), want2, op)
