@@ -512,13 +512,14 @@ __global__ __launch_bounds__(1024) void k_iov_lds(const IovDesc d, const OP op, 
 //                 (key, i) appended to its partition's bucket (an atomic on its counter:
 //                 an array per calling thread and device, zero at rest -- k_iov_part
 //                 zeroes its own after use, so no clearing launch)
-//   k_iov_part  : workgroup w reads its bucket into LDS, sorts it by (key, index) -- a
-//                 bitonic sort of about kIovPartMean entries -- and one lane per distinct
-//                 key applies its pairs in index order (iov_apply_chain), the
-//                 reference's (comex.c:7342-7351).  A bucket that overflowed (a skewed
-//                 scatter: thousands of pairs on a few destinations) is done in windows
-//                 of the input instead: the window's pairs of the partition gathered,
-//                 sorted and applied, window after window -- input order per key kept.
+//   k_iov_part  : workgroup w reads its bucket into LDS and applies it (iov_part_apply:
+//                 keys alone in the bucket at once, repeated keys sorted by (key, index)
+//                 and applied in index order, the reference's, comex.c:7342-7351).  A
+//                 bucket that overflowed (a skewed scatter: thousands of pairs on a few
+//                 destinations) is done in windows of the input instead -- the window's
+//                 pairs of the partition gathered and applied, window after window, so
+//                 input order per key is kept -- or, above kIovPartWindowMax pairs, left
+//                 to the caller's radix fallback (IovPartState).
 // A first version without buckets (each workgroup scanned every key for its own) grew
 // with n x G: 53 us at 64 Ki random pairs against 26 for the hashed path; one with a
 // memset clearing the counters before each call: 25 us at 4 Ki pairs, 39 at 64 Ki.
@@ -619,10 +620,11 @@ __global__ __launch_bounds__(1024) void k_iov_keyof(const uint64_t *dst_list, ui
 // applied at once, the repeated ones are sorted by (key, index) in `aux`, their
 // source-side products computed by all lanes, and one lane per distinct key adds them to
 // its destination in index order (a run of hundreds of pairs on one destination: one
-// lane's chain of source loads took ~90 us at 32 Ki pairs on 200 destinations).  (Sorting every entry instead -- a bitonic sort of about
-// kIovPartMean -- cost ~13 us a partition at 128 threads and ~21 at 64: latency of the
-// barrier stages, where a random scatter has no repeats to order.)  Every thread of the
-// workgroup calls it (barriers inside).
+// lane's chain of source loads took ~90 us at 32 Ki pairs on 200 destinations).
+// (Sorting every entry instead -- a bitonic sort of about kIovPartMean -- cost ~13 us a
+// partition at 128 threads and ~21 at 64: latency of the barrier stages, where a random
+// scatter has no repeats to order.)  Every thread of the workgroup calls it (barriers
+// inside).
 constexpr uint32_t kIovPartTabLog = 11;     // 2048 slots for at most kIovPartCap entries
 template <class OP, int W, bool SYS>
 __device__ __forceinline__ void iov_part_apply(const IovDesc &d, const OP &op, uint64_t dlo, const uint64_t *ent,
