@@ -45,12 +45,23 @@ __device__ __forceinline__ void iov_apply_chain(const IovDesc &d, const OP &op, 
         if constexpr (OP::kReadsDst) y = vload<W, false>(dp + (size_t)v * W);
         uint32_t j = 0;
         constexpr uint32_t B = 16, b = 4;
-        for (; j + B <= cnt; j += B) {
-            V x[B];
+        if (cnt >= B) {
+            // software-pipelined: the next batch's source addresses (the index loads) are
+            // in flight with this batch's source loads
+            const char *sp[B];
 #pragma unroll
-            for (uint32_t k = 0; k < B; ++k) x[k] = src_load<W, SYS>(src(j + k) + (size_t)v * W);
+            for (uint32_t k = 0; k < B; ++k) sp[k] = src(k);
+            for (; j + B <= cnt; j += B) {
+                V x[B];
 #pragma unroll
-            for (uint32_t k = 0; k < B; ++k) y = op.template apply<W>(y, x[k]);
+                for (uint32_t k = 0; k < B; ++k) x[k] = src_load<W, SYS>(sp[k] + (size_t)v * W);
+                if (j + 2 * B <= cnt) {
+#pragma unroll
+                    for (uint32_t k = 0; k < B; ++k) sp[k] = src(j + B + k);
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < B; ++k) y = op.template apply<W>(y, x[k]);
+            }
         }
         for (; j + b <= cnt; j += b) {
             V x[b];
@@ -140,8 +151,20 @@ __global__ __launch_bounds__(256) void k_iov_runs(const IovDesc d, const OP op) 
     if (j0 >= d.n) return;
     const uint32_t key = d.run_key[j0];
     if (key == kIovRunSkip || (j0 > 0 && d.run_key[j0 - 1] == key)) return;
-    uint32_t cnt = 1;
-    while (j0 + cnt < d.n && d.run_key[j0 + cnt] == key) ++cnt;
+    // the run's end: galloping, then a binary search (keys are sorted) -- a long run
+    // (thousands of pairs on one destination) no longer walks its keys one by one
+    uint32_t lo = j0 + 1, hi = j0 + 1, step = 1;   // run_key[lo - 1] == key
+    while (hi < d.n && d.run_key[hi] == key) {
+        lo = hi + 1;
+        hi = (d.n - hi > step) ? hi + step : d.n;
+        step <<= 1;
+    }
+    while (lo < hi) {                                // first position past the run in [lo, hi]
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if (d.run_key[mid] == key) lo = mid + 1;
+        else hi = mid;
+    }
+    const uint32_t cnt = lo - j0;
     const uint32_t *perm = d.run_perm + j0;
     iov_apply_chain<OP, W, SYS>(d, op, (char *)d.dst_list[perm[0]], cnt, [&](uint32_t j) { return perm[j]; });
 }
