@@ -725,7 +725,14 @@ __device__ __forceinline__ void iov_part_apply(const IovDesc &d, const OP &op, u
                 char *dp = (char *)(dlo + (uint64_t)key * (uint64_t)d.bytes) + (size_t)v * W;
                 typename Vec<W>::T y{};
                 if constexpr (OP::kReadsDst) y = vload<W, false>(dp);
-                for (uint32_t j = u; j < mr && (uint32_t)(aux[j] >> 32) == key; ++j) y = op.template add<W>(y, pv[j]);
+                uint32_t lo = u + 1, hi = mr;                 // the run's end (aux is sorted)
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if ((uint32_t)(aux[mid] >> 32) == key) lo = mid + 1;
+                    else hi = mid;
+                }
+#pragma unroll 8
+                for (uint32_t j = u; j < lo; ++j) y = op.template add<W>(y, pv[j]);
                 vstore<W, false>(dp, y);
             }
             __syncthreads();
