@@ -126,7 +126,8 @@ int gaamd_peers_unmapped(void);
 int gaamd_owner_counts(unsigned long long counts[4]);
 /* keys: "kind" (0 auto, 1 rows, 2 flat, 3 serial, 4 ordered), "block" (0 auto/64/128),
  * "flat_max_nvec", "align", "flat_line_min", "ordered_cols" (column-sliced ordered
- * kernel), "streams"; returns the previous value or -1 */
+ * kernel), "streams", "iov_lds" (1: io-vectors with repeated destinations ordered in
+ * LDS up to 1 Mi pairs; 0: the hashed / radix paths); returns the previous value or -1 */
 int gaamd_set_tuning(const char *key, int value);
 int gaamd_get_tuning(const char *key);
 
