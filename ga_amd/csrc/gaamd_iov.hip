@@ -379,7 +379,7 @@ __device__ __forceinline__ uint32_t iov_lds_step(uint32_t key) {
     return ((key * 0x85EBCA6Bu) >> (32 - kIovLdsLog)) | 1u;
 }
 
-// the LDS table of k_iov_lds / k_iov_order: keys[0..n) in LDS -> rep (bit i: pair i's
+// the LDS table of k_iov_lds: keys[0..n) in LDS -> rep (bit i: pair i's
 // destination has more than one pair).  Insert: the lane whose compare-and-swap claims
 // an empty slot is its key's first pair; a lane that finds its key in a slot marks that
 // slot repeated.  Then every pair looks its key up again and copies the mark.  (Every

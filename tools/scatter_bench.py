@@ -41,7 +41,7 @@ def main():
                     help="interleaved A/B of the one-workgroup LDS path (tuning iov_lds=1) against the hashed "
                          "three-launch path (iov_lds=0): 5 alternations of --steps calls each")
     ap.add_argument("--ab-key", default="iov_lds",
-                    help="the tuning key --ab alternates between 1 and 0 (iov_lds, iov_flag)")
+                    help="the tuning key --ab alternates between 1 and 0 (iov_lds; iov_flag was a round-6 experiment, since removed)")
     ap.add_argument("--nb", action="store_true",
                     help="also time --steps non-blocking calls back to back (comex_nbaccv, one wait at the end)")
     ap.add_argument("--ga", action="store_true",
