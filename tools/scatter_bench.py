@@ -38,8 +38,9 @@ def main():
     ap.add_argument("--slots", type=int, default=0,
                     help="destinations drawn from this many f64 slots (repeats) instead of the whole 1 GiB")
     ap.add_argument("--ab", action="store_true",
-                    help="interleaved A/B of the one-workgroup LDS path (tuning iov_lds=1) against the hashed "
-                         "three-launch path (iov_lds=0): 5 alternations of --steps calls each")
+                    help="interleaved A/B of the LDS ordering paths (tuning iov_lds=1: one workgroup below 1 Ki "
+                         "pairs, hash partitions up to 1 Mi) against the hashed / radix paths (iov_lds=0): "
+                         "5 alternations of --steps calls each")
     ap.add_argument("--ab-key", default="iov_lds",
                     help="the tuning key --ab alternates between 1 and 0 (iov_lds; iov_flag was a round-6 experiment, since removed)")
     ap.add_argument("--nb", action="store_true",
@@ -102,8 +103,9 @@ def main():
                     old = ga_amd.set_tuning(args.ab_key, val)
                     runs[val].append(timed())
                     ga_amd.set_tuning(args.ab_key, old)
-            names = {"iov_lds": ("lds_one_launch", "hashed_three_launches"),
-                     "iov_flag": ("flag_wait", "stream_sync")}.get(args.ab_key, ("on", "off"))
+            # (files written before the partitioned path named these "lds_one_launch" /
+            # "hashed_three_launches")
+            names = {"iov_lds": ("lds_paths", "hashed_radix_paths")}.get(args.ab_key, ("on", "off"))
             line["ab_key"] = args.ab_key
             line["ab_ms_per_call"] = {names[0]: [round(x * 1e3, 4) for x in runs[1]],
                                       names[1]: [round(x * 1e3, 4) for x in runs[0]]}
