@@ -477,9 +477,10 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         char *up_dev = nullptr;   // the device view of the pinned upload buffer
         GA_HIP(hipHostGetDevicePointer((void **)&up_dev, up, 0));
         if (n <= (int)kIovPartMax && !src_peer && tuning().iov_lds) {
-            // up to 1 Mi pairs: ordered in LDS, the lists (and packed sources) read in
-            // place from the pinned staging -- below 1 Ki pairs one launch of one
-            // workgroup, from 1 Ki the keys and then one workgroup per hash partition
+            // up to 1 Mi pairs: ordered in LDS, the destination list read in place from
+            // the pinned staging -- below 1 Ki pairs one launch of one workgroup (which
+            // reads the sources there too), from 1 Ki the keys and then one workgroup per
+            // hash partition
             IovDesc z = d;
             z.dst_list = (const uint64_t *)(up_dev + o_dst);
             // the partitioned path reads sources in destination-hash order, not pair order:
