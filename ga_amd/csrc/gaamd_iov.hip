@@ -568,8 +568,9 @@ IovPartCounts::~IovPartCounts() {
     for (int i = 0; i < 64; ++i)
         if (dev[i]) g_part_pool[i].push_back(dev[i]);
 }
+static thread_local IovPartCounts t_part_counts;
 static uint32_t *iov_part_counts() {
-    static thread_local IovPartCounts mine;
+    IovPartCounts &mine = t_part_counts;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
     if (mine.dev[dev]) return mine.dev[dev];
@@ -584,6 +585,18 @@ static uint32_t *iov_part_counts() {
     if (hipMemset(p, 0, kIovPartGMax * 4) != hipSuccess) return nullptr;
     mine.dev[dev] = p;
     return p;
+}
+
+// comex_finalize (streams idle): the pool's arrays and the calling thread's are freed;
+// arrays of other threads still running go back to the pool when those end
+void iov_part_release() {
+    std::lock_guard<std::mutex> g(g_part_mu);
+    for (int i = 0; i < 64; ++i) {
+        for (uint32_t *p : g_part_pool[i]) (void)hipFree(p);
+        g_part_pool[i].clear();
+        if (t_part_counts.dev[i]) (void)hipFree(t_part_counts.dev[i]);
+        t_part_counts.dev[i] = nullptr;
+    }
 }
 
 __device__ __forceinline__ uint32_t iov_part_of(uint32_t key, uint32_t lg) {

@@ -209,6 +209,7 @@ struct IovPartState {
     uint32_t lg = 0;                // out: log2 of its partitions
 };
 constexpr uint32_t kIovPartWindowMax = 1u << 16;
+void iov_part_release();   // comex_finalize: the partition counters (streams idle)
 constexpr uint32_t kIovLdsMax = 16384;
 constexpr uint32_t kIovLdsRoute = 1024;
 constexpr uint32_t kIovPartMax = 1u << 20;

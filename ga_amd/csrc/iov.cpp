@@ -30,6 +30,8 @@ static size_t g_iov_scratch_bytes = 0;
 std::atomic<unsigned long long> g_iov_path[4];
 
 static char *g_iov_host = nullptr;
+// the partitioned path's overflow flag (mapped pinned; deferred partitions, launch_mu held)
+static uint32_t *g_part_flag_host = nullptr, *g_part_flag_dev = nullptr;
 static size_t g_iov_host_bytes = 0;
 
 // COMEX_AMD_DEBUG >= 3: the host phases of each io-vector call on stderr (time since
@@ -497,23 +499,22 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
             if (work < iov_lds_scratch_bytes((uint32_t)n)) fatal("io-vector scratch too small for the LDS path");
             // above kIovPartWindowMax pairs, partitions with more pairs than their bucket
             // (heavy repeats) are deferred to the radix path, masked, once the stream is done
-            static uint32_t *s_flag_host = nullptr, *s_flag_dev = nullptr;
             IovPartState ps;
             const bool defer = n > (int)kIovPartWindowMax;
             if (defer) {
-                if (!s_flag_host) {
-                    GA_HIP(hipHostMalloc((void **)&s_flag_host, 64, hipHostMallocMapped));
-                    GA_HIP(hipHostGetDevicePointer((void **)&s_flag_dev, s_flag_host, 0));
+                if (!g_part_flag_host) {
+                    GA_HIP(hipHostMalloc((void **)&g_part_flag_host, 64, hipHostMallocMapped));
+                    GA_HIP(hipHostGetDevicePointer((void **)&g_part_flag_dev, g_part_flag_host, 0));
                 }
-                *(volatile uint32_t *)s_flag_host = 0;
-                ps.flag_dev = s_flag_dev;
+                *(volatile uint32_t *)g_part_flag_host = 0;
+                ps.flag_dev = g_part_flag_dev;
             }
             rc = launch_iov_lds(cop, scale, z, align_or, dlo, units, r.streams[si], false, dev + o_work,
                                 defer ? &ps : nullptr);
             if (rc == 0) g_iov_path[3].fetch_add(1, std::memory_order_relaxed);
             if (rc == 0 && defer) {
                 GA_HIP(hipStreamSynchronize(r.streams[si]));
-                if (*(volatile uint32_t *)s_flag_host) {
+                if (*(volatile uint32_t *)g_part_flag_host) {
                     // counted as "lds" and "radix" both
                     if (up_hi > up_lo) upload_pinned(dev + up_lo, up + up_lo, up_hi - up_lo, r.streams[si]);
                     g_iov_path[2].fetch_add(1, std::memory_order_relaxed);
@@ -874,6 +875,9 @@ void iov_finalize() {
     if (g_riov_pin) (void)hipHostFree(g_riov_pin);
     g_riov_pin = nullptr;
     g_riov_pin_bytes = 0;
+    if (g_part_flag_host) (void)hipHostFree(g_part_flag_host);
+    g_part_flag_host = g_part_flag_dev = nullptr;
+    iov_part_release();
 }
 
 }  // namespace gaamd
