@@ -42,10 +42,16 @@ RECIPES = {
     "putget": [(f"{x}_H", 200, f"python3 bench.py --xfer {x} --steps 50 --warmup 5 --no-cpu --no-host", "json")
                for x in ("put", "get")],
     "evidence": [("evidence", 900, "bash tools/evidence.sh r06", "log")],
-    "iov": [("iov_tests", 300, PYTEST.format(t=120) + " -m gpu tests/test_gpu_parity.py -k 'one_workgroup or accv "
+    "iov": [("iov_tests", 300, PYTEST.format(t=120) + " -m gpu tests/test_gpu_parity.py -k 'one_workgroup or partitions_large or accv "
                                                      "or getv or putv'", "log"),
             ("scatter_ab", 240, "python3 tools/scatter_bench.py --pairs 512,1024,2048,4096,8192,16384,32768,65536 "
                                 "--steps 50 --ab --nb", "jsonl")],
+    "iov_probe": [("probe_random", 300, "./tools/iov_lds_probe", "jsonl"),
+                  ("probe_200slots", 300, "./tools/iov_lds_probe 200", "jsonl")],
+    "iov_pmc": [("pmc_iov_1Mi", 300, "python3 tools/pmc_iov.py --pairs 1048576 --outdir gpurun_out/{tag}/pmc1mi",
+                 "json"),
+                ("pmc_iov_64Ki", 300, "python3 tools/pmc_iov.py --pairs 65536 --outdir gpurun_out/{tag}/pmc64ki",
+                 "json")],
     "iov_trace": [("iov_trace", 200, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/{tag}/iovprof "
                                      "-o iov -- python3 tools/scatter_bench.py --pairs 16384 --no-cpu --steps 200",
                    "jsonl")],
