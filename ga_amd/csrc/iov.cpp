@@ -13,6 +13,9 @@
 #include <string.h>
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -178,18 +181,70 @@ struct ViewCache {
 
 // Host passes over io-vector lists (tens of MiB at GA scatter sizes) split into
 // contiguous ranges over a few threads: fn(t, i0, i1) for t < T, T = one thread
-// per 256 Ki pairs, at most 8.  Each range's results are combined by the caller
+// per 64 Ki pairs, at most 8 (one per 256 Ki before the pool: interleaved A/B, whole
+// calls 256 Ki 0.148 -> 0.110 ms, 1 Mi 0.332 -> 0.30, from host memory 256 Ki 0.418 ->
+// 0.284, profiles/r06/host_pool/).  Each range's results are combined by the caller
 // in range order, so the outcome does not depend on T.
-static int par_threads(long n) {   // one per 256 Ki pairs, at most 8 (the former COMEX_AMD_HOST_THREADS)
-    return (int)std::max(1L, std::min(8L, n >> 18));
+static int par_threads(long n) {   // one per 64 Ki pairs, at most 8 (the former COMEX_AMD_HOST_THREADS)
+    return (int)std::max(1L, std::min(8L, n >> 16));
 }
+// The ranges run on a few persistent workers (started on first use, blocked on a
+// condition variable between calls) and the caller: creating T - 1 threads per pass
+// cost more than the pass itself at 256 Ki-1 Mi pairs.  One job at a time (run_mu);
+// the workers are never joined (they stay blocked at process exit).
+class HostPool {
+  public:
+    static HostPool &get() {
+        static HostPool *p = new HostPool();   // never destroyed: no join at exit
+        return *p;
+    }
+    void run(int T, const std::function<void(int)> &fn) {   // fn(t) for t < T; t = 0 here
+        std::lock_guard<std::mutex> one(run_mu_);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            while ((int)workers_.size() < T - 1) {
+                const int id = (int)workers_.size() + 1;
+                workers_.emplace_back([this, id] { loop(id); });
+            }
+            job_ = &fn;
+            njobs_ = T;
+            pending_ = T - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [this] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void loop(int id) {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            cv_.wait(g, [&] { return gen_ != seen; });
+            seen = gen_;
+            if (id >= njobs_) continue;
+            const std::function<void(int)> *f = job_;
+            g.unlock();
+            (*f)(id);
+            g.lock();
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> workers_;
+    const std::function<void(int)> *job_ = nullptr;
+    int njobs_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+};
+
 template <class F> static void par_for(long n, int T, F fn) {
     if (T <= 1) { fn(0, 0L, n); return; }
-    std::vector<std::thread> th;
-    th.reserve((size_t)T - 1);
-    for (int t = 1; t < T; ++t) th.emplace_back([&, t] { fn(t, n * t / T, n * (t + 1) / T); });
-    fn(0, 0L, n / T);
-    for (std::thread &x : th) x.join();
+    const std::function<void(int)> job = [&](int t) { fn(t, n * t / T, n * (t + 1) / T); };
+    HostPool::get().run(T, job);
 }
 
 // Is every byte of [lo, hi) ordinary CPU memory of this process (readable, and if
