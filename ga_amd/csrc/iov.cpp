@@ -47,12 +47,21 @@ static void phase(const char *what) {
     last = t;
 }
 
+static char *g_iov_host_dev = nullptr;   // its device view (looked up once per allocation)
 static char *iov_host_scratch(size_t bytes) {   // pinned upload staging; caller holds launch_mu
     if (bytes <= g_iov_host_bytes) return g_iov_host;
     if (g_iov_host) GA_HIP(hipHostFree(g_iov_host));
     g_iov_host_bytes = std::max<size_t>(bytes, 1 << 20);
     GA_HIP(hipHostMalloc((void **)&g_iov_host, g_iov_host_bytes, hipHostMallocMapped));
+    GA_HIP(hipHostGetDevicePointer((void **)&g_iov_host_dev, g_iov_host, 0));
     return g_iov_host;
+}
+// the device view of a pinned pointer: inside the upload staging without a runtime call
+static char *pinned_dev(const char *p) {
+    if (g_iov_host && p >= g_iov_host && p < g_iov_host + g_iov_host_bytes) return g_iov_host_dev + (p - g_iov_host);
+    void *dev = nullptr;
+    GA_HIP(hipHostGetDevicePointer(&dev, (void *)p, 0));
+    return (char *)dev;
 }
 
 static char *g_riov_pin = nullptr;   // remote io-vector request upload (pinned)
@@ -68,8 +77,7 @@ static char *remote_iov_pinned(size_t bytes) {   // caller holds launch_mu; no u
 // copy `bytes` of the pinned (device-mapped) upload buffer into staging with the
 // copy kernel on `st` (one launch, no runtime staging of the host bytes)
 static void upload_pinned(char *stage, const char *pin, size_t bytes, hipStream_t st) {
-    void *dev = nullptr;
-    GA_HIP(hipHostGetDevicePointer(&dev, (void *)pin, 0));
+    const char *dev = pinned_dev(pin);
     int count[1] = {(int)bytes};
     const int rc = launch_strided(kOpCopy, nullptr, (const char *)dev, nullptr, stage, nullptr, count, 0, st, nullptr);
     if (rc) fatal("io-vector upload failed (%d)", rc);
@@ -515,7 +523,7 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     const bool zero_copy = !runs && !serial && up_hi - up_lo <= kIovZeroCopyMax && bytes <= 32;
     if (zero_copy) {
         char *up_dev = nullptr;
-        GA_HIP(hipHostGetDevicePointer((void **)&up_dev, up, 0));
+        up_dev = pinned_dev(up);
         if (d.src_list) d.src_list = (const uint64_t *)(up_dev + o_src);
         else if (!src_listed) d.src_base = up_dev + o_src;
         if (d.dst_list) d.dst_list = (const uint64_t *)(up_dev + o_dst);
@@ -532,7 +540,7 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         static IovHash *g_hash = nullptr;
         rc = 1;
         char *up_dev = nullptr;   // the device view of the pinned upload buffer
-        GA_HIP(hipHostGetDevicePointer((void **)&up_dev, up, 0));
+        up_dev = pinned_dev(up);
         if (n <= (int)kIovPartMax && !src_peer && tuning().iov_lds) {
             // up to 1 Mi pairs: ordered in LDS, the destination list read in place from
             // the pinned staging -- below 1 Ki pairs one launch of one workgroup (which
@@ -925,7 +933,7 @@ void iov_finalize() {
     g_iov_scratch = nullptr;
     g_iov_scratch_bytes = 0;
     if (g_iov_host) (void)hipHostFree(g_iov_host);
-    g_iov_host = nullptr;
+    g_iov_host = g_iov_host_dev = nullptr;
     g_iov_host_bytes = 0;
     if (g_riov_pin) (void)hipHostFree(g_riov_pin);
     g_riov_pin = nullptr;
