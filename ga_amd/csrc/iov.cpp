@@ -371,8 +371,8 @@ constexpr int kIovMapsMin = 65536;
 // One descriptor on this GPU.  `src` lists device addresses, or is empty when
 // `host_src` holds the n source runs packed on the host (gathered from pageable
 // memory by the caller); `dst` lists device addresses, or is empty when the
-// results go packed to `host_dst` (getv into pageable memory: the caller
-// scatters them).  Reference: nb_accv / nb_putv / nb_getv to a self/SMP target,
+// results go to the pageable addresses `host_dst` (getv into host memory: copied down
+// packed into the pinned staging, then scattered from there on the host).  Reference: nb_accv / nb_putv / nb_getv to a self/SMP target,
 // comex.c:7327-7400 (one _acc / memcpy per pair, in order).
 // `bounds` (the fast path of xfer_vec): {src lo, src hi, dst lo, dst hi} of the
 // allocations the first pair's addresses lie in, with sdelta / ddelta their device-view
@@ -380,7 +380,7 @@ constexpr int kIovMapsMin = 65536;
 // anything is uploaded or launched (the caller classifies per address instead).
 // `src_peer`: the listed sources lie in another GPU's memory (getv): system-scope loads.
 static bool iov_local(int cop, const void *scale, const uint64_t *src, const uint64_t *dst, int bytes, int n,
-                      const char *host_src = nullptr, char *host_dst = nullptr, int64_t sdelta = 0,
+                      const char *host_src = nullptr, void *const *host_dst = nullptr, int64_t sdelta = 0,
                       int64_t ddelta = 0, void *const *gather_src = nullptr, const uint64_t *bounds = nullptr,
                       bool src_peer = false) {
     Runtime &r = rt();
@@ -393,7 +393,8 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     const size_t o_res = o_src + (src_listed ? nb : pk);
     std::unique_lock<std::mutex> g(r.launch_mu);
     sched_sync_all();   // the previous io-vector kernel and its upload are done with both scratches
-    char *up = iov_host_scratch(o_res);
+    const size_t o_down = (o_res + 255) & ~(size_t)255;   // packed results coming down (host_dst)
+    char *up = iov_host_scratch(dst_listed ? o_res : o_down + pk);
     phase("drain");
     uint64_t align_or = 0, slo = ~0ull, shi = 0, dlo = ~0ull, dhi = 0, dxor = 0;
     // translate a list into the staging, taking its OR / min / max and the OR of every
@@ -424,9 +425,12 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         shi += (uint64_t)bytes;
     } else if (gather_src) {
         // pageable sources gathered straight into the pinned staging, in pair order, on
-        // one thread: split over 8 threads it measured no faster on the boxes' shared
-        // host cores (profiles/r01/iov_host_threads.jsonl)
-        gather_runs(up + o_src, gather_src, n, bytes);
+        // the pool (one thread: host-sourced 1 Mi pairs 0.87-0.94 ms against 0.59-0.71,
+        // interleaved A/B, profiles/r06/host_pool/; round 1 had measured threads created
+        // per call no faster)
+        par_for(n, par_threads(n), [&](int, long i0, long i1) {
+            gather_runs(up + o_src + i0 * (long)bytes, gather_src + i0, (int)(i1 - i0), bytes);
+        });
     } else {
         memcpy(up + o_src, host_src, (size_t)n * (size_t)bytes);
     }
@@ -617,8 +621,12 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
     if (!dst_listed) {
         GA_HIP(hipStreamSynchronize(r.streams[si]));
         phase("kernels");
-        GA_HIP(hipMemcpy(host_dst, dev + o_res, (size_t)n * (size_t)bytes, hipMemcpyDeviceToHost));
+        GA_HIP(hipMemcpy(up + o_down, dev + o_res, (size_t)n * (size_t)bytes, hipMemcpyDeviceToHost));
         phase("results down");
+        par_for(n, par_threads(n), [&](int, long i0, long i1) {
+            scatter_runs(host_dst + i0, up + o_down + i0 * (long)bytes, (int)(i1 - i0), bytes);
+        });
+        phase("host scatter");
     }
     // completion (blocking call) or the handle (non-blocking) is taken by xfer_vec
     return true;
@@ -744,11 +752,7 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
             if (n >= kIovMapsMin && sdev && !ddev && cop == kOpCopy &&
                 host_cpu_range(dmin, dmax + (uint64_t)bytes, true)) {
                 phase("host side");
-                static std::vector<char> g_hpack;
-                if (g_hpack.size() < (size_t)n * (size_t)bytes) g_hpack.resize((size_t)n * (size_t)bytes);
-                iov_local(cop, scale, rs, nullptr, bytes, n, nullptr, g_hpack.data(), sdel, 0);
-                scatter_runs(darr[k].dst, g_hpack.data(), n, bytes);
-                phase("host scatter");
+                iov_local(cop, scale, rs, nullptr, bytes, n, nullptr, darr[k].dst, sdel, 0);
                 continue;
             }
         }
@@ -809,11 +813,8 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
             if (src_host) {   // gathered straight into the pinned upload staging
                 iov_local(cop, scale, nullptr, dv, bytes, n, nullptr, nullptr, 0, 0, darr[k].src);
             } else {
-                static std::vector<char> g_packed;   // kept across calls (no page faults per call)
-                if (g_packed.size() < (size_t)n * (size_t)bytes) g_packed.resize((size_t)n * (size_t)bytes);
-                iov_local(cop, scale, sv, nullptr, bytes, n, nullptr, g_packed.data(), 0, 0, nullptr, nullptr,
+                iov_local(cop, scale, sv, nullptr, bytes, n, nullptr, darr[k].dst, 0, 0, nullptr, nullptr,
                           getv_peer);
-                scatter_runs(darr[k].dst, g_packed.data(), n, bytes);
             }
             continue;
         }

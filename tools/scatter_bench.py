@@ -164,14 +164,27 @@ def ga_main(L, args):
                          ("NGA_Gather_flat", lambda: L.NGA_Gather_flat(g, ctypes.c_void_p(out.ctypes.data), sp, n))):
             fn()
             ga_amd.sync()
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                fn()
-            ga_amd.sync()
-            el = (time.perf_counter() - t0) / args.steps
-            print(json.dumps({"tool": "scatter_bench", "api": name, "elements": n, "ga": f"{side}^2 f64, 1 rank",
-                              "steps": args.steps, "ms_per_call": round(el * 1e3, 3),
-                              "Melems_per_s": round(n / el / 1e6, 2)}), flush=True)
+
+            def timed():
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    fn()
+                ga_amd.sync()
+                return (time.perf_counter() - t0) / args.steps
+            el = timed()
+            line = {"tool": "scatter_bench", "api": name, "elements": n, "ga": f"{side}^2 f64, 1 rank",
+                    "steps": args.steps, "ms_per_call": round(el * 1e3, 3), "Melems_per_s": round(n / el / 1e6, 2)}
+            if args.ab:   # interleaved: --ab-key at 1, then 0, five times
+                runs = {1: [], 0: []}
+                for _ in range(5):
+                    for val in (1, 0):
+                        old = ga_amd.set_tuning(args.ab_key, val)
+                        runs[val].append(timed())
+                        ga_amd.set_tuning(args.ab_key, old)
+                line["ab_key"] = args.ab_key
+                line["ab_ms_per_call"] = {"on": [round(x * 1e3, 3) for x in runs[1]],
+                                          "off": [round(x * 1e3, 3) for x in runs[0]]}
+            print(json.dumps(line), flush=True)
     L.GA_Terminate()
 
 
