@@ -274,6 +274,8 @@ SIGNATURES = {
     "gaamd_route_counts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     "gaamd_toggle_counts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     "gaamd_iov_path_counts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
+    "gaamd_host_parallel": (ctypes.c_int, [ctypes.c_int, ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_void_p),
+                                           ctypes.c_void_p]),
     "gaamd_one_pass_count": (ctypes.c_ulonglong, []),
     "gaamd_segment_cache_reuse": (ctypes.c_ulonglong, []),
     "gaamd_segment_remaps": (ctypes.c_ulonglong, []),

@@ -1215,7 +1215,7 @@ int gaamd_diag(const char *key, long long value, unsigned long long *out, int no
     return -1;
 }
 
-int gaamd_iov_path_counts(unsigned long long counts[3]) {
+int gaamd_iov_path_counts(unsigned long long counts[4]) {
     for (int k = 0; k < 4; ++k) counts[k] = g_iov_path[k].load(std::memory_order_relaxed);
     return 0;
 }

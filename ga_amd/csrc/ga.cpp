@@ -549,13 +549,11 @@ static void gatscat(GatScat op, int g_a, void *v, int *const *csubs, const int *
             rem[j] = (char *)a.ptr[pr] + (long)size * o;
         }
     };
-    auto run = [&](const std::function<void(int)> &fn) {
+    auto run = [&](const std::function<void(int)> &fn) {   // on libga_amd's host worker pool
         if (T == 1) { fn(0); return; }
-        std::vector<std::thread> th;
-        th.reserve(T - 1);
-        for (int t = 1; t < T; t++) th.emplace_back(fn, t);
-        fn(0);
-        for (std::thread &x : th) x.join();
+        if (gaamd_host_parallel(T, [](int t, void *f) { (*(const std::function<void(int)> *)f)(t); },
+                                (void *)&fn))
+            fatal("gather/scatter: host pool refused %d threads", T);
     };
     run(locate);
     std::vector<long> nelem(P, 0), first(P, 0);

@@ -249,6 +249,22 @@ class HostPool {
     uint64_t gen_ = 0;
 };
 
+}  // namespace gaamd
+
+// the pool for callers above the C ABI (the GA layer's gatscat passes)
+extern "C" int gaamd_host_parallel(int T, void (*fn)(int t, void *ctx), void *ctx) {
+    if (T < 1 || T > 16 || !fn) return -1;
+    if (T == 1) {
+        fn(0, ctx);
+        return 0;
+    }
+    const std::function<void(int)> job = [&](int t) { fn(t, ctx); };
+    gaamd::HostPool::get().run(T, job);
+    return 0;
+}
+
+namespace gaamd {
+
 template <class F> static void par_for(long n, int T, F fn) {
     if (T <= 1) { fn(0, 0L, n); return; }
     const std::function<void(int)> job = [&](int t) { fn(t, n * t / T, n * (t + 1) / T); };

@@ -103,6 +103,10 @@ int gaamd_toggle_counts(unsigned long long counts[3]);
  * partitions [3] deferred), [3] ordered in LDS: one workgroup below 1 Ki pairs, hash
  * partitions up to 1 Mi pairs (tuning iov_lds=0 routes to [0]-[2] instead). */
 int gaamd_iov_path_counts(unsigned long long counts[4]);
+/* runs fn(t, ctx) for t = 0 .. T-1 (1 <= T <= 16) on the library's persistent host worker
+ * pool, t = 0 on the calling thread, and returns when all have; -1 on bad arguments.
+ * One job at a time (concurrent callers wait); fn must not call back into this function. */
+int gaamd_host_parallel(int T, void (*fn)(int t, void *ctx), void *ctx);
 /* one-pass accumulates this rank applied into the segment of a rank on the same GPU */
 unsigned long long gaamd_one_pass_count(void);
 /* comex_malloc calls served by a freed segment block kept for reuse (with its IPC export) */
