@@ -894,8 +894,12 @@ int xfer_vec(Xfer kind, int op, void *scale, comex_giov_t *darr, int len, int pr
                 char *pin = remote_iov_pinned((size_t)len_b);
                 memcpy(pin + loff, dv + i0, (size_t)m * 8);
                 if (src_host) {
-                    // pageable sources (GA's MA buffer): gathered on the host, one upload
-                    gather_runs(pin, darr[k].src + i0, m, bytes);
+                    // pageable sources (GA's MA buffer): gathered on the host (on the pool),
+                    // one upload
+                    void *const *sp = darr[k].src + i0;
+                    par_for(m, par_threads(m), [&](int, long j0, long j1) {
+                        gather_runs(pin + j0 * (long)bytes, sp + j0, (int)(j1 - j0), bytes);
+                    });
                     sched_join();
                     upload_pinned(stage, pin, (size_t)len_b, r.streams[0]);
                 } else {
