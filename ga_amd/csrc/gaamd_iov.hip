@@ -599,6 +599,14 @@ void iov_part_release() {
     }
 }
 
+// log2 of the partitions for n pairs: about kIovPartMean pairs each, at most kIovPartGMax
+// partitions (above 1 Mi pairs the partitions grow instead: 512 pairs each at 4 Mi)
+static uint32_t iov_part_lg(uint32_t n) {
+    uint32_t lg = 0;
+    while ((n >> lg) > kIovPartMean && (1u << lg) < kIovPartGMax) ++lg;
+    return lg;
+}
+
 __device__ __forceinline__ uint32_t iov_part_of(uint32_t key, uint32_t lg) {
     return lg ? (key * 0x9E3779B1u) >> (32 - lg) : 0u;
 }
@@ -1038,8 +1046,7 @@ static int radix_sort_pairs(uint32_t *const k[2], uint32_t *const v[2], uint32_t
 }
 
 size_t iov_lds_scratch_bytes(uint32_t n) {
-    uint32_t lg = 0;
-    while ((n >> lg) > kIovPartMean) ++lg;
+    const uint32_t lg = iov_part_lg(n);
     return (((size_t)n * 4 + 255) & ~(size_t)255) + ((size_t)kIovPartCap * 8 << lg);
 }
 
@@ -1209,8 +1216,7 @@ int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint
     uint32_t *keys = nullptr, *counts = nullptr;
     if (scratch && d.n >= kIovLdsRoute) {
         if (d.n > kIovPartMax) return 1;
-        while ((d.n >> lg) > kIovPartMean) ++lg;
-        if ((1u << lg) > kIovPartGMax) return -6;
+        lg = iov_part_lg(d.n);
         counts = iov_part_counts();
         if (!counts) return -7;
         keys = (uint32_t *)scratch;

@@ -212,7 +212,7 @@ constexpr uint32_t kIovPartWindowMax = 1u << 16;
 void iov_part_release();   // comex_finalize: the partition counters (streams idle)
 constexpr uint32_t kIovLdsMax = 16384;
 constexpr uint32_t kIovLdsRoute = 1024;
-constexpr uint32_t kIovPartMax = 1u << 20;
+constexpr uint32_t kIovPartMax = 1u << 22;
 size_t iov_lds_scratch_bytes(uint32_t n);   // keys and partition buckets (~68 B a pair)
 int launch_iov_lds(int op, const void *scale, IovDesc d, uint64_t align_or, uint64_t dlo, uint64_t units,
                    hipStream_t stream, bool src_peer = false, void *scratch = nullptr,

@@ -562,7 +562,7 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
         char *up_dev = nullptr;   // the device view of the pinned upload buffer
         up_dev = pinned_dev(up);
         if (n <= (int)kIovPartMax && !src_peer && tuning().iov_lds) {
-            // up to 1 Mi pairs: ordered in LDS, the destination list read in place from
+            // up to 4 Mi pairs: ordered in LDS, the destination list read in place from
             // the pinned staging -- below 1 Ki pairs one launch of one workgroup (which
             // reads the sources there too), from 1 Ki the keys and then one workgroup per
             // hash partition
@@ -571,7 +571,10 @@ static bool iov_local(int cop, const void *scale, const uint64_t *src, const uin
             // the partitioned path reads sources in destination-hash order, not pair order:
             // a source list or gathered sources go up to HBM first (the copy kernel reads
             // the pinned staging in order) -- read across PCIe in that order, 1 Mi pairs
-            // from pageable host memory took 4.2 ms against 1.5 ms uploaded
+            // from pageable host memory took 4.2 ms against 1.5 ms uploaded.  (Uploading the
+            // destination list too, so that a deferral's radix pass would not bring it across
+            // PCIe again, cost random calls more than it saved heavy repeats: 1 Mi pairs
+            // 0.37-0.40 ms against 0.32-0.33, profiles/r06/iov_part/to_4mi/)
             const bool src_in_staging = o_res > o_src && !(src_listed && src_seq);
             if (src_in_staging && n >= (int)kIovLdsRoute) {
                 upload_pinned(dev + o_src, up + o_src, o_res - o_src, r.streams[si]);

@@ -101,7 +101,7 @@ int gaamd_toggle_counts(unsigned long long counts[3]);
  * LDS), [1] hashed, then the radix path for the pairs it could not order (more than
  * 8192 such pairs), [2] the radix path (above the other paths' range, or for the
  * partitions [3] deferred), [3] ordered in LDS: one workgroup below 1 Ki pairs, hash
- * partitions up to 1 Mi pairs (tuning iov_lds=0 routes to [0]-[2] instead). */
+ * partitions up to 4 Mi pairs (tuning iov_lds=0 routes to [0]-[2] instead). */
 int gaamd_iov_path_counts(unsigned long long counts[4]);
 /* runs fn(t, ctx) for t = 0 .. T-1 (1 <= T <= 16) on the library's persistent host worker
  * pool, t = 0 on the calling thread, and returns when all have; -1 on bad arguments.
@@ -131,7 +131,7 @@ int gaamd_owner_counts(unsigned long long counts[4]);
 /* keys: "kind" (0 auto, 1 rows, 2 flat, 3 serial, 4 ordered), "block" (0 auto/64/128),
  * "flat_max_nvec", "align", "flat_line_min", "ordered_cols" (column-sliced ordered
  * kernel), "streams", "iov_lds" (1: io-vectors with repeated destinations ordered in
- * LDS up to 1 Mi pairs; 0: the hashed / radix paths); returns the previous value or -1 */
+ * LDS up to 4 Mi pairs; 0: the hashed / radix paths); returns the previous value or -1 */
 int gaamd_set_tuning(const char *key, int value);
 int gaamd_get_tuning(const char *key);
 

@@ -730,15 +730,18 @@ def test_accv_large_repeated_destinations(gpu_lib, oracle, op, nbytes, slots, sh
         assert paths2[key] == paths1[key] + 1, (conflicting, paths1, paths2)
 
 
+PART_MAX = 1 << 22   # kIovPartMax (gaamd_kernels.h): the partitioned LDS path's largest call
+
+
 @pytest.mark.parametrize("op,nbytes,slots,n", [(C.DBL, 8, 150000, 600037), (C.FLT, 4, 900, 530001),
                                                (C.LNG, 8, 70000, 4 * 2 ** 18 + 5)])
 def test_accv_radix_path(gpu_lib, oracle, op, nbytes, slots, n):
     """Above 2^19 pairs the hashed path is skipped: with tuning iov_lds=0 (and by default
-    above 2^20 pairs, where the partitioned LDS path stops) every destination is sorted on
+    above PART_MAX pairs, where the partitioned LDS path stops) every destination is sorted on
     the GPU by the library's own stable LSD radix sort (k_rs_*; 8-bit digits, 2 passes at
     900 slots, 3 at 70 000 and 150 000; ragged last tile) and each destination's pairs
     applied in input order -- bit-exact against the pairs applied one by one; by default,
-    up to 2^20 pairs, the partitioned path gives the same bytes."""
+    up to PART_MAX pairs, the partitioned path gives the same bytes."""
     rng = np.random.default_rng(n)
     src = C.fill_bytes(op, n * nbytes, 11)
     dst = C.fill_bytes(op, slots * nbytes, 12)
@@ -760,7 +763,7 @@ def test_accv_radix_path(gpu_lib, oracle, op, nbytes, slots, n):
             paths1 = ga_amd.iov_path_counts()
         finally:
             ga_amd.set_tuning("iov_lds", old)
-        key = "lds" if lds and n <= 1 << 20 else "radix"
+        key = "lds" if lds and n <= PART_MAX else "radix"
         assert paths1[key] == paths0[key] + 1, (lds, paths0, paths1)
         got = db.download(np.uint8, dst.size)
         assert same_bits_nan_aware(got, want, op), f"iov_lds={lds}"
