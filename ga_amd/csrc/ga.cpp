@@ -555,7 +555,17 @@ static void gatscat(GatScat op, int g_a, void *v, int *const *csubs, const int *
                                 (void *)&fn))
             fatal("gather/scatter: host pool refused %d threads", T);
     };
-    run(locate);
+    if (a.nproc_grid == 1) {
+        // one block: every element is its owner's (rank 0 of the grid) -- no counting pass
+        // (the placing pass still checks every subscript)
+        for (int t = 0; t < T; ++t) {
+            long k0, k1;
+            range(t, &k0, &k1);
+            cnt[(size_t)t * P] = k1 - k0;
+        }
+    } else {
+        run(locate);
+    }
     std::vector<long> nelem(P, 0), first(P, 0);
     long acc = 0;
     for (int p = 0; p < P; p++) {
